@@ -1,0 +1,132 @@
+"""ctypes front-end of the CPU restatement (oracle/bine_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, by ``__graft_entry__.smoke()`` as
+the checker, and by bench.py's ``cpu_baseline`` leg.  The product package
+(pico_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+
+DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 5,
+          "int64": 6, "uint64": 7, "float": 8, "double": 9}
+NP_DTYPES = {"int8": np.int8, "uint8": np.uint8, "int16": np.int16, "uint16": np.uint16,
+             "int32": np.int32, "uint32": np.uint32, "int64": np.int64, "uint64": np.uint64,
+             "float": np.float32, "double": np.float64}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+OK, ERR_ARG, ERR_SIZE, ASSERT, DEADLOCK = 0, 12, 51, -2, -3
+
+_lib = None
+
+
+def build() -> str:
+    """Compile liboracle.so (gcc) if missing or stale."""
+    src = os.path.join(_HERE, "bine_oracle.c")
+    if (not os.path.exists(_LIB)) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", _HERE, "liboracle.so"], check=True)
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.orc_fill.argtypes = [vp, ctypes.c_int, sz, ctypes.c_uint]
+        L.orc_reduce_local.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_int]
+        L.orc_pi.argtypes = [ctypes.c_int] * 3
+        L.orc_remap_rank.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_remap_rank.restype = ctypes.c_uint32
+        L.orc_get_nu.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_get_nu.restype = ctypes.c_uint32
+        L.orc_static_tables.argtypes = [ctypes.c_int, vp, vp, vp]
+        L.orc_allreduce.argtypes = [ctypes.c_char_p, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int,
+                                    sz, ctypes.c_int, vp, vp, vp]
+        L.orc_reduce_scatter.argtypes = [ctypes.c_char_p, ctypes.c_int, vp, ctypes.c_int,
+                                         ctypes.c_int, vp, vp, vp]
+        L.orc_reduce.argtypes = [ctypes.c_char_p, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if a is not None else None for a in arrs])
+
+
+def fill(dtype: str, n: int, seed: int) -> np.ndarray:
+    """pico_core's generator (pico_core_utils.c:883-928) with seed `seed`."""
+    a = np.empty(n, dtype=NP_DTYPES[dtype])
+    lib().orc_fill(a.ctypes.data, DTYPES[dtype], n, seed)
+    return a
+
+
+def inputs(dtype: str, n: int, P: int, seed_base: int = 1234):
+    return [fill(dtype, n, seed_base + r) for r in range(P)]
+
+
+def reduce_local(inp: np.ndarray, inout: np.ndarray, dtype: str, op: str = "sum") -> None:
+    """MPI_Reduce_local(in, inout) with MPICH 3.3.2 semantics (in place on inout)."""
+    lib().orc_reduce_local(inp.ctypes.data, inout.ctypes.data, inout.size, DTYPES[dtype], OPS[op])
+
+
+def remap_rank(P: int, r: int) -> int:
+    return int(lib().orc_remap_rank(P, r))
+
+
+def pi(r: int, s: int, P: int) -> int:
+    return int(lib().orc_pi(r, s, P))
+
+
+def static_tables(P: int):
+    n = P.bit_length() - 1
+    perm = np.zeros(P, np.int32)
+    st = np.zeros(P * n, np.int32)
+    rt = np.zeros(P * n, np.int32)
+    if lib().orc_static_tables(P, perm.ctypes.data, st.ctypes.data, rt.ctypes.data):
+        raise ValueError(P)
+    return perm, st.reshape(P, n), rt.reshape(P, n)
+
+
+def allreduce(algo, sbufs, dtype, op="sum", segsize=0, ref_bugs=False):
+    P, n = len(sbufs), sbufs[0].size
+    rbufs = [np.zeros(n, dtype=NP_DTYPES[dtype]) for _ in range(P)]
+    rets = np.zeros(P, np.int32)
+    if lib().orc_allreduce(algo.encode(), P, n, DTYPES[dtype], OPS[op], segsize, int(ref_bugs),
+                           _ptrs(sbufs), _ptrs(rbufs), rets.ctypes.data):
+        raise ValueError(algo)
+    return rbufs, rets.tolist()
+
+
+def reduce_scatter(algo, sbufs, rcounts, dtype, op="sum"):
+    P = len(sbufs)
+    rc = np.asarray(rcounts, dtype=np.int32)
+    rbufs = [np.zeros(max(int(c), 1), dtype=NP_DTYPES[dtype]) for c in rc]
+    rets = np.zeros(P, np.int32)
+    if lib().orc_reduce_scatter(algo.encode(), P, rc.ctypes.data, DTYPES[dtype], OPS[op],
+                                _ptrs(sbufs), _ptrs(rbufs), rets.ctypes.data):
+        raise ValueError(algo)
+    return [b[:int(c)] for b, c in zip(rbufs, rc)], rets.tolist()
+
+
+def reduce(algo, sbufs, dtype, op="sum", root=0):
+    P, n = len(sbufs), sbufs[0].size
+    rbufs = [np.zeros(n, dtype=NP_DTYPES[dtype]) if r == root else None for r in range(P)]
+    rets = np.zeros(P, np.int32)
+    if lib().orc_reduce(algo.encode(), P, n, DTYPES[dtype], OPS[op], root,
+                        _ptrs(sbufs), _ptrs(rbufs), rets.ctypes.data):
+        raise ValueError(algo)
+    return rbufs[root], rets.tolist()
+
+
+def rs_rcounts(N: int, P: int, kind: str = "even"):
+    """Block sizes used by the golden capture (oracle/ref_golden.c)."""
+    return [N // P + ((i % 3) if kind == "ragged" else 0) for i in range(P)]

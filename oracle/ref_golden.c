@@ -1,0 +1,176 @@
+/*
+ * ref_golden.c -- golden-vector capture harness for the REAL reference libbine.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This program is never shipped and never part of
+ * the product path.  It is linked against oracle/_ref/libbine_ref.so, which
+ * oracle/Makefile (target `ref`) compiles directly from the reference sources
+ * where they lie (/root/reference/libbine/{libbine_allreduce,
+ * libbine_reduce_scatter,libbine_reduce,libbine_utils_bitmaps}.c) against the
+ * image's MPICH 3.3.2 (/opt/conda).  Run under mpiexec -n P by
+ * tools/make_golden.py, it fills each rank's send buffer with pico_core's own
+ * distributions (pico_core/pico_core_utils.c:883-928, seed = base + rank instead
+ * of time(NULL) + rank so that the vectors are reproducible), calls one libbine
+ * entry point (include/libbine.h:30-78) and dumps per-rank input digest, output
+ * and return code.
+ *
+ * usage: ref_golden <outdir> <coll> <algo> <op> <segsize> <rcounts_kind>
+ *                   <seed_base> <dtype,dtype,...> <N,N,...>
+ *   coll         allreduce | reduce_scatter | reduce | fill (dump the inputs)
+ *   rcounts_kind even   -> rcounts[i] = N / P  (pico_core_utils.c:535-536)
+ *                ragged -> rcounts[i] = N / P + (i % 3)   (exercises displs)
+ */
+#include <mpi.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "libbine.h"
+
+typedef int (*ar_fn)(const void *, void *, size_t, MPI_Datatype, MPI_Op, MPI_Comm);
+typedef int (*rs_fn)(const void *, void *, const int *, MPI_Datatype, MPI_Op, MPI_Comm);
+typedef int (*rd_fn)(const void *, void *, size_t, MPI_Datatype, MPI_Op, int, MPI_Comm);
+
+static ar_fn pick_allreduce(const char *a) {
+  if (!strcmp(a, "recursivedoubling")) return allreduce_recursivedoubling;
+  if (!strcmp(a, "ring")) return allreduce_ring;
+  if (!strcmp(a, "rabenseifner")) return allreduce_rabenseifner;
+  if (!strcmp(a, "bine_lat")) return allreduce_bine_lat;
+  if (!strcmp(a, "bine_bdw_static")) return allreduce_bine_bdw_static;
+  if (!strcmp(a, "bine_bdw_remap")) return allreduce_bine_bdw_remap;
+  if (!strcmp(a, "bine_bdw_remap_segmented")) return allreduce_bine_bdw_remap_segmented;
+  if (!strcmp(a, "bine_block_by_block_any_even")) return allreduce_bine_block_by_block_any_even;
+  return NULL;
+}
+
+static rs_fn pick_reduce_scatter(const char *a) {
+  if (!strcmp(a, "recursivehalving")) return reduce_scatter_recursivehalving;
+  if (!strcmp(a, "recursive_distance_doubling")) return reduce_scatter_recursive_distance_doubling;
+  if (!strcmp(a, "ring")) return reduce_scatter_ring;
+  if (!strcmp(a, "butterfly")) return reduce_scatter_butterfly;
+  if (!strcmp(a, "bine_static")) return reduce_scatter_bine_static;
+  if (!strcmp(a, "bine_send_remap")) return reduce_scatter_bine_send_remap;
+  if (!strcmp(a, "bine_permute_remap")) return reduce_scatter_bine_permute_remap;
+  if (!strcmp(a, "bine_block_by_block")) return reduce_scatter_bine_block_by_block;
+  if (!strcmp(a, "bine_block_by_block_any_even")) return reduce_scatter_bine_block_by_block_any_even;
+  return NULL;
+}
+
+static rd_fn pick_reduce(const char *a) {
+  if (!strcmp(a, "bine_lat")) return reduce_bine_lat;
+  if (!strcmp(a, "bine_bdw")) return reduce_bine_bdw;
+  return NULL;
+}
+
+static int dtype_of(const char *s, MPI_Datatype *dt, size_t *sz) {
+  if (!strcmp(s, "float"))  { *dt = MPI_FLOAT;         *sz = 4; return 0; }
+  if (!strcmp(s, "double")) { *dt = MPI_DOUBLE;        *sz = 8; return 0; }
+  if (!strcmp(s, "int8"))   { *dt = MPI_INT8_T;        *sz = 1; return 0; }
+  if (!strcmp(s, "int16"))  { *dt = MPI_INT16_T;       *sz = 2; return 0; }
+  if (!strcmp(s, "int32"))  { *dt = MPI_INT32_T;       *sz = 4; return 0; }
+  if (!strcmp(s, "int64"))  { *dt = MPI_INT64_T;       *sz = 8; return 0; }
+  if (!strcmp(s, "uint8"))  { *dt = MPI_UNSIGNED_CHAR; *sz = 1; return 0; }
+  return -1;
+}
+
+static int op_of(const char *s, MPI_Op *op) {
+  if (!strcmp(s, "sum"))  { *op = MPI_SUM;  return 0; }
+  if (!strcmp(s, "prod")) { *op = MPI_PROD; return 0; }
+  if (!strcmp(s, "max"))  { *op = MPI_MAX;  return 0; }
+  if (!strcmp(s, "min"))  { *op = MPI_MIN;  return 0; }
+  return -1;
+}
+
+/* pico_core's generator (pico_core_utils.c:902-923), glibc rand_r. */
+static void fill(void *buf, const char *dt, size_t n, unsigned int seed) {
+  for (size_t i = 0; i < n; i++) {
+    if (!strcmp(dt, "int8"))        ((int8_t *)buf)[i] = (int8_t)((rand_r(&seed) % 256) - 128);
+    else if (!strcmp(dt, "int16"))  ((int16_t *)buf)[i] = (int16_t)((rand_r(&seed) % 65536) - 32768);
+    else if (!strcmp(dt, "int32"))  ((int32_t *)buf)[i] = (int32_t)rand_r(&seed);
+    else if (!strcmp(dt, "int64"))  { int64_t hi = (int64_t)rand_r(&seed) << 32; ((int64_t *)buf)[i] = hi | rand_r(&seed); }
+    else if (!strcmp(dt, "float"))  ((float *)buf)[i] = (float)rand_r(&seed) / (float)RAND_MAX * 100.0f;
+    else if (!strcmp(dt, "double")) ((double *)buf)[i] = (double)rand_r(&seed) / (double)RAND_MAX * 100.0;
+    else if (!strcmp(dt, "uint8"))  ((unsigned char *)buf)[i] = (unsigned char)(rand_r(&seed) % 256);
+  }
+}
+
+static int split_csv(char *s, char **out, int max) {
+  int n = 0;
+  for (char *tok = strtok(s, ","); tok && n < max; tok = strtok(NULL, ",")) out[n++] = tok;
+  return n;
+}
+
+int main(int argc, char **argv) {
+  MPI_Init(&argc, &argv);
+  int rank, P;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &P);
+  if (argc != 10) {
+    if (!rank) fprintf(stderr, "bad args\n");
+    MPI_Abort(MPI_COMM_WORLD, 2);
+  }
+  const char *outdir = argv[1], *coll = argv[2], *algo = argv[3], *ops = argv[4];
+  size_t segsize = (size_t)strtoull(argv[5], NULL, 10);
+  const char *rk = argv[6];
+  unsigned seed_base = (unsigned)strtoul(argv[7], NULL, 10);
+  char *dts[16], *ns[32];
+  int ndt = split_csv(argv[8], dts, 16);
+  int nn = split_csv(argv[9], ns, 32);
+  MPI_Op op;
+  if (op_of(ops, &op)) MPI_Abort(MPI_COMM_WORLD, 3);
+  bine_allreduce_segsize = segsize;
+
+  for (int d = 0; d < ndt; d++) {
+    MPI_Datatype dt; size_t esz;
+    if (dtype_of(dts[d], &dt, &esz)) MPI_Abort(MPI_COMM_WORLD, 4);
+    for (int k = 0; k < nn; k++) {
+      size_t N = (size_t)strtoull(ns[k], NULL, 10);
+      int *rcounts = (int *)malloc(sizeof(int) * (size_t)P);
+      size_t total = N, outn = N;
+      if (!strcmp(coll, "reduce_scatter")) {
+        total = 0;
+        for (int i = 0; i < P; i++) {
+          rcounts[i] = (int)(N / (size_t)P) + (!strcmp(rk, "ragged") ? (i % 3) : 0);
+          total += (size_t)rcounts[i];
+        }
+        outn = (size_t)rcounts[rank];
+      }
+      void *sbuf = malloc(total * esz + 16);
+      void *rbuf = calloc(total * esz + 16, 1);
+      fill(sbuf, dts[d], total, seed_base + (unsigned)rank);
+      int ret = -12345;
+      if (!strcmp(coll, "fill")) {           /* pins the input generator itself */
+        memcpy(rbuf, sbuf, total * esz);
+        ret = 0;
+      } else if (!strcmp(coll, "allreduce")) {
+        ar_fn f = pick_allreduce(algo);
+        if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
+        ret = f(sbuf, rbuf, N, dt, op, MPI_COMM_WORLD);
+      } else if (!strcmp(coll, "reduce_scatter")) {
+        rs_fn f = pick_reduce_scatter(algo);
+        if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
+        ret = f(sbuf, rbuf, rcounts, dt, op, MPI_COMM_WORLD);
+      } else if (!strcmp(coll, "reduce")) {
+        rd_fn f = pick_reduce(algo);
+        if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
+        /* pico_core passes rbuf = NULL on non-roots (pico_core_reduce_utils.c:24-31) */
+        ret = f(sbuf, rank == 0 ? rbuf : NULL, N, dt, op, 0, MPI_COMM_WORLD);
+        if (rank != 0) outn = 0;
+      } else {
+        MPI_Abort(MPI_COMM_WORLD, 6);
+      }
+      char path[1024];
+      snprintf(path, sizeof path, "%s/%s.N%zu.r%d.bin", outdir, dts[d], N, rank);
+      FILE *fp = fopen(path, "wb");
+      if (!fp) MPI_Abort(MPI_COMM_WORLD, 7);
+      int64_t hdr[2] = {ret, (int64_t)outn};
+      fwrite(hdr, sizeof hdr, 1, fp);
+      if (outn) fwrite(rbuf, esz, outn, fp);
+      fclose(fp);
+      free(sbuf); free(rbuf); free(rcounts);
+      MPI_Barrier(MPI_COMM_WORLD);
+    }
+  }
+  MPI_Finalize();
+  return 0;
+}

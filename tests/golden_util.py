@@ -1,0 +1,71 @@
+"""Loaders for the golden vectors captured from the real reference libbine.
+
+The fixtures (tests/golden/index.json + outputs.npz) were produced by
+tools/make_golden.py from oracle/_ref (the reference's own libbine sources
+compiled against MPICH 3.3.2); see that script for the case matrix.
+"""
+from __future__ import annotations
+
+import functools
+import hashlib
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NP = {"float": np.float32, "double": np.float64, "int8": np.int8, "int16": np.int16,
+      "int32": np.int32, "int64": np.int64, "uint8": np.uint8}
+
+
+@functools.lru_cache(maxsize=None)
+def cases():
+    with open(os.path.join(GOLDEN, "index.json")) as f:
+        return json.load(f)["cases"]
+
+
+@functools.lru_cache(maxsize=None)
+def _npz():
+    return np.load(os.path.join(GOLDEN, "outputs.npz"), allow_pickle=False)
+
+
+def select(**kw):
+    out = []
+    for c in cases():
+        if all(c.get(k) == v for k, v in kw.items()):
+            out.append(c)
+    return out
+
+
+def rcounts(c):
+    P, N = c["P"], c["N"]
+    return [N // P + ((i % 3) if c["rcounts"] == "ragged" else 0) for i in range(P)]
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def outputs(c):
+    """Per-rank expected outputs of a stored case (list of arrays), else None."""
+    if not c.get("stored"):
+        return None
+    raw = _npz()[c["id"]].tobytes()
+    dt = NP[c["dtype"]]
+    if c["stored"] == "rank0":
+        a = np.frombuffer(raw, dtype=dt)
+        return [a] * c["P"]
+    res, off = [], 0
+    esz = np.dtype(dt).itemsize
+    for n in c["outn"]:
+        res.append(np.frombuffer(raw[off:off + n * esz], dtype=dt))
+        off += n * esz
+    return res
+
+
+def check_rank_outputs(c, got, ranks=None):
+    """Assert that per-rank outputs `got` equal the golden bit-for-bit
+    (digest comparison; identical to a byte compare)."""
+    ranks = range(c["P"]) if ranks is None else ranks
+    bad = [r for r in ranks if sha(np.asarray(got[r])[: c["outn"][r]]) != c["sha256"][r]]
+    return bad

@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""Capture golden vectors from the REAL reference libbine (test infrastructure).
+
+Runs ``oracle/_ref/ref_golden`` (built by ``make -C oracle ref`` from the sources
+under /root/reference, against the image's MPICH 3.3.2) under ``mpiexec -n P``
+and writes:
+
+* ``tests/golden/index.json`` -- one record per (collective, algorithm, op,
+  dtype, P, N, segsize, rcounts kind): per-rank return codes, output lengths and
+  SHA-256 digests of the outputs;
+* ``tests/golden/outputs.npz`` -- the full per-rank outputs of the small cases
+  (concatenated over ranks, raw bytes as uint8).
+
+Inputs are not stored: they are regenerated from ``seed_base + rank`` with
+pico_core's generator (pico_core/pico_core_utils.c:883-928); the ``fill`` cases
+pin that generator itself.  This script needs /root/reference and is run by hand
+in the build container only; the fixtures it writes are what travels.
+"""
+from __future__ import annotations
+
+import hashlib
+import itertools
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
+OUT = os.path.join(ROOT, "tests", "golden")
+MPI = "/opt/conda/bin"
+SEED = 1234
+ESZ = {"float": 4, "double": 8, "int8": 1, "int16": 2, "int32": 4, "int64": 8, "uint8": 1}
+
+SMALL_N = [1, 2, 7, 8, 13, 64, 333]
+MID_N = [4096, 65537]
+ALL_DT = ["float", "double", "int32", "int64", "int8", "uint8", "int16"]
+FEW_DT = ["float", "int64"]
+
+AR_BINE = ["bine_bdw_remap", "bine_bdw_static", "bine_lat", "bine_block_by_block_any_even"]
+AR_CLASSIC = ["recursivedoubling", "ring", "rabenseifner"]
+AR_NONPOW2 = {"recursivedoubling", "ring", "rabenseifner", "bine_lat",
+              "bine_bdw_remap_segmented", "bine_block_by_block_any_even",
+              "bine_bdw_remap", "bine_bdw_static"}  # the last two return MPI_ERR_ARG
+RS_BINE = ["bine_permute_remap", "bine_send_remap", "bine_static", "bine_block_by_block",
+           "bine_block_by_block_any_even"]
+RS_CLASSIC = ["recursivehalving", "recursive_distance_doubling", "ring", "butterfly"]
+# reduce_scatter algorithms that honour per-block rcounts (displs); permute_remap
+# copies block i into the slot of block remap(i) and needs equal blocks.
+RS_RAGGED_OK = {"recursivehalving", "recursive_distance_doubling", "ring", "butterfly",
+                "bine_static", "bine_send_remap", "bine_block_by_block",
+                "bine_block_by_block_any_even"}
+# non-power-of-two sizes: these hang in the reference -- skipped
+RS_NONPOW2 = {"recursivehalving", "ring", "butterfly", "bine_block_by_block_any_even",
+              "bine_static", "recursive_distance_doubling"}
+
+
+def run_case(P, coll, algo, op, segsize, rk, dtypes, ns, timeout=120):
+    tmp = tempfile.mkdtemp(prefix="golden_")
+    env = dict(os.environ, PATH=MPI + ":" + os.environ.get("PATH", ""))
+    cmd = [os.path.join(MPI, "mpiexec"), "-n", str(P), BIN, tmp, coll, algo, op, str(segsize),
+           rk, str(SEED), ",".join(dtypes), ",".join(str(n) for n in ns)]
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, timeout=timeout)
+        failed = p.returncode != 0
+    except subprocess.TimeoutExpired:
+        failed = True
+    recs = []
+    for dt in dtypes:
+        for n in ns:
+            rets, outs = [], []
+            for r in range(P):
+                path = os.path.join(tmp, f"{dt}.N{n}.r{r}.bin")
+                if not os.path.exists(path):
+                    rets = None
+                    break
+                raw = open(path, "rb").read()
+                ret, outn = np.frombuffer(raw[:16], dtype=np.int64)
+                rets.append(int(ret))
+                outs.append(raw[16:16 + int(outn) * ESZ[dt]])
+            recs.append((dt, n, rets, outs, failed))
+    shutil.rmtree(tmp, ignore_errors=True)
+    return recs
+
+
+def main():
+    if not os.path.exists(BIN):
+        sys.exit("build the reference first: make -C oracle ref")
+    os.makedirs(OUT, exist_ok=True)
+    jobs = []  # (P, coll, algo, op, segsize, rk, dtypes, ns, store_small)
+    # input generator pin
+    jobs.append((8, "fill", "-", "sum", 0, "even", ALL_DT, [64], True))
+    for P in (1, 2, 4, 8):
+        for a in AR_BINE:
+            jobs.append((P, "allreduce", a, "sum", 0, "even", ALL_DT, SMALL_N + MID_N, True))
+        for seg in (0, 16, 64, 4096):
+            jobs.append((P, "allreduce", "bine_bdw_remap_segmented", "sum", seg, "even",
+                         ["float", "int64", "int8"], SMALL_N + MID_N, True))
+        for a in AR_CLASSIC:
+            jobs.append((P, "allreduce", a, "sum", 0, "even", FEW_DT, SMALL_N + MID_N, True))
+        for a in RS_BINE + RS_CLASSIC:
+            dts = ALL_DT if a in RS_BINE else FEW_DT
+            jobs.append((P, "reduce_scatter", a, "sum", 0, "even", dts, [P * k for k in (1, 3, 16)] + [P * 8192 + 0], True))
+            if a in RS_RAGGED_OK and P > 1:
+                jobs.append((P, "reduce_scatter", a, "sum", 0, "ragged", FEW_DT, [P * 4, P * 50], True))
+        for a in ("bine_lat", "bine_bdw"):
+            jobs.append((P, "reduce", a, "sum", 0, "even", ALL_DT, SMALL_N + MID_N, True))
+        for op in ("max", "min", "prod"):
+            jobs.append((P, "allreduce", "bine_bdw_remap", op, 0, "even", ["float", "double", "int32"], [13, 4096], True))
+            jobs.append((P, "reduce_scatter", "bine_permute_remap", op, 0, "even", ["float", "int32"], [P * 3, P * 1024], True))
+            jobs.append((P, "reduce", "bine_bdw", op, 0, "even", ["float", "int32"], [13, 4096], True))
+    for P in (3, 6):
+        for a in sorted(AR_NONPOW2):
+            seg = 64 if a == "bine_bdw_remap_segmented" else 0
+            jobs.append((P, "allreduce", a, "sum", seg, "even", FEW_DT, [1, 7, 13, 333, 4096], True))
+        for a in sorted(RS_NONPOW2):
+            jobs.append((P, "reduce_scatter", a, "sum", 0, "even", FEW_DT, [P, P * 5, P * 1000], True))
+        for a in ("bine_lat", "bine_bdw"):
+            jobs.append((P, "reduce", a, "sum", 0, "even", ["float"], [13], True))
+    # large: digests only (the headline schedule at a non-power-of-two-friendly size)
+    for a, seg in (("bine_bdw_remap", 0), ("bine_bdw_static", 0), ("bine_bdw_remap_segmented", 65536),
+                   ("bine_bdw_remap_segmented", 0)):
+        jobs.append((8, "allreduce", a, "sum", seg, "even", ["float"], [1000003], False))
+    jobs.append((8, "reduce_scatter", "bine_permute_remap", "sum", 0, "even", ["float"], [8 * 131072 + 8 * 3], False))
+    jobs.append((8, "allreduce", "bine_bdw_remap", "sum", 0, "even", ["double", "int64"], [262147], False))
+
+    index, arrays = [], {}
+    for (P, coll, algo, op, seg, rk, dts, ns, store) in jobs:
+        recs = run_case(P, coll, algo, op, seg, rk, dts, ns)
+        if any(r[2] is None for r in recs):
+            # one crashing case (e.g. the static variant's tmp_buf overflow,
+            # libbine_allreduce.c:724 vs :749-765) kills the whole mpiexec:
+            # re-run the missing cases one at a time
+            fixed = []
+            for rec in recs:
+                if rec[2] is None:
+                    rec = run_case(P, coll, algo, op, seg, rk, [rec[0]], [rec[1]])[0]
+                fixed.append(rec)
+            recs = fixed
+        for dt, n, rets, outs, failed in recs:
+            cid = f"{coll}.{algo}.{op}.{dt}.P{P}.N{n}.seg{seg}.{rk}"
+            rec = {"id": cid, "coll": coll, "algo": algo, "op": op, "dtype": dt, "P": P, "N": n,
+                   "segsize": seg, "rcounts": rk, "seed_base": SEED}
+            if rets is None:
+                rec["status"] = "no_output"  # reference aborted / hung
+            else:
+                rec["status"] = "ok"
+                rec["rets"] = rets
+                rec["outn"] = [len(o) // ESZ[dt] for o in outs]
+                rec["sha256"] = [hashlib.sha256(o).hexdigest() for o in outs]
+                # identical outputs on every rank (allreduce) are stored once
+                same = len(set(rec["sha256"])) == 1
+                blob = outs[0] if same else b"".join(outs)
+                small = store and len(blob) <= 16 * 1024
+                if small:
+                    arrays[cid] = np.frombuffer(blob, dtype=np.uint8)
+                rec["stored"] = ("rank0" if same else "all") if small else None
+            index.append(rec)
+        print(f"P={P} {coll} {algo} {op} seg={seg} {rk}: {len(recs)} cases", flush=True)
+    with open(os.path.join(OUT, "index.json"), "w") as f:
+        json.dump({"generator": "tools/make_golden.py", "reference": "HLC-Lab/pico libbine @ 2025-07-25",
+                   "mpi": "MPICH 3.3.2 (ch3:nemesis)", "cases": index}, f, separators=(",", ":"))
+    np.savez_compressed(os.path.join(OUT, "outputs.npz"), **arrays)
+    print(len(index), "cases,", len(arrays), "stored")
+
+
+if __name__ == "__main__":
+    main()
