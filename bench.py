@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Bine reduce-family path (BASELINE.json metric:
+"device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X").
+
+N = 1 (default): BASELINE config C2, the workload the metric's single-GPU
+configuration names -- the fp32 MPI_Reduce_local replacement kernel on 64 MiB
+(inout = inout + in, 16,777,216 elements), i.e. the per-step arithmetic of the
+Bine allreduce.  value = HBM GB/s = 3 * 64 MiB / t (read in, read inout, write
+inout).  Buffers rotate over 4 independent sets (768 MiB)
+so that no launch is served from the 256 MiB Infinity Cache.
+
+N > 1 (torch.distributed.run, one process per GPU): BASELINE config C3,
+allreduce_bine_bdw_remap fp32 256 MiB per rank over RCCL P2P / xGMI.
+value = whole-job algorithmic throughput = N * 256 MiB / t; per-rank busbw
+2 (N-1)/N * S / t and algbw S / t are reported beside it.
+
+Timing: W untimed warm-up steps, then K steps between a barrier +
+device synchronize on both sides, HIP events on the stream the kernels run on,
+max over ranks.  One JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
+XGMI_LINK_GBS = 153.0          # one xGMI link (task statement); 7 links per GPU
+C2_ELEMS = 16_777_216          # 64 MiB fp32
+C3_ELEMS = 67_108_864          # 256 MiB fp32
+MIB = 1 << 20
+
+
+def _pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    PMC passes (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel_prefix]
+        return float(k["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline_c2(budget_s: float = 10.0):
+    """The oracle's MPI_Reduce_local (MPICH semantics, one host core) on the C2
+    workload, bounded to ~budget_s of CPU time."""
+    import numpy as np
+    from oracle import oracle as O
+    a = O.fill("float", C2_ELEMS, 1234)
+    b = O.fill("float", C2_ELEMS, 1235)
+    O.reduce_local(a, b, "float")  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.reduce_local(a, b, "float")
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 2000:
+            break
+    per = el / n
+    return {"value": round(3 * C2_ELEMS * 4 / per / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle orc_reduce_local fp32 SUM, 64 MiB, {n} calls in {el:.1f} s on one host core "
+                      f"({per * 1e3:.2f} ms/call)"}
+
+
+def bench_c2(steps: int, warmup: int):
+    import torch
+    import pico_amd
+    dev = torch.device("cuda:0")
+    sets = 4
+    ins, ios = [], []
+    for k in range(sets):
+        a = torch.empty(C2_ELEMS, dtype=torch.float32, device=dev)
+        b = torch.empty(C2_ELEMS, dtype=torch.float32, device=dev)
+        pico_amd.fill_pico(a, C2_ELEMS, "float", 1234 + 2 * k)
+        pico_amd.fill_pico(b, C2_ELEMS, "float", 1235 + 2 * k)
+        ins.append(a)
+        ios.append(b)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    for i in range(warmup):
+        pico_amd.reduce_local(ins[i % sets], ios[i % sets], C2_ELEMS, "float", "sum", stream=stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(steps):
+        pico_amd.reduce_local(ins[i % sets], ios[i % sets], C2_ELEMS, "float", "sum", stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / steps
+    alg_bytes = 3 * C2_ELEMS * 4
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    traffic = _pmc_traffic("k_reduce")
+    return {
+        "metric": "device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X",
+        "value": round(gbs, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (pico_core rand_r distribution, generated on device)",
+        "config": {"workload": "C2: fp32 MPI_Reduce_local replacement kernel, inout=inout+in, 64 MiB "
+                               "(16,777,216 elem), 1 MI355X, 4 rotating buffer sets",
+                   "value_definition": "HBM GB/s = 3*64MiB/t (BASELINE.md 3)"},
+        "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "kernel": "bine::k_reduce<float,SUM>", "algorithmic_bytes_per_launch": alg_bytes},
+        "wall_s": round(wall, 4),
+    }
+
+
+def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str):
+    import torch
+    import torch.distributed as dist
+    import pico_amd
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo")
+    comm = pico_amd.Comm.from_torch_distributed(local)
+    dev = torch.device("cuda", local)
+    sbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
+    rbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
+    pico_amd.fill_pico(sbuf, nelem, "float", 1234 + rank)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
+    torch.cuda.synchronize()
+    comm.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    comm.synchronize()
+    wall = time.perf_counter() - t0
+    dist.barrier()
+    ms_local = e0.elapsed_time(e1) / steps
+    t = torch.tensor([ms_local, wall], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms, wall = float(t[0]), float(t[1])
+    S = nelem * 4
+    algbw = S / (ms * 1e-3) / 1e9
+    busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X",
+            "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (pico_core rand_r distribution, generated on device)",
+            "config": {"workload": f"C3: allreduce_{algo} fp32 {S // MIB} MiB/rank over RCCL P2P (xGMI), "
+                                   f"{world} x MI355X", "value_definition": "N * S / t (whole job)",
+                       "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2)},
+            "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": XGMI_LINK_GBS, "unit": "GB/s",
+                         "frac": round(busbw / XGMI_LINK_GBS, 4), "traffic": None,
+                         "note": "faithful Bine: one peer (one xGMI link) per step; aggregate 7-link peak "
+                                 f"{7 * XGMI_LINK_GBS:.0f} GB/s -> frac {busbw / (7 * XGMI_LINK_GBS):.4f}"},
+            "wall_s": round(wall, 4),
+        }
+    comm.destroy()
+    dist.destroy_process_group()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--algo", default="bine_bdw_remap")
+    ap.add_argument("--elems", type=int, default=C3_ELEMS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+    if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+        return
+    res = bench_c2(args.steps, args.warmup)
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_c2(args.cpu_budget)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,190 @@
+/*
+ * bine_amd.h -- core C ABI of the MI355X Bine reduce-family library
+ * (libbine_amd.so).  Plain pointers and sizes; no MPI, torch or HIP types in
+ * the signatures (HIP streams travel as void*).
+ *
+ * This is the layer the libbine.h drop-in (include/libbine_amd.h, built as
+ * libbine.so) sits on, and the layer Python binds through ctypes.  Every
+ * collective entry point replaces one function of the reference's public API
+ * (reference include/libbine.h:30-78); the mapping is listed next to each
+ * enumerator of bine_algo below.
+ *
+ * Device pointers only: the buffers passed here must live in the memory of the
+ * communicator's device.  Operations are stream-ordered: they are enqueued on
+ * `stream` (NULL = the communicator's own stream) and return once enqueued;
+ * bine_comm_synchronize() or a synchronize on `stream` waits for completion.
+ */
+#ifndef BINE_AMD_H
+#define BINE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types; same numbering as the test oracle (oracle/bine_oracle.h) */
+typedef enum {
+  BINE_INT8 = 0, BINE_UINT8 = 1, BINE_INT16 = 2, BINE_UINT16 = 3,
+  BINE_INT32 = 4, BINE_UINT32 = 5, BINE_INT64 = 6, BINE_UINT64 = 7,
+  BINE_FLOAT = 8, BINE_DOUBLE = 9, BINE_NUM_DTYPES = 10
+} bine_dtype_t;
+
+/* reduction operators, MPI_Reduce_local semantics of MPICH 3.3.2:
+ * inout[i] = inout[i] (op) in[i]; MAX/MIN select inout when inout > in
+ * (resp. <), else in (NaN behaviour follows from that). */
+typedef enum { BINE_SUM = 0, BINE_PROD = 1, BINE_MAX = 2, BINE_MIN = 3, BINE_NUM_OPS = 4 } bine_op_t;
+
+typedef enum {
+  BINE_SUCCESS = 0,
+  BINE_ERR_ARG = 1,          /* reference returns MPI_ERR_ARG (e.g. non-power-of-two remap) */
+  BINE_ERR_SIZE = 2,         /* reference returns MPI_ERR_SIZE */
+  BINE_ERR_NO_MEM = 3,
+  BINE_ERR_HIP = 4,          /* a HIP runtime call failed */
+  BINE_ERR_RCCL = 5,         /* an RCCL call failed */
+  BINE_ERR_UNSUPPORTED = 6,  /* algorithm / dtype / op not provided */
+  BINE_ERR_INTERNAL = 7
+} bine_status_t;
+
+/* Algorithms.  Names are the libbine function names without the collective
+ * prefix; bine_algo_from_name() also accepts the full function name and the
+ * pico_core selector strings (pico_core_utils.c:103-249, e.g.
+ * "bine_bdw_remap_over"). */
+typedef enum {
+  /* allreduce_* -- libbine_allreduce.c */
+  BINE_AR_RECURSIVEDOUBLING = 0,      /* allreduce_recursivedoubling      :17   */
+  BINE_AR_RING = 1,                   /* allreduce_ring                   :138  */
+  BINE_AR_RABENSEIFNER = 2,           /* allreduce_rabenseifner           :441  */
+  BINE_AR_BINE_LAT = 3,               /* allreduce_bine_lat               :321  */
+  BINE_AR_BINE_BDW_STATIC = 4,        /* allreduce_bine_bdw_static        :696  */
+  BINE_AR_BINE_BDW_REMAP = 5,         /* allreduce_bine_bdw_remap         :820  */
+  BINE_AR_BINE_BDW_REMAP_SEGMENTED = 6, /* allreduce_bine_bdw_remap_segmented :1093 */
+  BINE_AR_BINE_BLOCK_BY_BLOCK_ANY_EVEN = 7, /* allreduce_bine_block_by_block_any_even :925 */
+  /* reduce_scatter_* -- libbine_reduce_scatter.c */
+  BINE_RS_RECURSIVEHALVING = 16,      /* :15   */
+  BINE_RS_RECURSIVE_DISTANCE_DOUBLING = 17, /* :259 */
+  BINE_RS_RING = 18,                  /* :421  */
+  BINE_RS_BUTTERFLY = 19,             /* :575  */
+  BINE_RS_BINE_STATIC = 20,           /* :763  */
+  BINE_RS_BINE_SEND_REMAP = 21,       /* :906  */
+  BINE_RS_BINE_PERMUTE_REMAP = 22,    /* :985  */
+  BINE_RS_BINE_BLOCK_BY_BLOCK = 23,   /* :1066 */
+  BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN = 24, /* :1176 */
+  /* reduce_* -- libbine_reduce.c */
+  BINE_RD_BINE_LAT = 32,              /* reduce_bine_lat :16 */
+  BINE_RD_BINE_BDW = 33               /* reduce_bine_bdw :83 */
+} bine_algo_t;
+
+/* the reference's MPI_IN_PLACE (mpi.h: (void *)-1) */
+#define BINE_IN_PLACE ((const void *)(intptr_t)-1)
+
+typedef struct bine_comm *bine_comm_t;
+
+const char *bine_status_string(int status);
+/* text of the last HIP/RCCL failure seen by this thread */
+const char *bine_last_error(void);
+/* reduce-kernel launch shape (tuning; also env BINE_REDUCE_UNROLL /
+ * BINE_REDUCE_MAXBLOCKS / BINE_REDUCE_NT): 16-B vectors in flight per lane
+ * (1, 2, 4, 8), grid cap (0 = 2048), non-temporal loads of `in` (fp32 SUM only) */
+int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);
+size_t bine_dtype_size(int dtype);
+/* -1 if unknown; `collective` = "allreduce" | "reduce_scatter" | "reduce" */
+int bine_algo_from_name(const char *collective, const char *name);
+const char *bine_algo_name(int algo);
+
+/* ---- the arithmetic boundary: MPI_Reduce_local on the GPU ------------------
+ * inout[i] = inout[i] (op) in[i]  (replaces every MPI_Reduce_local call site,
+ * e.g. libbine_allreduce.c:888).  `stream` is a hipStream_t (NULL = default). */
+int bine_reduce_local(const void *in, void *inout, size_t count, int dtype, int op, void *stream);
+/* out[i] = b[i] (op) a[i]  (out may alias b): the copy-free form used for the
+ * first step of a non-in-place collective. */
+int bine_reduce3(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream);
+
+/* pico_core's input distribution (pico_core_utils.c:902-923) generated on the
+ * device: element i of buffer `seed` equals what glibc rand_r(&seed) would
+ * produce for pico_core (LCG jump-ahead, bit-exact). */
+int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
+/* Order-independent 64-bit digest of a buffer: sum over i of
+ * mix64(bits(x[i]) + i * 0x9E3779B97F4A7C15) mod 2^64 (bits zero-extended).
+ * Result written to *out (host pointer) after an internal synchronize. */
+int bine_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
+
+/* ---- communicators ---------------------------------------------------------- */
+#define BINE_UNIQUE_ID_BYTES 128
+int bine_get_unique_id(void *id /* BINE_UNIQUE_ID_BYTES */);
+/* One process per GPU, RCCL P2P over xGMI.  `id` from rank 0's
+ * bine_get_unique_id(), broadcast by the caller (MPI, torch.distributed...). */
+int bine_comm_init_rccl(bine_comm_t *comm, int nranks, int rank, const void *id, int device);
+/* nranks virtual ranks on ONE device inside this process (in-process peer
+ * copies instead of RCCL).  Each rank must be driven from its own host thread
+ * (see bine_loopback_run_* below for a ready-made driver). */
+int bine_comm_init_loopback(bine_comm_t *comms /* [nranks] */, int nranks, int device);
+int bine_comm_destroy(bine_comm_t comm);
+int bine_comm_rank(bine_comm_t comm);
+int bine_comm_size(bine_comm_t comm);
+int bine_comm_device(bine_comm_t comm);
+void *bine_comm_stream(bine_comm_t comm);
+int bine_comm_synchronize(bine_comm_t comm);
+
+/* ---- collectives (device pointers, stream-ordered) ------------------------- */
+/* allreduce_* (libbine.h:30-37).  `segsize` plays bine_allreduce_segsize
+ * (libbine.h:28) for BINE_AR_BINE_BDW_REMAP_SEGMENTED and is the pipelining
+ * chunk of the other bandwidth variants (0 = library default). */
+int bine_allreduce(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count,
+                   int dtype, int op, size_t segsize, void *stream);
+/* reduce_scatter_* (libbine.h:69-77) */
+int bine_reduce_scatter(bine_comm_t comm, int algo, const void *sbuf, void *rbuf,
+                        const int *rcounts, int dtype, int op, void *stream);
+/* reduce_* (libbine.h:64-65).  rbuf is only read on `root` (may be NULL elsewhere). */
+int bine_reduce(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count,
+                int dtype, int op, int root, void *stream);
+
+/* ---- loopback drivers: run one collective on all virtual ranks ---------------
+ * (one host thread per rank; returns the first non-success status) */
+int bine_loopback_run_allreduce(bine_comm_t *comms, int nranks, int algo,
+                                const void *const *sbufs, void *const *rbufs, size_t count,
+                                int dtype, int op, size_t segsize, int *statuses);
+int bine_loopback_run_reduce_scatter(bine_comm_t *comms, int nranks, int algo,
+                                     const void *const *sbufs, void *const *rbufs,
+                                     const int *rcounts, int dtype, int op, int *statuses);
+int bine_loopback_run_reduce(bine_comm_t *comms, int nranks, int algo,
+                             const void *const *sbufs, void *const *rbufs, size_t count,
+                             int dtype, int op, int root, int *statuses);
+
+/* ---- schedule introspection (host only, no GPU needed) ----------------------
+ * A plan is the ordered list of primitives one rank executes. */
+typedef enum { BINE_PRIM_SEND = 1, BINE_PRIM_RECV = 2, BINE_PRIM_REDUCE = 3,
+               BINE_PRIM_REDUCE3 = 4, BINE_PRIM_COPY = 5 } bine_prim_type_t;
+typedef enum { BINE_BUF_SBUF = 0, BINE_BUF_RBUF = 1, BINE_BUF_TMP0 = 2, BINE_BUF_TMP1 = 3,
+               BINE_BUF_TMP2 = 4 } bine_buf_t;
+#define BINE_PRIM_PIPELINE 1  /* flags: exchange whose receive feeds the next
+                                 REDUCE(3) element for element -- both may be
+                                 split into chunks and overlapped */
+typedef struct {
+  int32_t type;      /* bine_prim_type_t */
+  int32_t group;     /* consecutive SEND/RECV with equal group form one exchange */
+  int32_t peer;      /* SEND/RECV peer rank */
+  int32_t flags;     /* BINE_PRIM_PIPELINE */
+  int32_t src_buf;   /* SEND: source; REDUCE/REDUCE3: `in` (a); COPY: source */
+  int32_t dst_buf;   /* RECV: destination; REDUCE: inout; REDUCE3: out; COPY: dest */
+  int32_t aux_buf;   /* REDUCE3: b */
+  int32_t pad_;
+  uint64_t src_off;  /* element offsets */
+  uint64_t dst_off;
+  uint64_t aux_off;
+  uint64_t count;    /* elements */
+} bine_prim_t;
+
+/* Fills up to `cap` primitives of rank `rank`'s plan; returns the number of
+ * primitives (may exceed cap) or -status on error.  tmp_elems[3] receives the
+ * workspace sizes (elements).  For reduce_scatter `count_or_root` is ignored and
+ * rcounts is used; for reduce it is the root and `count` the element count. */
+int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcounts, int root,
+                  size_t esz, size_t segsize, int in_place, bine_prim_t *prims, int64_t cap,
+                  uint64_t *tmp_elems);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BINE_AMD_H */

@@ -1,0 +1,118 @@
+"""ctypes binding of libbine_amd.so (include/bine_amd.h).
+
+The product path is the HIP library; there is no Python or CPU fallback.  If the
+shared library is missing this module raises at import time.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "lib")
+CORE = os.path.join(LIBDIR, "libbine_amd.so")
+SHIM = os.path.join(LIBDIR, "libbine.so")
+
+# include/bine_amd.h enums
+DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 5,
+          "int64": 6, "uint64": 7, "float": 8, "double": 9}
+DTYPE_SIZE = {"int8": 1, "uint8": 1, "int16": 2, "uint16": 2, "int32": 4, "uint32": 4,
+              "int64": 8, "uint64": 8, "float": 4, "double": 8}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+STATUS = {0: "SUCCESS", 1: "ERR_ARG", 2: "ERR_SIZE", 3: "ERR_NO_MEM", 4: "ERR_HIP", 5: "ERR_RCCL",
+          6: "ERR_UNSUPPORTED", 7: "ERR_INTERNAL"}
+ALGOS = {
+    "allreduce": {"recursivedoubling": 0, "ring": 1, "rabenseifner": 2, "bine_lat": 3,
+                  "bine_bdw_static": 4, "bine_bdw_remap": 5, "bine_bdw_remap_segmented": 6,
+                  "bine_block_by_block_any_even": 7},
+    "reduce_scatter": {"recursivehalving": 16, "recursive_distance_doubling": 17, "ring": 18,
+                       "butterfly": 19, "bine_static": 20, "bine_send_remap": 21,
+                       "bine_permute_remap": 22, "bine_block_by_block": 23,
+                       "bine_block_by_block_any_even": 24},
+    "reduce": {"bine_lat": 32, "bine_bdw": 33},
+}
+IN_PLACE = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)
+UNIQUE_ID_BYTES = 128
+
+
+class Prim(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("group", ctypes.c_int32), ("peer", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("src_buf", ctypes.c_int32), ("dst_buf", ctypes.c_int32),
+                ("aux_buf", ctypes.c_int32), ("pad_", ctypes.c_int32), ("src_off", ctypes.c_uint64),
+                ("dst_off", ctypes.c_uint64), ("aux_off", ctypes.c_uint64), ("count", ctypes.c_uint64)]
+
+
+PRIM_NAMES = {1: "SEND", 2: "RECV", 3: "REDUCE", 4: "REDUCE3", 5: "COPY"}
+
+
+class BineError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = STATUS.get(status, str(status))
+        detail = ""
+        try:
+            detail = lib().bine_last_error().decode()
+        except Exception:  # pragma: no cover
+            pass
+        super().__init__(f"{what}: {msg} {detail}".strip())
+
+
+_lib = None
+
+
+def lib():
+    """Load libbine_amd.so (build it with __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(CORE):
+        raise ImportError(f"{CORE} not built -- run __graft_entry__.build() (make -C pico_amd/csrc)")
+    L = ctypes.CDLL(CORE)
+    vp, sz, i, u32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+    sigs = {
+        "bine_status_string": ([i], ctypes.c_char_p),
+        "bine_last_error": ([], ctypes.c_char_p),
+        "bine_dtype_size": ([i], sz),
+        "bine_algo_from_name": ([ctypes.c_char_p, ctypes.c_char_p], i),
+        "bine_algo_name": ([i], ctypes.c_char_p),
+        "bine_set_reduce_tuning": ([i, i, i], i),
+        "bine_reduce_local": ([vp, vp, sz, i, i, vp], i),
+        "bine_reduce3": ([vp, vp, vp, sz, i, i, vp], i),
+        "bine_fill_pico": ([vp, sz, i, u32, vp], i),
+        "bine_checksum": ([vp, sz, i, ctypes.POINTER(u64), vp], i),
+        "bine_get_unique_id": ([vp], i),
+        "bine_comm_init_rccl": ([ctypes.POINTER(vp), i, i, vp, i], i),
+        "bine_comm_init_loopback": ([vp, i, i], i),
+        "bine_comm_destroy": ([vp], i),
+        "bine_comm_rank": ([vp], i),
+        "bine_comm_size": ([vp], i),
+        "bine_comm_device": ([vp], i),
+        "bine_comm_stream": ([vp], vp),
+        "bine_comm_synchronize": ([vp], i),
+        "bine_allreduce": ([vp, i, vp, vp, sz, i, i, sz, vp], i),
+        "bine_reduce_scatter": ([vp, i, vp, vp, vp, i, i, vp], i),
+        "bine_reduce": ([vp, i, vp, vp, sz, i, i, i, vp], i),
+        "bine_loopback_run_allreduce": ([vp, i, i, vp, vp, sz, i, i, sz, vp], i),
+        "bine_loopback_run_reduce_scatter": ([vp, i, i, vp, vp, vp, i, i, vp], i),
+        "bine_loopback_run_reduce": ([vp, i, i, vp, vp, sz, i, i, i, vp], i),
+        "bine_plan": ([i, i, i, sz, vp, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(u64)],
+                      ctypes.c_int64),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        raise BineError(status, what)
+
+
+def exported_symbols(path: str):
+    """Dynamic symbols a shared library defines (host-side check, no GPU)."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}

@@ -1,0 +1,280 @@
+"""Python mirror of libbine's reduce-family operator interface on MI355X.
+
+Every function named after a libbine entry point (reference include/libbine.h:
+30-78) takes the same arguments in the same order --
+``allreduce_bine_bdw_remap(sbuf, rbuf, count, dtype, op, comm)`` -- where the
+buffers are device tensors (torch, ROCm) or raw device addresses, ``dtype`` is a
+libbine element-type name ("float", "double", "int32", ...) or a torch dtype,
+``op`` is "sum" | "prod" | "max" | "min", and ``comm`` is a :class:`Comm`.
+Errors raise :class:`BineError` carrying the status the reference would return
+as an MPI error class.  The work runs in libbine_amd.so (HIP kernels + RCCL);
+there is no fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+from . import _lib
+from ._lib import ALGOS, DTYPES, OPS, BineError, check, lib
+
+IN_PLACE = "IN_PLACE"   # libbine's MPI_IN_PLACE
+
+_TORCH_DT = None
+
+
+def _torch_dtypes():
+    global _TORCH_DT
+    if _TORCH_DT is None:
+        import torch
+        _TORCH_DT = {torch.float32: "float", torch.float64: "double", torch.int8: "int8",
+                     torch.uint8: "uint8", torch.int16: "int16", torch.int32: "int32",
+                     torch.int64: "int64"}
+    return _TORCH_DT
+
+
+def _dtype(dtype, *bufs) -> int:
+    if dtype is None:
+        for b in bufs:
+            if hasattr(b, "dtype"):
+                dtype = b.dtype
+                break
+    if not isinstance(dtype, str):
+        dtype = _torch_dtypes()[dtype]
+    return DTYPES[dtype]
+
+
+def _ptr(buf):
+    if buf is None:
+        return None
+    if isinstance(buf, str) and buf == IN_PLACE:
+        return _lib.IN_PLACE.value
+    if hasattr(buf, "data_ptr"):
+        return buf.data_ptr()
+    return int(buf)
+
+
+def _stream(stream, comm: Optional["Comm"]):
+    if stream is not None:
+        return stream if isinstance(stream, int) else getattr(stream, "cuda_stream", stream)
+    try:
+        import torch
+        if torch.cuda.is_available():
+            dev = comm.device if comm is not None else torch.cuda.current_device()
+            return torch.cuda.current_stream(dev).cuda_stream
+    except Exception:  # pragma: no cover
+        pass
+    return comm.stream if comm is not None else None
+
+
+class Comm:
+    """A bine communicator: one rank of an RCCL communicator (one process per
+    GPU) or one virtual rank of an in-process loopback group."""
+
+    def __init__(self, handle: int, kind: str):
+        self.handle = ctypes.c_void_p(handle)
+        self.kind = kind
+
+    # -- construction --------------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(_lib.UNIQUE_ID_BYTES)
+        check(lib().bine_get_unique_id(buf), "bine_get_unique_id")
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, rank: int, size: int, unique_id: bytes, device: int = 0) -> "Comm":
+        h = ctypes.c_void_p()
+        idbuf = ctypes.create_string_buffer(unique_id, _lib.UNIQUE_ID_BYTES)
+        check(lib().bine_comm_init_rccl(ctypes.byref(h), size, rank, idbuf, device), "bine_comm_init_rccl")
+        return cls(h.value, "rccl")
+
+    @classmethod
+    def from_torch_distributed(cls, device: int, group=None) -> "Comm":
+        """Bootstrap over an initialised torch.distributed group (any backend):
+        rank 0 creates the RCCL unique id and broadcasts it."""
+        import torch
+        import torch.distributed as dist
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+        uid = cls.unique_id() if rank == 0 else bytes(_lib.UNIQUE_ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        if dist.get_backend(group) == "nccl":
+            t = t.cuda(device)
+        dist.broadcast(t, 0, group=group)
+        return cls.rccl(rank, size, bytes(t.cpu().tolist()), device)
+
+    @classmethod
+    def loopback(cls, nranks: int, device: int = 0) -> list["Comm"]:
+        arr = (ctypes.c_void_p * nranks)()
+        check(lib().bine_comm_init_loopback(arr, nranks, device), "bine_comm_init_loopback")
+        return [cls(arr[r], "loopback") for r in range(nranks)]
+
+    # -- properties ----------------------------------------------------------
+    @property
+    def rank(self) -> int:
+        return lib().bine_comm_rank(self.handle)
+
+    @property
+    def size(self) -> int:
+        return lib().bine_comm_size(self.handle)
+
+    @property
+    def device(self) -> int:
+        return lib().bine_comm_device(self.handle)
+
+    @property
+    def stream(self) -> int:
+        return lib().bine_comm_stream(self.handle)
+
+    def synchronize(self) -> None:
+        check(lib().bine_comm_synchronize(self.handle), "bine_comm_synchronize")
+
+    def destroy(self) -> None:
+        if self.handle:
+            lib().bine_comm_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+# ---- arithmetic boundary ------------------------------------------------------
+
+def reduce_local(inbuf, inoutbuf, count: int, dtype=None, op: str = "sum", stream=None) -> None:
+    """MPI_Reduce_local on the GPU: inout = inout (op) in."""
+    check(lib().bine_reduce_local(_ptr(inbuf), _ptr(inoutbuf), count, _dtype(dtype, inbuf), OPS[op],
+                                  _stream(stream, None)), "bine_reduce_local")
+
+
+def reduce3(a, b, out, count: int, dtype=None, op: str = "sum", stream=None) -> None:
+    """out = b (op) a (out may alias b)."""
+    check(lib().bine_reduce3(_ptr(a), _ptr(b), _ptr(out), count, _dtype(dtype, a), OPS[op],
+                             _stream(stream, None)), "bine_reduce3")
+
+
+def fill_pico(buf, count: int, dtype=None, seed: int = 1234, stream=None) -> None:
+    """pico_core's rand_r() input distribution, generated on the device."""
+    check(lib().bine_fill_pico(_ptr(buf), count, _dtype(dtype, buf), seed, _stream(stream, None)),
+          "bine_fill_pico")
+
+
+def checksum(buf, count: int, dtype=None, stream=None) -> int:
+    out = ctypes.c_uint64()
+    check(lib().bine_checksum(_ptr(buf), count, _dtype(dtype, buf), ctypes.byref(out), _stream(stream, None)),
+          "bine_checksum")
+    return out.value
+
+
+def set_reduce_tuning(unroll: int = 4, maxblocks: int = 0, nontemporal: int = 0) -> None:
+    lib().bine_set_reduce_tuning(unroll, maxblocks, nontemporal)
+
+
+# ---- generic collectives -------------------------------------------------------
+
+def _algo(coll: str, algo) -> int:
+    return algo if isinstance(algo, int) else ALGOS[coll][algo]
+
+
+def allreduce(algo, sbuf, rbuf, count: int, dtype, op: str, comm: Comm, segsize: int = 0, stream=None) -> None:
+    check(lib().bine_allreduce(comm.handle, _algo("allreduce", algo), _ptr(sbuf), _ptr(rbuf), count,
+                               _dtype(dtype, rbuf), OPS[op], segsize, _stream(stream, comm)), f"allreduce_{algo}")
+
+
+def reduce_scatter(algo, sbuf, rbuf, rcounts: Sequence[int], dtype, op: str, comm: Comm, stream=None) -> None:
+    rc = (ctypes.c_int * len(rcounts))(*rcounts)
+    check(lib().bine_reduce_scatter(comm.handle, _algo("reduce_scatter", algo), _ptr(sbuf), _ptr(rbuf), rc,
+                                    _dtype(dtype, rbuf), OPS[op], _stream(stream, comm)), f"reduce_scatter_{algo}")
+
+
+def reduce(algo, sbuf, rbuf, count: int, dtype, op: str, root: int, comm: Comm, stream=None) -> None:
+    check(lib().bine_reduce(comm.handle, _algo("reduce", algo), _ptr(sbuf), _ptr(rbuf), count,
+                            _dtype(dtype, sbuf if rbuf is None else rbuf), OPS[op], root, _stream(stream, comm)),
+          f"reduce_{algo}")
+
+
+# ---- loopback group drivers (all virtual ranks of one device) -------------------
+
+def _ptrs(bufs):
+    return (ctypes.c_void_p * len(bufs))(*[_ptr(b) for b in bufs])
+
+
+def loopback_allreduce(comms, algo, sbufs, rbufs, count, dtype, op="sum", segsize=0):
+    st = (ctypes.c_int * len(comms))()
+    hs = (ctypes.c_void_p * len(comms))(*[c.handle.value for c in comms])
+    rc = lib().bine_loopback_run_allreduce(hs, len(comms), _algo("allreduce", algo), _ptrs(sbufs), _ptrs(rbufs),
+                                           count, _dtype(dtype, rbufs[0]), OPS[op], segsize, st)
+    return rc, list(st)
+
+
+def loopback_reduce_scatter(comms, algo, sbufs, rbufs, rcounts, dtype, op="sum"):
+    st = (ctypes.c_int * len(comms))()
+    hs = (ctypes.c_void_p * len(comms))(*[c.handle.value for c in comms])
+    rcs = (ctypes.c_int * len(rcounts))(*rcounts)
+    rc = lib().bine_loopback_run_reduce_scatter(hs, len(comms), _algo("reduce_scatter", algo), _ptrs(sbufs),
+                                                _ptrs(rbufs), rcs, _dtype(dtype, rbufs[0]), OPS[op], st)
+    return rc, list(st)
+
+
+def loopback_reduce(comms, algo, sbufs, rbufs, count, dtype, op="sum", root=0):
+    st = (ctypes.c_int * len(comms))()
+    hs = (ctypes.c_void_p * len(comms))(*[c.handle.value for c in comms])
+    rc = lib().bine_loopback_run_reduce(hs, len(comms), _algo("reduce", algo), _ptrs(sbufs), _ptrs(rbufs),
+                                        count, _dtype(dtype, sbufs[0]), OPS[op], root, st)
+    return rc, list(st)
+
+
+# ---- schedule introspection ------------------------------------------------------
+
+def plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, root: int = 0,
+         esz: int = 4, segsize: int = 0, in_place: bool = False):
+    """Rank `rank`'s primitive list (host only).  Returns (prims, tmp_elems) or
+    raises BineError with the reference's error status."""
+    a = _algo(coll, algo)
+    rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
+    tmp = (ctypes.c_uint64 * 3)()
+    n = lib().bine_plan(a, nranks, rank, count, rc, root, esz, segsize, int(in_place), None, 0, tmp)
+    if n < 0:
+        raise BineError(int(-n), f"plan {coll}_{algo}")
+    arr = (_lib.Prim * max(int(n), 1))()
+    lib().bine_plan(a, nranks, rank, count, rc, root, esz, segsize, int(in_place), arr, n, tmp)
+    prims = [{f: getattr(arr[k], f) for f, _ in _lib.Prim._fields_ if f != "pad_"} for k in range(int(n))]
+    for p in prims:
+        p["type"] = _lib.PRIM_NAMES[p["type"]]
+    return prims, list(tmp)
+
+
+# ---- libbine-named entry points (include/libbine.h:30-78) --------------------------
+
+def _mk_ar(name):
+    def f(sbuf, rbuf, count, dtype, op, comm, stream=None, segsize: int = 0):
+        allreduce(name, sbuf, rbuf, count, dtype, op, comm, segsize=segsize, stream=stream)
+    f.__name__ = "allreduce_" + name
+    f.__doc__ = f"allreduce_{name} (libbine_allreduce.c) on MI355X."
+    return f
+
+
+def _mk_rs(name):
+    def f(sbuf, rbuf, rcounts, dtype, op, comm, stream=None):
+        reduce_scatter(name, sbuf, rbuf, rcounts, dtype, op, comm, stream=stream)
+    f.__name__ = "reduce_scatter_" + name
+    f.__doc__ = f"reduce_scatter_{name} (libbine_reduce_scatter.c) on MI355X."
+    return f
+
+
+def _mk_rd(name):
+    def f(sbuf, rbuf, count, dtype, op, root, comm, stream=None):
+        reduce(name, sbuf, rbuf, count, dtype, op, root, comm, stream=stream)
+    f.__name__ = "reduce_" + name
+    f.__doc__ = f"reduce_{name} (libbine_reduce.c) on MI355X."
+    return f
+
+
+ENTRY_POINTS = {}
+for _n in ALGOS["allreduce"]:
+    ENTRY_POINTS["allreduce_" + _n] = _mk_ar(_n)
+for _n in ALGOS["reduce_scatter"]:
+    ENTRY_POINTS["reduce_scatter_" + _n] = _mk_rs(_n)
+for _n in ALGOS["reduce"]:
+    ENTRY_POINTS["reduce_" + _n] = _mk_rd(_n)
+globals().update(ENTRY_POINTS)
+
+__all__ = ["Comm", "BineError", "IN_PLACE", "reduce_local", "reduce3", "fill_pico", "checksum",
+           "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
+           "loopback_reduce_scatter", "loopback_reduce", "plan"] + list(ENTRY_POINTS)

@@ -1,0 +1,51 @@
+// bine_internal.h -- shared declarations of libbine_amd.so (not installed).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "bine_amd.h"
+
+namespace bine {
+
+// ---- schedule (schedule.cpp) ------------------------------------------------
+
+// One primitive of a per-rank plan (same layout as bine_prim_t).
+using Prim = bine_prim_t;
+
+struct Plan {
+  std::vector<Prim> prims;
+  uint64_t tmp_elems[3] = {0, 0, 0};  // workspace per TMP buffer, elements
+  int status = BINE_SUCCESS;          // non-success: the reference's error return
+};
+
+struct PlanArgs {
+  int algo = -1;
+  int P = 1, rank = 0;
+  size_t count = 0;                 // allreduce / reduce
+  std::vector<int> rcounts;         // reduce_scatter
+  int root = 0;                     // reduce
+  size_t esz = 4;
+  size_t segsize = 0;               // bytes; segmented variant's segment
+  bool in_place = false;
+};
+
+Plan make_plan(const PlanArgs &a);
+
+// schedule math (libbine_utils.h restated for the planner)
+int pi(int rank, int step, int P);
+uint32_t remap_rank(uint32_t P, uint32_t rank);
+uint32_t get_nu(uint32_t rank, uint32_t size);
+int log2_ceil(int v);
+bool is_pow2(int v);
+void static_perm(int P, std::vector<int> &perm);
+
+// ---- kernels (kernels.hip) ----------------------------------------------------
+int launch_reduce(const void *a, const void *b, void *out, size_t count, int dtype, int op,
+                  void *stream);   // out = b (op) a
+int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
+int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
+
+}  // namespace bine

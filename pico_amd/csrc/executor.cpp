@@ -1,0 +1,647 @@
+// executor.cpp -- communicators, transports and the device plan executor of
+// libbine_amd.so, plus the C ABI of include/bine_amd.h.
+//
+// Execution model (one process per GPU, one communicator per process):
+//   * compute stream K = the caller's stream: every REDUCE / REDUCE3 / COPY;
+//   * comm stream C (the communicator's own, high priority): every exchange,
+//     i.e. RCCL ncclSend/ncclRecv inside one ncclGroupStart/End (RCCL P2P over
+//     xGMI), or the in-process loopback copies;
+//   * hipEvents hand work between the two.  An exchange whose receive feeds the
+//     following reduction element-for-element (plan flag BINE_PRIM_PIPELINE --
+//     every reduce-scatter step of the Bine schedules) is cut into chunks: the
+//     receive of chunk k+1 on C overlaps the reduction of chunk k on K.  This
+//     is the device form of the segmented variant's double-buffered
+//     Irecv/Reduce_local loop (libbine_allreduce.c:1218-1253).
+//   * workspace (TMP0..2) and plans are cached per communicator.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bine_internal.h"
+
+namespace bine {
+
+static thread_local std::string g_err;
+
+static void set_err(const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      set_err("%s:%d %s -> %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
+      return BINE_ERR_HIP;                                                         \
+    }                                                                              \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                 \
+  do {                                                                                 \
+    ncclResult_t r_ = (expr);                                                          \
+    if (r_ != ncclSuccess) {                                                           \
+      set_err("%s:%d %s -> %s", __FILE__, __LINE__, #expr, ncclGetErrorString(r_));    \
+      return BINE_ERR_RCCL;                                                            \
+    }                                                                                  \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// transports
+// ---------------------------------------------------------------------------
+
+struct XSend { int peer; const void *ptr; size_t bytes; };
+struct XRecv { int peer; void *ptr; size_t bytes; };
+
+struct Transport {
+  virtual ~Transport() = default;
+  virtual int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) = 0;
+  virtual void retire() {}
+};
+
+struct RcclTransport final : Transport {
+  ncclComm_t comm = nullptr;
+  ~RcclTransport() override {
+    if (comm) ncclCommDestroy(comm);
+  }
+  int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
+    NCCL_TRY(ncclGroupStart());
+    for (const auto &x : s) NCCL_TRY(ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, comm, st));
+    for (const auto &x : r) NCCL_TRY(ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, comm, st));
+    NCCL_TRY(ncclGroupEnd());
+    return BINE_SUCCESS;
+  }
+};
+
+// In-process peer copies between virtual ranks on one device.  A send posts
+// {pointer, ready-event}; the receiver waits for the event on its own stream,
+// copies, records done; the sender's stream then waits for done before anything
+// that could overwrite the send buffer -- ncclSend/ncclRecv semantics.
+struct LoopbackHub {
+  struct Post {
+    const void *ptr = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ready = nullptr, done = nullptr;
+    bool consumed = false;
+  };
+  int P;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::deque<Post *>> box;  // [src * P + dst]
+  std::atomic<int> mismatches{0};
+  explicit LoopbackHub(int n) : P(n), box((size_t)n * (size_t)n) {}
+};
+
+struct LoopbackTransport final : Transport {
+  std::shared_ptr<LoopbackHub> hub;
+  int rank;
+  std::vector<LoopbackHub::Post *> retired;
+  LoopbackTransport(std::shared_ptr<LoopbackHub> h, int r) : hub(std::move(h)), rank(r) {}
+  ~LoopbackTransport() override { retire(); }
+  void retire() override {  // caller guarantees the streams are idle
+    for (auto *p : retired) {
+      (void)hipEventDestroy(p->ready);
+      (void)hipEventDestroy(p->done);
+      delete p;
+    }
+    retired.clear();
+  }
+  int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
+    const int P = hub->P;
+    std::vector<LoopbackHub::Post *> mine;
+    for (const auto &x : s) {
+      auto *p = new LoopbackHub::Post;
+      p->ptr = x.ptr;
+      p->bytes = x.bytes;
+      HIP_TRY(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(p->ready, st));
+      {
+        std::lock_guard<std::mutex> g(hub->mu);
+        hub->box[(size_t)rank * (size_t)P + (size_t)x.peer].push_back(p);
+      }
+      hub->cv.notify_all();
+      mine.push_back(p);
+    }
+    for (const auto &x : r) {
+      LoopbackHub::Post *p;
+      {
+        std::unique_lock<std::mutex> g(hub->mu);
+        auto &q = hub->box[(size_t)x.peer * (size_t)P + (size_t)rank];
+        hub->cv.wait(g, [&] { return !q.empty(); });
+        p = q.front();
+        q.pop_front();
+      }
+      if (p->bytes != x.bytes) hub->mismatches++;
+      HIP_TRY(hipStreamWaitEvent(st, p->ready, 0));
+      const size_t nb = std::min(p->bytes, x.bytes);
+      if (nb) HIP_TRY(hipMemcpyAsync(x.ptr, p->ptr, nb, hipMemcpyDeviceToDevice, st));
+      HIP_TRY(hipEventRecord(p->done, st));
+      {
+        std::lock_guard<std::mutex> g(hub->mu);
+        p->consumed = true;
+      }
+      hub->cv.notify_all();
+    }
+    for (auto *p : mine) {
+      {
+        std::unique_lock<std::mutex> g(hub->mu);
+        hub->cv.wait(g, [&] { return p->consumed; });
+      }
+      HIP_TRY(hipStreamWaitEvent(st, p->done, 0));
+      retired.push_back(p);
+    }
+    return BINE_SUCCESS;
+  }
+};
+
+}  // namespace bine
+
+// ---------------------------------------------------------------------------
+// communicator
+// ---------------------------------------------------------------------------
+
+struct bine_comm {
+  int rank = 0, size = 1, device = 0;
+  hipStream_t stream = nullptr;   // default compute stream
+  hipStream_t cstream = nullptr;  // comm stream
+  std::unique_ptr<bine::Transport> tx;
+  std::shared_ptr<bine::LoopbackHub> hub;
+  void *tmp[3] = {nullptr, nullptr, nullptr};
+  size_t tmp_bytes[3] = {0, 0, 0};
+  std::vector<hipEvent_t> ev;
+  size_t ev_next = 0;
+  std::map<std::string, bine::Plan> plans;
+  std::mutex mu;
+};
+
+namespace bine {
+
+static int comm_setup(bine_comm *c) {
+  HIP_TRY(hipSetDevice(c->device));
+  int lo = 0, hi = 0;
+  HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi));
+  c->ev.resize(128);
+  for (auto &e : c->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return BINE_SUCCESS;
+}
+
+static hipEvent_t next_event(bine_comm *c) {
+  hipEvent_t e = c->ev[c->ev_next];
+  c->ev_next = (c->ev_next + 1) % c->ev.size();
+  return e;
+}
+
+// `dst` waits for all work enqueued so far on `src`
+static int stream_join(bine_comm *c, hipStream_t dst, hipStream_t src) {
+  hipEvent_t e = next_event(c);
+  HIP_TRY(hipEventRecord(e, src));
+  HIP_TRY(hipStreamWaitEvent(dst, e, 0));
+  return BINE_SUCCESS;
+}
+
+static int ensure_workspace(bine_comm *c, const Plan &p, size_t esz, hipStream_t user) {
+  bool grow = false;
+  for (int t = 0; t < 3; t++) grow |= p.tmp_elems[t] * esz > c->tmp_bytes[t];
+  if (!grow) return BINE_SUCCESS;
+  // old buffers may still be read by enqueued work
+  HIP_TRY(hipStreamSynchronize(user));
+  HIP_TRY(hipStreamSynchronize(c->cstream));
+  for (int t = 0; t < 3; t++) {
+    const size_t need = p.tmp_elems[t] * esz;
+    if (need <= c->tmp_bytes[t]) continue;
+    if (c->tmp[t]) HIP_TRY(hipFree(c->tmp[t]));
+    c->tmp[t] = nullptr;
+    c->tmp_bytes[t] = 0;
+    const size_t alloc = (need + 255) & ~(size_t)255;
+    HIP_TRY(hipMalloc(&c->tmp[t], alloc));
+    c->tmp_bytes[t] = alloc;
+  }
+  return BINE_SUCCESS;
+}
+
+static size_t default_chunk_bytes() {
+  static size_t v = [] {
+    const char *e = getenv("BINE_CHUNK_BYTES");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)16 << 20;
+  }();
+  return v;
+}
+
+// Walk `plan` on the device.  `chunk_bytes` = 0: no chunking.
+static int execute(bine_comm *c, const Plan &plan, const void *sbuf, void *rbuf, size_t esz, int dtype,
+                   int op, size_t chunk_bytes, hipStream_t K) {
+  char *base[5];
+  base[BINE_BUF_SBUF] = (char *)sbuf;
+  base[BINE_BUF_RBUF] = (char *)rbuf;
+  for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
+  auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
+  hipStream_t C = c->cstream;
+  size_t ch = chunk_bytes / esz;
+  if (ch) ch = std::max<size_t>(16 / esz, ch / (16 / esz) * (16 / esz));  // keep chunks 16-B aligned
+
+  bool k_dirty = true, c_dirty = false;  // C must first see everything already on K
+  const auto &pr = plan.prims;
+  size_t i = 0;
+  std::vector<XSend> sends;
+  std::vector<XRecv> recvs;
+  while (i < pr.size()) {
+    const Prim &p = pr[i];
+    if (p.type == BINE_PRIM_SEND || p.type == BINE_PRIM_RECV) {
+      size_t j = i;
+      while (j < pr.size() && (pr[j].type == BINE_PRIM_SEND || pr[j].type == BINE_PRIM_RECV) &&
+             pr[j].group == p.group)
+        j++;
+      if (k_dirty) { int rc = stream_join(c, C, K); if (rc) return rc; k_dirty = false; }
+      const bool pipe = ch && (p.flags & BINE_PRIM_PIPELINE) && j < pr.size() &&
+                        (pr[j].flags & BINE_PRIM_PIPELINE) &&
+                        (pr[j].type == BINE_PRIM_REDUCE || pr[j].type == BINE_PRIM_REDUCE3);
+      if (pipe) {
+        const Prim *S = nullptr, *R = nullptr;
+        for (size_t k = i; k < j; k++) (pr[k].type == BINE_PRIM_SEND ? S : R) = &pr[k];
+        const Prim &Q = pr[j];
+        const size_t nch = std::max((S->count + ch - 1) / ch, (R->count + ch - 1) / ch);
+        for (size_t k = 0; k < nch; k++) {
+          sends.clear();
+          recvs.clear();
+          const uint64_t o = (uint64_t)(k * ch);
+          if (o < S->count) sends.push_back({S->peer, ptr(S->src_buf, S->src_off + o), std::min<uint64_t>(ch, S->count - o) * esz});
+          if (o < R->count) recvs.push_back({R->peer, ptr(R->dst_buf, R->dst_off + o), std::min<uint64_t>(ch, R->count - o) * esz});
+          int rc = c->tx->exchange(sends, recvs, C);
+          if (rc) return rc;
+          if (o < R->count) {
+            rc = stream_join(c, K, C);
+            if (rc) return rc;
+            const uint64_t n = std::min<uint64_t>(ch, Q.count - std::min<uint64_t>(o, Q.count));
+            if (n) {
+              const void *b = Q.type == BINE_PRIM_REDUCE3 ? ptr(Q.aux_buf, Q.aux_off + o) : ptr(Q.dst_buf, Q.dst_off + o);
+              rc = launch_reduce(ptr(Q.src_buf, Q.src_off + o), b, ptr(Q.dst_buf, Q.dst_off + o), n, dtype, op, K);
+              if (rc) { set_err("reduce launch failed"); return rc; }
+            }
+          }
+        }
+        // make sure nothing later on K reads the receive region before the last chunk
+        int rc = stream_join(c, K, C);
+        if (rc) return rc;
+        i = j + 1;
+        k_dirty = true;
+        c_dirty = false;
+        continue;
+      }
+      sends.clear();
+      recvs.clear();
+      for (size_t k = i; k < j; k++) {
+        const Prim &x = pr[k];
+        if (x.type == BINE_PRIM_SEND) sends.push_back({x.peer, ptr(x.src_buf, x.src_off), x.count * esz});
+        else recvs.push_back({x.peer, ptr(x.dst_buf, x.dst_off), x.count * esz});
+      }
+      int rc = c->tx->exchange(sends, recvs, C);
+      if (rc) return rc;
+      c_dirty = true;
+      i = j;
+      continue;
+    }
+    if (c_dirty) { int rc = stream_join(c, K, C); if (rc) return rc; c_dirty = false; }
+    int rc = BINE_SUCCESS;
+    if (p.type == BINE_PRIM_REDUCE)
+      rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.dst_buf, p.dst_off), ptr(p.dst_buf, p.dst_off), p.count, dtype, op, K);
+    else if (p.type == BINE_PRIM_REDUCE3)
+      rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count, dtype, op, K);
+    else if (p.type == BINE_PRIM_COPY)
+      HIP_TRY(hipMemcpyAsync(ptr(p.dst_buf, p.dst_off), ptr(p.src_buf, p.src_off), p.count * esz,
+                             hipMemcpyDeviceToDevice, K));
+    if (rc) { set_err("local primitive failed"); return rc; }
+    k_dirty = true;
+    i++;
+  }
+  if (c_dirty) { int rc = stream_join(c, K, C); if (rc) return rc; }
+  return BINE_SUCCESS;
+}
+
+static std::string plan_key(const PlanArgs &a) {
+  std::string k;
+  char buf[160];
+  snprintf(buf, sizeof buf, "%d|%zu|%zu|%zu|%d|%d|", a.algo, a.count, a.esz, a.segsize, (int)a.in_place, a.root);
+  k = buf;
+  for (int x : a.rcounts) { k += std::to_string(x); k += ','; }
+  return k;
+}
+
+static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbuf, int dtype, int op,
+                          size_t chunk_bytes, void *stream) {
+  if (!c) return BINE_ERR_ARG;
+  if (dtype < 0 || dtype >= BINE_NUM_DTYPES) return BINE_ERR_UNSUPPORTED;
+  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  a.P = c->size;
+  a.rank = c->rank;
+  a.esz = bine_dtype_size(dtype);
+  a.in_place = sbuf == BINE_IN_PLACE;
+  const std::string key = plan_key(a);
+  auto it = c->plans.find(key);
+  if (it == c->plans.end()) it = c->plans.emplace(key, make_plan(a)).first;
+  const Plan &plan = it->second;
+  if (plan.status != BINE_SUCCESS) return plan.status;
+  hipStream_t K = stream ? (hipStream_t)stream : c->stream;
+  int rc = ensure_workspace(c, plan, a.esz, K);
+  if (rc) return rc;
+  return execute(c, plan, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, chunk_bytes, K);
+}
+
+}  // namespace bine
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+
+using namespace bine;
+
+template <typename F>
+static int run_threads(bine_comm_t *comms, int n, int *statuses, F f) {
+  std::vector<std::thread> th;
+  std::vector<int> st((size_t)n, BINE_SUCCESS);
+  for (int r = 0; r < n; r++)
+    th.emplace_back([&, r] {
+      int rc = f(r);
+      if (rc == BINE_SUCCESS) rc = bine_comm_synchronize(comms[r]);
+      if (comms[r]->tx) comms[r]->tx->retire();
+      st[(size_t)r] = rc;
+    });
+  for (auto &t : th) t.join();
+  int first = BINE_SUCCESS;
+  for (int r = 0; r < n; r++) {
+    if (statuses) statuses[r] = st[(size_t)r];
+    if (first == BINE_SUCCESS) first = st[(size_t)r];
+  }
+  return first;
+}
+
+
+extern "C" {
+
+const char *bine_status_string(int s) {
+  switch (s) {
+    case BINE_SUCCESS: return "success";
+    case BINE_ERR_ARG: return "invalid argument (reference: MPI_ERR_ARG)";
+    case BINE_ERR_SIZE: return "unsupported communicator size (reference: MPI_ERR_SIZE)";
+    case BINE_ERR_NO_MEM: return "out of memory";
+    case BINE_ERR_HIP: return "HIP runtime error";
+    case BINE_ERR_RCCL: return "RCCL error";
+    case BINE_ERR_UNSUPPORTED: return "unsupported algorithm, datatype or operator";
+    default: return "internal error";
+  }
+}
+
+const char *bine_last_error(void) { return g_err.c_str(); }
+
+size_t bine_dtype_size(int dt) {
+  switch (dt) {
+    case BINE_INT8: case BINE_UINT8: return 1;
+    case BINE_INT16: case BINE_UINT16: return 2;
+    case BINE_INT32: case BINE_UINT32: case BINE_FLOAT: return 4;
+    case BINE_INT64: case BINE_UINT64: case BINE_DOUBLE: return 8;
+    default: return 0;
+  }
+}
+
+static const struct { int algo; const char *coll, *name, *selector; } kAlgos[] = {
+    {BINE_AR_RECURSIVEDOUBLING, "allreduce", "recursivedoubling", "recursive_doubling_over"},
+    {BINE_AR_RING, "allreduce", "ring", "ring_over"},
+    {BINE_AR_RABENSEIFNER, "allreduce", "rabenseifner", "rabenseifner_over"},
+    {BINE_AR_BINE_LAT, "allreduce", "bine_lat", "bine_lat_over"},
+    {BINE_AR_BINE_BDW_STATIC, "allreduce", "bine_bdw_static", "bine_bdw_static_over"},
+    {BINE_AR_BINE_BDW_REMAP, "allreduce", "bine_bdw_remap", "bine_bdw_remap_over"},
+    {BINE_AR_BINE_BDW_REMAP_SEGMENTED, "allreduce", "bine_bdw_remap_segmented", "bine_bdw_remap_segmented_over"},
+    {BINE_AR_BINE_BLOCK_BY_BLOCK_ANY_EVEN, "allreduce", "bine_block_by_block_any_even", "bine_block_by_block_any_even"},
+    {BINE_RS_RECURSIVEHALVING, "reduce_scatter", "recursivehalving", "recursive_halving_over"},
+    {BINE_RS_RECURSIVE_DISTANCE_DOUBLING, "reduce_scatter", "recursive_distance_doubling", "recursive_distance_doubling_over"},
+    {BINE_RS_RING, "reduce_scatter", "ring", "ring_over"},
+    {BINE_RS_BUTTERFLY, "reduce_scatter", "butterfly", "butterfly_over"},
+    {BINE_RS_BINE_STATIC, "reduce_scatter", "bine_static", "bine_static_over"},
+    {BINE_RS_BINE_SEND_REMAP, "reduce_scatter", "bine_send_remap", "bine_send_remap_over"},
+    {BINE_RS_BINE_PERMUTE_REMAP, "reduce_scatter", "bine_permute_remap", "bine_permute_remap_over"},
+    {BINE_RS_BINE_BLOCK_BY_BLOCK, "reduce_scatter", "bine_block_by_block", "bine_block_by_block_over"},
+    {BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN, "reduce_scatter", "bine_block_by_block_any_even", "bine_block_by_block_any_even"},
+    {BINE_RD_BINE_LAT, "reduce", "bine_lat", "bine_lat_over"},
+    {BINE_RD_BINE_BDW, "reduce", "bine_bdw", "bine_bdw_over"},
+};
+
+int bine_algo_from_name(const char *coll, const char *name) {
+  if (!coll || !name) return -1;
+  for (const auto &a : kAlgos) {
+    if (strcmp(a.coll, coll)) continue;
+    std::string full = std::string(a.coll) + "_" + a.name;
+    if (!strcmp(name, a.name) || !strcmp(name, a.selector) || full == name) return a.algo;
+  }
+  return -1;
+}
+
+const char *bine_algo_name(int algo) {
+  for (const auto &a : kAlgos)
+    if (a.algo == algo) return a.name;
+  return "unknown";
+}
+
+int bine_reduce_local(const void *in, void *inout, size_t count, int dtype, int op, void *stream) {
+  return launch_reduce(in, inout, inout, count, dtype, op, stream);
+}
+
+int bine_reduce3(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream) {
+  return launch_reduce(a, b, out, count, dtype, op, stream);
+}
+
+int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream) {
+  return launch_fill_pico(buf, count, dtype, seed, stream);
+}
+
+int bine_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream) {
+  if (!bine_dtype_size(dtype) || !out) return BINE_ERR_ARG;
+  return launch_checksum(buf, count, dtype, out, stream);
+}
+
+int bine_get_unique_id(void *id) {
+  static_assert(sizeof(ncclUniqueId) == BINE_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return BINE_SUCCESS;
+}
+
+int bine_comm_init_rccl(bine_comm_t *out, int nranks, int rank, const void *id, int device) {
+  if (!out || nranks < 1 || rank < 0 || rank >= nranks || !id) return BINE_ERR_ARG;
+  auto c = std::make_unique<bine_comm>();
+  c->rank = rank;
+  c->size = nranks;
+  c->device = device;
+  int rc = comm_setup(c.get());
+  if (rc) return rc;
+  auto tx = std::make_unique<RcclTransport>();
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  NCCL_TRY(ncclCommInitRank(&tx->comm, nranks, u, rank));
+  c->tx = std::move(tx);
+  *out = c.release();
+  return BINE_SUCCESS;
+}
+
+int bine_comm_init_loopback(bine_comm_t *comms, int nranks, int device) {
+  if (!comms || nranks < 1) return BINE_ERR_ARG;
+  auto hub = std::make_shared<LoopbackHub>(nranks);
+  for (int r = 0; r < nranks; r++) {
+    auto c = std::make_unique<bine_comm>();
+    c->rank = r;
+    c->size = nranks;
+    c->device = device;
+    int rc = comm_setup(c.get());
+    if (rc) return rc;
+    c->hub = hub;
+    c->tx = std::make_unique<LoopbackTransport>(hub, r);
+    comms[r] = c.release();
+  }
+  return BINE_SUCCESS;
+}
+
+int bine_comm_synchronize(bine_comm_t c) {
+  if (!c) return BINE_ERR_ARG;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipStreamSynchronize(c->cstream));
+  if (c->hub && c->hub->mismatches.load()) {
+    set_err("loopback: %d send/recv size mismatches", c->hub->mismatches.load());
+    return BINE_ERR_INTERNAL;
+  }
+  return BINE_SUCCESS;
+}
+
+int bine_comm_destroy(bine_comm_t c) {
+  if (!c) return BINE_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->cstream);
+  c->tx.reset();
+  for (int t = 0; t < 3; t++)
+    if (c->tmp[t]) (void)hipFree(c->tmp[t]);
+  for (auto e : c->ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  (void)hipStreamDestroy(c->cstream);
+  delete c;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_rank(bine_comm_t c) { return c ? c->rank : -1; }
+int bine_comm_size(bine_comm_t c) { return c ? c->size : -1; }
+int bine_comm_device(bine_comm_t c) { return c ? c->device : -1; }
+void *bine_comm_stream(bine_comm_t c) { return c ? (void *)c->stream : nullptr; }
+
+int bine_allreduce(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int op,
+                   size_t segsize, void *stream) {
+  if (algo < BINE_AR_RECURSIVEDOUBLING || algo > BINE_AR_BINE_BLOCK_BY_BLOCK_ANY_EVEN) return BINE_ERR_UNSUPPORTED;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  a.segsize = segsize;
+  // segmented: the reference's segment is the pipelining chunk (0 = one chunk)
+  size_t chunk = algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? segsize : (segsize ? segsize : default_chunk_bytes());
+  return run_collective(c, a, sbuf, rbuf, dtype, op, chunk, stream);
+}
+
+int bine_reduce_scatter(bine_comm_t c, int algo, const void *sbuf, void *rbuf, const int *rcounts, int dtype,
+                        int op, void *stream) {
+  if (algo < BINE_RS_RECURSIVEHALVING || algo > BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN) return BINE_ERR_UNSUPPORTED;
+  if (!c || !rcounts) return BINE_ERR_ARG;
+  PlanArgs a;
+  a.algo = algo;
+  a.rcounts.assign(rcounts, rcounts + c->size);
+  return run_collective(c, a, sbuf, rbuf, dtype, op, default_chunk_bytes(), stream);
+}
+
+int bine_reduce(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int op, int root,
+                void *stream) {
+  if (algo != BINE_RD_BINE_LAT && algo != BINE_RD_BINE_BDW) return BINE_ERR_UNSUPPORTED;
+  if (!c || root < 0 || root >= c->size) return BINE_ERR_ARG;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  a.root = root;
+  if (c->rank == root && sbuf == BINE_IN_PLACE) {
+    // handled by run_collective's in_place mapping
+  } else if (sbuf == BINE_IN_PLACE) {
+    return BINE_ERR_ARG;
+  }
+  return run_collective(c, a, sbuf, rbuf, dtype, op, default_chunk_bytes(), stream);
+}
+
+// ---- loopback drivers --------------------------------------------------------
+
+int bine_loopback_run_allreduce(bine_comm_t *comms, int n, int algo, const void *const *sbufs,
+                                void *const *rbufs, size_t count, int dtype, int op, size_t segsize,
+                                int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_allreduce(comms[r], algo, sbufs[r], rbufs[r], count, dtype, op, segsize, nullptr);
+  });
+}
+
+int bine_loopback_run_reduce_scatter(bine_comm_t *comms, int n, int algo, const void *const *sbufs,
+                                     void *const *rbufs, const int *rcounts, int dtype, int op, int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_reduce_scatter(comms[r], algo, sbufs[r], rbufs[r], rcounts, dtype, op, nullptr);
+  });
+}
+
+int bine_loopback_run_reduce(bine_comm_t *comms, int n, int algo, const void *const *sbufs, void *const *rbufs,
+                             size_t count, int dtype, int op, int root, int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_reduce(comms[r], algo, sbufs[r], rbufs[r], count, dtype, op, root, nullptr);
+  });
+}
+
+// ---- schedule introspection ------------------------------------------------------
+
+int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                  size_t segsize, int in_place, bine_prim_t *prims, int64_t cap, uint64_t *tmp_elems) {
+  PlanArgs a;
+  a.algo = algo;
+  a.P = nranks;
+  a.rank = rank;
+  a.count = count;
+  if (rcounts && algo >= BINE_RS_RECURSIVEHALVING && algo <= BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN)
+    a.rcounts.assign(rcounts, rcounts + nranks);
+  a.root = root;
+  a.esz = esz;
+  a.segsize = segsize;
+  a.in_place = in_place != 0;
+  Plan p = make_plan(a);
+  if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
+  for (int64_t k = 0; k < (int64_t)p.prims.size() && k < cap; k++) prims[k] = p.prims[(size_t)k];
+  if (tmp_elems)
+    for (int t = 0; t < 3; t++) tmp_elems[t] = p.tmp_elems[t];
+  return (int64_t)p.prims.size();
+}
+
+int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);
+
+}  // extern "C"

@@ -1,0 +1,360 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of libbine_amd.so.
+//
+//  * k_reduce: the element-wise reduction that replaces MPI_Reduce_local at all
+//    32 call sites of libbine's reduce family (e.g. libbine_allreduce.c:888):
+//    out[i] = b[i] (op) a[i], out may alias b.  HBM-bound streaming kernel:
+//    16 B per lane per access (global_load_dwordx4), U independent 16-B vectors
+//    per lane in flight, grid capped near the chip's resident-wave capacity and
+//    grid-strided.  No LDS: every byte is touched once, so staging through LDS
+//    would only add instructions.  Arithmetic follows MPICH 3.3.2 exactly
+//    (inout (op) in, no FMA contraction, no denormal flushing, integer wrap).
+//  * k_fill_pico: pico_core's rand_r() input distributions
+//    (pico_core_utils.c:902-923) generated in parallel by LCG jump-ahead,
+//    bit-identical to the sequential host generator.
+//  * k_checksum: order-independent 64-bit digest for size-independent parity
+//    checks at full sizes; per-lane partial sums reduced with wave64 shuffles,
+//    then through LDS, then one 64-bit atomic per workgroup.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+
+#include "bine_internal.h"
+
+namespace bine {
+
+// ----------------------------------------------------------------------------
+// element-wise reduction
+// ----------------------------------------------------------------------------
+
+template <typename T>
+using uint_of = std::conditional_t<sizeof(T) == 1, uint8_t,
+                std::conditional_t<sizeof(T) == 2, uint16_t,
+                std::conditional_t<sizeof(T) == 4, uint32_t, uint64_t>>>;
+
+// MPICH's MPIR_OP_TYPE_REDUCE_CASE: a = inout, b = in, a = OP(a, b)
+template <typename T, int OP>
+__device__ __forceinline__ T apply(T io, T in) {
+  if constexpr (OP == BINE_SUM) {
+    if constexpr (std::is_integral_v<T>) return (T)((uint_of<T>)io + (uint_of<T>)in);
+    else return io + in;
+  } else if constexpr (OP == BINE_PROD) {
+    if constexpr (std::is_integral_v<T>) return (T)((uint_of<T>)io * (uint_of<T>)in);
+    else return io * in;
+  } else if constexpr (OP == BINE_MAX) {
+    return io > in ? io : in;
+  } else {
+    return io < in ? io : in;
+  }
+}
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <typename T, int OP>
+__device__ __forceinline__ u32x4_t apply16(u32x4_t vb, u32x4_t va) {
+  constexpr int N = 16 / (int)sizeof(T);
+  T b[N], a[N];
+  __builtin_memcpy(b, &vb, 16);
+  __builtin_memcpy(a, &va, 16);
+#pragma unroll
+  for (int i = 0; i < N; i++) b[i] = apply<T, OP>(b[i], a[i]);
+  u32x4_t r;
+  __builtin_memcpy(&r, b, 16);
+  return r;
+}
+
+constexpr int kBlock = 256;
+using u32x4 = u32x4_t;  // one global_load/store_dwordx4 per lane
+
+// Elements [0, head) and [head + 16/sizeof(T) * nvec, n) are done scalar by
+// block 0; the 16-B aligned middle is vectorized.
+template <typename T, int OP, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_reduce(const T *__restrict__ a, const T *b, T *out,
+                                                   size_t head, size_t nvec, size_t n) {
+  constexpr size_t V = 16 / sizeof(T);
+  if (blockIdx.x == 0) {
+    for (size_t i = threadIdx.x; i < head; i += kBlock) out[i] = apply<T, OP>(b[i], a[i]);
+    for (size_t i = head + nvec * V + threadIdx.x; i < n; i += kBlock) out[i] = apply<T, OP>(b[i], a[i]);
+  }
+  const u32x4 *va = reinterpret_cast<const u32x4 *>(a + head);
+  const u32x4 *vb = reinterpret_cast<const u32x4 *>(b + head);
+  u32x4 *vo = reinterpret_cast<u32x4 *>(out + head);
+  const size_t tile = (size_t)kBlock * U;
+  const size_t stride = (size_t)gridDim.x * tile;
+  size_t base = (size_t)blockIdx.x * tile + threadIdx.x;
+  // full tiles: no bounds checks, U loads of each operand in flight per lane
+  for (; base + (U - 1) * (size_t)kBlock < nvec; base += stride) {
+    u32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if constexpr (NT) x[u] = __builtin_nontemporal_load(va + base + (size_t)u * kBlock);
+      else x[u] = va[base + (size_t)u * kBlock];
+      y[u] = vb[base + (size_t)u * kBlock];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) vo[base + (size_t)u * kBlock] = apply16<T, OP>(y[u], x[u]);
+  }
+  // last partial tile
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const size_t i = base + (size_t)u * kBlock;
+    if (i < nvec) vo[i] = apply16<T, OP>(vb[i], va[i]);
+  }
+}
+
+// dispatch -----------------------------------------------------------------
+
+static int g_unroll = 0, g_maxblocks = 0, g_nt = -1;
+
+static void read_tuning() {
+  if (g_unroll) return;
+  const char *u = getenv("BINE_REDUCE_UNROLL");
+  const char *m = getenv("BINE_REDUCE_MAXBLOCKS");
+  const char *t = getenv("BINE_REDUCE_NT");
+  int uu = u ? atoi(u) : 4;
+  g_unroll = (uu == 1 || uu == 2 || uu == 4 || uu == 8) ? uu : 4;
+  g_maxblocks = m ? atoi(m) : 0;
+  g_nt = t ? atoi(t) : 0;
+}
+
+template <typename T, int OP, int U, bool NT>
+static hipError_t run_reduce(const T *a, const T *b, T *out, size_t n, hipStream_t st) {
+  constexpr size_t V = 16 / sizeof(T);
+  const uintptr_t ao = (uintptr_t)a, bo = (uintptr_t)b, oo = (uintptr_t)out;
+  size_t head, nvec;
+  if (((ao ^ oo) & 15) == 0 && ((bo ^ oo) & 15) == 0 && (oo % sizeof(T)) == 0) {
+    head = ((16 - (oo & 15)) & 15) / sizeof(T);
+    if (head > n) head = n;
+    nvec = (n - head) / V;
+  } else {  // operands not co-aligned mod 16 B (small runs only, see reduce_t)
+    head = n;
+    nvec = 0;
+  }
+  int blocks;
+  if (nvec == 0) blocks = 1;
+  else {
+    const size_t tiles = (nvec + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
+    const int maxb = g_maxblocks > 0 ? g_maxblocks : 2048;
+    blocks = (int)(tiles < (size_t)maxb ? tiles : (size_t)maxb);
+  }
+  hipLaunchKernelGGL((k_reduce<T, OP, U, NT>), dim3(blocks), dim3(kBlock), 0, st, a, b, out, head, nvec, n);
+  return hipGetLastError();
+}
+
+// scalar grid-stride kernel for operands that are not co-aligned mod 16 bytes
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_scalar(const T *__restrict__ a, const T *b, T *out,
+                                                          size_t n) {
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock)
+    out[i] = apply<T, OP>(b[i], a[i]);
+}
+
+template <typename T, int OP>
+static hipError_t reduce_t(const void *a, const void *b, void *out, size_t n, hipStream_t st) {
+  const T *pa = (const T *)a, *pb = (const T *)b;
+  T *po = (T *)out;
+  const uintptr_t ao = (uintptr_t)a, bo = (uintptr_t)b, oo = (uintptr_t)out;
+  if ((((ao ^ oo) & 15) != 0 || ((bo ^ oo) & 15) != 0) && n > 4096) {
+    size_t blocks = (n + kBlock * 4 - 1) / (kBlock * 4);
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3((unsigned)blocks), dim3(kBlock), 0, st, pa, pb, po, n);
+    return hipGetLastError();
+  }
+  if constexpr (std::is_same_v<T, float> && OP == BINE_SUM) {
+    // tuning variants (BINE_REDUCE_UNROLL / _NT) for the headline dtype
+    if (g_nt == 1) {
+      switch (g_unroll) {
+        case 1: return run_reduce<T, OP, 1, true>(pa, pb, po, n, st);
+        case 2: return run_reduce<T, OP, 2, true>(pa, pb, po, n, st);
+        case 8: return run_reduce<T, OP, 8, true>(pa, pb, po, n, st);
+        default: return run_reduce<T, OP, 4, true>(pa, pb, po, n, st);
+      }
+    }
+    switch (g_unroll) {
+      case 1: return run_reduce<T, OP, 1, false>(pa, pb, po, n, st);
+      case 2: return run_reduce<T, OP, 2, false>(pa, pb, po, n, st);
+      case 8: return run_reduce<T, OP, 8, false>(pa, pb, po, n, st);
+      default: break;
+    }
+  }
+  return run_reduce<T, OP, 4, false>(pa, pb, po, n, st);
+}
+
+template <typename T>
+static hipError_t reduce_op(const void *a, const void *b, void *out, size_t n, int op, hipStream_t st) {
+  switch (op) {
+    case BINE_SUM: return reduce_t<T, BINE_SUM>(a, b, out, n, st);
+    case BINE_PROD: return reduce_t<T, BINE_PROD>(a, b, out, n, st);
+    case BINE_MAX: return reduce_t<T, BINE_MAX>(a, b, out, n, st);
+    case BINE_MIN: return reduce_t<T, BINE_MIN>(a, b, out, n, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int launch_reduce(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream) {
+  if (count == 0) return BINE_SUCCESS;
+  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+  read_tuning();
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case BINE_INT8: e = reduce_op<int8_t>(a, b, out, count, op, st); break;
+    case BINE_UINT8: e = reduce_op<uint8_t>(a, b, out, count, op, st); break;
+    case BINE_INT16: e = reduce_op<int16_t>(a, b, out, count, op, st); break;
+    case BINE_UINT16: e = reduce_op<uint16_t>(a, b, out, count, op, st); break;
+    case BINE_INT32: e = reduce_op<int32_t>(a, b, out, count, op, st); break;
+    case BINE_UINT32: e = reduce_op<uint32_t>(a, b, out, count, op, st); break;
+    case BINE_INT64: e = reduce_op<int64_t>(a, b, out, count, op, st); break;
+    case BINE_UINT64: e = reduce_op<uint64_t>(a, b, out, count, op, st); break;
+    case BINE_FLOAT: e = reduce_op<float>(a, b, out, count, op, st); break;
+    case BINE_DOUBLE: e = reduce_op<double>(a, b, out, count, op, st); break;
+    default: return BINE_ERR_UNSUPPORTED;
+  }
+  return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
+// pico_core input generator (glibc rand_r, LCG jump-ahead)
+// ----------------------------------------------------------------------------
+
+struct Affine { uint32_t m, c; };  // x -> m x + c (mod 2^32)
+
+__host__ __device__ inline Affine compose(Affine f, Affine g) {  // f(g(x))
+  return {f.m * g.m, f.m * g.c + f.c};
+}
+__host__ __device__ inline Affine lcg_pow(uint64_t k) {
+  Affine r{1u, 0u}, p{1103515245u, 12345u};
+  while (k) {
+    if (k & 1) r = compose(p, r);
+    p = compose(p, p);
+    k >>= 1;
+  }
+  return r;
+}
+// one glibc rand_r() call (three LCG steps, 11+10+10 bits)
+__device__ inline int32_t rand_r_step(uint32_t &s) {
+  s = s * 1103515245u + 12345u;
+  uint32_t r = (s >> 16) % 2048u;
+  s = s * 1103515245u + 12345u;
+  r = (r << 10) ^ ((s >> 16) % 1024u);
+  s = s * 1103515245u + 12345u;
+  r = (r << 10) ^ ((s >> 16) % 1024u);
+  return (int32_t)r;
+}
+
+constexpr int kFillPer = 16;  // consecutive elements per lane
+
+template <typename T, int DT>
+__global__ __launch_bounds__(kBlock) void k_fill_pico(T *buf, size_t n, uint32_t seed) {
+  constexpr int calls = (DT == BINE_INT64 || DT == BINE_UINT64) ? 2 : 1;
+  const size_t first = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kFillPer;
+  if (first >= n) return;
+  const Affine j = lcg_pow((uint64_t)first * 3u * calls);
+  uint32_t s = j.m * seed + j.c;
+  for (int k = 0; k < kFillPer && first + k < n; k++) {
+    T v;
+    if constexpr (DT == BINE_INT8) v = (T)((rand_r_step(s) % 256) - 128);
+    else if constexpr (DT == BINE_UINT8) v = (T)(rand_r_step(s) % 256);
+    else if constexpr (DT == BINE_INT16) v = (T)((rand_r_step(s) % 65536) - 32768);
+    else if constexpr (DT == BINE_UINT16) v = (T)(rand_r_step(s) % 65536);
+    else if constexpr (DT == BINE_INT32 || DT == BINE_UINT32) v = (T)rand_r_step(s);
+    else if constexpr (DT == BINE_INT64 || DT == BINE_UINT64) {
+      const int64_t hi = (int64_t)rand_r_step(s) << 32;
+      v = (T)(hi | (int64_t)rand_r_step(s));
+    } else if constexpr (DT == BINE_FLOAT) v = (float)rand_r_step(s) / (float)2147483647 * 100.0f;
+    else v = (double)rand_r_step(s) / (double)2147483647 * 100.0;
+    buf[first + k] = v;
+  }
+}
+
+int launch_fill_pico(void *buf, size_t n, int dtype, uint32_t seed, void *stream) {
+  if (n == 0) return BINE_SUCCESS;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lanes = (n + kFillPer - 1) / kFillPer;
+  const unsigned blocks = (unsigned)((lanes + kBlock - 1) / kBlock);
+#define FILL(T, DT) hipLaunchKernelGGL((k_fill_pico<T, DT>), dim3(blocks), dim3(kBlock), 0, st, (T *)buf, n, seed); break
+  switch (dtype) {
+    case BINE_INT8: FILL(int8_t, BINE_INT8);
+    case BINE_UINT8: FILL(uint8_t, BINE_UINT8);
+    case BINE_INT16: FILL(int16_t, BINE_INT16);
+    case BINE_UINT16: FILL(uint16_t, BINE_UINT16);
+    case BINE_INT32: FILL(int32_t, BINE_INT32);
+    case BINE_UINT32: FILL(uint32_t, BINE_UINT32);
+    case BINE_INT64: FILL(int64_t, BINE_INT64);
+    case BINE_UINT64: FILL(uint64_t, BINE_UINT64);
+    case BINE_FLOAT: FILL(float, BINE_FLOAT);
+    case BINE_DOUBLE: FILL(double, BINE_DOUBLE);
+    default: return BINE_ERR_UNSUPPORTED;
+  }
+#undef FILL
+  return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
+// order-independent checksum
+// ----------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finalizer
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <typename U>
+__global__ __launch_bounds__(kBlock) void k_checksum(const U *buf, size_t n, unsigned long long *out) {
+  uint64_t acc = 0;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock)
+    acc += mix64((uint64_t)buf[i] + (uint64_t)i * 0x9E3779B97F4A7C15ull);
+  // wave64 reduction (two 32-bit shuffles per step)
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)acc, off, 64);
+    const uint32_t hi = __shfl_xor((uint32_t)(acc >> 32), off, 64);
+    acc += ((uint64_t)hi << 32) | lo;
+  }
+  __shared__ uint64_t part[kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) part[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t s = 0;
+    for (int w = 0; w < kBlock / 64; w++) s += part[w];
+    atomicAdd(out, (unsigned long long)s);
+  }
+}
+
+int launch_checksum(const void *buf, size_t n, int dtype, uint64_t *host_out, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  unsigned long long *d = nullptr;
+  if (hipMalloc(&d, sizeof *d) != hipSuccess) return BINE_ERR_NO_MEM;
+  int rc = BINE_SUCCESS;
+  if (hipMemsetAsync(d, 0, sizeof *d, st) != hipSuccess) rc = BINE_ERR_HIP;
+  size_t blocks = (n + kBlock * 8 - 1) / (kBlock * 8);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) blocks = 1;
+  if (rc == BINE_SUCCESS) {
+    switch (bine_dtype_size(dtype)) {
+      case 1: hipLaunchKernelGGL((k_checksum<uint8_t>), dim3((unsigned)blocks), dim3(kBlock), 0, st, (const uint8_t *)buf, n, d); break;
+      case 2: hipLaunchKernelGGL((k_checksum<uint16_t>), dim3((unsigned)blocks), dim3(kBlock), 0, st, (const uint16_t *)buf, n, d); break;
+      case 4: hipLaunchKernelGGL((k_checksum<uint32_t>), dim3((unsigned)blocks), dim3(kBlock), 0, st, (const uint32_t *)buf, n, d); break;
+      case 8: hipLaunchKernelGGL((k_checksum<uint64_t>), dim3((unsigned)blocks), dim3(kBlock), 0, st, (const uint64_t *)buf, n, d); break;
+      default: rc = BINE_ERR_UNSUPPORTED;
+    }
+  }
+  unsigned long long h = 0;
+  if (rc == BINE_SUCCESS && (hipGetLastError() != hipSuccess ||
+                             hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                             hipStreamSynchronize(st) != hipSuccess))
+    rc = BINE_ERR_HIP;
+  (void)hipFree(d);
+  if (rc == BINE_SUCCESS) *host_out = h;
+  return rc;
+}
+
+}  // namespace bine
+
+extern "C" int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal) {
+  bine::g_unroll = (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) ? unroll : 4;
+  bine::g_maxblocks = maxblocks;
+  bine::g_nt = nontemporal;
+  return BINE_SUCCESS;
+}

@@ -1,0 +1,311 @@
+// mpi_shim.cpp -- libbine.so: the reference's include/libbine.h ABI on top of
+// libbine_amd.so (see include/libbine_amd.h for the contract).
+//
+// Compiled against the same mpi.h as pico_core (MPICH: MPI_Datatype / MPI_Op /
+// MPI_Comm are int handles).  The shim owns no algorithm: it maps MPI handles to
+// bine_* enums, finds (or creates) the RCCL-backed bine communicator of the
+// MPI communicator, stages host buffers through the device, and turns status
+// codes into MPI error classes.
+#include <hip/hip_runtime.h>
+#include <mpi.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "bine_amd.h"
+#include "libbine_amd.h"
+
+extern "C" {
+size_t bine_allreduce_segsize = 0;  // libbine.h:28, written by pico_core (pico_core_utils.c:317)
+}
+
+namespace {
+
+struct Entry {
+  bine_comm_t comm = nullptr;
+  int rank = 0, size = 1;
+  // staging for host buffers
+  void *dev[2] = {nullptr, nullptr};
+  size_t dev_bytes[2] = {0, 0};
+};
+
+int g_keyval = MPI_KEYVAL_INVALID;
+int g_self_keyval = MPI_KEYVAL_INVALID;
+std::vector<Entry *> g_entries;
+
+void release(Entry *e) {
+  if (!e) return;
+  if (e->comm) {
+    bine_comm_synchronize(e->comm);
+    bine_comm_destroy(e->comm);
+  }
+  for (int i = 0; i < 2; i++)
+    if (e->dev[i]) (void)hipFree(e->dev[i]);
+  delete e;
+}
+
+int comm_delete(MPI_Comm, int, void *val, void *) {
+  Entry *e = (Entry *)val;
+  for (auto &x : g_entries)
+    if (x == e) x = nullptr;
+  release(e);
+  return MPI_SUCCESS;
+}
+
+// MPI_Finalize deletes MPI_COMM_SELF's attributes first: release everything
+int self_delete(MPI_Comm, int, void *, void *) {
+  for (auto *e : g_entries) release(e);
+  g_entries.clear();
+  return MPI_SUCCESS;
+}
+
+int to_mpi(int st) {
+  switch (st) {
+    case BINE_SUCCESS: return MPI_SUCCESS;
+    case BINE_ERR_ARG: return MPI_ERR_ARG;
+    case BINE_ERR_SIZE: return MPI_ERR_SIZE;
+    case BINE_ERR_NO_MEM: return MPI_ERR_NO_MEM;
+    case BINE_ERR_UNSUPPORTED: return MPI_ERR_UNSUPPORTED_OPERATION;
+    default:
+      fprintf(stderr, "libbine(amd): %s: %s\n", bine_status_string(st), bine_last_error());
+      return MPI_ERR_OTHER;
+  }
+}
+
+int map_dtype(MPI_Datatype d) {
+  if (d == MPI_FLOAT) return BINE_FLOAT;
+  if (d == MPI_DOUBLE) return BINE_DOUBLE;
+  if (d == MPI_INT8_T || d == MPI_SIGNED_CHAR || d == MPI_CHAR) return BINE_INT8;
+  if (d == MPI_UINT8_T || d == MPI_UNSIGNED_CHAR || d == MPI_BYTE) return BINE_UINT8;
+  if (d == MPI_INT16_T || d == MPI_SHORT) return BINE_INT16;
+  if (d == MPI_UINT16_T || d == MPI_UNSIGNED_SHORT) return BINE_UINT16;
+  if (d == MPI_INT32_T || d == MPI_INT) return BINE_INT32;
+  if (d == MPI_UINT32_T || d == MPI_UNSIGNED) return BINE_UINT32;
+  if (d == MPI_INT64_T || d == MPI_LONG || d == MPI_LONG_LONG) return BINE_INT64;
+  if (d == MPI_UINT64_T || d == MPI_UNSIGNED_LONG || d == MPI_UNSIGNED_LONG_LONG) return BINE_UINT64;
+  return -1;
+}
+
+int map_op(MPI_Op o) {
+  if (o == MPI_SUM) return BINE_SUM;
+  if (o == MPI_PROD) return BINE_PROD;
+  if (o == MPI_MAX) return BINE_MAX;
+  if (o == MPI_MIN) return BINE_MIN;
+  return -1;
+}
+
+int get_entry(MPI_Comm comm, Entry **out) {
+  if (g_keyval == MPI_KEYVAL_INVALID) {
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, comm_delete, &g_keyval, nullptr);
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, self_delete, &g_self_keyval, nullptr);
+    MPI_Comm_set_attr(MPI_COMM_SELF, g_self_keyval, nullptr);
+  }
+  void *val = nullptr;
+  int flag = 0;
+  MPI_Comm_get_attr(comm, g_keyval, &val, &flag);
+  if (flag && val) { *out = (Entry *)val; return MPI_SUCCESS; }
+  auto *e = new Entry;
+  MPI_Comm_rank(comm, &e->rank);
+  MPI_Comm_size(comm, &e->size);
+  MPI_Comm local;
+  int lrank = 0;
+  MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, e->rank, MPI_INFO_NULL, &local);
+  MPI_Comm_rank(local, &lrank);
+  MPI_Comm_free(&local);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    fprintf(stderr, "libbine(amd): no HIP device visible\n");
+    delete e;
+    return MPI_ERR_OTHER;
+  }
+  const char *forced = getenv("BINE_DEVICE");
+  const int device = forced ? atoi(forced) : lrank % ndev;
+  unsigned char id[BINE_UNIQUE_ID_BYTES] = {0};
+  int st = BINE_SUCCESS;
+  if (e->rank == 0) st = bine_get_unique_id(id);
+  MPI_Bcast(&st, 1, MPI_INT, 0, comm);
+  if (st != BINE_SUCCESS) { delete e; return to_mpi(st); }
+  MPI_Bcast(id, BINE_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
+  st = bine_comm_init_rccl(&e->comm, e->size, e->rank, id, device);
+  if (st != BINE_SUCCESS) { delete e; return to_mpi(st); }
+  MPI_Comm_set_attr(comm, g_keyval, e);
+  g_entries.push_back(e);
+  *out = e;
+  return MPI_SUCCESS;
+}
+
+bool on_device(const void *p) {
+  if (!p || p == MPI_IN_PLACE) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+int stage(Entry *e, int slot, size_t bytes, void **dev) {
+  if (e->dev_bytes[slot] < bytes) {
+    if (e->dev[slot]) (void)hipFree(e->dev[slot]);
+    e->dev[slot] = nullptr;
+    e->dev_bytes[slot] = 0;
+    if (hipMalloc(&e->dev[slot], bytes) != hipSuccess) return MPI_ERR_NO_MEM;
+    e->dev_bytes[slot] = bytes;
+  }
+  *dev = e->dev[slot];
+  return MPI_SUCCESS;
+}
+
+// Run `body(dev_sbuf, dev_rbuf, stream)` with host buffers staged.
+template <typename F>
+int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes, bool read_rbuf, F body) {
+  hipStream_t st = (hipStream_t)bine_comm_stream(e->comm);
+  (void)hipSetDevice(bine_comm_device(e->comm));
+  const bool in_place = sbuf == MPI_IN_PLACE;
+  const void *ds = sbuf;
+  void *dr = rbuf;
+  bool stage_s = !in_place && sbuf && sbytes && !on_device(sbuf);
+  bool stage_r = rbuf && rbytes && !on_device(rbuf);
+  int rc;
+  if (stage_s) {
+    void *d;
+    if ((rc = stage(e, 0, sbytes, &d))) return rc;
+    if (hipMemcpyAsync(d, sbuf, sbytes, hipMemcpyHostToDevice, st) != hipSuccess) return MPI_ERR_OTHER;
+    ds = d;
+  }
+  if (stage_r) {
+    void *d;
+    if ((rc = stage(e, 1, rbytes, &d))) return rc;
+    if ((in_place || read_rbuf) && hipMemcpyAsync(d, rbuf, rbytes, hipMemcpyHostToDevice, st) != hipSuccess)
+      return MPI_ERR_OTHER;
+    dr = d;
+  }
+  int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (void *)st);
+  if (bst != BINE_SUCCESS) return to_mpi(bst);
+  if (stage_r && hipMemcpyAsync(rbuf, dr, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess) return MPI_ERR_OTHER;
+  if (hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
+  return to_mpi(bine_comm_synchronize(e->comm));
+}
+
+int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype dtype, MPI_Op op,
+                 MPI_Comm comm) {
+  const int dt = map_dtype(dtype), o = map_op(op);
+  if (dt < 0) return MPI_ERR_TYPE;
+  if (o < 0) return MPI_ERR_OP;
+  if (count == 0) return MPI_SUCCESS;
+  Entry *e;
+  int rc = get_entry(comm, &e);
+  if (rc) return rc;
+  const size_t bytes = count * bine_dtype_size(dt);
+  const size_t seg = bine_allreduce_segsize;
+  return with_buffers(e, sbuf, bytes, rbuf, bytes, false, [&](const void *s, void *r, void *st) {
+    return bine_allreduce(e->comm, algo, s, r, count, dt, o, algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? seg : 0, st);
+  });
+}
+
+int do_reduce_scatter(int algo, const void *sbuf, void *rbuf, const int rcounts[], MPI_Datatype dtype, MPI_Op op,
+                      MPI_Comm comm) {
+  const int dt = map_dtype(dtype), o = map_op(op);
+  if (dt < 0) return MPI_ERR_TYPE;
+  if (o < 0) return MPI_ERR_OP;
+  Entry *e;
+  int rc = get_entry(comm, &e);
+  if (rc) return rc;
+  size_t total = 0;
+  for (int i = 0; i < e->size; i++) total += (size_t)rcounts[i];
+  const size_t esz = bine_dtype_size(dt);
+  const bool in_place = sbuf == MPI_IN_PLACE;
+  // MPI_IN_PLACE: the input is the whole rbuf
+  const size_t rbytes = (in_place ? total : (size_t)rcounts[e->rank]) * esz;
+  return with_buffers(e, sbuf, total * esz, rbuf, rbytes, false, [&](const void *s, void *r, void *st) {
+    return bine_reduce_scatter(e->comm, algo, s, r, rcounts, dt, o, st);
+  });
+}
+
+int do_reduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype dtype, MPI_Op op, int root,
+              MPI_Comm comm) {
+  const int dt = map_dtype(dtype), o = map_op(op);
+  if (dt < 0) return MPI_ERR_TYPE;
+  if (o < 0) return MPI_ERR_OP;
+  if (count == 0) return MPI_SUCCESS;
+  Entry *e;
+  int rc = get_entry(comm, &e);
+  if (rc) return rc;
+  const size_t bytes = count * bine_dtype_size(dt);
+  void *r = e->rank == root ? rbuf : nullptr;
+  return with_buffers(e, sbuf, bytes, r, r ? bytes : 0, false, [&](const void *s, void *rr, void *st) {
+    return bine_reduce(e->comm, algo, s, rr, count, dt, o, root, st);
+  });
+}
+
+int unsupported(const char *name) {
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    fprintf(stderr, "libbine(amd): %s is outside the reduce family this library provides "
+                    "(allreduce / reduce_scatter / reduce); returning MPI_ERR_UNSUPPORTED_OPERATION\n", name);
+  });
+  return MPI_ERR_UNSUPPORTED_OPERATION;
+}
+
+}  // namespace
+
+extern "C" {
+
+#define AR(fn, id) \
+  int fn(BINE_ALLREDUCE_ARGS) { return do_allreduce(id, sbuf, rbuf, count, dtype, op, comm); }
+AR(allreduce_recursivedoubling, BINE_AR_RECURSIVEDOUBLING)
+AR(allreduce_ring, BINE_AR_RING)
+AR(allreduce_rabenseifner, BINE_AR_RABENSEIFNER)
+AR(allreduce_bine_lat, BINE_AR_BINE_LAT)
+AR(allreduce_bine_bdw_static, BINE_AR_BINE_BDW_STATIC)
+AR(allreduce_bine_bdw_remap, BINE_AR_BINE_BDW_REMAP)
+AR(allreduce_bine_bdw_remap_segmented, BINE_AR_BINE_BDW_REMAP_SEGMENTED)
+AR(allreduce_bine_block_by_block_any_even, BINE_AR_BINE_BLOCK_BY_BLOCK_ANY_EVEN)
+#undef AR
+
+#define RS(fn, id) \
+  int fn(BINE_REDUCE_SCATTER_ARGS) { return do_reduce_scatter(id, sbuf, rbuf, rcounts, dtype, op, comm); }
+RS(reduce_scatter_recursivehalving, BINE_RS_RECURSIVEHALVING)
+RS(reduce_scatter_recursive_distance_doubling, BINE_RS_RECURSIVE_DISTANCE_DOUBLING)
+RS(reduce_scatter_ring, BINE_RS_RING)
+RS(reduce_scatter_butterfly, BINE_RS_BUTTERFLY)
+RS(reduce_scatter_bine_static, BINE_RS_BINE_STATIC)
+RS(reduce_scatter_bine_send_remap, BINE_RS_BINE_SEND_REMAP)
+RS(reduce_scatter_bine_permute_remap, BINE_RS_BINE_PERMUTE_REMAP)
+RS(reduce_scatter_bine_block_by_block, BINE_RS_BINE_BLOCK_BY_BLOCK)
+RS(reduce_scatter_bine_block_by_block_any_even, BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN)
+#undef RS
+
+int reduce_bine_lat(BINE_REDUCE_ARGS) { return do_reduce(BINE_RD_BINE_LAT, sbuf, rbuf, count, dtype, op, root, comm); }
+int reduce_bine_bdw(BINE_REDUCE_ARGS) { return do_reduce(BINE_RD_BINE_BDW, sbuf, rbuf, count, dtype, op, root, comm); }
+
+#define NA(fn, args) \
+  int fn(args) { return unsupported(#fn); }
+NA(allgather_k_bruck, BINE_ALLGATHER_ARGS)
+NA(allgather_recursivedoubling, BINE_ALLGATHER_ARGS)
+NA(allgather_ring, BINE_ALLGATHER_ARGS)
+NA(allgather_sparbit, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_block_by_block, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_block_by_block_any_even, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_permute_static, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_send_static, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_permute_remap, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_send_remap, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_2_blocks, BINE_ALLGATHER_ARGS)
+NA(allgather_bine_2_blocks_dtype, BINE_ALLGATHER_ARGS)
+NA(alltoall_bine, BINE_ALLGATHER_ARGS)
+NA(bcast_scatter_allgather, BINE_BCAST_ARGS)
+NA(bcast_bine_lat, BINE_BCAST_ARGS)
+NA(bcast_bine_lat_reversed, BINE_BCAST_ARGS)
+NA(bcast_bine_lat_new, BINE_BCAST_ARGS)
+NA(bcast_bine_lat_i_new, BINE_BCAST_ARGS)
+NA(bcast_bine_bdw_static, BINE_BCAST_ARGS)
+NA(bcast_bine_bdw_remap, BINE_BCAST_ARGS)
+NA(gather_bine, BINE_GATHER_ARGS)
+NA(scatter_bine, BINE_GATHER_ARGS)
+#undef NA
+
+}  // extern "C"

@@ -1,0 +1,948 @@
+// schedule.cpp -- per-rank execution plans of libbine's reduce-family.
+//
+// The reference interleaves its schedule with MPI calls inside each algorithm
+// (libbine_allreduce.c, libbine_reduce_scatter.c, libbine_reduce.c).  Here the
+// schedule is computed once, on the host, into an immutable list of primitives
+// (SEND / RECV grouped into exchanges, REDUCE, REDUCE3, COPY) over five logical
+// buffers (SBUF, RBUF, TMP0..2).  The device executor (executor.cpp) walks the
+// list with RCCL P2P on one HIP stream and the CDNA4 reduce kernels on another.
+//
+// Differences from a literal reading of the reference, all deliberate:
+//  * every receive carries the exact element count its matching send carries
+//    (RCCL P2P needs equal counts; MPI only bounds them);
+//  * messages of zero elements are dropped on both sides;
+//  * an exchange with oneself becomes a local COPY;
+//  * the first reduce-scatter step of remap/static/segmented reads the send
+//    buffer directly (REDUCE3: rbuf = sbuf op recv) instead of copying sbuf to
+//    rbuf first (libbine_allreduce.c:849-852) -- same values, one pass of HBM
+//    traffic less;
+//  * reference defects are not reproduced: the segmented tail that is never
+//    reduced (libbine_allreduce.c:1211-1252), the static tmp_buf overflow
+//    (:724 vs :749-765), reduce_scatter_butterfly / _bine_block_by_block leaving
+//    rbuf untouched at P = 1 (libbine_reduce_scatter.c:585, :1098).
+//  * assert()/hang cases of the reference return BINE_ERR_ARG.
+#include <algorithm>
+#include <cstring>
+
+#include "bine_internal.h"
+
+namespace bine {
+
+// ---------------------------------------------------------------------------
+// schedule math (restates libbine_utils.h)
+// ---------------------------------------------------------------------------
+
+static int rho(int step) {  // rhos[] of libbine_utils.h:44-45
+  int v = 0, p = 1;
+  for (int i = 0; i <= step; i++) { v += p; p *= -2; }
+  return v;
+}
+
+int pi(int rank, int step, int P) {  // libbine_utils.h:129-138
+  int d = (rank & 1) == 0 ? (rank + rho(step)) % P : (rank - rho(step)) % P;
+  return d < 0 ? d + P : d;
+}
+
+bool is_pow2(int v) { return (v & (v - 1)) == 0; }
+
+int log2_ceil(int v) {  // log_2(), libbine_utils.h:279-288
+  if (v < 1) return -1;
+  int l = 31 - __builtin_clz((unsigned)v);
+  return is_pow2(v) ? l : l + 1;
+}
+
+static int floor_log2(int v) { return v < 1 ? -1 : 31 - __builtin_clz((unsigned)v); }  // hibit(v, 31)
+static int next_pow2(int v) { return v == 0 ? 1 : (int)(1u << (32 - __builtin_clz((unsigned)v))); }
+static int pmod(int a, int b) { int r = a % b; return r < 0 ? r + b : r; }
+static uint32_t to_nb(int32_t b) { const uint32_t m = 0xAAAAAAAAu; return (m + (uint32_t)b) ^ m; }
+static int32_t from_nb(uint32_t n) { const uint32_t m = 0xAAAAAAAAu; return (int32_t)((m ^ n) - m); }
+static int nb_min(int n) { int v = 0; for (int i = 1; i < n; i += 2) v -= 1 << i; return v; }
+static int nb_max(int n) { int v = 0; for (int i = 0; i < n; i += 2) v += 1 << i; return v; }
+static bool nb_fits(int x, int n) { return x >= nb_min(n) && x <= nb_max(n); }
+static uint32_t bitrev(uint32_t x) {
+  x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+  x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+  x = ((x >> 4) & 0x0f0f0f0fu) | ((x & 0x0f0f0f0fu) << 4);
+  x = ((x >> 8) & 0x00ff00ffu) | ((x & 0x00ff00ffu) << 8);
+  return (x >> 16) | (x << 16);
+}
+static uint32_t top_bits(uint32_t x, int n) { return n <= 0 ? 0 : bitrev(x) >> (32 - n); }
+
+// negabinary label of `rank` among P ranks: the (at most two) representable
+// values congruent to +-rank mod P (libbine_utils.h:537-570, including its
+// decimal-literal tie-break at :564)
+static void nb_candidates(uint32_t P, uint32_t rank, uint32_t *a, uint32_t *b, int *nbits) {
+  *a = *b = UINT32_MAX;
+  int n = log2_ceil((int)P);
+  *nbits = n;
+  int x = (int)rank, y = (int)rank - (int)P;
+  if (rank % 2 == 0) { x = -(int)rank; y = -(int)rank + (int)P; }
+  if (nb_fits(x, n)) *a = to_nb(x);
+  if (nb_fits(y, n)) *b = to_nb(y);
+}
+
+uint32_t remap_rank(uint32_t P, uint32_t rank) {  // libbine_utils.h:572-578
+  uint32_t a, b;
+  int n;
+  nb_candidates(P, rank, &a, &b, &n);
+  uint32_t v;
+  if (a == UINT32_MAX) v = b;
+  else if (b == UINT32_MAX) v = a;
+  else {
+    int sh = 32 - n;
+    uint32_t probe = (uint32_t)(sh < 32 ? (80000000 >> sh) : 80000000);
+    v = (a & probe) ? a : b;
+  }
+  if (v == UINT32_MAX) v = 0;
+  return top_bits(v ^ (v >> 1), n);
+}
+
+uint32_t get_nu(uint32_t rank, uint32_t size) {  // libbine_utils.h:611-648
+  uint32_t a, b;
+  int n;
+  nb_candidates(size, rank, &a, &b, &n);
+  auto nu = [&](uint32_t v) { return top_bits(v ^ (v >> 1), n); };
+  if (a == UINT32_MAX && b == UINT32_MAX) return 0;
+  if (a == UINT32_MAX) return nu(b);
+  if (b == UINT32_MAX) return nu(a);
+  return std::min((int)nu(a), (int)nu(b));
+}
+
+// libbine_utils_bitmaps.c:10-56 -- final block of each rank in the static
+// variants: the remap permutation with every last-step pair in rank order.
+void static_perm(int P, std::vector<int> &perm) {
+  int n = log2_ceil(P);
+  perm.assign((size_t)P, 0);
+  for (int r = 0; r < P; r++)
+    perm[(size_t)r] = (int)(remap_rank((uint32_t)P, (uint32_t)r) & ~1u) | (r > pi(r, n - 1, P) ? 1 : 0);
+}
+
+static int nb_partner(int r, int mask, int P) {  // e.g. libbine_reduce_scatter.c:936-940
+  int d = from_nb((uint32_t)((mask << 1) - 1));
+  return r % 2 == 0 ? pmod(r + d, P) : pmod(r - d, P);
+}
+
+// ---------------------------------------------------------------------------
+// plan builder
+// ---------------------------------------------------------------------------
+
+enum { SB = BINE_BUF_SBUF, RB = BINE_BUF_RBUF, T0 = BINE_BUF_TMP0, T1 = BINE_BUF_TMP1, T2 = BINE_BUF_TMP2 };
+
+namespace {
+struct Builder {
+  Plan p;
+  int rank;
+  int group = 0;
+  std::vector<Prim> pend_send, pend_recv;  // current exchange
+
+  explicit Builder(int r) : rank(r) {}
+
+  static Prim mk(int type) { Prim x; std::memset(&x, 0, sizeof x); x.type = type; x.aux_buf = -1; return x; }
+  void send(int peer, int buf, uint64_t off, uint64_t n) {
+    if (peer < 0 || n == 0) return;
+    Prim x = mk(BINE_PRIM_SEND); x.peer = peer; x.src_buf = buf; x.src_off = off; x.count = n;
+    pend_send.push_back(x);
+  }
+  void recv(int peer, int buf, uint64_t off, uint64_t n) {
+    if (peer < 0 || n == 0) return;
+    Prim x = mk(BINE_PRIM_RECV); x.peer = peer; x.dst_buf = buf; x.dst_off = off; x.count = n;
+    pend_recv.push_back(x);
+  }
+  // close the exchange; `pipeline` marks a {1 send, 1 recv} exchange whose
+  // receive is consumed element-for-element by the next REDUCE(3)
+  void end(bool pipeline = false) {
+    // an exchange with oneself is a local copy (send_remap's final step)
+    for (size_t i = 0; i < pend_send.size(); i++) {
+      if (pend_send[i].peer != rank) continue;
+      for (size_t j = 0; j < pend_recv.size(); j++) {
+        if (pend_recv[j].peer != rank) continue;
+        copy(pend_send[i].src_buf, pend_send[i].src_off, pend_recv[j].dst_buf, pend_recv[j].dst_off,
+             std::min(pend_send[i].count, pend_recv[j].count));
+        pend_send.erase(pend_send.begin() + (long)i);
+        pend_recv.erase(pend_recv.begin() + (long)j);
+        i--;
+        break;
+      }
+    }
+    bool pipe = pipeline && pend_send.size() == 1 && pend_recv.size() == 1 &&
+                pend_send[0].peer == pend_recv[0].peer;
+    for (auto &x : pend_send) { x.group = group; x.flags = pipe ? BINE_PRIM_PIPELINE : 0; p.prims.push_back(x); }
+    for (auto &x : pend_recv) { x.group = group; x.flags = pipe ? BINE_PRIM_PIPELINE : 0; p.prims.push_back(x); }
+    if (!pend_send.empty() || !pend_recv.empty()) group++;
+    pend_send.clear();
+    pend_recv.clear();
+  }
+  void reduce(int in, uint64_t in_off, int io, uint64_t io_off, uint64_t n, bool pipe = false) {
+    if (n == 0) return;
+    Prim x = mk(BINE_PRIM_REDUCE);
+    x.src_buf = in; x.src_off = in_off; x.dst_buf = io; x.dst_off = io_off; x.count = n;
+    x.flags = pipe ? BINE_PRIM_PIPELINE : 0;
+    p.prims.push_back(x);
+  }
+  // out = b (op) a
+  void reduce3(int a, uint64_t a_off, int b, uint64_t b_off, int out, uint64_t out_off, uint64_t n,
+               bool pipe = false) {
+    if (n == 0) return;
+    Prim x = mk(BINE_PRIM_REDUCE3);
+    x.src_buf = a; x.src_off = a_off; x.aux_buf = b; x.aux_off = b_off; x.dst_buf = out;
+    x.dst_off = out_off; x.count = n;
+    x.flags = pipe ? BINE_PRIM_PIPELINE : 0;
+    p.prims.push_back(x);
+  }
+  void copy(int src, uint64_t src_off, int dst, uint64_t dst_off, uint64_t n) {
+    if (n == 0 || (src == dst && src_off == dst_off)) return;
+    Prim x = mk(BINE_PRIM_COPY);
+    x.src_buf = src; x.src_off = src_off; x.dst_buf = dst; x.dst_off = dst_off; x.count = n;
+    p.prims.push_back(x);
+  }
+  void tmp(int t, uint64_t n) {
+    uint64_t &s = p.tmp_elems[t - T0];
+    s = std::max(s, n);
+  }
+  void fail(int st) { p.prims.clear(); p.status = st; }
+};
+
+// reduction "pipelined" only when the REDUCE directly follows its exchange
+constexpr bool PIPE = true;
+
+// ---------------------------------------------------------------------------
+// allreduce -- libbine_allreduce.c
+// ---------------------------------------------------------------------------
+
+// allreduce_recursivedoubling, :17-135
+void ar_recursivedoubling(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  const int src = a.in_place ? RB : SB;
+  if (P == 1) { b.copy(src, 0, RB, 0, n); return; }
+  b.tmp(T0, n);
+  b.copy(src, 0, T0, 0, n);  // inplacebuf
+  int tsend = T0, newrank;
+  const int adj = next_pow2(P) >> 1, extra = P - adj;
+  if (r < 2 * extra) {
+    if (r % 2 == 0) { b.send(r + 1, T0, 0, n); b.end(); newrank = -1; }
+    else { b.recv(r - 1, RB, 0, n); b.end(); b.reduce(RB, 0, T0, 0, n); newrank = r >> 1; }
+  } else newrank = r - extra;
+  for (int dist = 1; dist < adj && newrank >= 0; dist <<= 1) {
+    int nr = newrank ^ dist, remote = nr < extra ? nr * 2 + 1 : nr + extra;
+    b.send(remote, T0, 0, n); b.recv(remote, RB, 0, n); b.end(PIPE);
+    b.reduce(RB, 0, T0, 0, n, PIPE);
+  }
+  if (r < 2 * extra) {
+    if (r % 2 == 0) { b.recv(r + 1, RB, 0, n); b.end(); tsend = RB; }
+    else { b.send(r - 1, T0, 0, n); b.end(); }
+  }
+  if (tsend != RB) b.copy(T0, 0, RB, 0, n);
+}
+
+// COLL_BASE_COMPUTE_BLOCKCOUNT, libbine_utils.h:63-69
+struct Blocks {
+  uint64_t early, late;
+  int split;
+  Blocks(uint64_t count, int nb) {
+    early = late = count / (uint64_t)nb;
+    split = (int)(count % (uint64_t)nb);
+    if (split) early++;
+  }
+  uint64_t off(int blk) const { return blk < split ? (uint64_t)blk * early : (uint64_t)blk * late + (uint64_t)split; }
+  uint64_t cnt(int blk) const { return blk < split ? early : late; }
+  // a run of w blocks starting at `start` (libbine_allreduce.c:749-756)
+  uint64_t wcnt(int start, int w) const {
+    if (start + w <= split) return (uint64_t)w * early;
+    if (start >= split) return (uint64_t)w * late;
+    return (uint64_t)w * late + (uint64_t)(split - start);
+  }
+};
+
+// allreduce_ring, :138-319
+void ar_ring(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  const int src = a.in_place ? RB : SB;
+  if (P == 1) { b.copy(src, 0, RB, 0, n); return; }
+  if (n < (uint64_t)P) { ar_recursivedoubling(b, a); return; }
+  Blocks bl(n, P);
+  b.tmp(T0, bl.early); b.tmp(T1, bl.early);
+  const int ib[2] = {T0, T1};
+  b.copy(src, 0, RB, 0, n);
+  const int to = (r + 1) % P, from = (r + P - 1) % P;
+  int inbi = 0;
+  b.recv(from, ib[inbi], 0, bl.cnt(from)); b.send(to, RB, bl.off(r), bl.cnt(r)); b.end();
+  for (int k = 2; k < P; k++) {
+    const int prev = (r + P - k + 1) % P, incoming = (r + P - k) % P;
+    inbi ^= 1;
+    b.reduce(ib[inbi ^ 1], 0, RB, bl.off(prev), bl.cnt(prev));
+    b.recv(from, ib[inbi], 0, bl.cnt(incoming)); b.send(to, RB, bl.off(prev), bl.cnt(prev)); b.end();
+  }
+  const int last = (r + 1) % P;
+  b.reduce(ib[inbi], 0, RB, bl.off(last), bl.cnt(last));
+  for (int k = 0; k < P - 1; k++) {  // :282-304
+    const int rf = (r + P - k) % P, sf = (r + 1 + P - k) % P;
+    b.send(to, RB, bl.off(sf), bl.cnt(sf)); b.recv(from, RB, bl.off(rf), bl.cnt(rf)); b.end();
+  }
+}
+
+// allreduce_rabenseifner, :441-694
+void ar_rabenseifner(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  const int steps = floor_log2(P), adj = 1 << steps, rem = P - adj;
+  b.tmp(T0, n);
+  if (!a.in_place) b.copy(SB, 0, RB, 0, n);
+  const uint64_t lh = n / 2, rh = n - lh;
+  int vrank;
+  if (r < 2 * rem) {
+    if (r % 2) {
+      b.send(r - 1, RB, 0, lh); b.recv(r - 1, T0, lh, rh); b.end(PIPE);
+      b.reduce(T0, lh, RB, lh, rh, PIPE);
+      b.send(r - 1, RB, lh, rh); b.end();
+      vrank = -1;
+    } else {
+      b.send(r + 1, RB, lh, rh); b.recv(r + 1, T0, 0, lh); b.end(PIPE);
+      b.reduce(T0, 0, RB, 0, lh, PIPE);
+      b.recv(r + 1, RB, lh, rh); b.end();
+      vrank = r / 2;
+    }
+  } else vrank = r - rem;
+  if (vrank != -1) {
+    std::vector<uint64_t> ri(steps + 1), si(steps + 1), rc(steps + 1), sc(steps + 1);
+    uint64_t w = n;
+    int step = 0;
+    for (int mask = 1; mask < adj; mask <<= 1) {
+      int vdest = vrank ^ mask, dest = vdest < rem ? vdest * 2 : vdest + rem;
+      if (r < dest) { rc[step] = w / 2; sc[step] = w - rc[step]; si[step] = ri[step] + rc[step]; }
+      else { sc[step] = w / 2; rc[step] = w - sc[step]; ri[step] = si[step] + sc[step]; }
+      b.send(dest, RB, si[step], sc[step]); b.recv(dest, T0, ri[step], rc[step]); b.end(PIPE);
+      b.reduce(T0, ri[step], RB, ri[step], rc[step], PIPE);
+      if (step + 1 < steps) { ri[step + 1] = ri[step]; si[step + 1] = ri[step]; w = rc[step]; step++; }
+    }
+    step = steps - 1;
+    for (int mask = adj >> 1; mask > 0; mask >>= 1) {
+      int vdest = vrank ^ mask, dest = vdest < rem ? vdest * 2 : vdest + rem;
+      b.send(dest, RB, ri[step], rc[step]); b.recv(dest, RB, si[step], sc[step]); b.end();
+      step--;
+    }
+  }
+  if (r < 2 * rem) {
+    if (r % 2) b.recv(r - 1, RB, 0, n); else b.send(r + 1, RB, 0, n);
+    b.end();
+  }
+}
+
+// allreduce_bine_lat, :321-439
+void ar_bine_lat(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  const int src = a.in_place ? RB : SB;
+  if (P == 1) { b.copy(src, 0, RB, 0, n); return; }
+  b.tmp(T0, n);
+  b.copy(src, 0, T0, 0, n);
+  int tsend = T0;
+  const int steps = floor_log2(P), adj = 1 << steps, extra = P - adj;
+  const bool pw2 = is_pow2(P);
+  int nr = r;
+  bool idle = false;
+  if (r < 2 * extra) {
+    if (r % 2 == 0) { b.send(r + 1, T0, 0, n); b.end(); idle = true; }
+    else { b.recv(r - 1, RB, 0, n); b.end(); b.reduce(RB, 0, T0, 0, n); nr = r >> 1; }
+  } else nr = r - extra;
+  for (int s = 0; s < steps && !idle; s++) {
+    int vd = pi(nr, s, adj), dest = pw2 ? vd : (vd < extra ? (vd << 1) + 1 : vd + extra);
+    b.send(dest, T0, 0, n); b.recv(dest, RB, 0, n); b.end(PIPE);
+    b.reduce(RB, 0, T0, 0, n, PIPE);
+  }
+  if (r < 2 * extra) {
+    if (!idle) b.send(r - 1, T0, 0, n);
+    else { b.recv(r + 1, RB, 0, n); tsend = RB; }
+    b.end();
+  }
+  if (tsend != RB) b.copy(T0, 0, RB, 0, n);
+}
+
+// allreduce_bine_bdw_static, :696-817
+void ar_bine_bdw_static(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  const int steps = log2_ceil(P);
+  if (!is_pow2(P) || steps < 1) { b.fail(BINE_ERR_ARG); return; }
+  Blocks bl(n, P);
+  std::vector<int> perm;
+  static_perm(P, perm);
+  auto recv_start = [&](int rank, int s) { int w = P >> (s + 1); return perm[(size_t)rank] & ~(w - 1); };
+  b.tmp(T0, bl.wcnt(0, P / 2) + bl.early);
+  const bool elide = !a.in_place;  // step 0 reads sbuf, writes rbuf
+  int w = P;
+  for (int s = 0; s < steps; s++) {
+    w >>= 1;
+    const int dest = pi(r, s, P), sb = recv_start(dest, s), rb = recv_start(r, s);
+    const int sbuf = (elide && s == 0) ? SB : RB;
+    b.send(dest, sbuf, bl.off(sb), bl.wcnt(sb, w)); b.recv(dest, T0, 0, bl.wcnt(rb, w)); b.end(PIPE);
+    if (elide && s == 0) b.reduce3(T0, 0, SB, bl.off(rb), RB, bl.off(rb), bl.wcnt(rb, w), PIPE);
+    else b.reduce(T0, 0, RB, bl.off(rb), bl.wcnt(rb, w), PIPE);
+  }
+  for (int s = steps - 1; s >= 0; s--) {
+    const int dest = pi(r, s, P), sb = recv_start(dest, s), rb = recv_start(r, s);
+    b.send(dest, RB, bl.off(rb), bl.wcnt(rb, w)); b.recv(dest, RB, bl.off(sb), bl.wcnt(sb, w)); b.end();
+    w <<= 1;
+  }
+}
+
+// allreduce_bine_bdw_remap (:820-923) and allreduce_bine_bdw_remap_segmented
+// (:1093-1308; the non-power-of-two fold of :1148-1169 / :1282-1290, the
+// segment pipelining becomes the executor's chunked exchange+reduce overlap)
+void ar_bine_remap(Builder &b, const PlanArgs &a, bool segmented) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  int steps, adj, extra;
+  if (!segmented) {
+    steps = log2_ceil(P);
+    if (!is_pow2(P) || steps == -1) { b.fail(BINE_ERR_ARG); return; }
+    adj = P; extra = 0;
+  } else {
+    steps = floor_log2(P);
+    adj = 1 << steps; extra = P - adj;
+  }
+  const bool pw2 = extra == 0;
+  b.tmp(T0, n - n / 2);
+  int nr = r;
+  bool idle = false, elide = false;
+  if (r < 2 * extra) {
+    if (r % 2 == 0) { b.send(r + 1, a.in_place ? RB : SB, 0, n); b.end(); idle = true; }
+    else {
+      nr = r >> 1;
+      if (!a.in_place) {
+        b.recv(r - 1, RB, 0, n); b.end();
+        b.reduce(SB, 0, RB, 0, n);  // :1158 in = sbuf, inout = received
+      } else {
+        b.tmp(T1, n);
+        b.recv(r - 1, T1, 0, n); b.end();
+        b.reduce(RB, 0, T1, 0, n);
+        b.copy(T1, 0, RB, 0, n);
+      }
+    }
+  } else {
+    nr = r - extra;
+    if (!a.in_place) {
+      if (steps >= 1) elide = true;
+      else b.copy(SB, 0, RB, 0, n);
+    }
+  }
+  if (!idle) {
+    std::vector<uint64_t> ri(steps + 1), si(steps + 1), rc(steps + 1), sc(steps + 1);
+    std::vector<int> dst(steps + 1);
+    uint64_t w = n;
+    const uint32_t vrank = remap_rank((uint32_t)adj, (uint32_t)nr);
+    for (int s = 0; s < steps; s++) {
+      const int vd = pi(nr, s, adj);
+      dst[s] = pw2 ? vd : (vd < extra ? (vd << 1) + 1 : vd + extra);
+      const uint32_t vdest = remap_rank((uint32_t)adj, (uint32_t)vd);
+      if (vrank < vdest) { rc[s] = w / 2; sc[s] = w - rc[s]; si[s] = ri[s] + rc[s]; }
+      else { sc[s] = w / 2; rc[s] = w - sc[s]; ri[s] = si[s] + sc[s]; }
+      const bool first = elide && s == 0;
+      b.send(dst[s], first ? SB : RB, si[s], sc[s]); b.recv(dst[s], T0, 0, rc[s]); b.end(PIPE);
+      if (first) b.reduce3(T0, 0, SB, ri[s], RB, ri[s], rc[s], PIPE);
+      else b.reduce(T0, 0, RB, ri[s], rc[s], PIPE);
+      if (s + 1 < steps) { ri[s + 1] = ri[s]; si[s + 1] = ri[s]; w = rc[s]; }
+    }
+    for (int s = steps - 1; s >= 0; s--) {
+      b.send(dst[s], RB, ri[s], rc[s]); b.recv(dst[s], RB, si[s], sc[s]); b.end();
+    }
+  }
+  if (r < 2 * extra) {
+    if (!idle) b.send(r - 1, RB, 0, n); else b.recv(r + 1, RB, 0, n);
+    b.end();
+  }
+}
+
+// allreduce_bine_block_by_block_any_even, :925-1091
+void ar_bine_bbb_any_even(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  if (P % 2) { b.fail(BINE_ERR_ARG); return; }  // assert(size % 2 == 0), :931
+  Blocks bl(n, P);
+  b.tmp(T0, n);
+  if (!a.in_place) b.copy(SB, 0, RB, 0, n);
+  int mask = 1, rstep = log2_ceil(P) - 1;
+  std::vector<int> kof((size_t)P, -1);
+  for (int blk = 1; blk < P; blk++) kof[(size_t)blk] = 31 - __builtin_clz(get_nu((uint32_t)blk, (uint32_t)P));
+  while (mask < P) {
+    const int partner = nb_partner(r, mask, P);
+    std::vector<int> got;
+    for (int blk = 1; blk < P; blk++) {
+      if (kof[(size_t)blk] != rstep) continue;
+      int bts, brv;
+      if (r % 2 == 0) { bts = pmod(blk + r, P); brv = pmod(partner - blk, P); }
+      else { bts = pmod(r - blk, P); brv = pmod(blk + partner, P); }
+      if (bts != r) b.send(partner, RB, bl.off(bts), bl.cnt(bts));
+      if (brv != partner) { b.recv(partner, T0, bl.off(brv), bl.cnt(brv)); got.push_back(brv); }
+    }
+    b.end();
+    for (int blk : got) b.reduce(T0, bl.off(blk), RB, bl.off(blk), bl.cnt(blk));
+    mask <<= 1; rstep--;
+  }
+  int step = 0;
+  mask >>= 1;
+  while (mask > 0) {
+    const int partner = nb_partner(r, mask, P);
+    for (int blk = 1; blk < P; blk++) {
+      if (kof[(size_t)blk] != step) continue;
+      int bts, brv;
+      if (r % 2 == 0) { brv = pmod(blk + r, P); bts = pmod(partner - blk, P); }
+      else { brv = pmod(r - blk, P); bts = pmod(blk + partner, P); }
+      if (bts != partner) b.send(partner, RB, bl.off(bts), bl.cnt(bts));
+      if (brv != r) b.recv(partner, RB, bl.off(brv), bl.cnt(brv));
+    }
+    b.end();
+    mask >>= 1; step++;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// reduce_scatter -- libbine_reduce_scatter.c
+// ---------------------------------------------------------------------------
+
+struct Displs {
+  std::vector<uint64_t> d;
+  uint64_t total = 0;
+  uint64_t maxc = 0;
+  explicit Displs(const std::vector<int> &rc) {
+    d.resize(rc.size());
+    for (size_t i = 0; i < rc.size(); i++) {
+      d[i] = total;
+      total += (uint64_t)rc[i];
+      maxc = std::max(maxc, (uint64_t)rc[i]);
+    }
+  }
+};
+
+// reduce_scatter_recursivehalving, :15-257
+void rs_recursivehalving(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  Displs ds(rc);
+  const uint64_t count = ds.total;
+  if (!count) return;
+  const int src = a.in_place ? RB : SB;
+  b.tmp(T0, count); b.tmp(T1, count);  // recv_buf, result_buf
+  b.copy(src, 0, T1, 0, count);
+  const int tsz = next_pow2(P) >> 1, rem = P - tsz;
+  int tr;
+  if (r < 2 * rem) {
+    if ((r & 1) == 0) { b.send(r + 1, T1, 0, count); b.end(); tr = -1; }
+    else { b.recv(r - 1, T0, 0, count); b.end(); b.reduce(T0, 0, T1, 0, count); tr = r / 2; }
+  } else tr = r - rem;
+  if (tr >= 0) {
+    std::vector<uint64_t> trc((size_t)tsz), tds((size_t)tsz);
+    for (int i = 0; i < tsz; i++) trc[(size_t)i] = i < rem ? (uint64_t)rc[2 * i + 1] + (uint64_t)rc[2 * i] : (uint64_t)rc[i + rem];
+    for (int i = 0; i + 1 < tsz; i++) tds[(size_t)i + 1] = tds[(size_t)i] + trc[(size_t)i];
+    int sidx = 0, ridx = 0, last = tsz;
+    for (int mask = tsz >> 1; mask > 0; mask >>= 1) {
+      int tp = tr ^ mask, peer = tp < rem ? tp * 2 + 1 : tp + rem;
+      uint64_t scn = 0, rcn = 0;
+      if (tr < tp) {
+        sidx = ridx + mask;
+        for (int i = sidx; i < last; i++) scn += trc[(size_t)i];
+        for (int i = ridx; i < sidx; i++) rcn += trc[(size_t)i];
+      } else {
+        ridx = sidx + mask;
+        for (int i = sidx; i < ridx; i++) scn += trc[(size_t)i];
+        for (int i = ridx; i < last; i++) rcn += trc[(size_t)i];
+      }
+      const bool pipe = scn > 0 && rcn > 0;
+      b.recv(peer, T0, tds[(size_t)ridx], rcn); b.send(peer, T1, tds[(size_t)sidx], scn); b.end(pipe);
+      b.reduce(T0, tds[(size_t)ridx], T1, tds[(size_t)ridx], rcn, pipe);
+      sidx = ridx;
+      last = ridx + mask;
+    }
+    b.copy(T1, ds.d[(size_t)r], RB, 0, (uint64_t)rc[(size_t)r]);
+  }
+  if (r < 2 * rem) {
+    if ((r & 1) == 0) b.recv(r + 1, RB, 0, (uint64_t)rc[(size_t)r]);
+    else b.send(r - 1, T1, ds.d[(size_t)r - 1], (uint64_t)rc[(size_t)r - 1]);
+    b.end();
+  }
+}
+
+// reduce_scatter_recursive_distance_doubling, :259-419
+void rs_recursive_distance_doubling(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  const int steps = log2_ceil(P);
+  if (!is_pow2(P) || steps == -1) { b.fail(BINE_ERR_ARG); return; }
+  Displs ds(rc);
+  const uint64_t count = ds.total;
+  if (!count) return;
+  const int src = a.in_place ? RB : SB;
+  b.tmp(T0, count); b.tmp(T1, count);
+  b.copy(src, 0, T1, 0, count);
+  int w = P >> 1, dist = 1, sidx = 0, ridx = 0, last = P;
+  for (int s = 0; s < steps; s++) {
+    const int peer = r ^ dist;
+    uint64_t scn = 0, rcn = 0;
+    if (r < peer) {
+      sidx = ridx + w;
+      for (int i = sidx; i < last; i++) scn += (uint64_t)rc[(size_t)i];
+      for (int i = ridx; i < sidx; i++) rcn += (uint64_t)rc[(size_t)i];
+    } else {
+      ridx = sidx + w;
+      for (int i = sidx; i < ridx; i++) scn += (uint64_t)rc[(size_t)i];
+      for (int i = ridx; i < last; i++) rcn += (uint64_t)rc[(size_t)i];
+    }
+    const bool pipe = scn > 0 && rcn > 0;
+    b.recv(peer, T0, ds.d[(size_t)ridx], rcn); b.send(peer, T1, ds.d[(size_t)sidx], scn); b.end(pipe);
+    b.reduce(T0, ds.d[(size_t)ridx], T1, ds.d[(size_t)ridx], rcn, pipe);
+    sidx = ridx;
+    last = ridx + w;
+    w >>= 1; dist <<= 1;
+  }
+  const int inv = (int)top_bits((uint32_t)r, steps);  // inverse_rank(), libbine_utils.h:580-583
+  if (inv != r) {
+    b.send(inv, T1, ds.d[(size_t)inv], (uint64_t)rc[(size_t)inv]); b.recv(inv, RB, 0, (uint64_t)rc[(size_t)r]); b.end();
+  } else b.copy(T1, ds.d[(size_t)r], RB, 0, (uint64_t)rc[(size_t)r]);
+}
+
+// reduce_scatter_ring, :421-572
+void rs_ring(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  Displs ds(rc);
+  const int src = a.in_place ? RB : SB;
+  auto cnt = [&](int i) { return (uint64_t)rc[(size_t)i]; };
+  if (P == 1) { b.copy(src, 0, RB, 0, ds.total); return; }
+  b.tmp(T0, ds.total); b.tmp(T1, ds.maxc); b.tmp(T2, ds.maxc);
+  const int ib[2] = {T1, T2};
+  b.copy(src, 0, T0, 0, ds.total);
+  const int to = (r + 1) % P, from = (r + P - 1) % P;
+  int inbi = 0;
+  b.recv(from, ib[inbi], 0, cnt((r + P - 2) % P)); b.send(to, T0, ds.d[(size_t)from], cnt(from)); b.end();
+  for (int k = 2; k < P; k++) {
+    const int prev = (r + P - k) % P, incoming = (r + P - k - 1) % P;
+    inbi ^= 1;
+    b.reduce(ib[inbi ^ 1], 0, T0, ds.d[(size_t)prev], cnt(prev));
+    b.recv(from, ib[inbi], 0, cnt(incoming)); b.send(to, T0, ds.d[(size_t)prev], cnt(prev)); b.end();
+  }
+  b.reduce(ib[inbi], 0, T0, ds.d[(size_t)r], cnt(r));
+  b.copy(T0, ds.d[(size_t)r], RB, 0, cnt(r));
+}
+
+// sum_counts, libbine_utils.h:404-410
+static uint64_t sum_counts(const std::vector<int> &c, const Displs &ds, int rem, int lo, int hi) {
+  lo = lo < rem ? lo * 2 : lo + rem;
+  hi = hi < rem ? hi * 2 + 1 : hi + rem;
+  return ds.d[(size_t)hi] + (uint64_t)c[(size_t)hi] - ds.d[(size_t)lo];
+}
+
+static uint32_t mirror(uint32_t x, int nbits) { return top_bits(x, nbits); }  // :418-426
+
+// reduce_scatter_butterfly, :575-761
+void rs_butterfly(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  Displs ds(rc);
+  const int src = a.in_place ? RB : SB;
+  if (P < 2) { b.copy(src, 0, RB, 0, ds.total); return; }  // the reference returns without copying
+  const uint64_t total = ds.total;
+  b.tmp(T0, total); b.tmp(T1, total);
+  int ps = T0, pr = T1;
+  b.copy(src, 0, ps, 0, total);
+  const int pof2 = next_pow2(P) >> 1, rem = P - pof2, l2 = log2_ceil(pof2);
+  int vr;
+  if (r < 2 * rem) {
+    if (r % 2 == 0) { b.send(r + 1, ps, 0, total); b.end(); vr = -1; }
+    else { b.recv(r - 1, pr, 0, total); b.end(); b.reduce(pr, 0, ps, 0, total); vr = r / 2; }
+  } else vr = r - rem;
+  if (vr != -1) {
+    int nblocks = pof2, si = 0, ri = 0;
+    for (int mask = 1; mask < pof2; mask <<= 1) {
+      const int vp = vr ^ mask, peer = vp < rem ? vp * 2 + 1 : vp + rem;
+      nblocks /= 2;
+      if ((vr & mask) == 0) si += nblocks; else ri += nblocks;
+      const uint64_t scn = sum_counts(rc, ds, rem, si, si + nblocks - 1);
+      int ix = si < rem ? 2 * si : rem + si;
+      const uint64_t sd = ds.d[(size_t)ix];
+      const uint64_t rcn = sum_counts(rc, ds, rem, ri, ri + nblocks - 1);
+      ix = ri < rem ? 2 * ri : rem + ri;
+      const uint64_t rd = ds.d[(size_t)ix];
+      const bool pipe = scn > 0 && rcn > 0;
+      b.send(peer, ps, sd, scn); b.recv(peer, pr, rd, rcn); b.end(pipe);
+      if (vr < vp) { b.reduce(ps, rd, pr, rd, rcn, pipe); std::swap(ps, pr); }
+      else b.reduce(pr, rd, ps, rd, rcn, pipe);
+      si = ri;
+    }
+    const int vp = (int)mirror((uint32_t)vr, l2), peer = vp < rem ? vp * 2 + 1 : vp + rem;
+    int ix = si < rem ? 2 * si : rem + si;
+    if (vp < rem) b.send(peer - 1, ps, ds.d[(size_t)ix], (uint64_t)rc[(size_t)ix]);
+    if (vp < rem) ix++;
+    if (vp != vr) {
+      b.send(peer, ps, ds.d[(size_t)ix], (uint64_t)rc[(size_t)ix]); b.recv(peer, RB, 0, (uint64_t)rc[(size_t)r]);
+    }
+    b.end();
+    if (vp == vr) b.copy(ps, ds.d[(size_t)r], RB, 0, (uint64_t)rc[(size_t)r]);
+  } else {
+    const int vp = (int)mirror((uint32_t)((r + 1) / 2), l2), peer = vp < rem ? vp * 2 + 1 : vp + rem;
+    b.recv(peer, RB, 0, (uint64_t)rc[(size_t)r]); b.end();
+  }
+}
+
+// reduce_scatter_bine_static, :763-904
+void rs_bine_static(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  Displs ds(rc);
+  const uint64_t count = ds.total;
+  if (!count) return;
+  const int steps = log2_ceil(P);
+  if (!is_pow2(P) || steps < 1) { b.fail(BINE_ERR_SIZE); return; }
+  std::vector<int> perm;
+  static_perm(P, perm);
+  auto recv_start = [&](int rank, int s) { int w = P >> (s + 1); return perm[(size_t)rank] & ~(w - 1); };
+  auto run = [&](int start, int w) {
+    uint64_t c = 0;
+    for (int i = 0; i < w; i++) c += (uint64_t)rc[(size_t)(start + i)];
+    return c;
+  };
+  const int src = a.in_place ? RB : SB;
+  b.tmp(T0, count); b.tmp(T1, count);  // recv_buf, result_buf
+  b.copy(src, 0, T1, 0, count);
+  int w = P >> 1;
+  for (int s = 0; s < steps; s++) {
+    const int peer = pi(r, s, P), sb = recv_start(peer, s), rb = recv_start(r, s);
+    const uint64_t scn = run(sb, w), rcn = run(rb, w);
+    const bool pipe = scn > 0 && rcn > 0;
+    b.send(peer, T1, ds.d[(size_t)sb], scn); b.recv(peer, T0, ds.d[(size_t)rb], rcn); b.end(pipe);
+    b.reduce(T0, ds.d[(size_t)rb], T1, ds.d[(size_t)rb], rcn, pipe);
+    w >>= 1;
+  }
+  const int target = perm[(size_t)r];
+  if (target != r) {
+    int sender = -1;
+    for (int j = 0; j < P; j++) if (perm[(size_t)j] == r) { sender = j; break; }
+    b.send(target, T1, ds.d[(size_t)target], (uint64_t)rc[(size_t)target]);
+    b.recv(sender, RB, 0, (uint64_t)rc[(size_t)r]);
+    b.end();
+  } else b.copy(T1, ds.d[(size_t)r], RB, 0, (uint64_t)rc[(size_t)r]);
+}
+
+// reduce_scatter_bine_send_remap (:906-983) / _permute_remap (:985-1063)
+void rs_bine_remap(Builder &b, const PlanArgs &a, bool permute) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  if (!is_pow2(P)) { b.fail(BINE_ERR_ARG); return; }  // the reference hangs
+  Displs ds(rc);
+  const uint64_t count = ds.total;
+  const int src = a.in_place ? RB : SB;
+  b.tmp(T0, count); b.tmp(T1, count + ds.maxc);  // tmpbuf, resbuf
+  if (!permute) b.copy(src, 0, T1, 0, count);
+  else
+    for (int i = 0; i < P; i++)
+      b.copy(src, ds.d[(size_t)i], T1, ds.d[remap_rank((uint32_t)P, (uint32_t)i)], (uint64_t)rc[(size_t)i]);
+  const int steps = log2_ceil(P);
+  const int me = (int)remap_rank((uint32_t)P, (uint32_t)r);
+  int mask = 1, inv = steps >= 1 ? 1 << (steps - 1) : 0;
+  auto span = [&](int first, int lastb) { return ds.d[(size_t)lastb] - ds.d[(size_t)first] + (uint64_t)rc[(size_t)lastb]; };
+  while (mask < P) {
+    const int partner = nb_partner(r, mask, P);
+    const int bfm = ~(inv - 1);
+    const int sbf = (int)remap_rank((uint32_t)P, (uint32_t)partner) & bfm, sbl = sbf + inv - 1;
+    const int rbf = me & bfm, rbl = rbf + inv - 1;
+    const uint64_t scn = span(sbf, sbl), rcn = span(rbf, rbl);
+    const bool pipe = scn > 0 && rcn > 0;
+    b.send(partner, T1, ds.d[(size_t)sbf], scn); b.recv(partner, T0, ds.d[(size_t)rbf], rcn); b.end(pipe);
+    b.reduce(T0, ds.d[(size_t)rbf], T1, ds.d[(size_t)rbf], rcn, pipe);
+    mask <<= 1; inv >>= 1;
+  }
+  if (!permute) {  // :966-969, the any-source receive resolved to its one sender
+    int sender = r;
+    for (int j = 0; j < P; j++) if ((int)remap_rank((uint32_t)P, (uint32_t)j) == r) { sender = j; break; }
+    b.send(me, T1, ds.d[(size_t)me], (uint64_t)rc[(size_t)me]);
+    b.recv(sender, RB, 0, (uint64_t)rc[(size_t)r]);
+    b.end();
+  } else b.copy(T1, ds.d[(size_t)me], RB, 0, (uint64_t)rc[(size_t)r]);
+}
+
+// reduce_scatter_bine_block_by_block, :1066-1174
+void rs_bine_bbb(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  if (!is_pow2(P)) { b.fail(BINE_ERR_ARG); return; }  // the reference hangs
+  Displs ds(rc);
+  const int src = a.in_place ? RB : SB;
+  if (P == 1) { b.copy(src, 0, RB, 0, (uint64_t)rc[0]); return; }  // reference: rbuf untouched
+  std::vector<int> invr((size_t)P);
+  for (int i = 0; i < P; i++) invr[remap_rank((uint32_t)P, (uint32_t)i)] = i;
+  b.tmp(T0, ds.total); b.tmp(T1, ds.total);  // tmpbuf, resbuf
+  b.copy(src, 0, T1, 0, ds.total);
+  const int steps = log2_ceil(P);
+  const int me = (int)remap_rank((uint32_t)P, (uint32_t)r);
+  int mask = 1, inv = 1 << (steps - 1);
+  while (mask < P) {
+    const bool last = (mask << 1) >= P;
+    const int partner = nb_partner(r, mask, P);
+    const int bfm = ~(inv - 1);
+    const int sbf = (int)remap_rank((uint32_t)P, (uint32_t)partner) & bfm, sbl = sbf + inv - 1;
+    const int rbf = me & bfm, rbl = rbf + inv - 1;
+    for (int blk = rbf; blk <= rbl; blk++) {
+      const int o = invr[(size_t)blk];
+      b.recv(partner, last ? RB : T0, last ? 0 : ds.d[(size_t)o], (uint64_t)rc[(size_t)o]);
+    }
+    for (int blk = sbf; blk <= sbl; blk++) {
+      const int o = invr[(size_t)blk];
+      b.send(partner, T1, ds.d[(size_t)o], (uint64_t)rc[(size_t)o]);
+    }
+    b.end();
+    for (int blk = rbf; blk <= rbl; blk++) {
+      const int o = invr[(size_t)blk];
+      if (last) b.reduce(T1, ds.d[(size_t)o], RB, 0, (uint64_t)rc[(size_t)o]);  // :1143
+      else b.reduce(T0, ds.d[(size_t)o], T1, ds.d[(size_t)o], (uint64_t)rc[(size_t)o]);
+    }
+    mask <<= 1; inv >>= 1;
+  }
+}
+
+// reduce_scatter_bine_block_by_block_any_even, :1176-1298
+void rs_bine_bbb_any_even(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const auto &rc = a.rcounts;
+  Displs ds(rc);
+  const int src = a.in_place ? RB : SB;
+  if (P == 1) { b.copy(src, 0, RB, 0, (uint64_t)rc[0]); return; }
+  if (P % 2) { b.fail(BINE_ERR_ARG); return; }  // the reference hangs for odd P > 1
+  b.tmp(T0, ds.total); b.tmp(T1, ds.total);
+  b.copy(src, 0, T1, 0, ds.total);
+  std::vector<int> kof((size_t)P, -1);
+  for (int blk = 1; blk < P; blk++) kof[(size_t)blk] = 31 - __builtin_clz(get_nu((uint32_t)blk, (uint32_t)P));
+  int mask = 1, rstep = log2_ceil(P) - 1;
+  bool done = false;
+  while (mask < P) {
+    const bool last = (mask << 1) >= P;
+    const int partner = nb_partner(r, mask, P);
+    std::vector<int> got;
+    for (int blk = 1; blk < P; blk++) {
+      if (kof[(size_t)blk] != rstep) continue;
+      int bts, brv;
+      if (r % 2 == 0) { bts = pmod(blk + r, P); brv = pmod(partner - blk, P); }
+      else { bts = pmod(r - blk, P); brv = pmod(blk + partner, P); }
+      if (bts != r) b.send(partner, T1, ds.d[(size_t)bts], (uint64_t)rc[(size_t)bts]);
+      if (brv != partner) {
+        got.push_back(brv);
+        if (last) { b.recv(partner, RB, 0, (uint64_t)rc[(size_t)brv]); done = true; }
+        else b.recv(partner, T0, ds.d[(size_t)brv], (uint64_t)rc[(size_t)brv]);
+      }
+    }
+    b.end();
+    for (int blk : got) {
+      if (last) b.reduce(T1, ds.d[(size_t)blk], RB, 0, (uint64_t)rc[(size_t)blk]);
+      else b.reduce(T0, ds.d[(size_t)blk], T1, ds.d[(size_t)blk], (uint64_t)rc[(size_t)blk]);
+    }
+    mask <<= 1; rstep--;
+  }
+  if (!done) b.copy(T1, ds.d[(size_t)r], RB, 0, (uint64_t)rc[(size_t)r]);
+}
+
+// ---------------------------------------------------------------------------
+// reduce -- libbine_reduce.c
+// ---------------------------------------------------------------------------
+
+// reduce_bine_lat, :16-80
+void rd_bine_lat(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank, root = a.root;
+  const uint64_t n = a.count;
+  if (n == 0) return;
+  if (!is_pow2(P)) { b.fail(BINE_ERR_SIZE); return; }
+  const int src = (a.in_place && r == root) ? RB : SB;
+  const int acc = r == root ? RB : T1;
+  b.tmp(T0, n);
+  if (r != root) b.tmp(T1, n);
+  b.copy(src, 0, acc, 0, n);
+  const int vrank = pmod(r - root, P);
+  const int bv = (int)to_nb(vrank);
+  for (int mask = 1; mask < P; mask <<= 1) {
+    const int partner = pmod(from_nb((uint32_t)(bv ^ ((mask << 1) - 1))) + root, P);
+    const int ml = (mask << 2) - 1, lsbs = bv & ml;
+    const bool eq = lsbs == 0 || lsbs == ml;
+    if (!eq || ((mask << 1) >= P && r != root)) { b.send(partner, acc, 0, n); b.end(); break; }
+    b.recv(partner, T0, 0, n); b.end(PIPE);
+    b.reduce(T0, 0, acc, 0, n, PIPE);
+  }
+}
+
+// reduce_bine_bdw, :83-222
+void rd_bine_bdw(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t n = a.count;
+  if (a.root != 0) { b.fail(BINE_ERR_ARG); return; }  // assert(root == 0), :86
+  if (!is_pow2(P)) { b.fail(BINE_ERR_SIZE); return; }
+  const int steps = log2_ceil(P);
+  const uint64_t cpr = n / (uint64_t)P;
+  const int rem = (int)(n % (uint64_t)P);
+  const int src = (a.in_place && r == 0) ? RB : SB;
+  const int res = r == 0 ? RB : T1;
+  b.tmp(T0, n);
+  if (r != 0) b.tmp(T1, n);
+  b.copy(src, 0, res, 0, n);
+  const int me = (int)remap_rank((uint32_t)P, (uint32_t)r);
+  std::vector<uint64_t> ri(steps + 1), si(steps + 1), rc(steps + 1), sc(steps + 1);
+  auto first = [&](int blk) { return cpr * (uint64_t)blk + (uint64_t)std::min(blk, rem); };
+  auto span = [&](int f, int l) {
+    return cpr * (uint64_t)(l - f + 1) + (uint64_t)(std::min(l, rem) - std::min(f, rem)) + (l < rem ? 1u : 0u);
+  };
+  int mask = 1, inv = steps >= 1 ? 1 << (steps - 1) : 0, step = 0;
+  while (mask < P) {
+    const int partner = nb_partner(r, mask, P);
+    const int bfm = ~(inv - 1);
+    const int sbf = (int)remap_rank((uint32_t)P, (uint32_t)partner) & bfm, sbl = sbf + inv - 1;
+    const int rbf = me & bfm, rbl = rbf + inv - 1;
+    si[step] = first(sbf); sc[step] = span(sbf, sbl);
+    ri[step] = first(rbf); rc[step] = span(rbf, rbl);
+    const bool pipe = sc[step] > 0 && rc[step] > 0;
+    b.send(partner, res, si[step], sc[step]); b.recv(partner, T0, ri[step], rc[step]); b.end(pipe);
+    b.reduce(T0, ri[step], res, ri[step], rc[step], pipe);
+    mask <<= 1; inv >>= 1; step++;
+  }
+  mask >>= 1;
+  inv = 1;
+  step = steps - 1;
+  const unsigned recvmask = me ? 1u << (__builtin_ffs(me) - 1) : 0x80000000u;  // :172 (1 << -1 on x86)
+  while (mask > 0) {
+    const int partner = nb_partner(r, mask, P);
+    if ((unsigned)inv & recvmask) { b.send(partner, res, ri[step], rc[step]); b.end(); break; }
+    b.recv(partner, res, si[step], sc[step]); b.end();
+    mask >>= 1; inv <<= 1; step--;
+  }
+}
+
+}  // namespace
+
+Plan make_plan(const PlanArgs &a) {
+  Builder b(a.rank);
+  if (a.P < 1 || a.rank < 0 || a.rank >= a.P || a.esz == 0) { b.fail(BINE_ERR_ARG); return b.p; }
+  const bool rs = a.algo >= BINE_RS_RECURSIVEHALVING && a.algo <= BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN;
+  if (rs && (int)a.rcounts.size() != a.P) { b.fail(BINE_ERR_ARG); return b.p; }
+  if (!rs && a.count == 0) return b.p;  // nothing to move
+  switch (a.algo) {
+    case BINE_AR_RECURSIVEDOUBLING: ar_recursivedoubling(b, a); break;
+    case BINE_AR_RING: ar_ring(b, a); break;
+    case BINE_AR_RABENSEIFNER: ar_rabenseifner(b, a); break;
+    case BINE_AR_BINE_LAT: ar_bine_lat(b, a); break;
+    case BINE_AR_BINE_BDW_STATIC: ar_bine_bdw_static(b, a); break;
+    case BINE_AR_BINE_BDW_REMAP: ar_bine_remap(b, a, false); break;
+    case BINE_AR_BINE_BDW_REMAP_SEGMENTED: ar_bine_remap(b, a, true); break;
+    case BINE_AR_BINE_BLOCK_BY_BLOCK_ANY_EVEN: ar_bine_bbb_any_even(b, a); break;
+    case BINE_RS_RECURSIVEHALVING: rs_recursivehalving(b, a); break;
+    case BINE_RS_RECURSIVE_DISTANCE_DOUBLING: rs_recursive_distance_doubling(b, a); break;
+    case BINE_RS_RING: rs_ring(b, a); break;
+    case BINE_RS_BUTTERFLY: rs_butterfly(b, a); break;
+    case BINE_RS_BINE_STATIC: rs_bine_static(b, a); break;
+    case BINE_RS_BINE_SEND_REMAP: rs_bine_remap(b, a, false); break;
+    case BINE_RS_BINE_PERMUTE_REMAP: rs_bine_remap(b, a, true); break;
+    case BINE_RS_BINE_BLOCK_BY_BLOCK: rs_bine_bbb(b, a); break;
+    case BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN: rs_bine_bbb_any_even(b, a); break;
+    case BINE_RD_BINE_LAT: rd_bine_lat(b, a); break;
+    case BINE_RD_BINE_BDW: rd_bine_bdw(b, a); break;
+    default: b.fail(BINE_ERR_UNSUPPORTED); break;
+  }
+  if (!b.pend_send.empty() || !b.pend_recv.empty()) b.end();
+  return b.p;
+}
+
+}  // namespace bine

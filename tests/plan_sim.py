@@ -1,0 +1,139 @@
+"""Host simulator of the product's per-rank plans (test infrastructure).
+
+Executes the primitive lists that libbine_amd.so's planner emits for ALL ranks
+of a communicator, with RCCL's rendezvous semantics: the sends and receives of
+one exchange group are posted together, a transfer happens when the head send
+and the head receive of a (src, dst) pair are both posted, the group completes
+when all its transfers did, and a rank cannot post its next group before the
+current one completed.  A receive whose matching send carries a different
+element count is an error (RCCL needs equal counts).  No progress while some
+rank is unfinished = deadlock.  The element arithmetic of REDUCE / REDUCE3 is
+MPICH's (oracle.reduce_local), so results are comparable bit-for-bit with the
+oracle's restatement of the reference.
+"""
+from __future__ import annotations
+
+import collections
+
+import numpy as np
+
+import pico_amd
+from oracle import oracle as O
+
+SB, RB, T0, T1, T2 = range(5)
+
+
+class PlanError(AssertionError):
+    pass
+
+
+def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_place=False,
+        rbufs=None):
+    P = len(sbufs)
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    count = sbufs[0].size
+    plans, bufs = [], []
+    for r in range(P):
+        prims, tmp = pico_amd.plan(coll, algo, P, r, count=count, rcounts=rcounts, root=root, esz=esz,
+                                   segsize=segsize, in_place=in_place)
+        plans.append(prims)
+        if rbufs is not None:
+            rb = rbufs[r]
+        elif coll == "reduce_scatter":
+            rb = np.zeros(max(rcounts[r], 1), O.NP_DTYPES[dtype])
+        else:
+            rb = np.zeros(max(count, 1), O.NP_DTYPES[dtype])
+        sb = sbufs[r].copy()
+        if in_place:
+            if coll == "reduce_scatter":
+                rb = sbufs[r].copy()
+            else:
+                rb = sbufs[r].copy()
+            sb = rb
+        tbufs = [np.zeros(max(int(t), 1) + 16, O.NP_DTYPES[dtype]) for t in tmp]
+        bufs.append([sb, rb] + tbufs)
+    pc = [0] * P
+    sendq = collections.defaultdict(collections.deque)  # (src, dst) -> [(rank, idx)]
+    recvq = collections.defaultdict(collections.deque)
+    posted = [None] * P      # (start, end) of the currently posted group
+    pending = [0] * P        # untransferred ops in the posted group
+
+    def view(r, buf, off, n):
+        b = bufs[r][buf]
+        if off + n > b.size:
+            raise PlanError(f"rank {r}: buffer {buf} overflow ({off}+{n} > {b.size})")
+        return b[off:off + n]
+
+    def local(r, p):
+        n = p["count"]
+        if p["type"] == "COPY":
+            view(r, p["dst_buf"], p["dst_off"], n)[:] = view(r, p["src_buf"], p["src_off"], n).copy()
+        elif p["type"] == "REDUCE":
+            io = view(r, p["dst_buf"], p["dst_off"], n)
+            tmp = io.copy()
+            O.reduce_local(np.ascontiguousarray(view(r, p["src_buf"], p["src_off"], n)), tmp, dtype, op)
+            io[:] = tmp
+        elif p["type"] == "REDUCE3":
+            b = view(r, p["aux_buf"], p["aux_off"], n).copy()
+            O.reduce_local(np.ascontiguousarray(view(r, p["src_buf"], p["src_off"], n)), b, dtype, op)
+            view(r, p["dst_buf"], p["dst_off"], n)[:] = b
+
+    def try_transfer(key):
+        moved = False
+        while sendq[key] and recvq[key]:
+            (sr, si), (rr, ri) = sendq[key][0], recvq[key][0]
+            s, rv = plans[sr][si], plans[rr][ri]
+            if s["count"] != rv["count"]:
+                raise PlanError(f"{key}: send {s['count']} vs recv {rv['count']}")
+            # the executor chunks PIPELINE exchanges on both sides: the flag must
+            # be symmetric or the chunk sizes of the two ends would not match
+            if (s["flags"] & 1) != (rv["flags"] & 1):
+                raise PlanError(f"{key}: pipelined on one side only")
+            data = view(sr, s["src_buf"], s["src_off"], s["count"]).copy()
+            view(rr, rv["dst_buf"], rv["dst_off"], rv["count"])[:] = data
+            sendq[key].popleft(); recvq[key].popleft()
+            pending[sr] -= 1; pending[rr] -= 1
+            moved = True
+        return moved
+
+    while True:
+        progress = False
+        for r in range(P):
+            while pc[r] < len(plans[r]) and posted[r] is None:
+                p = plans[r][pc[r]]
+                if p["type"] in ("SEND", "RECV"):
+                    j = pc[r]
+                    while j < len(plans[r]) and plans[r][j]["type"] in ("SEND", "RECV") and \
+                            plans[r][j]["group"] == p["group"]:
+                        x = plans[r][j]
+                        if x["type"] == "SEND":
+                            sendq[(r, x["peer"])].append((r, j))
+                        else:
+                            recvq[(x["peer"], r)].append((r, j))
+                        j += 1
+                    posted[r] = (pc[r], j)
+                    pending[r] = j - pc[r]
+                    progress = True
+                else:
+                    local(r, p)
+                    pc[r] += 1
+                    progress = True
+        for key in list(sendq.keys()):
+            progress |= try_transfer(key)
+        for r in range(P):
+            if posted[r] is not None and pending[r] == 0:
+                pc[r] = posted[r][1]
+                posted[r] = None
+                progress = True
+        if all(pc[r] >= len(plans[r]) and posted[r] is None for r in range(P)):
+            break
+        if not progress:
+            raise PlanError(f"deadlock: pcs={pc}")
+    outs = []
+    for r in range(P):
+        rb = bufs[r][RB]
+        if coll == "reduce_scatter":
+            outs.append(rb[:rcounts[r]])
+        else:
+            outs.append(rb[:count])
+    return outs

@@ -1,0 +1,56 @@
+"""The C ABI: libraries load and export every symbol include/*.h declares
+(host-only: no compute call, no GPU needed)."""
+import os
+import re
+
+import pico_amd
+from pico_amd import _lib
+
+INC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+
+
+def _declared(header):
+    text = open(os.path.join(INC, header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(\w+)\s*\(", text, flags=re.M)) - {"defined"}
+
+
+def test_core_library_exports_header():
+    pico_amd.lib()
+    names = _declared("bine_amd.h")
+    assert "bine_allreduce" in names and "bine_reduce_local" in names
+    missing = names - _lib.exported_symbols(_lib.CORE)
+    assert not missing, missing
+
+
+def test_dropin_exports_every_libbine_prototype():
+    """pico_core's selectors reference every prototype of libbine.h
+    (pico_core_utils.c:103-249): the drop-in must export all 41 + the segsize global."""
+    names = _declared("libbine_amd.h")
+    assert len(names) == 41, len(names)
+    syms = _lib.exported_symbols(_lib.SHIM)
+    assert not names - syms, names - syms
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.SHIM], capture_output=True, text=True).stdout
+    assert re.search(r" [BD] bine_allreduce_segsize$", out, flags=re.M)
+
+
+def test_algorithm_names_and_pico_core_selectors():
+    L = pico_amd.lib()
+    for coll, algos in pico_amd.ALGOS.items():
+        for name, code in algos.items():
+            assert L.bine_algo_from_name(coll.encode(), name.encode()) == code
+            assert L.bine_algo_from_name(coll.encode(), f"{coll}_{name}".encode()) == code
+    # pico_core's own selector strings (pico_core_utils.c:104-111, 206-207, 222-230)
+    sel = {("allreduce", "bine_bdw_remap_over"): 5, ("allreduce", "recursive_doubling_over"): 0,
+           ("allreduce", "bine_block_by_block_any_even"): 7, ("reduce", "bine_bdw_over"): 33,
+           ("reduce_scatter", "bine_permute_remap_over"): 22, ("reduce_scatter", "recursive_halving_over"): 16}
+    for (coll, s), code in sel.items():
+        assert L.bine_algo_from_name(coll.encode(), s.encode()) == code
+    assert L.bine_algo_from_name(b"allreduce", b"nope") == -1
+
+
+def test_dtype_sizes():
+    L = pico_amd.lib()
+    for name, code in pico_amd.DTYPES.items():
+        assert L.bine_dtype_size(code) == _lib.DTYPE_SIZE[name]

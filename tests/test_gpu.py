@@ -1,0 +1,278 @@
+"""GPU parity tests: the HIP path (libbine_amd.so through its C ABI) against the
+reference's own golden vectors and the oracle.  Bit-exact for every dtype: the
+schedule fixes the per-element association order, and the kernels reproduce
+MPICH's IEEE arithmetic (fp32/fp64 tolerance used: 0 ulp).
+
+Multi-rank cases run on ONE GPU through the loopback transport (virtual ranks,
+in-process peer copies); the RCCL transport is exercised at P = 1 here and at
+P = 2..8 by the driver's multi-GPU bench.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import golden_util as G
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import pico_amd  # noqa: E402
+
+ALL_DT = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64", "float", "double"]
+STATUS_OF_MPI = {12: 1, 51: 2}   # MPI_ERR_ARG -> BINE_ERR_ARG, MPI_ERR_SIZE -> BINE_ERR_SIZE
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+def to_dev(a: np.ndarray, pad: int = 0):
+    raw = np.ascontiguousarray(a).view(np.uint8)
+    t = torch.zeros(raw.size + pad, dtype=torch.uint8, device="cuda:0")
+    if raw.size:
+        t[: raw.size] = torch.from_numpy(raw.copy()).to("cuda:0")
+    return t
+
+
+def from_dev(t, dtype: str, n: int, off_bytes: int = 0) -> np.ndarray:
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    raw = t[off_bytes: off_bytes + n * esz].cpu().numpy()
+    return raw.view(O.NP_DTYPES[dtype]).copy()
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ---- the arithmetic boundary -------------------------------------------------------
+
+@pytest.mark.parametrize("dtype", ALL_DT)
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min"])
+def test_reduce_local_bit_exact(dev, dtype, op):
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for n in (1, 3, 17, 1000, 100003):
+        for shift_a, shift_b in ((0, 0), (1, 1), (1, 0), (0, 3)):
+            a = O.fill(dtype, n, 11 + n)
+            b = O.fill(dtype, n, 97 + n)
+            ta = to_dev(np.concatenate([np.zeros(shift_a, a.dtype), a]))
+            tb = to_dev(np.concatenate([np.zeros(shift_b, b.dtype), b]))
+            pico_amd.reduce_local(ta.data_ptr() + shift_a * esz, tb.data_ptr() + shift_b * esz, n, dtype, op)
+            torch.cuda.synchronize()
+            exp = b.copy()
+            O.reduce_local(a, exp, dtype, op)
+            got = from_dev(tb, dtype, n, shift_b * esz)
+            assert got.tobytes() == exp.tobytes(), (dtype, op, n, shift_a, shift_b)
+
+
+@pytest.mark.parametrize("dtype", ["float", "double"])
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min"])
+def test_reduce_local_special_values(dev, dtype, op):
+    npdt = O.NP_DTYPES[dtype]
+    tiny = np.finfo(npdt).tiny
+    vals = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, tiny / 4, -tiny / 8, 3e38 if dtype == "float" else 1e300],
+                    dtype=npdt)
+    a = np.repeat(vals, vals.size)
+    b = np.tile(vals, vals.size)
+    ta, tb = to_dev(a), to_dev(b)
+    pico_amd.reduce_local(ta, tb.data_ptr(), a.size, dtype, op)
+    torch.cuda.synchronize()
+    exp = b.copy()
+    O.reduce_local(a, exp, dtype, op)
+    assert from_dev(tb, dtype, a.size).tobytes() == exp.tobytes()   # NaN payloads, signed zeros, denormals
+
+
+def test_reduce3_out_of_place(dev):
+    a, b = O.fill("float", 5003, 1), O.fill("float", 5003, 2)
+    ta, tb, to = to_dev(a), to_dev(b), to_dev(np.zeros_like(a))
+    pico_amd.reduce3(ta, tb, to, a.size, "float", "sum")
+    torch.cuda.synchronize()
+    exp = b.copy()
+    O.reduce_local(a, exp, "float")
+    assert from_dev(to, "float", a.size).tobytes() == exp.tobytes()
+    assert from_dev(tb, "float", a.size).tobytes() == b.tobytes()
+
+
+@pytest.mark.parametrize("dtype", ALL_DT)
+def test_fill_pico_matches_host_generator(dev, dtype):
+    for n, seed in ((1, 1234), (1000, 1235), (70001, 99)):
+        esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+        t = torch.zeros(n * esz, dtype=torch.uint8, device=dev)
+        pico_amd.fill_pico(t, n, dtype, seed)
+        torch.cuda.synchronize()
+        assert from_dev(t, dtype, n).tobytes() == O.fill(dtype, n, seed).tobytes(), (dtype, n)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def host_checksum(a: np.ndarray) -> int:
+    bits = a.view({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize]).astype(np.uint64)
+    idx = np.arange(a.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        return int(_mix64(bits + idx).sum(dtype=np.uint64))
+
+
+def test_checksum_matches_host(dev):
+    for dtype in ("float", "int64", "int8"):
+        a = O.fill(dtype, 123457, 5)
+        assert pico_amd.checksum(to_dev(a), a.size, dtype) == host_checksum(a)
+
+
+# ---- collectives vs the reference's golden vectors (loopback ranks) ----------------
+
+_COMMS = {}
+
+
+def comms(P):
+    if P not in _COMMS:
+        _COMMS[P] = pico_amd.Comm.loopback(P, 0)
+    return _COMMS[P]
+
+
+def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, root=0, in_place=False):
+    P = len(sbufs)
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    n = sbufs[0].size
+    ds = [to_dev(x, pad=64) for x in sbufs]
+    if coll == "allreduce":
+        dr = ds if in_place else [torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0") for _ in range(P)]
+        torch.cuda.synchronize()
+        rc, st = pico_amd.loopback_allreduce(comms(P), algo, [pico_amd.IN_PLACE] * P if in_place else ds, dr, n,
+                                             dtype, op, segsize)
+        outs = [from_dev(d, dtype, n) for d in dr]
+    elif coll == "reduce_scatter":
+        dr = ds if in_place else [torch.zeros(max(c, 1) * esz + 64, dtype=torch.uint8, device="cuda:0") for c in rcounts]
+        torch.cuda.synchronize()
+        rc, st = pico_amd.loopback_reduce_scatter(comms(P), algo, [pico_amd.IN_PLACE] * P if in_place else ds, dr,
+                                                  rcounts, dtype, op)
+        outs = [from_dev(d, dtype, c) for d, c in zip(dr, rcounts)]
+    else:
+        dr = [torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0") if r == root else None for r in range(P)]
+        torch.cuda.synchronize()
+        rc, st = pico_amd.loopback_reduce(comms(P), algo, ds, dr, n, dtype, op, root)
+        outs = [from_dev(dr[root], dtype, n)] + [np.zeros(0)] * (P - 1)
+    return outs, st
+
+
+def _golden_groups():
+    g = {}
+    for c in G.cases():
+        if c["coll"] == "fill" or c["N"] > 300000:
+            continue
+        g.setdefault((c["coll"], c["algo"]), []).append(c)
+    return sorted(g.items())
+
+
+@pytest.mark.parametrize("key,cs", _golden_groups(), ids=lambda x: ".".join(x) if isinstance(x, tuple) else "")
+def test_collectives_match_reference_goldens(dev, key, cs):
+    coll, algo = key
+    bad = []
+    for c in cs:
+        P, N, dt = c["P"], c["N"], c["dtype"]
+        rk = G.rcounts(c) if coll == "reduce_scatter" else None
+        sb = O.inputs(dt, sum(rk) if rk else N, P, c["seed_base"])
+        outs, st = run_loopback(coll, algo, sb, dt, c["op"], rk, c["segsize"])
+        if c["status"] != "ok" or any(c["rets"]):
+            # the reference errors (rets), asserts or hangs (no_output): the product
+            # returns the mapped status, or -- where the reference crashed on its own
+            # heap overflow (static, N=333) -- the correct result
+            if c["status"] == "ok":
+                exp_st = [STATUS_OF_MPI[x] for x in c["rets"]]
+                if st != exp_st:
+                    bad.append((c["id"], "status", st, exp_st))
+            elif any(st):
+                if not all(x == 1 for x in st):
+                    bad.append((c["id"], "status", st))
+            else:
+                want, _ = O.allreduce(algo, sb, dt, c["op"], c["segsize"], ref_bugs=False)
+                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                    bad.append((c["id"], "vs-oracle"))
+            continue
+        if any(st):
+            bad.append((c["id"], "status", st))
+            continue
+        miss = G.check_rank_outputs(c, outs)
+        if miss:
+            # documented deviations: the segmented tail bug and the P=1 no-ops
+            if algo == "bine_bdw_remap_segmented":
+                want, _ = O.allreduce(algo, sb, dt, c["op"], c["segsize"], ref_bugs=False)
+            elif P == 1 and algo in ("butterfly", "bine_block_by_block"):
+                want = [sb[0][: rk[0]]]
+            else:
+                want = None
+            if want is None or any(sha(outs[r]) != sha(want[r]) for r in miss):
+                bad.append((c["id"], "ranks", miss))
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("algo", ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented"])
+def test_large_allreduce_digest_matches_reference(dev, algo):
+    """N = 1,000,003 fp32, P = 8 against the reference's digests (segmented: the
+    reference's own output carries its tail bug -> compared with remap's)."""
+    seg = 65536 if algo == "bine_bdw_remap_segmented" else 0
+    gal = "bine_bdw_remap" if algo == "bine_bdw_remap_segmented" else algo
+    c = G.select(coll="allreduce", algo=gal, P=8, N=1000003, dtype="float", segsize=0)[0]
+    sb = O.inputs("float", 1000003, 8)
+    outs, st = run_loopback("allreduce", algo, sb, "float", segsize=seg)
+    assert not any(st)
+    assert G.check_rank_outputs(c, outs) == []
+
+
+@pytest.mark.parametrize("chunk", [64, 4096, 1 << 20])
+def test_pipelined_chunks_bit_exact(dev, chunk):
+    """The executor's chunked exchange/reduce overlap must not change a bit."""
+    P, n = 8, 300007
+    sb = O.inputs("float", n, P)
+    want, _ = O.allreduce("bine_bdw_remap", sb, "float")
+    outs, st = run_loopback("allreduce", "bine_bdw_remap", sb, "float", segsize=chunk)
+    assert not any(st)
+    assert all(sha(o) == sha(w) for o, w in zip(outs, want))
+
+
+@pytest.mark.parametrize("algo", list(pico_amd.ALGOS["allreduce"]))
+def test_in_place_allreduce(dev, algo):
+    P = 4
+    sb = O.inputs("double", 1001, P)
+    want, _ = O.allreduce(algo, sb, "double", segsize=64)
+    outs, st = run_loopback("allreduce", algo, sb, "double", segsize=64, in_place=True)
+    assert not any(st)
+    assert all(sha(o) == sha(w) for o, w in zip(outs, want))
+
+
+def test_large_reduce_scatter_checksum(dev):
+    """C4 shape scaled to one GPU: permute_remap RS, P = 8, 4 Mi elements per
+    rank-block; checksum of each rank's block against the oracle's."""
+    P, per = 8, 1 << 19
+    rc = [per] * P
+    sb = O.inputs("float", per * P, P)
+    want, _ = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
+    outs, st = run_loopback("reduce_scatter", "bine_permute_remap", sb, "float", rcounts=rc)
+    assert not any(st)
+    assert [host_checksum(o) for o in outs] == [host_checksum(w) for w in want]
+
+
+# ---- RCCL transport (single rank on this box) --------------------------------------
+
+def test_rccl_single_rank(dev):
+    uid = pico_amd.Comm.unique_id()
+    c = pico_amd.Comm.rccl(0, 1, uid, 0)
+    try:
+        a = O.fill("float", 4097, 3)
+        ta = to_dev(a)
+        tr = torch.zeros_like(ta)
+        pico_amd.allreduce_bine_bdw_remap(ta, tr, a.size, "float", "sum", c)
+        c.synchronize()
+        torch.cuda.synchronize()
+        assert from_dev(tr, "float", a.size).tobytes() == a.tobytes()
+        with pytest.raises(pico_amd.BineError) as ei:
+            pico_amd.allreduce_bine_bdw_static(ta, tr, a.size, "float", "sum", c)   # reference: MPI_ERR_ARG at P=1
+        assert ei.value.status == 1
+    finally:
+        c.destroy()

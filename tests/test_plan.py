@@ -1,0 +1,140 @@
+"""The product's schedule planner (libbine_amd.so, host only) against the oracle.
+
+Every plan of every rank is executed by tests/plan_sim.py under RCCL rendezvous
+semantics (exact message sizes, no buffering, deadlock detection) and the
+outputs must equal the oracle's restatement of the reference bit-for-bit --
+including fp32/fp64, whose association order is fixed by the schedule.
+"""
+import numpy as np
+import pytest
+
+import pico_amd
+from oracle import oracle as O
+import plan_sim
+
+AR = list(pico_amd.ALGOS["allreduce"])
+RS = list(pico_amd.ALGOS["reduce_scatter"])
+RD = list(pico_amd.ALGOS["reduce"])
+
+# where the product deliberately differs from the reference ("Deviations")
+POW2_ONLY_AR = {"bine_bdw_remap", "bine_bdw_static"}
+POW2_ONLY_RS = {"bine_static", "bine_send_remap", "bine_permute_remap", "bine_block_by_block",
+                "recursive_distance_doubling"}
+
+
+def _ok_ar(algo, P):
+    if algo in POW2_ONLY_AR and P & (P - 1):
+        return False
+    if algo == "bine_bdw_static" and P == 1:
+        return False
+    if algo == "bine_block_by_block_any_even" and P % 2:
+        return False
+    return True
+
+
+@pytest.mark.parametrize("algo", AR)
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 6, 8, 16])
+@pytest.mark.parametrize("dtype", ["float", "int64"])
+def test_allreduce_plans_match_oracle(algo, P, dtype):
+    if not _ok_ar(algo, P):
+        with pytest.raises(pico_amd.BineError):
+            pico_amd.plan("allreduce", algo, P, 0, count=13)
+        return
+    for n in (1, 5, 13, 64, 1000):
+        sb = O.inputs(dtype, n, P)
+        seg = 64 if algo == "bine_bdw_remap_segmented" else 0
+        exp, rets = O.allreduce(algo, sb, dtype, segsize=seg, ref_bugs=False)
+        assert all(x == 0 for x in rets)
+        got = plan_sim.run("allreduce", algo, sb, dtype, segsize=seg)
+        for r in range(P):
+            assert np.array_equal(got[r], exp[r]), (algo, P, n, r)
+
+
+@pytest.mark.parametrize("algo", AR)
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_allreduce_in_place_equals_out_of_place(algo, P):
+    if not _ok_ar(algo, P):
+        return
+    sb = O.inputs("float", 333, P)
+    exp, _ = O.allreduce(algo, sb, "float", segsize=64, ref_bugs=False)
+    got = plan_sim.run("allreduce", algo, sb, "float", segsize=64, in_place=True)
+    for r in range(P):
+        assert np.array_equal(got[r], exp[r]), (algo, P, r)
+
+
+def _ok_rs(algo, P):
+    if algo in POW2_ONLY_RS and P & (P - 1):
+        return False
+    if algo == "bine_static" and P == 1:
+        return False
+    if algo == "bine_block_by_block_any_even" and P % 2 and P > 1:
+        return False
+    return True
+
+
+@pytest.mark.parametrize("algo", RS)
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 6, 8, 16])
+@pytest.mark.parametrize("kind", ["even", "ragged"])
+def test_reduce_scatter_plans_match_oracle(algo, P, kind):
+    if not _ok_rs(algo, P):
+        with pytest.raises(pico_amd.BineError):
+            pico_amd.plan("reduce_scatter", algo, P, 0, rcounts=[4] * P)
+        return
+    if kind == "ragged" and algo == "bine_permute_remap":
+        return  # the reference copies block i into block remap(i)'s slot: needs equal blocks
+    for per in (1, 3, 50):
+        rc = O.rs_rcounts(per * P, P, kind)
+        sb = O.inputs("float", sum(rc), P)
+        got = plan_sim.run("reduce_scatter", algo, sb, "float", rcounts=rc)
+        if P == 1 and algo in ("butterfly", "bine_block_by_block"):
+            # the reference leaves rbuf untouched at P = 1; the product copies
+            assert np.array_equal(got[0], sb[0][: rc[0]])
+            continue
+        exp, rets = O.reduce_scatter(algo, sb, rc, "float")
+        assert all(x == 0 for x in rets)
+        for r in range(P):
+            assert np.array_equal(got[r], exp[r]), (algo, P, per, r)
+
+
+@pytest.mark.parametrize("algo", RD)
+@pytest.mark.parametrize("P", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("dtype", ["float", "int32"])
+def test_reduce_plans_match_oracle(algo, P, dtype):
+    for n in (1, 7, 13, 100):
+        sb = O.inputs(dtype, n, P)
+        exp, rets = O.reduce(algo, sb, dtype)
+        got = plan_sim.run("reduce", algo, sb, dtype)
+        assert np.array_equal(got[0], exp), (algo, P, n)
+
+
+@pytest.mark.parametrize("op", ["max", "min", "prod"])
+def test_ops_through_plans(op):
+    for algo in ("bine_bdw_remap", "ring", "bine_lat"):
+        sb = O.inputs("double", 97, 8)
+        exp, _ = O.allreduce(algo, sb, "double", op=op)
+        got = plan_sim.run("allreduce", algo, sb, "double", op=op)
+        assert all(np.array_equal(g, e) for g, e in zip(got, exp))
+
+
+def test_error_statuses_follow_reference():
+    # libbine_allreduce.c:835-838 / :709-712 -> MPI_ERR_ARG; libbine_reduce_scatter.c:797-800 and
+    # libbine_reduce.c:29,98 -> MPI_ERR_SIZE
+    cases = [("allreduce", "bine_bdw_remap", 6, 1), ("allreduce", "bine_bdw_static", 1, 1),
+             ("reduce_scatter", "bine_static", 1, 2), ("reduce_scatter", "bine_static", 6, 2),
+             ("reduce", "bine_lat", 6, 2), ("reduce", "bine_bdw", 6, 2)]
+    for coll, algo, P, status in cases:
+        with pytest.raises(pico_amd.BineError) as ei:
+            pico_amd.plan(coll, algo, P, 0, count=16, rcounts=[4] * P)
+        assert ei.value.status == status, (coll, algo, P)
+
+
+def test_remap_plan_shape():
+    """allreduce_bine_bdw_remap at P=8: 3 reduce-scatter exchanges + 3 allgather
+    exchanges per rank, peers pi(r, s), first step copy-free."""
+    prims, tmp = pico_amd.plan("allreduce", "bine_bdw_remap", 8, 0, count=1 << 20)
+    sends = [p for p in prims if p["type"] == "SEND"]
+    assert [p["peer"] for p in sends] == [1, 7, 3, 3, 7, 1]
+    assert prims[2]["type"] == "REDUCE3"                      # rbuf = sbuf + recv (no memcpy)
+    assert [p["count"] for p in sends[:3]] == [1 << 19, 1 << 18, 1 << 17]
+    assert tmp[0] == 1 << 19
+    assert all(p["flags"] == 1 for p in prims[:9])             # RS steps are pipelined
