@@ -67,8 +67,16 @@ constexpr int kBlock = 256;
 using u32x4 = u32x4_t;  // one global_load/store_dwordx4 per lane
 
 // Elements [0, head) and [head + 16/sizeof(T) * nvec, n) are done scalar by
-// block 0; the 16-B aligned middle is vectorized.
-template <typename T, int OP, int U, bool NT>
+// block 0; the 16-B aligned middle is vectorized.  NT is a cache-policy mask:
+// bit 0 = non-temporal loads of `a` (the received operand, read exactly once),
+// bit 1 = of `b`, bit 2 = non-temporal stores of `out`.
+template <int NTBIT>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p) {
+  if constexpr (NTBIT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <typename T, int OP, int U, int NT>
 __global__ __launch_bounds__(kBlock) void k_reduce(const T *__restrict__ a, const T *b, T *out,
                                                    size_t head, size_t nvec, size_t n) {
   constexpr size_t V = 16 / sizeof(T);
@@ -87,12 +95,15 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const T *__restrict__ a, cons
     u32x4 x[U], y[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      if constexpr (NT) x[u] = __builtin_nontemporal_load(va + base + (size_t)u * kBlock);
-      else x[u] = va[base + (size_t)u * kBlock];
-      y[u] = vb[base + (size_t)u * kBlock];
+      x[u] = ld<NT & 1>(va + base + (size_t)u * kBlock);
+      y[u] = ld<NT & 2>(vb + base + (size_t)u * kBlock);
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) vo[base + (size_t)u * kBlock] = apply16<T, OP>(y[u], x[u]);
+    for (int u = 0; u < U; u++) {
+      const u32x4 r = apply16<T, OP>(y[u], x[u]);
+      if constexpr (NT & 4) __builtin_nontemporal_store(r, vo + base + (size_t)u * kBlock);
+      else vo[base + (size_t)u * kBlock] = r;
+    }
   }
   // last partial tile
 #pragma unroll
@@ -104,7 +115,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const T *__restrict__ a, cons
 
 // dispatch -----------------------------------------------------------------
 
-static int g_unroll = 0, g_maxblocks = 0, g_nt = -1;
+// Defaults measured on MI355X (profiles/r1_explore.txt, C2 fp32 SUM 64 MiB):
+// 4 vectors per lane, one tile per workgroup (no grid cap below 16384
+// workgroups), non-temporal loads of the once-read operand.
+constexpr int kDefaultUnroll = 4, kDefaultMaxBlocks = 16384, kDefaultNT = 1;
+static int g_unroll = 0, g_maxblocks = 0, g_nt = kDefaultNT;
 
 static void read_tuning() {
   if (g_unroll) return;
@@ -114,10 +129,10 @@ static void read_tuning() {
   int uu = u ? atoi(u) : 4;
   g_unroll = (uu == 1 || uu == 2 || uu == 4 || uu == 8) ? uu : 4;
   g_maxblocks = m ? atoi(m) : 0;
-  g_nt = t ? atoi(t) : 0;
+  g_nt = t ? atoi(t) : kDefaultNT;
 }
 
-template <typename T, int OP, int U, bool NT>
+template <typename T, int OP, int U, int NT>
 static hipError_t run_reduce(const T *a, const T *b, T *out, size_t n, hipStream_t st) {
   constexpr size_t V = 16 / sizeof(T);
   const uintptr_t ao = (uintptr_t)a, bo = (uintptr_t)b, oo = (uintptr_t)out;
@@ -134,7 +149,7 @@ static hipError_t run_reduce(const T *a, const T *b, T *out, size_t n, hipStream
   if (nvec == 0) blocks = 1;
   else {
     const size_t tiles = (nvec + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    const int maxb = g_maxblocks > 0 ? g_maxblocks : 2048;
+    const int maxb = g_maxblocks > 0 ? g_maxblocks : kDefaultMaxBlocks;
     blocks = (int)(tiles < (size_t)maxb ? tiles : (size_t)maxb);
   }
   hipLaunchKernelGGL((k_reduce<T, OP, U, NT>), dim3(blocks), dim3(kBlock), 0, st, a, b, out, head, nvec, n);
@@ -161,23 +176,26 @@ static hipError_t reduce_t(const void *a, const void *b, void *out, size_t n, hi
     return hipGetLastError();
   }
   if constexpr (std::is_same_v<T, float> && OP == BINE_SUM) {
-    // tuning variants (BINE_REDUCE_UNROLL / _NT) for the headline dtype
-    if (g_nt == 1) {
-      switch (g_unroll) {
-        case 1: return run_reduce<T, OP, 1, true>(pa, pb, po, n, st);
-        case 2: return run_reduce<T, OP, 2, true>(pa, pb, po, n, st);
-        case 8: return run_reduce<T, OP, 8, true>(pa, pb, po, n, st);
-        default: return run_reduce<T, OP, 4, true>(pa, pb, po, n, st);
-      }
+    // tuning variants (bine_set_reduce_tuning / BINE_REDUCE_*) for the headline dtype
+#define NTSW(U)                                                               \
+    switch (g_nt) {                                                           \
+      case 0: return run_reduce<T, OP, U, 0>(pa, pb, po, n, st);              \
+      case 2: return run_reduce<T, OP, U, 2>(pa, pb, po, n, st);              \
+      case 3: return run_reduce<T, OP, U, 3>(pa, pb, po, n, st);              \
+      case 4: return run_reduce<T, OP, U, 4>(pa, pb, po, n, st);              \
+      case 5: return run_reduce<T, OP, U, 5>(pa, pb, po, n, st);              \
+      case 7: return run_reduce<T, OP, U, 7>(pa, pb, po, n, st);              \
+      default: return run_reduce<T, OP, U, 1>(pa, pb, po, n, st);             \
     }
     switch (g_unroll) {
-      case 1: return run_reduce<T, OP, 1, false>(pa, pb, po, n, st);
-      case 2: return run_reduce<T, OP, 2, false>(pa, pb, po, n, st);
-      case 8: return run_reduce<T, OP, 8, false>(pa, pb, po, n, st);
-      default: break;
+      case 1: NTSW(1)
+      case 2: NTSW(2)
+      case 8: NTSW(8)
+      default: NTSW(4)
     }
+#undef NTSW
   }
-  return run_reduce<T, OP, 4, false>(pa, pb, po, n, st);
+  return run_reduce<T, OP, kDefaultUnroll, kDefaultNT>(pa, pb, po, n, st);
 }
 
 template <typename T>
@@ -353,7 +371,7 @@ int launch_checksum(const void *buf, size_t n, int dtype, uint64_t *host_out, vo
 }  // namespace bine
 
 extern "C" int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal) {
-  bine::g_unroll = (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) ? unroll : 4;
+  bine::g_unroll = (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) ? unroll : bine::kDefaultUnroll;
   bine::g_maxblocks = maxblocks;
   bine::g_nt = nontemporal;
   return BINE_SUCCESS;

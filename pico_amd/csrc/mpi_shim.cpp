@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <set>
 #include <vector>
 
 #include "bine_amd.h"
@@ -34,7 +35,7 @@ struct Entry {
 
 int g_keyval = MPI_KEYVAL_INVALID;
 int g_self_keyval = MPI_KEYVAL_INVALID;
-std::vector<Entry *> g_entries;
+std::set<Entry *> g_entries;  // live entries; an attribute may outlive its entry
 
 void release(Entry *e) {
   if (!e) return;
@@ -49,9 +50,7 @@ void release(Entry *e) {
 
 int comm_delete(MPI_Comm, int, void *val, void *) {
   Entry *e = (Entry *)val;
-  for (auto &x : g_entries)
-    if (x == e) x = nullptr;
-  release(e);
+  if (g_entries.erase(e)) release(e);  // already released if MPI_COMM_SELF went first
   return MPI_SUCCESS;
 }
 
@@ -106,7 +105,7 @@ int get_entry(MPI_Comm comm, Entry **out) {
   void *val = nullptr;
   int flag = 0;
   MPI_Comm_get_attr(comm, g_keyval, &val, &flag);
-  if (flag && val) { *out = (Entry *)val; return MPI_SUCCESS; }
+  if (flag && val && g_entries.count((Entry *)val)) { *out = (Entry *)val; return MPI_SUCCESS; }
   auto *e = new Entry;
   MPI_Comm_rank(comm, &e->rank);
   MPI_Comm_size(comm, &e->size);
@@ -132,7 +131,7 @@ int get_entry(MPI_Comm comm, Entry **out) {
   st = bine_comm_init_rccl(&e->comm, e->size, e->rank, id, device);
   if (st != BINE_SUCCESS) { delete e; return to_mpi(st); }
   MPI_Comm_set_attr(comm, g_keyval, e);
-  g_entries.push_back(e);
+  g_entries.insert(e);
   *out = e;
   return MPI_SUCCESS;
 }

@@ -1,0 +1,127 @@
+"""Multi-process (world_size 2 and 4, gloo, CPU) execution of the product's
+per-rank plans: every process builds ITS OWN plan with libbine_amd.so's planner
+and executes it with torch.distributed point-to-point (one batch of isend /
+irecv per exchange group = ncclGroupStart/End semantics), the element
+arithmetic done by the oracle's MPI_Reduce_local.  Results must equal the
+oracle's restatement of the reference bit-for-bit on every rank.  This is the
+N > 1 path of the executor with the transport swapped for gloo."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    ("allreduce", "bine_bdw_remap", "float", 1001),
+    ("allreduce", "bine_bdw_static", "float", 999),
+    ("allreduce", "bine_bdw_remap_segmented", "double", 777),
+    ("allreduce", "bine_lat", "int64", 129),
+    ("allreduce", "ring", "float", 1000),
+    ("allreduce", "rabenseifner", "float", 1000),
+    ("allreduce", "recursivedoubling", "int32", 65),
+    ("allreduce", "bine_block_by_block_any_even", "float", 1003),
+    ("reduce_scatter", "bine_permute_remap", "float", 64),
+    ("reduce_scatter", "bine_send_remap", "float", 64),
+    ("reduce_scatter", "bine_static", "double", 64),
+    ("reduce_scatter", "bine_block_by_block", "float", 64),
+    ("reduce_scatter", "bine_block_by_block_any_even", "float", 64),
+    ("reduce_scatter", "ring", "float", 64),
+    ("reduce_scatter", "butterfly", "float", 64),
+    ("reduce_scatter", "recursivehalving", "float", 64),
+    ("reduce_scatter", "recursive_distance_doubling", "float", 64),
+    ("reduce", "bine_bdw", "float", 1000),
+    ("reduce", "bine_lat", "float", 1000),
+]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, P, port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    import torch
+    import torch.distributed as dist
+    import pico_amd
+    from oracle import oracle as O
+    dist.init_process_group("gloo", rank=rank, world_size=P, init_method=f"tcp://127.0.0.1:{port}")
+    bad = []
+    for coll, algo, dtype, n in CASES:
+        npdt = O.NP_DTYPES[dtype]
+        esz = np.dtype(npdt).itemsize
+        rc = [n // P] * P if coll == "reduce_scatter" else None
+        total = sum(rc) if rc else n
+        sb = O.inputs(dtype, total, P)
+        if coll == "allreduce":
+            want = O.allreduce(algo, sb, dtype, segsize=64)[0][rank]
+        elif coll == "reduce_scatter":
+            want = O.reduce_scatter(algo, sb, rc, dtype)[0][rank]
+        else:
+            want = O.reduce(algo, sb, dtype)[0] if rank == 0 else None
+        prims, tmp = pico_amd.plan(coll, algo, P, rank, count=n, rcounts=rc, esz=esz, segsize=64)
+        out_n = rc[rank] if rc else n
+        bufs = [sb[rank].copy(), np.zeros(max(out_n, 1), npdt)] + [np.zeros(int(t) + 1, npdt) for t in tmp]
+
+        def v(b, off, cnt):
+            return bufs[b][off:off + cnt]
+
+        i = 0
+        while i < len(prims):
+            p = prims[i]
+            if p["type"] in ("SEND", "RECV"):
+                reqs, j = [], i
+                while j < len(prims) and prims[j]["type"] in ("SEND", "RECV") and prims[j]["group"] == p["group"]:
+                    x = prims[j]
+                    if x["type"] == "SEND":
+                        t = torch.from_numpy(v(x["src_buf"], x["src_off"], x["count"]).copy().view(np.uint8))
+                        reqs.append(dist.isend(t, x["peer"]))
+                    else:
+                        t = torch.from_numpy(v(x["dst_buf"], x["dst_off"], x["count"]).view(np.uint8))
+                        reqs.append(dist.irecv(t, x["peer"]))
+                    j += 1
+                for r in reqs:
+                    r.wait()
+                i = j
+                continue
+            cnt = p["count"]
+            if p["type"] == "COPY":
+                v(p["dst_buf"], p["dst_off"], cnt)[:] = v(p["src_buf"], p["src_off"], cnt).copy()
+            elif p["type"] == "REDUCE":
+                io = v(p["dst_buf"], p["dst_off"], cnt)
+                tmpio = io.copy()
+                O.reduce_local(np.ascontiguousarray(v(p["src_buf"], p["src_off"], cnt)), tmpio, dtype)
+                io[:] = tmpio
+            else:
+                b = v(p["aux_buf"], p["aux_off"], cnt).copy()
+                O.reduce_local(np.ascontiguousarray(v(p["src_buf"], p["src_off"], cnt)), b, dtype)
+                v(p["dst_buf"], p["dst_off"], cnt)[:] = b
+            i += 1
+        if want is not None and not np.array_equal(bufs[1][:out_n], want):
+            bad.append((coll, algo))
+        dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, bad))
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_plans_over_gloo(P):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, P, port, q)) for r in range(P)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(P)]
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps)
+    bad = [x for _, b in res for x in b]
+    assert not bad, bad

@@ -22,7 +22,7 @@ for k in range(sets):
     pico_amd.fill_pico(ios[k], N, "float", 100 + k)
 torch.cuda.synchronize()
 st = torch.cuda.current_stream()
-variants = [(u, m, nt) for u in (1, 2, 4, 8) for m in (0, 512, 1024, 4096, 8192) for nt in (0, 1)]
+variants = [(u, m, nt) for u in (2, 4, 8) for m in (0, 1024, 2048) for nt in (0, 1, 2, 3, 4, 5, 7)]
 res = {v: [] for v in variants}
 for rnd in range(5):
     for v in variants:
@@ -56,3 +56,24 @@ e1.record(st)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 40
 print(f"copy64MiB ms={ms:.4f} GB/s(2S/t)={2 * N * 4 / (ms * 1e-3) / 1e9:.1f}")
+
+# C3 step windows with the default shape (NT=1): per-launch sizes of the remap
+# reduce-scatter at P=8 (128, 64, 32 MiB)
+pico_amd.set_reduce_tuning(4, 0, 1)
+big_a = torch.empty(1 << 26, dtype=torch.float32, device=dev)
+big_b = torch.empty(1 << 26, dtype=torch.float32, device=dev)
+pico_amd.fill_pico(big_a, 1 << 26, "float", 5)
+pico_amd.fill_pico(big_b, 1 << 26, "float", 6)
+for n in (1 << 25, 1 << 24, 1 << 23, 1 << 20, 1 << 16):
+    offs = [0, n, 2 * n if 3 * n <= (1 << 26) else 0]
+    for _ in range(3):
+        pico_amd.reduce_local(big_a[offs[0]:], big_b[offs[0]:], n, "float", "sum", stream=st)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for i in range(20):
+        o = offs[i % len(offs)]
+        pico_amd.reduce_local(big_a[o:], big_b[o:], n, "float", "sum", stream=st)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    print(f"window n={n} ({n * 4 >> 20} MiB) ms={ms:.4f} GB/s={3 * n * 4 / (ms * 1e-3) / 1e9:.1f}", flush=True)
