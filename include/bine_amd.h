@@ -184,6 +184,26 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
                   size_t esz, size_t segsize, int in_place, bine_prim_t *prims, int64_t cap,
                   uint64_t *tmp_elems);
 
+/* The two-stream issue schedule the executor derives from a plan (inspection /
+ * testing): one entry per primitive; entries with equal `op` form one unit of
+ * work -- an exchange group on the comm stream (xchg = 1) or one local
+ * primitive on the caller's stream.  `wait` = index of the op of the other
+ * stream this op waits for (-1: none).  PIPELINE exchanges appear cut into
+ * `chunk_bytes` pieces (0: uncut).  *c_join = 1 if the comm stream first waits
+ * for the caller's prior work; *final_wait = op the caller's stream waits for
+ * at the end (-1: none).  Returns the number of entries (may exceed cap) or
+ * -status. */
+typedef struct {
+  int32_t op;
+  int32_t xchg;
+  int64_t wait;
+  bine_prim_t prim;
+} bine_sched_entry_t;
+
+int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root,
+                           size_t esz, size_t segsize, int in_place, size_t chunk_bytes,
+                           bine_sched_entry_t *out, int64_t cap, int *c_join, int64_t *final_wait);
+
 #ifdef __cplusplus
 }
 #endif

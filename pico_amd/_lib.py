@@ -42,6 +42,10 @@ class Prim(ctypes.Structure):
                 ("dst_off", ctypes.c_uint64), ("aux_off", ctypes.c_uint64), ("count", ctypes.c_uint64)]
 
 
+class SchedEntry(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("xchg", ctypes.c_int32), ("wait", ctypes.c_int64), ("prim", Prim)]
+
+
 PRIM_NAMES = {1: "SEND", 2: "RECV", 3: "REDUCE", 4: "REDUCE3", 5: "COPY"}
 
 
@@ -97,6 +101,8 @@ def lib():
         "bine_loopback_run_reduce": ([vp, i, i, vp, vp, sz, i, i, i, vp], i),
         "bine_plan": ([i, i, i, sz, vp, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(u64)],
                       ctypes.c_int64),
+        "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
+                                ctypes.POINTER(ctypes.c_int64)], ctypes.c_int64),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -240,6 +240,30 @@ def plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, 
     return prims, list(tmp)
 
 
+def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, root: int = 0,
+             esz: int = 4, segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0):
+    """The executor's two-stream issue schedule of rank `rank` (host only).
+    Returns (ops, c_join, final_wait); ops[i] = {"xchg", "wait", "prims"}."""
+    a = _algo(coll, algo)
+    rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
+    cj, fw = ctypes.c_int(), ctypes.c_int64()
+    args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes)
+    n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw))
+    if n < 0:
+        raise BineError(int(-n), f"schedule {coll}_{algo}")
+    arr = (_lib.SchedEntry * max(int(n), 1))()
+    lib().bine_plan_schedule(*args, arr, n, ctypes.byref(cj), ctypes.byref(fw))
+    ops = []
+    for k in range(int(n)):
+        e = arr[k]
+        p = {f: getattr(e.prim, f) for f, _ in _lib.Prim._fields_ if f != "pad_"}
+        p["type"] = _lib.PRIM_NAMES[p["type"]]
+        if not ops or e.op != len(ops) - 1:
+            ops.append({"xchg": bool(e.xchg), "wait": int(e.wait), "prims": []})
+        ops[-1]["prims"].append(p)
+    return ops, bool(cj.value), int(fw.value)
+
+
 # ---- libbine-named entry points (include/libbine.h:30-78) --------------------------
 
 def _mk_ar(name):
@@ -275,6 +299,6 @@ for _n in ALGOS["reduce"]:
     ENTRY_POINTS["reduce_" + _n] = _mk_rd(_n)
 globals().update(ENTRY_POINTS)
 
-__all__ = ["Comm", "BineError", "IN_PLACE", "reduce_local", "reduce3", "fill_pico", "checksum",
+__all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan"] + list(ENTRY_POINTS)

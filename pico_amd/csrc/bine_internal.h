@@ -42,6 +42,28 @@ int log2_ceil(int v);
 bool is_pow2(int v);
 void static_perm(int P, std::vector<int> &perm);
 
+// ---- issue schedule (schedule.cpp) -------------------------------------------
+// A plan turned into device work for two streams: exchange groups go to the
+// comm stream, local primitives to the compute stream.  PIPELINE exchanges are
+// cut into `chunk` element pieces, each feeding the matching piece of the
+// following reduction.  `wait` = index of the op of the OTHER stream this op
+// must wait for (the newest one touching overlapping memory), -1 = none; ops of
+// one stream are ordered by the stream.
+
+struct SOp {
+  bool xchg;
+  std::vector<Prim> prims;
+  int64_t wait;
+};
+
+struct Schedule {
+  std::vector<SOp> ops;
+  bool c_join = false;      // comm stream waits for the caller's prior work
+  int64_t final_wait = -1;  // op of the comm stream the caller's stream waits for at the end
+};
+
+void make_schedule(const Plan &plan, size_t chunk, bool in_place, Schedule &out);
+
 // ---- kernels (kernels.hip) ----------------------------------------------------
 int launch_reduce(const void *a, const void *b, void *out, size_t count, int dtype, int op,
                   void *stream);   // out = b (op) a

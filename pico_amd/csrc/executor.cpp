@@ -6,13 +6,15 @@
 //   * comm stream C (the communicator's own, high priority): every exchange,
 //     i.e. RCCL ncclSend/ncclRecv inside one ncclGroupStart/End (RCCL P2P over
 //     xGMI), or the in-process loopback copies;
-//   * hipEvents hand work between the two.  An exchange whose receive feeds the
+//   * hipEvents hand work between the two, only where memory regions overlap
+//     (make_schedule, schedule.cpp).  An exchange whose receive feeds the
 //     following reduction element-for-element (plan flag BINE_PRIM_PIPELINE --
 //     every reduce-scatter step of the Bine schedules) is cut into chunks: the
-//     receive of chunk k+1 on C overlaps the reduction of chunk k on K.  This
-//     is the device form of the segmented variant's double-buffered
+//     receive of chunk k+1 on C overlaps the reduction of chunk k on K, and the
+//     next step's first chunks go out while this step's last ones are reduced.
+//     This is the device form of the segmented variant's double-buffered
 //     Irecv/Reduce_local loop (libbine_allreduce.c:1218-1253).
-//   * workspace (TMP0..2) and plans are cached per communicator.
+//   * workspace (TMP0..2), plans and their schedules are cached per communicator.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -189,7 +191,10 @@ struct bine_comm {
   size_t tmp_bytes[3] = {0, 0, 0};
   std::vector<hipEvent_t> ev;
   size_t ev_next = 0;
-  std::map<std::string, bine::Plan> plans;
+  std::map<std::string, std::pair<bine::Plan, bine::Schedule>> plans;
+  std::vector<hipEvent_t> op_ev;  // scratch of execute()
+  std::vector<bine::XSend> xs;
+  std::vector<bine::XRecv> xr;
   std::mutex mu;
 };
 
@@ -201,7 +206,7 @@ static int comm_setup(bine_comm *c) {
   HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi));
-  c->ev.resize(128);
+  c->ev.resize(1024);
   for (auto &e : c->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return BINE_SUCCESS;
 }
@@ -248,94 +253,71 @@ static size_t default_chunk_bytes() {
   return v;
 }
 
-// Walk `plan` on the device.  `chunk_bytes` = 0: no chunking.
-static int execute(bine_comm *c, const Plan &plan, const void *sbuf, void *rbuf, size_t esz, int dtype,
-                   int op, size_t chunk_bytes, hipStream_t K) {
+// ---------------------------------------------------------------------------
+// plan execution
+// ---------------------------------------------------------------------------
+
+// Issue a schedule (make_schedule): exchanges on the comm stream C, local
+// primitives on the caller's stream K, one event per op, and a cross-stream
+// wait only where the schedule names one.
+static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
+                   hipStream_t K) {
   char *base[5];
   base[BINE_BUF_SBUF] = (char *)sbuf;
   base[BINE_BUF_RBUF] = (char *)rbuf;
   for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
   hipStream_t C = c->cstream;
-  size_t ch = chunk_bytes / esz;
-  if (ch) ch = std::max<size_t>(16 / esz, ch / (16 / esz) * (16 / esz));  // keep chunks 16-B aligned
-
-  bool k_dirty = true, c_dirty = false;  // C must first see everything already on K
-  const auto &pr = plan.prims;
-  size_t i = 0;
-  std::vector<XSend> sends;
-  std::vector<XRecv> recvs;
-  while (i < pr.size()) {
-    const Prim &p = pr[i];
-    if (p.type == BINE_PRIM_SEND || p.type == BINE_PRIM_RECV) {
-      size_t j = i;
-      while (j < pr.size() && (pr[j].type == BINE_PRIM_SEND || pr[j].type == BINE_PRIM_RECV) &&
-             pr[j].group == p.group)
-        j++;
-      if (k_dirty) { int rc = stream_join(c, C, K); if (rc) return rc; k_dirty = false; }
-      const bool pipe = ch && (p.flags & BINE_PRIM_PIPELINE) && j < pr.size() &&
-                        (pr[j].flags & BINE_PRIM_PIPELINE) &&
-                        (pr[j].type == BINE_PRIM_REDUCE || pr[j].type == BINE_PRIM_REDUCE3);
-      if (pipe) {
-        const Prim *S = nullptr, *R = nullptr;
-        for (size_t k = i; k < j; k++) (pr[k].type == BINE_PRIM_SEND ? S : R) = &pr[k];
-        const Prim &Q = pr[j];
-        const size_t nch = std::max((S->count + ch - 1) / ch, (R->count + ch - 1) / ch);
-        for (size_t k = 0; k < nch; k++) {
-          sends.clear();
-          recvs.clear();
-          const uint64_t o = (uint64_t)(k * ch);
-          if (o < S->count) sends.push_back({S->peer, ptr(S->src_buf, S->src_off + o), std::min<uint64_t>(ch, S->count - o) * esz});
-          if (o < R->count) recvs.push_back({R->peer, ptr(R->dst_buf, R->dst_off + o), std::min<uint64_t>(ch, R->count - o) * esz});
-          int rc = c->tx->exchange(sends, recvs, C);
-          if (rc) return rc;
-          if (o < R->count) {
-            rc = stream_join(c, K, C);
-            if (rc) return rc;
-            const uint64_t n = std::min<uint64_t>(ch, Q.count - std::min<uint64_t>(o, Q.count));
-            if (n) {
-              const void *b = Q.type == BINE_PRIM_REDUCE3 ? ptr(Q.aux_buf, Q.aux_off + o) : ptr(Q.dst_buf, Q.dst_off + o);
-              rc = launch_reduce(ptr(Q.src_buf, Q.src_off + o), b, ptr(Q.dst_buf, Q.dst_off + o), n, dtype, op, K);
-              if (rc) { set_err("reduce launch failed"); return rc; }
-            }
-          }
-        }
-        // make sure nothing later on K reads the receive region before the last chunk
-        int rc = stream_join(c, K, C);
-        if (rc) return rc;
-        i = j + 1;
-        k_dirty = true;
-        c_dirty = false;
-        continue;
-      }
+  if (sc.c_join) {
+    int rc = stream_join(c, C, K);
+    if (rc) return rc;
+  }
+  std::vector<hipEvent_t> &evs = c->op_ev;
+  evs.resize(sc.ops.size());
+  std::vector<XSend> &sends = c->xs;
+  std::vector<XRecv> &recvs = c->xr;
+  for (size_t i = 0; i < sc.ops.size(); i++) {
+    const SOp &o = sc.ops[i];
+    hipStream_t st = o.xchg ? C : K;
+    if (o.wait >= 0) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
+    int rc = BINE_SUCCESS;
+    if (o.xchg) {
       sends.clear();
       recvs.clear();
-      for (size_t k = i; k < j; k++) {
-        const Prim &x = pr[k];
+      for (const Prim &x : o.prims) {
         if (x.type == BINE_PRIM_SEND) sends.push_back({x.peer, ptr(x.src_buf, x.src_off), x.count * esz});
         else recvs.push_back({x.peer, ptr(x.dst_buf, x.dst_off), x.count * esz});
       }
-      int rc = c->tx->exchange(sends, recvs, C);
+      rc = c->tx->exchange(sends, recvs, C);
       if (rc) return rc;
-      c_dirty = true;
-      i = j;
-      continue;
+    } else {
+      const Prim &p = o.prims[0];
+      if (p.type == BINE_PRIM_REDUCE)
+        rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.dst_buf, p.dst_off), ptr(p.dst_buf, p.dst_off), p.count,
+                           dtype, op, K);
+      else if (p.type == BINE_PRIM_REDUCE3)
+        rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count,
+                           dtype, op, K);
+      else
+        HIP_TRY(hipMemcpyAsync(ptr(p.dst_buf, p.dst_off), ptr(p.src_buf, p.src_off), p.count * esz,
+                               hipMemcpyDeviceToDevice, K));
+      if (rc) { set_err("local primitive failed (%s)", bine_status_string(rc)); return rc; }
     }
-    if (c_dirty) { int rc = stream_join(c, K, C); if (rc) return rc; c_dirty = false; }
-    int rc = BINE_SUCCESS;
-    if (p.type == BINE_PRIM_REDUCE)
-      rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.dst_buf, p.dst_off), ptr(p.dst_buf, p.dst_off), p.count, dtype, op, K);
-    else if (p.type == BINE_PRIM_REDUCE3)
-      rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count, dtype, op, K);
-    else if (p.type == BINE_PRIM_COPY)
-      HIP_TRY(hipMemcpyAsync(ptr(p.dst_buf, p.dst_off), ptr(p.src_buf, p.src_off), p.count * esz,
-                             hipMemcpyDeviceToDevice, K));
-    if (rc) { set_err("local primitive failed"); return rc; }
-    k_dirty = true;
-    i++;
+    // an event of the pool may be re-recorded by a later op once the pool
+    // wraps: any later record only delays a waiter, never lets it run early
+    evs[i] = next_event(c);
+    HIP_TRY(hipEventRecord(evs[i], st));
   }
-  if (c_dirty) { int rc = stream_join(c, K, C); if (rc) return rc; }
+  if (sc.final_wait >= 0) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
   return BINE_SUCCESS;
+}
+
+// pipelining chunk in elements, kept 16-B aligned (0 = no chunking)
+static size_t chunk_elems(size_t chunk_bytes, size_t esz) {
+  size_t ch = chunk_bytes / esz;
+  if (!ch) return 0;
+  const size_t v = 16 / esz;
+  return std::max(v, ch / v * v);
 }
 
 static std::string plan_key(const PlanArgs &a) {
@@ -358,15 +340,21 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   a.rank = c->rank;
   a.esz = bine_dtype_size(dtype);
   a.in_place = sbuf == BINE_IN_PLACE;
-  const std::string key = plan_key(a);
+  const size_t ch = chunk_elems(chunk_bytes, a.esz);
+  const std::string key = plan_key(a) + "|" + std::to_string(ch);
   auto it = c->plans.find(key);
-  if (it == c->plans.end()) it = c->plans.emplace(key, make_plan(a)).first;
-  const Plan &plan = it->second;
+  if (it == c->plans.end()) {
+    std::pair<Plan, Schedule> v;
+    v.first = make_plan(a);
+    if (v.first.status == BINE_SUCCESS) make_schedule(v.first, ch, a.in_place, v.second);
+    it = c->plans.emplace(key, std::move(v)).first;
+  }
+  const Plan &plan = it->second.first;
   if (plan.status != BINE_SUCCESS) return plan.status;
   hipStream_t K = stream ? (hipStream_t)stream : c->stream;
   int rc = ensure_workspace(c, plan, a.esz, K);
   if (rc) return rc;
-  return execute(c, plan, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, chunk_bytes, K);
+  return execute(c, it->second.second, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K);
 }
 
 }  // namespace bine
@@ -621,8 +609,8 @@ int bine_loopback_run_reduce(bine_comm_t *comms, int n, int algo, const void *co
 
 // ---- schedule introspection ------------------------------------------------------
 
-int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
-                  size_t segsize, int in_place, bine_prim_t *prims, int64_t cap, uint64_t *tmp_elems) {
+static Plan plan_for(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                     size_t segsize, int in_place) {
   PlanArgs a;
   a.algo = algo;
   a.P = nranks;
@@ -634,12 +622,36 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
   a.esz = esz;
   a.segsize = segsize;
   a.in_place = in_place != 0;
-  Plan p = make_plan(a);
+  return make_plan(a);
+}
+
+int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                  size_t segsize, int in_place, bine_prim_t *prims, int64_t cap, uint64_t *tmp_elems) {
+  Plan p = plan_for(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
   if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
   for (int64_t k = 0; k < (int64_t)p.prims.size() && k < cap; k++) prims[k] = p.prims[(size_t)k];
   if (tmp_elems)
     for (int t = 0; t < 3; t++) tmp_elems[t] = p.tmp_elems[t];
   return (int64_t)p.prims.size();
+}
+
+int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                           size_t segsize, int in_place, size_t chunk_bytes, bine_sched_entry_t *out, int64_t cap,
+                           int *c_join, int64_t *final_wait) {
+  if (!esz) return -(int64_t)BINE_ERR_ARG;
+  Plan p = plan_for(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
+  if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
+  Schedule sc;
+  make_schedule(p, chunk_elems(chunk_bytes, esz), in_place != 0, sc);
+  int64_t n = 0;
+  for (size_t i = 0; i < sc.ops.size(); i++)
+    for (const Prim &x : sc.ops[i].prims) {
+      if (n < cap) out[n] = {(int32_t)i, sc.ops[i].xchg ? 1 : 0, sc.ops[i].wait, x};
+      n++;
+    }
+  if (c_join) *c_join = sc.c_join ? 1 : 0;
+  if (final_wait) *final_wait = sc.final_wait;
+  return n;
 }
 
 int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);

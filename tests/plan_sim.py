@@ -27,8 +27,23 @@ class PlanError(AssertionError):
     pass
 
 
+def scheduled_prims(coll, algo, P, r, chunk_bytes, **kw):
+    """The executor's issue schedule (pico_amd.schedule) flattened back into a
+    primitive list in issue order, one exchange group per op."""
+    ops, _, _ = pico_amd.schedule(coll, algo, P, r, chunk_bytes=chunk_bytes, **kw)
+    out = []
+    for i, o in enumerate(ops):
+        for p in o["prims"]:
+            q = dict(p)
+            q["group"] = i
+            out.append(q)
+    return out
+
+
 def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_place=False,
-        rbufs=None):
+        rbufs=None, chunk_bytes=None):
+    """chunk_bytes != None: run the executor's chunked issue schedule instead of
+    the plan itself (same semantics when ops run in issue order)."""
     P = len(sbufs)
     esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
     count = sbufs[0].size
@@ -36,6 +51,9 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
     for r in range(P):
         prims, tmp = pico_amd.plan(coll, algo, P, r, count=count, rcounts=rcounts, root=root, esz=esz,
                                    segsize=segsize, in_place=in_place)
+        if chunk_bytes is not None:
+            prims = scheduled_prims(coll, algo, P, r, chunk_bytes, count=count, rcounts=rcounts, root=root,
+                                    esz=esz, segsize=segsize, in_place=in_place)
         plans.append(prims)
         if rbufs is not None:
             rb = rbufs[r]

@@ -1,0 +1,161 @@
+"""The executor's two-stream issue schedule (make_schedule, schedule.cpp),
+checked on the host through bine_plan_schedule:
+
+* race freedom -- every pair of ops on different streams (comm stream C:
+  exchanges; caller's stream K: reductions / copies) whose memory regions
+  conflict (read-after-write, write-after-read, write-after-write) is ordered
+  by the happens-before relation the schedule's stream order and event waits
+  create (vector clocks);
+* the comm stream joins the caller's prior work and the caller's stream ends
+  after the last exchange;
+* chunking -- the chunked schedule, run in issue order by the rendezvous
+  simulator, gives the oracle's (= the reference's) result bit-for-bit.
+
+Race freedom plus issue-order equivalence means every interleaving the GPU may
+pick computes the reference's result."""
+import numpy as np
+import pytest
+
+import pico_amd
+import plan_sim
+from oracle import oracle as O
+
+SB, RB = 0, 1
+
+AR = ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented", "bine_lat", "ring", "rabenseifner",
+      "recursivedoubling", "bine_block_by_block_any_even"]
+RS = ["bine_permute_remap", "bine_send_remap", "bine_static", "bine_block_by_block", "bine_block_by_block_any_even",
+      "ring", "butterfly", "recursivehalving", "recursive_distance_doubling"]
+RD = ["bine_bdw", "bine_lat"]
+
+
+def _regions(p, in_place):
+    def reg(b, off, n):
+        return ((RB if (in_place and b == SB) else b), off, off + n)
+    t, n = p["type"], p["count"]
+    if t == "SEND":
+        return [reg(p["src_buf"], p["src_off"], n)], []
+    if t == "RECV":
+        return [], [reg(p["dst_buf"], p["dst_off"], n)]
+    if t == "REDUCE":
+        d = reg(p["dst_buf"], p["dst_off"], n)
+        return [reg(p["src_buf"], p["src_off"], n), d], [d]
+    if t == "REDUCE3":
+        return [reg(p["src_buf"], p["src_off"], n), reg(p["aux_buf"], p["aux_off"], n)], \
+            [reg(p["dst_buf"], p["dst_off"], n)]
+    return [reg(p["src_buf"], p["src_off"], n)], [reg(p["dst_buf"], p["dst_off"], n)]
+
+
+def _overlap(a, b):
+    return any(x[0] == y[0] and x[1] < y[2] and y[1] < x[2] for x in a for y in b)
+
+
+def check_race_free(ops, c_join, final_wait, in_place):
+    n = len(ops)
+    # vc[i][s] = newest op of stream s that happens-before-or-is op i
+    vc = []
+    last = [None, None]
+    for i, o in enumerate(ops):
+        s = 1 if o["xchg"] else 0
+        w = o["wait"]
+        assert w < i
+        if w >= 0:
+            assert ops[w]["xchg"] != o["xchg"], "wait on own stream"
+        v = [-1, -1]
+        for src in (last[s], w if w >= 0 else None):
+            if src is not None:
+                v = [max(v[0], vc[src][0]), max(v[1], vc[src][1])]
+        v[s] = i
+        vc.append(v)
+        last[s] = i
+    regs = []
+    for o in ops:
+        rd, wr = [], []
+        for p in o["prims"]:
+            a, b = _regions(p, in_place)
+            rd += a
+            wr += b
+        regs.append((rd, wr))
+    for j in range(n):
+        sj = 1 if ops[j]["xchg"] else 0
+        for i in range(j):
+            si = 1 if ops[i]["xchg"] else 0
+            if si == sj:
+                continue
+            (ri, wi), (rj, wj) = regs[i], regs[j]
+            if _overlap(wi, rj) or _overlap(wi, wj) or _overlap(ri, wj):
+                assert vc[j][si] >= i, f"race: op {i} ({ops[i]['prims'][0]['type']}) vs op {j}"
+    xs = [i for i, o in enumerate(ops) if o["xchg"]]
+    if xs:
+        assert c_join
+        ks = [i for i, o in enumerate(ops) if not o["xchg"]]
+        covered = max(final_wait, vc[ks[-1]][1] if ks else -1)
+        assert covered >= xs[-1], "caller's stream does not wait for the last exchange"
+
+
+def _cases():
+    for P in (2, 3, 4, 5, 6, 8, 16):
+        for a in AR:
+            yield "allreduce", a, P
+        for a in RS:
+            yield "reduce_scatter", a, P
+        for a in RD:
+            yield "reduce", a, P
+
+
+@pytest.mark.parametrize("chunk", [0, 64, 4096])
+@pytest.mark.parametrize("in_place", [False, True])
+def test_schedules_race_free(chunk, in_place):
+    checked = 0
+    for coll, algo, P in _cases():
+        for rank in range(P):
+            kw = dict(count=1003, esz=4, segsize=128, in_place=in_place)
+            if coll == "reduce_scatter":
+                kw = dict(rcounts=[37 + (i % 3) for i in range(P)], esz=4, in_place=in_place)
+            try:
+                ops, cj, fw = pico_amd.schedule(coll, algo, P, rank, chunk_bytes=chunk, **kw)
+            except pico_amd.BineError:
+                continue
+            check_race_free(ops, cj, fw, in_place)
+            checked += 1
+    assert checked > 300
+
+
+def test_chunking_overlaps_steps():
+    """With chunks, the first chunk of a step waits for the reduction of the
+    region it sends, not for the whole previous step."""
+    ops, _, _ = pico_amd.schedule("allreduce", "bine_bdw_remap", 8, 3, count=1 << 16, chunk_bytes=4096)
+    red = [i for i, o in enumerate(ops) if not o["xchg"]]
+    xch = [i for i, o in enumerate(ops) if o["xchg"]]
+    # some exchange is issued while a reduction issued earlier is not waited for
+    assert any(0 <= ops[j]["wait"] < max(i for i in red if i < j) for j in xch if any(i < j for i in red))
+
+
+@pytest.mark.parametrize("coll,algo,P", [
+    ("allreduce", "bine_bdw_remap", 4), ("allreduce", "bine_bdw_static", 8), ("allreduce", "rabenseifner", 6),
+    ("allreduce", "bine_bdw_remap_segmented", 4), ("allreduce", "ring", 5),
+    ("reduce_scatter", "bine_permute_remap", 8), ("reduce_scatter", "bine_static", 4),
+    ("reduce_scatter", "ring", 3), ("reduce_scatter", "recursivehalving", 8),
+    ("reduce", "bine_bdw", 8),
+])
+@pytest.mark.parametrize("chunk", [16, 200])
+def test_chunked_schedule_matches_oracle(coll, algo, P, chunk):
+    dtype = "float"
+    if coll == "reduce_scatter":
+        rc = [29 + 3 * (i % 2) for i in range(P)]
+        sb = O.inputs(dtype, sum(rc), P)
+        want = O.reduce_scatter(algo, sb, rc, dtype)[0]
+        got = plan_sim.run(coll, algo, sb, dtype, rcounts=rc, chunk_bytes=chunk)
+        for r in range(P):
+            assert np.array_equal(got[r], want[r])
+        return
+    sb = O.inputs(dtype, 997, P)
+    if coll == "allreduce":
+        want = O.allreduce(algo, sb, dtype, segsize=64)[0]
+        got = plan_sim.run(coll, algo, sb, dtype, segsize=64, chunk_bytes=chunk)
+        for r in range(P):
+            assert np.array_equal(got[r], want[r])
+    else:
+        want = O.reduce(algo, sb, dtype)[0]
+        got = plan_sim.run(coll, algo, sb, dtype, chunk_bytes=chunk)
+        assert np.array_equal(got[0], want)
