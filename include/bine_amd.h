@@ -127,6 +127,15 @@ int bine_comm_device(bine_comm_t comm);
 void *bine_comm_stream(bine_comm_t comm);
 int bine_comm_synchronize(bine_comm_t comm);
 
+/* Multi-link relay for permutation steps (every rank sends one block to one
+ * peer): each pipelining chunk is split into a direct part and P-2 parts that
+ * travel two hops through the other ranks, so one step loads every xGMI link
+ * instead of one.  Results are unchanged bit for bit (only routes differ).
+ * min_part_bytes = smallest relayed part (chunks smaller than P times this go
+ * direct); 0 = off (default unless BINE_RELAY_MIN_BYTES is set).  Collective:
+ * every rank of the communicator must use the same setting. */
+int bine_comm_set_relay(bine_comm_t comm, size_t min_part_bytes);
+
 /* ---- collectives (device pointers, stream-ordered) ------------------------- */
 /* allreduce_* (libbine.h:30-37).  `segsize` plays bine_allreduce_segsize
  * (libbine.h:28) for BINE_AR_BINE_BDW_REMAP_SEGMENTED and is the pipelining
@@ -157,7 +166,9 @@ int bine_loopback_run_reduce(bine_comm_t *comms, int nranks, int algo,
 typedef enum { BINE_PRIM_SEND = 1, BINE_PRIM_RECV = 2, BINE_PRIM_REDUCE = 3,
                BINE_PRIM_REDUCE3 = 4, BINE_PRIM_COPY = 5 } bine_prim_type_t;
 typedef enum { BINE_BUF_SBUF = 0, BINE_BUF_RBUF = 1, BINE_BUF_TMP0 = 2, BINE_BUF_TMP1 = 3,
-               BINE_BUF_TMP2 = 4 } bine_buf_t;
+               BINE_BUF_TMP2 = 4,
+               BINE_BUF_STAGE = 5  /* relay staging; appears in issue schedules only */
+} bine_buf_t;
 #define BINE_PRIM_PIPELINE 1  /* flags: exchange whose receive feeds the next
                                  REDUCE(3) element for element -- both may be
                                  split into chunks and overlapped */
@@ -191,7 +202,9 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
  * stream this op waits for (-1: none).  PIPELINE exchanges appear cut into
  * `chunk_bytes` pieces (0: uncut).  *c_join = 1 if the comm stream first waits
  * for the caller's prior work; *final_wait = op the caller's stream waits for
- * at the end (-1: none).  Returns the number of entries (may exceed cap) or
+ * at the end (-1: none); *stage_elems = relay staging workspace (elements).
+ * relay_min_bytes > 0 selects relay mode as
+ * bine_comm_set_relay does.  Returns the number of entries (may exceed cap) or
  * -status. */
 typedef struct {
   int32_t op;
@@ -202,7 +215,8 @@ typedef struct {
 
 int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root,
                            size_t esz, size_t segsize, int in_place, size_t chunk_bytes,
-                           bine_sched_entry_t *out, int64_t cap, int *c_join, int64_t *final_wait);
+                           size_t relay_min_bytes, bine_sched_entry_t *out, int64_t cap, int *c_join,
+                           int64_t *final_wait, uint64_t *stage_elems);
 
 #ifdef __cplusplus
 }

@@ -101,8 +101,9 @@ def lib():
         "bine_loopback_run_reduce": ([vp, i, i, vp, vp, sz, i, i, i, vp], i),
         "bine_plan": ([i, i, i, sz, vp, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(u64)],
                       ctypes.c_int64),
-        "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
-                                ctypes.POINTER(ctypes.c_int64)], ctypes.c_int64),
+        "bine_comm_set_relay": ([vp, sz], i),
+        "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
+                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(u64)], ctypes.c_int64),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

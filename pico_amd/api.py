@@ -129,6 +129,10 @@ class Comm:
     def synchronize(self) -> None:
         check(lib().bine_comm_synchronize(self.handle), "bine_comm_synchronize")
 
+    def set_relay(self, min_part_bytes: int) -> None:
+        """Multi-link relay for permutation steps (0 = off); collective."""
+        check(lib().bine_comm_set_relay(self.handle, min_part_bytes), "bine_comm_set_relay")
+
     def destroy(self) -> None:
         if self.handle:
             lib().bine_comm_destroy(self.handle)
@@ -241,18 +245,20 @@ def plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, 
 
 
 def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, root: int = 0,
-             esz: int = 4, segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0):
+             esz: int = 4, segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0,
+             relay_min_bytes: int = 0, info: bool = False):
     """The executor's two-stream issue schedule of rank `rank` (host only).
-    Returns (ops, c_join, final_wait); ops[i] = {"xchg", "wait", "prims"}."""
+    Returns (ops, c_join, final_wait); ops[i] = {"xchg", "wait", "prims"}.
+    With info=True a 4th item: {"stage_elems": relay staging workspace}."""
     a = _algo(coll, algo)
     rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
-    cj, fw = ctypes.c_int(), ctypes.c_int64()
-    args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes)
-    n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw))
+    cj, fw, se = ctypes.c_int(), ctypes.c_int64(), ctypes.c_uint64()
+    args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes, relay_min_bytes)
+    n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw), ctypes.byref(se))
     if n < 0:
         raise BineError(int(-n), f"schedule {coll}_{algo}")
     arr = (_lib.SchedEntry * max(int(n), 1))()
-    lib().bine_plan_schedule(*args, arr, n, ctypes.byref(cj), ctypes.byref(fw))
+    lib().bine_plan_schedule(*args, arr, n, ctypes.byref(cj), ctypes.byref(fw), ctypes.byref(se))
     ops = []
     for k in range(int(n)):
         e = arr[k]
@@ -261,6 +267,8 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
         if not ops or e.op != len(ops) - 1:
             ops.append({"xchg": bool(e.xchg), "wait": int(e.wait), "prims": []})
         ops[-1]["prims"].append(p)
+    if info:
+        return ops, bool(cj.value), int(fw.value), {"stage_elems": int(se.value)}
     return ops, bool(cj.value), int(fw.value)
 
 

@@ -58,10 +58,21 @@ struct SOp {
 
 struct Schedule {
   std::vector<SOp> ops;
-  bool c_join = false;      // comm stream waits for the caller's prior work
-  int64_t final_wait = -1;  // op of the comm stream the caller's stream waits for at the end
+  bool c_join = false;        // comm stream waits for the caller's prior work
+  int64_t final_wait = -1;    // op of the comm stream the caller's stream waits for at the end
+  uint64_t stage_elems = 0;   // BINE_BUF_STAGE workspace (relay mode)
+  int relayed_steps = 0;
 };
 
+struct SchedCfg {
+  size_t chunk = 0;       // pipelining chunk, elements (0: none)
+  bool in_place = false;
+  size_t relay_min = 0;   // relay mode: smallest relayed part, elements (0: off)
+};
+
+// issue.cpp.  `all` = the plans of every rank (same arguments, rank varied);
+// needed only for relay mode (null: no relay).
+void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, const SchedCfg &cfg, Schedule &out);
 void make_schedule(const Plan &plan, size_t chunk, bool in_place, Schedule &out);
 
 // ---- kernels (kernels.hip) ----------------------------------------------------

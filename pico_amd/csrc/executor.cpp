@@ -187,8 +187,9 @@ struct bine_comm {
   hipStream_t cstream = nullptr;  // comm stream
   std::unique_ptr<bine::Transport> tx;
   std::shared_ptr<bine::LoopbackHub> hub;
-  void *tmp[3] = {nullptr, nullptr, nullptr};
-  size_t tmp_bytes[3] = {0, 0, 0};
+  void *tmp[4] = {nullptr, nullptr, nullptr, nullptr};  // TMP0..2, STAGE
+  size_t tmp_bytes[4] = {0, 0, 0, 0};
+  size_t relay_min_bytes = 0;  // relay mode: smallest relayed part (0: off)
   std::vector<hipEvent_t> ev;
   size_t ev_next = 0;
   std::map<std::string, std::pair<bine::Plan, bine::Schedule>> plans;
@@ -208,6 +209,7 @@ static int comm_setup(bine_comm *c) {
   HIP_TRY(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi));
   c->ev.resize(1024);
   for (auto &e : c->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (const char *e = getenv("BINE_RELAY_MIN_BYTES")) c->relay_min_bytes = (size_t)strtoull(e, nullptr, 10);
   return BINE_SUCCESS;
 }
 
@@ -225,15 +227,15 @@ static int stream_join(bine_comm *c, hipStream_t dst, hipStream_t src) {
   return BINE_SUCCESS;
 }
 
-static int ensure_workspace(bine_comm *c, const Plan &p, size_t esz, hipStream_t user) {
+static int ensure_workspace(bine_comm *c, const uint64_t *elems, size_t esz, hipStream_t user) {
   bool grow = false;
-  for (int t = 0; t < 3; t++) grow |= p.tmp_elems[t] * esz > c->tmp_bytes[t];
+  for (int t = 0; t < 4; t++) grow |= elems[t] * esz > c->tmp_bytes[t];
   if (!grow) return BINE_SUCCESS;
   // old buffers may still be read by enqueued work
   HIP_TRY(hipStreamSynchronize(user));
   HIP_TRY(hipStreamSynchronize(c->cstream));
-  for (int t = 0; t < 3; t++) {
-    const size_t need = p.tmp_elems[t] * esz;
+  for (int t = 0; t < 4; t++) {
+    const size_t need = elems[t] * esz;
     if (need <= c->tmp_bytes[t]) continue;
     if (c->tmp[t]) HIP_TRY(hipFree(c->tmp[t]));
     c->tmp[t] = nullptr;
@@ -262,10 +264,11 @@ static size_t default_chunk_bytes() {
 // wait only where the schedule names one.
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
                    hipStream_t K) {
-  char *base[5];
+  char *base[6];
   base[BINE_BUF_SBUF] = (char *)sbuf;
   base[BINE_BUF_RBUF] = (char *)rbuf;
   for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
+  base[BINE_BUF_STAGE] = (char *)c->tmp[3];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
   hipStream_t C = c->cstream;
   if (sc.c_join) {
@@ -329,6 +332,27 @@ static std::string plan_key(const PlanArgs &a) {
   return k;
 }
 
+// own plan + issue schedule; relay mode needs every rank's plan
+static void build(const PlanArgs &a, size_t ch, size_t relay_min_bytes, Plan &plan, Schedule &sc) {
+  plan = make_plan(a);
+  if (plan.status != BINE_SUCCESS) return;
+  SchedCfg cfg;
+  cfg.chunk = ch;
+  cfg.in_place = a.in_place;
+  if (relay_min_bytes && a.P >= 3) {
+    cfg.relay_min = std::max<size_t>(1, (relay_min_bytes + a.esz - 1) / a.esz);
+    std::vector<Plan> all((size_t)a.P);
+    for (int x = 0; x < a.P; x++) {
+      PlanArgs b = a;
+      b.rank = x;
+      all[(size_t)x] = x == a.rank ? plan : make_plan(b);
+    }
+    make_schedule(plan, &all, a.rank, cfg, sc);
+  } else {
+    make_schedule(plan, nullptr, a.rank, cfg, sc);
+  }
+}
+
 static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbuf, int dtype, int op,
                           size_t chunk_bytes, void *stream) {
   if (!c) return BINE_ERR_ARG;
@@ -341,20 +365,21 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   a.esz = bine_dtype_size(dtype);
   a.in_place = sbuf == BINE_IN_PLACE;
   const size_t ch = chunk_elems(chunk_bytes, a.esz);
-  const std::string key = plan_key(a) + "|" + std::to_string(ch);
+  const std::string key = plan_key(a) + "|" + std::to_string(ch) + "|" + std::to_string(c->relay_min_bytes);
   auto it = c->plans.find(key);
   if (it == c->plans.end()) {
     std::pair<Plan, Schedule> v;
-    v.first = make_plan(a);
-    if (v.first.status == BINE_SUCCESS) make_schedule(v.first, ch, a.in_place, v.second);
+    build(a, ch, c->relay_min_bytes, v.first, v.second);
     it = c->plans.emplace(key, std::move(v)).first;
   }
   const Plan &plan = it->second.first;
+  const Schedule &sc = it->second.second;
   if (plan.status != BINE_SUCCESS) return plan.status;
   hipStream_t K = stream ? (hipStream_t)stream : c->stream;
-  int rc = ensure_workspace(c, plan, a.esz, K);
+  const uint64_t need[4] = {plan.tmp_elems[0], plan.tmp_elems[1], plan.tmp_elems[2], sc.stage_elems};
+  int rc = ensure_workspace(c, need, a.esz, K);
   if (rc) return rc;
-  return execute(c, it->second.second, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K);
+  return execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K);
 }
 
 }  // namespace bine
@@ -528,7 +553,7 @@ int bine_comm_destroy(bine_comm_t c) {
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->cstream);
   c->tx.reset();
-  for (int t = 0; t < 3; t++)
+  for (int t = 0; t < 4; t++)
     if (c->tmp[t]) (void)hipFree(c->tmp[t]);
   for (auto e : c->ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -609,8 +634,8 @@ int bine_loopback_run_reduce(bine_comm_t *comms, int n, int algo, const void *co
 
 // ---- schedule introspection ------------------------------------------------------
 
-static Plan plan_for(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
-                     size_t segsize, int in_place) {
+static PlanArgs plan_args(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                          size_t segsize, int in_place) {
   PlanArgs a;
   a.algo = algo;
   a.P = nranks;
@@ -622,12 +647,12 @@ static Plan plan_for(int algo, int nranks, int rank, size_t count, const int *rc
   a.esz = esz;
   a.segsize = segsize;
   a.in_place = in_place != 0;
-  return make_plan(a);
+  return a;
 }
 
 int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
                   size_t segsize, int in_place, bine_prim_t *prims, int64_t cap, uint64_t *tmp_elems) {
-  Plan p = plan_for(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
+  Plan p = make_plan(plan_args(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place));
   if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
   for (int64_t k = 0; k < (int64_t)p.prims.size() && k < cap; k++) prims[k] = p.prims[(size_t)k];
   if (tmp_elems)
@@ -636,13 +661,15 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
 }
 
 int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
-                           size_t segsize, int in_place, size_t chunk_bytes, bine_sched_entry_t *out, int64_t cap,
-                           int *c_join, int64_t *final_wait) {
+                           size_t segsize, int in_place, size_t chunk_bytes, size_t relay_min_bytes,
+                           bine_sched_entry_t *out, int64_t cap, int *c_join, int64_t *final_wait,
+                           uint64_t *stage_elems) {
   if (!esz) return -(int64_t)BINE_ERR_ARG;
-  Plan p = plan_for(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
-  if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
+  PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
+  Plan p;
   Schedule sc;
-  make_schedule(p, chunk_elems(chunk_bytes, esz), in_place != 0, sc);
+  build(a, chunk_elems(chunk_bytes, esz), relay_min_bytes, p, sc);
+  if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
   int64_t n = 0;
   for (size_t i = 0; i < sc.ops.size(); i++)
     for (const Prim &x : sc.ops[i].prims) {
@@ -651,7 +678,15 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
     }
   if (c_join) *c_join = sc.c_join ? 1 : 0;
   if (final_wait) *final_wait = sc.final_wait;
+  if (stage_elems) *stage_elems = sc.stage_elems;
   return n;
+}
+
+int bine_comm_set_relay(bine_comm_t c, size_t min_part_bytes) {
+  if (!c) return BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->relay_min_bytes = min_part_bytes;
+  return BINE_SUCCESS;
 }
 
 int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);

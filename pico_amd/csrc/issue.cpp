@@ -1,0 +1,375 @@
+// issue.cpp -- turns a per-rank plan (schedule.cpp) into the executor's
+// two-stream issue schedule (see Schedule in bine_internal.h).
+//
+// Three transformations, none of which changes a single value the plan
+// computes (each reduction still sees the same operands in the same order):
+//
+//  1. chunking: an exchange flagged BINE_PRIM_PIPELINE (one send + one receive
+//     whose received block is consumed element-for-element by the following
+//     REDUCE / REDUCE3) is cut into pieces, each feeding the matching piece of
+//     the reduction -- the device form of the segmented variant's
+//     Irecv/Reduce_local double buffering (libbine_allreduce.c:1218-1253);
+//
+//  2. region-based dependencies: every op records which element ranges of which
+//     buffer it reads and writes; an op waits only for the newest op of the
+//     OTHER stream it conflicts with (RAW / WAR / WAW).  Chunk k+1's transfer
+//     overlaps chunk k's reduction, and the next step's first chunks go out
+//     while this step's last chunks are still being reduced;
+//
+//  3. multi-link relay (optional, cfg.relay_min > 0): a Bine step is a
+//     permutation -- every rank sends one block to one partner and receives one
+//     block from another -- so a literal execution uses ONE of the seven xGMI
+//     links of an MI355X per step.  Relay mode splits each chunk of such a step
+//     into a direct part and P-2 parts routed over two hops through the other
+//     ranks (first hop origin -> relay, second hop relay -> destination, the
+//     relay forwarding from a staging buffer one round later).  With direct
+//     part 2M/P and relay parts M/P every directed link carries 2M/P per step
+//     instead of M on one link: P/2 times less time per step on a fully
+//     connected node.  The bytes that land in each receive buffer are the
+//     same; only their route differs.  Rounds are lock-step across ranks and
+//     every directed link carries at most one first-hop part followed by at
+//     most one forwarded part per round, posted in the same order at both ends
+//     (RCCL matches sends and receives of a peer pair in posting order).
+#include <algorithm>
+
+#include "bine_internal.h"
+
+namespace bine {
+
+namespace {
+
+struct Reg { int b; uint64_t lo, hi; };
+
+struct Rec {
+  bool xchg;
+  std::vector<Reg> rd, wr;
+};
+
+bool hit(const std::vector<Reg> &a, const std::vector<Reg> &b) {
+  for (const auto &x : a)
+    for (const auto &y : b)
+      if (x.b == y.b && x.lo < y.hi && y.lo < x.hi) return true;
+  return false;
+}
+
+bool is_x(const Prim &p) { return p.type == BINE_PRIM_SEND || p.type == BINE_PRIM_RECV; }
+
+// [start, end) prim index ranges of the exchange groups of a plan
+std::vector<std::pair<size_t, size_t>> groups_of(const Plan &pl) {
+  std::vector<std::pair<size_t, size_t>> g;
+  const auto &pr = pl.prims;
+  for (size_t i = 0; i < pr.size();) {
+    if (!is_x(pr[i])) { i++; continue; }
+    size_t j = i;
+    while (j < pr.size() && is_x(pr[j]) && pr[j].group == pr[i].group) j++;
+    g.push_back({i, j});
+    i = j;
+  }
+  return g;
+}
+
+// one rank's single send / single receive of a permutation step
+struct Perm {
+  Prim send, recv;
+};
+
+bool one_send_one_recv(const Plan &pl, std::pair<size_t, size_t> g, Perm &out) {
+  if (g.second - g.first != 2) return false;
+  const Prim &a = pl.prims[g.first], &b = pl.prims[g.first + 1];
+  if (a.type == b.type) return false;
+  out.send = a.type == BINE_PRIM_SEND ? a : b;
+  out.recv = a.type == BINE_PRIM_RECV ? a : b;
+  return true;
+}
+
+Prim mk(int type, int peer, int buf, uint64_t off, uint64_t count) {
+  Prim p{};
+  p.type = type;
+  p.peer = peer;
+  if (type == BINE_PRIM_SEND) { p.src_buf = buf; p.src_off = off; }
+  else { p.dst_buf = buf; p.dst_off = off; }
+  p.count = count;
+  return p;
+}
+
+Prim slice(const Prim &q, uint64_t o, uint64_t n) {
+  Prim x = q;
+  x.src_off += o;
+  x.dst_off += o;
+  x.aux_off += o;
+  x.count = n;
+  return x;
+}
+
+// Relay rounds of one permutation step at rank r.  steps[x] = rank x's
+// send/recv of this step.  Optional pipelined reduction q follows chunk by chunk.
+void emit_relay(const std::vector<Perm> &steps, int r, size_t ch, size_t relay_min, const Prim *q,
+                std::vector<SOp> &ops, uint64_t &stage_elems) {
+  const int P = (int)steps.size();
+  std::vector<int> to((size_t)P), from((size_t)P);
+  for (int x = 0; x < P; x++) {
+    to[(size_t)x] = steps[(size_t)x].send.peer;
+    from[(size_t)to[(size_t)x]] = x;
+  }
+  auto S = [&](int x) { return (uint64_t)steps[(size_t)x].send.count; };
+  uint64_t cmax = 0;
+  for (int x = 0; x < P; x++) cmax = std::max(cmax, S(x));
+  const uint64_t cht = ch ? ch : cmax;
+  auto nch = [&](int x) { return (S(x) + cht - 1) / cht; };
+  auto clen = [&](int x, uint64_t j) { return std::min<uint64_t>(cht, S(x) - j * cht); };
+  // relay part size of chunk j of pair x (0: chunk goes direct only)
+  auto u_of = [&](int x, uint64_t j) -> uint64_t {
+    const uint64_t c = clen(x, j);
+    return c >= (uint64_t)relay_min * (uint64_t)P ? c / (uint64_t)P : 0;
+  };
+  auto d_of = [&](int x, uint64_t j) { return clen(x, j) - (uint64_t)(P - 2) * u_of(x, j); };
+  // relays of pair x: ranks other than x and to[x], increasing
+  auto relays = [&](int x) {
+    std::vector<int> v;
+    for (int k = 0; k < P; k++)
+      if (k != x && k != to[(size_t)x]) v.push_back(k);
+    return v;
+  };
+  // pairs rank r relays for (x != r, to[x] != r), increasing x -> staging index
+  std::vector<int> mine;
+  for (int x = 0; x < P; x++)
+    if (x != r && to[(size_t)x] != r) mine.push_back(x);
+  uint64_t umax = 0;
+  for (int x = 0; x < P; x++)
+    for (uint64_t j = 0; j < nch(x); j++) umax = std::max(umax, u_of(x, j));
+  stage_elems = std::max(stage_elems, 2 * (uint64_t)mine.size() * umax);
+  auto stage_off = [&](uint64_t slot, size_t idx) { return (slot * mine.size() + idx) * umax; };
+
+  uint64_t rounds = 0;
+  for (int x = 0; x < P; x++) rounds = std::max(rounds, nch(x) + 1);
+  const Perm &me = steps[(size_t)r];
+  const int qsrc = from[(size_t)r];
+  const std::vector<int> my_relays = relays(r), in_relays = relays(qsrc);
+  uint64_t reduced = 0;  // pipelined reduction chunks emitted so far
+  for (uint64_t j = 0; j < rounds; j++) {
+    SOp o{true, {}, -1};
+    // sends: direct and first hops of my chunk j, then forwards of chunk j-1
+    if (j < nch(r)) {
+      const uint64_t base = me.send.src_off + j * cht, d = d_of(r, j), u = u_of(r, j);
+      o.prims.push_back(mk(BINE_PRIM_SEND, to[(size_t)r], me.send.src_buf, base, d));
+      if (u)
+        for (size_t i = 0; i < my_relays.size(); i++)
+          o.prims.push_back(mk(BINE_PRIM_SEND, my_relays[i], me.send.src_buf, base + d + i * u, u));
+    }
+    if (j >= 1)
+      for (size_t idx = 0; idx < mine.size(); idx++) {
+        const int x = mine[idx];
+        if (j - 1 < nch(x) && u_of(x, j - 1))
+          o.prims.push_back(mk(BINE_PRIM_SEND, to[(size_t)x], BINE_BUF_STAGE, stage_off((j - 1) % 2, idx),
+                               u_of(x, j - 1)));
+      }
+    // receives: direct part of chunk j, first hops I relay, second hops of chunk j-1
+    if (j < nch(qsrc))
+      o.prims.push_back(mk(BINE_PRIM_RECV, qsrc, me.recv.dst_buf, me.recv.dst_off + j * cht, d_of(qsrc, j)));
+    for (size_t idx = 0; idx < mine.size(); idx++) {
+      const int x = mine[idx];
+      if (j < nch(x) && u_of(x, j))
+        o.prims.push_back(mk(BINE_PRIM_RECV, x, BINE_BUF_STAGE, stage_off(j % 2, idx), u_of(x, j)));
+    }
+    if (j >= 1 && j - 1 < nch(qsrc) && u_of(qsrc, j - 1)) {
+      const uint64_t u = u_of(qsrc, j - 1), base = me.recv.dst_off + (j - 1) * cht + d_of(qsrc, j - 1);
+      for (size_t i = 0; i < in_relays.size(); i++)
+        o.prims.push_back(mk(BINE_PRIM_RECV, in_relays[i], me.recv.dst_buf, base + i * u, u));
+    }
+    if (!o.prims.empty()) ops.push_back(std::move(o));
+    // chunk j-1 of my receive is complete after round j
+    if (q && j >= 1) {
+      const uint64_t lo = (j - 1) * cht;
+      if (lo < q->count) {
+        ops.push_back({false, {slice(*q, lo, std::min<uint64_t>(cht, q->count - lo))}, -1});
+        reduced = j;
+      }
+    }
+  }
+  if (q)
+    for (uint64_t k = reduced; k * cht < q->count; k++)
+      ops.push_back({false, {slice(*q, k * cht, std::min<uint64_t>(cht, q->count - k * cht))}, -1});
+}
+
+// chunked (or whole) exchange group g of `pl`, plus the pipelined reduction
+// that follows it when `pipe`
+void emit_direct(const Plan &pl, std::pair<size_t, size_t> g, bool pipe, size_t ch, std::vector<SOp> &ops) {
+  const auto &pr = pl.prims;
+  if (!pipe) {
+    ops.push_back({true, std::vector<Prim>(pr.begin() + (long)g.first, pr.begin() + (long)g.second), -1});
+    return;
+  }
+  const Prim &S = pr[g.first].type == BINE_PRIM_SEND ? pr[g.first] : pr[g.first + 1];
+  const Prim &R = pr[g.first].type == BINE_PRIM_RECV ? pr[g.first] : pr[g.first + 1];
+  const Prim &Q = pr[g.second];
+  // both ends derive the chunk count from the same two sizes (my send is the
+  // peer's receive and vice versa), so the k-th groups pair up
+  const uint64_t nch = std::max((S.count + ch - 1) / ch, (R.count + ch - 1) / ch);
+  for (uint64_t k = 0; k < nch; k++) {
+    const uint64_t o = k * ch;
+    SOp x{true, {}, -1};
+    if (o < S.count) {
+      Prim a = S;
+      a.src_off += o;
+      a.count = std::min<uint64_t>(ch, S.count - o);
+      x.prims.push_back(a);
+    }
+    if (o < R.count) {
+      Prim a = R;
+      a.dst_off += o;
+      a.count = std::min<uint64_t>(ch, R.count - o);
+      x.prims.push_back(a);
+    }
+    ops.push_back(x);
+    if (o < Q.count) ops.push_back({false, {slice(Q, o, std::min<uint64_t>(ch, Q.count - o))}, -1});
+  }
+}
+
+bool pipelined(const Plan &pl, std::pair<size_t, size_t> g, size_t ch) {
+  const auto &pr = pl.prims;
+  return ch && (pr[g.first].flags & BINE_PRIM_PIPELINE) && g.second - g.first == 2 && g.second < pr.size() &&
+         (pr[g.second].flags & BINE_PRIM_PIPELINE) &&
+         (pr[g.second].type == BINE_PRIM_REDUCE || pr[g.second].type == BINE_PRIM_REDUCE3);
+}
+
+}  // namespace
+
+void make_schedule(const Plan &plan, size_t ch, bool in_place, Schedule &out) {
+  SchedCfg cfg;
+  cfg.chunk = ch;
+  cfg.in_place = in_place;
+  make_schedule(plan, nullptr, 0, cfg, out);
+}
+
+void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, const SchedCfg &cfg, Schedule &out) {
+  const size_t ch = cfg.chunk;
+  out.ops.clear();
+  out.c_join = false;
+  out.final_wait = -1;
+  out.stage_elems = 0;
+  out.relayed_steps = 0;
+
+  // ---- which exchange groups are relayable permutation steps ----
+  const auto mg = groups_of(plan);
+  std::vector<std::vector<Perm>> perm(mg.size());
+  if (cfg.relay_min && all && all->size() >= 3) {
+    const int P = (int)all->size();
+    std::vector<std::vector<std::pair<size_t, size_t>>> gs((size_t)P);
+    bool same = true;
+    for (int x = 0; x < P && same; x++) {
+      gs[(size_t)x] = groups_of((*all)[(size_t)x]);
+      same = gs[(size_t)x].size() == mg.size();
+    }
+    for (size_t t = 0; same && t < mg.size(); t++) {
+      std::vector<Perm> st((size_t)P);
+      std::vector<int> hits((size_t)P, 0);
+      bool ok = true;
+      for (int x = 0; x < P && ok; x++) {
+        ok = one_send_one_recv((*all)[(size_t)x], gs[(size_t)x][t], st[(size_t)x]);
+        if (!ok) break;
+        const int y = st[(size_t)x].send.peer;
+        ok = y != x && y >= 0 && y < P;
+        if (ok) hits[(size_t)y]++;
+      }
+      for (int x = 0; x < P && ok; x++) ok = hits[(size_t)x] == 1;
+      for (int x = 0; x < P && ok; x++) {
+        const Perm &a = st[(size_t)x];
+        const Perm &b = st[(size_t)a.send.peer];  // the receiver
+        ok = b.recv.peer == x && b.recv.count == a.send.count;
+      }
+      if (ok) perm[t] = std::move(st);
+    }
+  }
+
+  // ---- ops in issue order ----
+  const auto &pr = plan.prims;
+  size_t t = 0;
+  for (size_t i = 0; i < pr.size();) {
+    if (!is_x(pr[i])) {
+      out.ops.push_back({false, {pr[i]}, -1});
+      i++;
+      continue;
+    }
+    const auto g = mg[t];
+    const bool pipe = pipelined(plan, g, ch);
+    if (!perm[t].empty()) {
+      const bool qpipe = (pr[g.first].flags & BINE_PRIM_PIPELINE) && g.second < pr.size() &&
+                         (pr[g.second].flags & BINE_PRIM_PIPELINE) &&
+                         (pr[g.second].type == BINE_PRIM_REDUCE || pr[g.second].type == BINE_PRIM_REDUCE3);
+      emit_relay(perm[t], rank, ch, cfg.relay_min, qpipe ? &pr[g.second] : nullptr, out.ops, out.stage_elems);
+      out.relayed_steps++;
+      i = g.second + (qpipe ? 1 : 0);
+    } else {
+      emit_direct(plan, g, pipe, ch, out.ops);
+      i = g.second + (pipe ? 1 : 0);
+    }
+    t++;
+  }
+
+  // ---- dependencies ----
+  auto reg = [&](int buf, uint64_t off, uint64_t n) {
+    return Reg{(cfg.in_place && buf == BINE_BUF_SBUF) ? BINE_BUF_RBUF : buf, off, off + n};
+  };
+  std::vector<Rec> hist;
+  hist.reserve(out.ops.size());
+  int64_t waited[2] = {-1, -1};  // per stream: newest op of the other stream already waited for
+  // bounded scan: past kWindow non-conflicting ops of the other stream, wait
+  // for the oldest of them instead, which orders everything older as well
+  constexpr int kWindow = 64;
+  for (auto &o : out.ops) {
+    Rec r;
+    r.xchg = o.xchg;
+    for (const Prim &p : o.prims) {
+      switch (p.type) {
+        case BINE_PRIM_SEND: r.rd.push_back(reg(p.src_buf, p.src_off, p.count)); break;
+        case BINE_PRIM_RECV: r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count)); break;
+        case BINE_PRIM_REDUCE:
+          r.rd.push_back(reg(p.src_buf, p.src_off, p.count));
+          r.rd.push_back(reg(p.dst_buf, p.dst_off, p.count));
+          r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
+          break;
+        case BINE_PRIM_REDUCE3:
+          r.rd.push_back(reg(p.src_buf, p.src_off, p.count));
+          r.rd.push_back(reg(p.aux_buf, p.aux_off, p.count));
+          r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
+          break;
+        default:  // COPY
+          r.rd.push_back(reg(p.src_buf, p.src_off, p.count));
+          r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
+      }
+    }
+    // the comm stream first orders itself after the caller's prior work
+    if (o.xchg) out.c_join = true;
+    const int s = o.xchg ? 1 : 0;
+    int64_t dep = -1, oldest = -1;
+    int seen = 0;
+    for (int64_t j = (int64_t)hist.size() - 1; j > waited[s]; j--) {
+      const Rec &h = hist[(size_t)j];
+      if (h.xchg == o.xchg) continue;
+      if (hit(h.wr, r.rd) || hit(h.wr, r.wr) || hit(h.rd, r.wr)) {
+        dep = j;
+        break;
+      }
+      oldest = j;
+      if (++seen >= kWindow) {
+        for (int64_t k = j - 1; k > waited[s]; k--)
+          if (hist[(size_t)k].xchg != o.xchg) {
+            dep = oldest;
+            break;
+          }
+        break;
+      }
+    }
+    if (dep >= 0) waited[s] = dep;
+    o.wait = dep;
+    hist.push_back(std::move(r));
+  }
+  // the caller's stream ends after the last exchange
+  for (int64_t j = (int64_t)out.ops.size() - 1; j >= 0; j--)
+    if (out.ops[(size_t)j].xchg) {
+      if (j > waited[0]) out.final_wait = j;
+      break;
+    }
+}
+
+}  // namespace bine

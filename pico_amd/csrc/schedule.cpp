@@ -945,152 +945,4 @@ Plan make_plan(const PlanArgs &a) {
   return b.p;
 }
 
-// ---------------------------------------------------------------------------
-// issue schedule (see bine_internal.h)
-// ---------------------------------------------------------------------------
-
-namespace {
-
-struct Reg { int b; uint64_t lo, hi; };
-
-struct Rec {
-  bool xchg;
-  std::vector<Reg> rd, wr;
-};
-
-bool hit(const std::vector<Reg> &a, const std::vector<Reg> &b) {
-  for (const auto &x : a)
-    for (const auto &y : b)
-      if (x.b == y.b && x.lo < y.hi && y.lo < x.hi) return true;
-  return false;
-}
-
-void expand_chunks(const Plan &plan, size_t ch, std::vector<SOp> &ops) {
-  const auto &pr = plan.prims;
-  ops.clear();
-  size_t i = 0;
-  while (i < pr.size()) {
-    const Prim &p = pr[i];
-    if (p.type != BINE_PRIM_SEND && p.type != BINE_PRIM_RECV) {
-      ops.push_back({false, {p}, -1});
-      i++;
-      continue;
-    }
-    size_t j = i;
-    while (j < pr.size() && (pr[j].type == BINE_PRIM_SEND || pr[j].type == BINE_PRIM_RECV) && pr[j].group == p.group)
-      j++;
-    const bool pipe = ch && (p.flags & BINE_PRIM_PIPELINE) && j - i == 2 && j < pr.size() &&
-                      (pr[j].flags & BINE_PRIM_PIPELINE) &&
-                      (pr[j].type == BINE_PRIM_REDUCE || pr[j].type == BINE_PRIM_REDUCE3);
-    if (!pipe) {
-      ops.push_back({true, std::vector<Prim>(pr.begin() + (long)i, pr.begin() + (long)j), -1});
-      i = j;
-      continue;
-    }
-    const Prim &S = pr[i].type == BINE_PRIM_SEND ? pr[i] : pr[i + 1];
-    const Prim &R = pr[i].type == BINE_PRIM_RECV ? pr[i] : pr[i + 1];
-    const Prim &Q = pr[j];
-    // both ends derive the chunk count from the same two sizes (my send is the
-    // peer's receive and vice versa), so the k-th groups pair up
-    const uint64_t nch = std::max((S.count + ch - 1) / ch, (R.count + ch - 1) / ch);
-    for (uint64_t k = 0; k < nch; k++) {
-      const uint64_t o = k * ch;
-      SOp x{true, {}, -1};
-      if (o < S.count) {
-        Prim a = S;
-        a.src_off += o;
-        a.count = std::min<uint64_t>(ch, S.count - o);
-        x.prims.push_back(a);
-      }
-      if (o < R.count) {
-        Prim a = R;
-        a.dst_off += o;
-        a.count = std::min<uint64_t>(ch, R.count - o);
-        x.prims.push_back(a);
-      }
-      ops.push_back(x);
-      if (o < Q.count) {
-        Prim q = Q;
-        q.src_off += o;
-        q.dst_off += o;
-        q.aux_off += o;
-        q.count = std::min<uint64_t>(ch, Q.count - o);
-        ops.push_back({false, {q}, -1});
-      }
-    }
-    i = j + 1;
-  }
-}
-
-}  // namespace
-
-void make_schedule(const Plan &plan, size_t ch, bool in_place, Schedule &out) {
-  expand_chunks(plan, ch, out.ops);
-  out.c_join = false;
-  out.final_wait = -1;
-  auto reg = [&](int buf, uint64_t off, uint64_t n) {
-    return Reg{(in_place && buf == BINE_BUF_SBUF) ? BINE_BUF_RBUF : buf, off, off + n};
-  };
-  std::vector<Rec> hist;
-  hist.reserve(out.ops.size());
-  int64_t waited[2] = {-1, -1};  // per stream: newest op of the other stream already waited for
-  // bounded scan: past kWindow non-conflicting ops of the other stream, wait
-  // for the oldest of them instead, which orders everything older as well
-  constexpr int kWindow = 64;
-  for (auto &o : out.ops) {
-    Rec r;
-    r.xchg = o.xchg;
-    for (const Prim &p : o.prims) {
-      switch (p.type) {
-        case BINE_PRIM_SEND: r.rd.push_back(reg(p.src_buf, p.src_off, p.count)); break;
-        case BINE_PRIM_RECV: r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count)); break;
-        case BINE_PRIM_REDUCE:
-          r.rd.push_back(reg(p.src_buf, p.src_off, p.count));
-          r.rd.push_back(reg(p.dst_buf, p.dst_off, p.count));
-          r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
-          break;
-        case BINE_PRIM_REDUCE3:
-          r.rd.push_back(reg(p.src_buf, p.src_off, p.count));
-          r.rd.push_back(reg(p.aux_buf, p.aux_off, p.count));
-          r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
-          break;
-        default:  // COPY
-          r.rd.push_back(reg(p.src_buf, p.src_off, p.count));
-          r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
-      }
-    }
-    // the comm stream first orders itself after the caller's prior work
-    if (o.xchg && !out.c_join) out.c_join = true;
-    const int s = o.xchg ? 1 : 0;
-    int64_t dep = -1, oldest = -1;
-    int seen = 0;
-    for (int64_t j = (int64_t)hist.size() - 1; j > waited[s]; j--) {
-      const Rec &h = hist[(size_t)j];
-      if (h.xchg == o.xchg) continue;
-      if (hit(h.wr, r.rd) || hit(h.wr, r.wr) || hit(h.rd, r.wr)) {
-        dep = j;
-        break;
-      }
-      oldest = j;
-      if (++seen >= kWindow) {
-        for (int64_t k = j - 1; k > waited[s]; k--)
-          if (hist[(size_t)k].xchg != o.xchg) {
-            dep = oldest;
-            break;
-          }
-        break;
-      }
-    }
-    if (dep >= 0) waited[s] = dep;
-    o.wait = dep;
-    hist.push_back(std::move(r));
-  }
-  // the caller's stream ends after the last exchange
-  for (int64_t j = (int64_t)out.ops.size() - 1; j >= 0; j--)
-    if (out.ops[(size_t)j].xchg) {
-      if (j > waited[0]) out.final_wait = j;
-      break;
-    }
-}
-
 }  // namespace bine

@@ -27,21 +27,22 @@ class PlanError(AssertionError):
     pass
 
 
-def scheduled_prims(coll, algo, P, r, chunk_bytes, **kw):
+def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, **kw):
     """The executor's issue schedule (pico_amd.schedule) flattened back into a
     primitive list in issue order, one exchange group per op."""
-    ops, _, _ = pico_amd.schedule(coll, algo, P, r, chunk_bytes=chunk_bytes, **kw)
+    ops, _, _, info = pico_amd.schedule(coll, algo, P, r, chunk_bytes=chunk_bytes, relay_min_bytes=relay,
+                                        info=True, **kw)
     out = []
     for i, o in enumerate(ops):
         for p in o["prims"]:
             q = dict(p)
             q["group"] = i
             out.append(q)
-    return out
+    return out, info["stage_elems"]
 
 
 def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_place=False,
-        rbufs=None, chunk_bytes=None):
+        rbufs=None, chunk_bytes=None, relay=0):
     """chunk_bytes != None: run the executor's chunked issue schedule instead of
     the plan itself (same semantics when ops run in issue order)."""
     P = len(sbufs)
@@ -52,7 +53,7 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         prims, tmp = pico_amd.plan(coll, algo, P, r, count=count, rcounts=rcounts, root=root, esz=esz,
                                    segsize=segsize, in_place=in_place)
         if chunk_bytes is not None:
-            prims = scheduled_prims(coll, algo, P, r, chunk_bytes, count=count, rcounts=rcounts, root=root,
+            prims, stage = scheduled_prims(coll, algo, P, r, chunk_bytes, relay=relay, count=count, rcounts=rcounts, root=root,
                                     esz=esz, segsize=segsize, in_place=in_place)
         plans.append(prims)
         if rbufs is not None:
@@ -69,6 +70,8 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
                 rb = sbufs[r].copy()
             sb = rb
         tbufs = [np.zeros(max(int(t), 1) + 16, O.NP_DTYPES[dtype]) for t in tmp]
+        # relay staging (BINE_BUF_STAGE), exactly as large as the executor allocates
+        tbufs.append(np.zeros(stage if chunk_bytes is not None else 0, O.NP_DTYPES[dtype]))
         bufs.append([sb, rb] + tbufs)
     pc = [0] * P
     sendq = collections.defaultdict(collections.deque)  # (src, dst) -> [(rank, idx)]

@@ -136,8 +136,10 @@ def comms(P):
     return _COMMS[P]
 
 
-def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, root=0, in_place=False):
+def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, root=0, in_place=False, relay=0):
     P = len(sbufs)
+    for c in comms(P):
+        c.set_relay(relay)
     esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
     n = sbufs[0].size
     ds = [to_dev(x, pad=64) for x in sbufs]
@@ -170,15 +172,20 @@ def _golden_groups():
     return sorted(g.items())
 
 
+@pytest.mark.parametrize("relay", [0, 16], ids=["direct", "relay"])
 @pytest.mark.parametrize("key,cs", _golden_groups(), ids=lambda x: ".".join(x) if isinstance(x, tuple) else "")
-def test_collectives_match_reference_goldens(dev, key, cs):
+def test_collectives_match_reference_goldens(dev, key, cs, relay):
+    """relay: the same cases with the multi-link relay schedule (two-hop
+    routes through the other ranks) -- results must not change a bit."""
     coll, algo = key
     bad = []
     for c in cs:
         P, N, dt = c["P"], c["N"], c["dtype"]
+        if relay and P < 3:
+            continue
         rk = G.rcounts(c) if coll == "reduce_scatter" else None
         sb = O.inputs(dt, sum(rk) if rk else N, P, c["seed_base"])
-        outs, st = run_loopback(coll, algo, sb, dt, c["op"], rk, c["segsize"])
+        outs, st = run_loopback(coll, algo, sb, dt, c["op"], rk, c["segsize"], relay=relay)
         if c["status"] != "ok" or any(c["rets"]):
             # the reference errors (rets), asserts or hangs (no_output): the product
             # returns the mapped status, or -- where the reference crashed on its own
@@ -212,15 +219,16 @@ def test_collectives_match_reference_goldens(dev, key, cs):
     assert not bad, bad[:8]
 
 
+@pytest.mark.parametrize("relay", [0, 4096], ids=["direct", "relay"])
 @pytest.mark.parametrize("algo", ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented"])
-def test_large_allreduce_digest_matches_reference(dev, algo):
+def test_large_allreduce_digest_matches_reference(dev, algo, relay):
     """N = 1,000,003 fp32, P = 8 against the reference's digests (segmented: the
     reference's own output carries its tail bug -> compared with remap's)."""
     seg = 65536 if algo == "bine_bdw_remap_segmented" else 0
     gal = "bine_bdw_remap" if algo == "bine_bdw_remap_segmented" else algo
     c = G.select(coll="allreduce", algo=gal, P=8, N=1000003, dtype="float", segsize=0)[0]
     sb = O.inputs("float", 1000003, 8)
-    outs, st = run_loopback("allreduce", algo, sb, "float", segsize=seg)
+    outs, st = run_loopback("allreduce", algo, sb, "float", segsize=seg, relay=relay)
     assert not any(st)
     assert G.check_rank_outputs(c, outs) == []
 
@@ -253,9 +261,10 @@ def test_large_reduce_scatter_checksum(dev):
     rc = [per] * P
     sb = O.inputs("float", per * P, P)
     want, _ = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
-    outs, st = run_loopback("reduce_scatter", "bine_permute_remap", sb, "float", rcounts=rc)
-    assert not any(st)
-    assert [host_checksum(o) for o in outs] == [host_checksum(w) for w in want]
+    for relay in (0, 65536):
+        outs, st = run_loopback("reduce_scatter", "bine_permute_remap", sb, "float", rcounts=rc, relay=relay)
+        assert not any(st)
+        assert [host_checksum(o) for o in outs] == [host_checksum(w) for w in want]
 
 
 # ---- RCCL transport (single rank on this box) --------------------------------------

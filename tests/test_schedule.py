@@ -159,3 +159,91 @@ def test_chunked_schedule_matches_oracle(coll, algo, P, chunk):
         want = O.reduce(algo, sb, dtype)[0]
         got = plan_sim.run(coll, algo, sb, dtype, chunk_bytes=chunk)
         assert np.array_equal(got[0], want)
+
+
+# ---- multi-link relay ---------------------------------------------------------
+
+RELAY_CASES = [
+    ("allreduce", "bine_bdw_remap", 4), ("allreduce", "bine_bdw_remap", 8), ("allreduce", "bine_bdw_static", 8),
+    ("allreduce", "rabenseifner", 6), ("allreduce", "bine_lat", 8), ("allreduce", "ring", 5), ("allreduce", "rabenseifner", 8),
+    ("allreduce", "bine_bdw_remap_segmented", 8), ("allreduce", "recursivedoubling", 4),
+    ("reduce_scatter", "bine_permute_remap", 8), ("reduce_scatter", "bine_send_remap", 4),
+    ("reduce_scatter", "bine_static", 8), ("reduce_scatter", "recursivehalving", 8), ("reduce_scatter", "ring", 6),
+    ("reduce_scatter", "butterfly", 8),
+    ("reduce", "bine_bdw", 8),
+]
+
+
+def _run_relay(coll, algo, P, chunk, relay, n=997):
+    dtype = "float"
+    if coll == "reduce_scatter":
+        rc = [n // P + (i % 2) for i in range(P)]
+        sb = O.inputs(dtype, sum(rc), P)
+        want = O.reduce_scatter(algo, sb, rc, dtype)[0]
+        got = plan_sim.run(coll, algo, sb, dtype, rcounts=rc, chunk_bytes=chunk, relay=relay)
+        return all(np.array_equal(got[r], want[r]) for r in range(P))
+    sb = O.inputs(dtype, n, P)
+    if coll == "allreduce":
+        want = O.allreduce(algo, sb, dtype, segsize=256)[0]
+        got = plan_sim.run(coll, algo, sb, dtype, segsize=256, chunk_bytes=chunk, relay=relay)
+        return all(np.array_equal(got[r], want[r]) for r in range(P))
+    want = O.reduce(algo, sb, dtype)[0]
+    got = plan_sim.run(coll, algo, sb, dtype, chunk_bytes=chunk, relay=relay)
+    return np.array_equal(got[0], want)
+
+
+@pytest.mark.parametrize("coll,algo,P", RELAY_CASES)
+@pytest.mark.parametrize("chunk,relay", [(0, 4), (256, 4), (1024, 16)])
+def test_relay_schedule_matches_oracle(coll, algo, P, chunk, relay):
+    assert _run_relay(coll, algo, P, chunk, relay)
+
+
+@pytest.mark.parametrize("coll,algo,P", RELAY_CASES)
+def test_relay_schedules_race_free(coll, algo, P):
+    for rank in range(P):
+        kw = dict(count=4099, esz=4, segsize=512)
+        if coll == "reduce_scatter":
+            kw = dict(rcounts=[500 + (i % 3) for i in range(P)], esz=4)
+        for chunk in (0, 1024):
+            ops, cj, fw = pico_amd.schedule(coll, algo, P, rank, chunk_bytes=chunk, relay_min_bytes=8, **kw)
+            check_race_free(ops, cj, fw, False)
+
+
+def _link_loads(coll, algo, P, **kw):
+    """bytes per directed link (src, dst) summed over each rank's schedule"""
+    loads = {}
+    for r in range(P):
+        ops, _, _ = pico_amd.schedule(coll, algo, P, r, **kw)
+        for o in ops:
+            for p in o["prims"]:
+                if p["type"] == "SEND":
+                    loads[(r, p["peer"])] = loads.get((r, p["peer"]), 0) + p["count"]
+    return loads
+
+
+def test_relay_spreads_steps_over_all_links():
+    """remap allreduce at P=8: direct execution puts each step on one link per
+    rank (3 peers per rank over the whole collective); relay uses all 7 links
+    and the busiest link carries ~4x less than direct execution's busiest."""
+    n = 1 << 20
+    kw = dict(count=n, esz=4, chunk_bytes=1 << 16)
+    direct = _link_loads("allreduce", "bine_bdw_remap", 8, **kw)
+    relay = _link_loads("allreduce", "bine_bdw_remap", 8, relay_min_bytes=1024, **kw)
+    assert {len({d for (s, d) in direct if s == r}) for r in range(8)} == {3}
+    assert {len({d for (s, d) in relay if s == r}) for r in range(8)} == {7}
+    assert sum(relay.values()) > sum(direct.values())  # two-hop parts cost extra bytes
+    # direct execution uses one link at a time: its time ~ a rank's total bytes;
+    # relay keeps all links busy: time ~ the busiest link's bytes (P/2 = 4x less)
+    direct_time = max(sum(v for (s, d), v in direct.items() if s == r) for r in range(8))
+    assert max(relay.values()) * 3.9 < direct_time
+
+
+def test_relay_off_for_non_permutation_steps():
+    """block-by-block exchanges of several blocks per group are left as they
+    are; only its final one-block step is relayed"""
+    a, _, _ = pico_amd.schedule("reduce_scatter", "bine_block_by_block", 8, 0, rcounts=[64] * 8)
+    b, _, _ = pico_amd.schedule("reduce_scatter", "bine_block_by_block", 8, 0, rcounts=[64] * 8,
+                                relay_min_bytes=4)
+    multi = [i for i, o in enumerate(a) if o["xchg"] and len(o["prims"]) > 2]
+    assert multi and a[:max(multi) + 1] == b[:max(multi) + 1]
+    assert len(b) > len(a)

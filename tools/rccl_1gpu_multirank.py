@@ -6,7 +6,7 @@ so each rank claims a different host id (NCCL_HOSTID) and RCCL connects them
 over its socket network transport on the loopback interface.  This validates
 the executor's RCCL path (grouping, stream/event hand-offs, chunked pipeline,
 exact counts) with real multi-process RCCL; it says nothing about xGMI speed.
-usage: python tools/rccl_1gpu_multirank.py [P]
+usage: python tools/rccl_1gpu_multirank.py [P] [relay_min_bytes]
 """
 import os
 import sys
@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(rank, P, port, q):
+def worker(rank, P, port, q, relay=0):
     os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
@@ -28,6 +28,7 @@ def worker(rank, P, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
     comm = pico_amd.Comm.from_torch_distributed(0)
+    comm.set_relay(relay)
     ok = True
     for algo, n, seg in (("bine_bdw_remap", 100003, 0), ("bine_bdw_remap", 100003, 4096),
                          ("bine_bdw_static", 4099, 0), ("ring", 4099, 0), ("bine_lat", 333, 0),
@@ -41,7 +42,7 @@ def worker(rank, P, port, q):
         comm.synchronize()
         same = np.array_equal(r.cpu().numpy(), want[rank])
         ok &= same
-        print(f"rank {rank} {algo} n={n} seg={seg}: {'ok' if same else 'MISMATCH'}", flush=True)
+        print(f"rank {rank} {algo} n={n} seg={seg} relay={relay}: {'ok' if same else 'MISMATCH'}", flush=True)
     rc = [4096] * P
     sb = O.inputs("float", sum(rc), P)
     want, _ = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
@@ -60,9 +61,10 @@ def worker(rank, P, port, q):
 if __name__ == "__main__":
     import multiprocessing as mp
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    relay = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, P, 29555, q)) for r in range(P)]
+    ps = [ctx.Process(target=worker, args=(r, P, 29555, q, relay)) for r in range(P)]
     for p in ps:
         p.start()
     for p in ps:
