@@ -12,7 +12,10 @@ so that no launch is served from the 256 MiB Infinity Cache.
 N > 1 (torch.distributed.run, one process per GPU): BASELINE config C3,
 allreduce_bine_bdw_remap fp32 256 MiB per rank over RCCL P2P / xGMI.
 value = whole-job algorithmic throughput = N * 256 MiB / t; per-rank busbw
-2 (N-1)/N * S / t and algbw S / t are reported beside it.
+2 (N-1)/N * S / t and algbw S / t are reported beside it.  The transport is
+either the literal Bine schedule (one peer per step) or its multi-link relay
+(same schedule, parts routed over two hops through the other ranks, identical
+results); --relay auto (default) times both briefly and keeps the faster.
 
 Timing: W untimed warm-up steps, then K steps between a barrier +
 device synchronize on both sides, HIP events on the stream the kernels run on,
@@ -116,21 +119,8 @@ def bench_c2(steps: int, warmup: int):
     }
 
 
-def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str):
-    import torch
-    import torch.distributed as dist
-    import pico_amd
-    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    dist.init_process_group("gloo")
-    comm = pico_amd.Comm.from_torch_distributed(local)
-    dev = torch.device("cuda", local)
-    sbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
-    rbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
-    pico_amd.fill_pico(sbuf, nelem, "float", 1234 + rank)
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
+def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup):
+    """max-over-ranks ms per allreduce and wall seconds of `steps` timed calls"""
     for _ in range(warmup):
         pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
     torch.cuda.synchronize()
@@ -147,13 +137,58 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str):
     comm.synchronize()
     wall = time.perf_counter() - t0
     dist.barrier()
-    ms_local = e0.elapsed_time(e1) / steps
-    t = torch.tensor([ms_local, wall], dtype=torch.float64)
+    t = torch.tensor([e0.elapsed_time(e1) / steps, wall], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ms, wall = float(t[0]), float(t[1])
+    return float(t[0]), float(t[1])
+
+
+RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
+
+
+def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str):
+    import torch
+    import torch.distributed as dist
+    import pico_amd
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if os.environ.get("BINE_FAKE_HOSTS") == "1":
+        # rehearsal with several ranks on one GPU: RCCL needs distinct host ids
+        # (socket transport on lo; says nothing about xGMI speed)
+        os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    local %= torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo")
+    comm = pico_amd.Comm.from_torch_distributed(local)
+    dev = torch.device("cuda", local)
+    sbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
+    rbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
+    pico_amd.fill_pico(sbuf, nelem, "float", 1234 + rank)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    # transport: direct (one peer per step, the literal Bine schedule) or the
+    # multi-link relay of the same schedule (identical results); "auto" times
+    # both briefly and keeps the faster -- all ranks see the same max timings
+    modes = {"off": [0], "auto": [0, RELAY_MIN_BYTES]}.get(relay, None) or [int(relay)]
+    trials = {}
+    if len(modes) > 1 and world > 2:
+        for m in modes:
+            comm.set_relay(m)
+            trials[m] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
+        chosen = min(trials, key=trials.get)
+    else:
+        chosen = modes[0] if world > 2 else 0
+    comm.set_relay(chosen)
+    ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
+    # bytes this rank puts on xGMI per allreduce (from the executed schedule)
+    ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4,
+                                  chunk_bytes=16 << 20, relay_min_bytes=chosen)
+    egress = 4 * sum(p["count"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND")
+    peers = len({p["peer"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND"})
+    link_peak = XGMI_LINK_GBS * (7 if chosen else 1)
     out = None
     if rank == 0:
         out = {
@@ -163,11 +198,16 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str):
             "dtype": "f32", "data": "synthetic (pico_core rand_r distribution, generated on device)",
             "config": {"workload": f"C3: allreduce_{algo} fp32 {S // MIB} MiB/rank over RCCL P2P (xGMI), "
                                    f"{world} x MI355X", "value_definition": "N * S / t (whole job)",
-                       "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2)},
-            "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": XGMI_LINK_GBS, "unit": "GB/s",
-                         "frac": round(busbw / XGMI_LINK_GBS, 4), "traffic": None,
-                         "note": "faithful Bine: one peer (one xGMI link) per step; aggregate 7-link peak "
-                                 f"{7 * XGMI_LINK_GBS:.0f} GB/s -> frac {busbw / (7 * XGMI_LINK_GBS):.4f}"},
+                       "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
+                       "transport": "relay" if chosen else "direct", "relay_min_bytes": chosen,
+                       "transport_trials_ms": {("relay" if m else "direct"): round(v, 4) for m, v in trials.items()},
+                       "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers},
+            "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
+                         "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
+                         "traffic": egress,
+                         "note": "achieved = this rank's xGMI egress bytes (schedule) / t; peak = "
+                                 + ("7 links x 153 GB/s (relay keeps all links busy)" if chosen else
+                                    "one 153 GB/s link (direct Bine: one peer per step)")},
             "wall_s": round(wall, 4),
         }
     comm.destroy()
@@ -182,11 +222,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--algo", default="bine_bdw_remap")
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
+    ap.add_argument("--relay", default="auto", help="auto | off | <min relayed part bytes> (N > 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo)
+        res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay)
         if res is not None:
             print(json.dumps(res), flush=True)
         return
