@@ -73,7 +73,20 @@ typedef enum {
   BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN = 24, /* :1176 */
   /* reduce_* -- libbine_reduce.c */
   BINE_RD_BINE_LAT = 32,              /* reduce_bine_lat :16 */
-  BINE_RD_BINE_BDW = 33               /* reduce_bine_bdw :83 */
+  BINE_RD_BINE_BDW = 33,              /* reduce_bine_bdw :83 */
+  /* allgather, libbine_allgather.c */
+  BINE_AG_RECURSIVEDOUBLING = 48,     /* :18   */
+  BINE_AG_K_BRUCK = 49,               /* :88   */
+  BINE_AG_RING = 50,                  /* :213  */
+  BINE_AG_SPARBIT = 51,               /* :327  */
+  BINE_AG_BINE_BLOCK_BY_BLOCK = 52,   /* :410  */
+  BINE_AG_BINE_BLOCK_BY_BLOCK_ANY_EVEN = 53, /* :492 */
+  BINE_AG_BINE_PERMUTE_STATIC = 54,   /* :563  */
+  BINE_AG_BINE_SEND_STATIC = 55,      /* :642  */
+  BINE_AG_BINE_PERMUTE_REMAP = 56,    /* :725  */
+  BINE_AG_BINE_SEND_REMAP = 57,       /* :811  */
+  BINE_AG_BINE_2_BLOCKS = 58,         /* :892  */
+  BINE_AG_BINE_2_BLOCKS_DTYPE = 59    /* :999  */
 } bine_algo_t;
 
 /* the reference's MPI_IN_PLACE (mpi.h: (void *)-1) */
@@ -148,6 +161,14 @@ int bine_reduce_scatter(bine_comm_t comm, int algo, const void *sbuf, void *rbuf
 /* reduce_* (libbine.h:64-65).  rbuf is only read on `root` (may be NULL elsewhere). */
 int bine_reduce(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count,
                 int dtype, int op, int root, void *stream);
+/* allgather_* (libbine.h:39-50), scount = rcount = `count` elements per rank of
+ * one type (as pico_core calls them, pico_core_utils.c:511-514); rbuf holds
+ * nranks * count elements.  sbuf = BINE_IN_PLACE follows the reference: rank
+ * r's block is expected where that algorithm's in-place path expects it (block
+ * r; block perm[r] / remap[r] for the permute variants); the send and
+ * any_even variants have no in-place path (BINE_ERR_ARG). */
+int bine_allgather(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count,
+                   int dtype, void *stream);
 
 /* ---- loopback drivers: run one collective on all virtual ranks ---------------
  * (one host thread per rank; returns the first non-success status) */
@@ -160,6 +181,9 @@ int bine_loopback_run_reduce_scatter(bine_comm_t *comms, int nranks, int algo,
 int bine_loopback_run_reduce(bine_comm_t *comms, int nranks, int algo,
                              const void *const *sbufs, void *const *rbufs, size_t count,
                              int dtype, int op, int root, int *statuses);
+int bine_loopback_run_allgather(bine_comm_t *comms, int nranks, int algo,
+                                const void *const *sbufs, void *const *rbufs, size_t count,
+                                int dtype, int *statuses);
 
 /* ---- schedule introspection (host only, no GPU needed) ----------------------
  * A plan is the ordered list of primitives one rank executes. */

@@ -248,32 +248,35 @@ int orc_static_tables(int P, int *perm, int *send_tab, int *recv_tab) {
 
 #define ANY_SRC (-7)
 
-typedef struct { int src, dst; size_t bytes; char *data; int used; } msg_t;
-typedef struct { int src, dst; char *ptr; size_t cap; } rcv_t;
+typedef struct { int src, dst, tag; size_t bytes; char *data; int used; } msg_t;
+typedef struct { int src, dst, tag; char *ptr; size_t cap; } rcv_t;
 typedef struct {
   msg_t *m; int nm, cm;
   rcv_t *r; int nr, cr;
 } board_t;
 
-static void b_send(board_t *b, int src, int dst, const void *p, size_t bytes) {
+static void b_send_t(board_t *b, int src, int dst, const void *p, size_t bytes, int tag) {
   if (dst < 0) return;                       /* MPI_PROC_NULL */
   if (b->nm == b->cm) { b->cm = b->cm ? 2 * b->cm : 16; b->m = (msg_t *)realloc(b->m, sizeof(msg_t) * (size_t)b->cm); }
   msg_t *x = &b->m[b->nm++];
-  x->src = src; x->dst = dst; x->bytes = bytes; x->used = 0;
+  x->src = src; x->dst = dst; x->tag = tag; x->bytes = bytes; x->used = 0;
   x->data = (char *)malloc(bytes ? bytes : 1);
   if (bytes) memcpy(x->data, p, bytes);
 }
 
-static void b_recv(board_t *b, int dst, int src, void *p, size_t cap) {
+static void b_recv_t(board_t *b, int dst, int src, void *p, size_t cap, int tag) {
   if (src == -1) return;                     /* MPI_PROC_NULL */
   if (b->nr == b->cr) { b->cr = b->cr ? 2 * b->cr : 16; b->r = (rcv_t *)realloc(b->r, sizeof(rcv_t) * (size_t)b->cr); }
   rcv_t *x = &b->r[b->nr++];
-  x->src = src; x->dst = dst; x->ptr = (char *)p; x->cap = cap;
+  x->src = src; x->dst = dst; x->tag = tag; x->ptr = (char *)p; x->cap = cap;
 }
 
-/* Deliver every posted receive (per-pair FIFO, MPI's non-overtaking rule).
- * Truncation marks the receiving rank's return code; an unmatched send or
- * receive means the reference would block forever. */
+static void b_send(board_t *b, int src, int dst, const void *p, size_t bytes) { b_send_t(b, src, dst, p, bytes, 0); }
+static void b_recv(board_t *b, int dst, int src, void *p, size_t cap) { b_recv_t(b, dst, src, p, cap, 0); }
+
+/* Deliver every posted receive (per-pair, per-tag FIFO: MPI's non-overtaking
+ * rule).  Truncation marks the receiving rank's return code; an unmatched send
+ * or receive means the reference would block forever. */
 static int b_deliver(board_t *b, int *rets) {
   int status = 0;
   for (int i = 0; i < b->nr; i++) {
@@ -281,7 +284,7 @@ static int b_deliver(board_t *b, int *rets) {
     msg_t *hit = NULL;
     for (int j = 0; j < b->nm; j++) {
       msg_t *m = &b->m[j];
-      if (!m->used && m->dst == r->dst && (r->src == ANY_SRC || m->src == r->src)) { hit = m; break; }
+      if (!m->used && m->dst == r->dst && m->tag == r->tag && (r->src == ANY_SRC || m->src == r->src)) { hit = m; break; }
     }
     if (!hit) { status = ORC_DEADLOCK; continue; }
     hit->used = 1;
@@ -1330,6 +1333,331 @@ int orc_reduce(const char *algo, int P, size_t count, int dtype, int op,
   int known = 1;
   if (!strcmp(algo, "bine_lat")) rd_bine_lat(&c, count, root, S, R, rets);
   else if (!strcmp(algo, "bine_bdw")) rd_bine_bdw(&c, count, root, S, R, rets);
+  else known = 0;
+  if (c.dead) for (int r = 0; r < P; r++) if (rets[r] == ORC_OK) rets[r] = c.dead;
+  b_free(&c.b);
+  return known ? 0 : -1;
+}
+
+/* ----------------------------------------------------------------------- */
+/* allgather -- libbine_allgather.c                                          */
+/* ----------------------------------------------------------------------- */
+/* R[r] holds P * count elements (pico_core callocs it,
+ * pico_core_allgather_utils.c:20).  inpl = MPI_IN_PLACE: S is unused and rank
+ * r's block already sits in R[r] where the algorithm expects it.  Each
+ * COPY_BUFF_DIFF_DT / copy_buffer with a zero count returns MPI_ERR_UNKNOWN
+ * (libbine_utils.h:176-215). */
+
+#define BLK(r, b) EL(R[r], (size_t)(b) * count)
+
+/* copy_buffer_different_dt with equal types, libbine_utils.h:207-228 */
+static int cpy(const void *src, void *dst, size_t n, size_t esz) {
+  if (n == 0 || !src || !dst) return ORC_ERR_UNKNOWN;
+  memmove(dst, src, n * esz);
+  return ORC_OK;
+}
+
+/* allgather_recursivedoubling, :18-86.  Non-power-of-two P jumps to the error
+ * label with err still MPI_SUCCESS (:31-34): nothing happens, success. */
+static void ag_recursivedoubling(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets) {
+  int P = c->P; size_t esz = c->esz;
+  if (!is_pow2(P)) return;
+  for (int r = 0; r < P; r++)
+    if (!inpl && (rets[r] = cpy(S[r], BLK(r, r), count, esz))) return;
+  int *sbl = (int *)malloc(sizeof(int) * (size_t)P);
+  for (int r = 0; r < P; r++) sbl[r] = r;
+  for (int d = 1; d < P; d <<= 1) {
+    for (int r = 0; r < P; r++) {
+      int remote = r ^ d;
+      int rb = r < remote ? sbl[r] + d : sbl[r] - d;
+      b_send(&c->b, r, remote, BLK(r, sbl[r]), (size_t)d * count * esz);
+      b_recv(&c->b, r, remote, BLK(r, rb), (size_t)d * count * esz);
+      if (r > remote) sbl[r] -= d;
+    }
+    deliver(c, rets);
+  }
+  free(sbl);
+}
+
+/* allgather_k_bruck, radix 2, :88-211 */
+static void ag_k_bruck(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets) {
+  int P = c->P; size_t esz = c->esz;
+  for (int r = 0; r < P; r++) {
+    if (!inpl) rets[r] = cpy(S[r], BLK(r, 0), count, esz);
+    else if (r != 0) rets[r] = cpy(BLK(r, r), BLK(r, 0), count, esz);
+    if (rets[r]) return;
+  }
+  for (int d = 1; d < P; d *= 2) {                                   /* :158-181 */
+    size_t rc = d <= P / 2 ? (size_t)d : (size_t)(d < P - d ? d : P - d);
+    for (int r = 0; r < P; r++) {
+      b_recv(&c->b, r, (r + d) % P, BLK(r, d), rc * count * esz);
+      b_send(&c->b, r, (r - d + P) % P, BLK(r, 0), rc * count * esz);
+    }
+    deliver(c, rets);
+  }
+  for (int r = 1; r < P; r++) {                                      /* :185-196 */
+    size_t hi = (size_t)(P - r) * count;
+    char *t = (char *)malloc(hi * esz);
+    memcpy(t, BLK(r, 0), hi * esz);
+    memmove(BLK(r, 0), BLK(r, P - r), (size_t)r * count * esz);
+    memcpy(BLK(r, r), t, hi * esz);
+    free(t);
+  }
+}
+
+/* allgather_ring, :213-270 */
+static void ag_ring(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets) {
+  int P = c->P; size_t esz = c->esz;
+  for (int r = 0; r < P; r++)
+    if (!inpl && (rets[r] = cpy(S[r], BLK(r, r), count, esz))) return;
+  for (int i = 0; i < P - 1; i++) {
+    for (int r = 0; r < P; r++) {
+      b_send(&c->b, r, (r + 1) % P, BLK(r, (r - i + P) % P), count * esz);
+      b_recv(&c->b, r, (r - 1 + P) % P, BLK(r, (r - i - 1 + P) % P), count * esz);
+    }
+    deliver(c, rets);
+  }
+}
+
+/* allgather_sparbit, :327-408 (tags = block displacement) */
+static void ag_sparbit(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets) {
+  int P = c->P; size_t esz = c->esz;
+  for (int r = 0; r < P; r++)
+    if (!inpl && (rets[r] = cpy(S[r], BLK(r, r), count, esz))) return;
+  int L = log_2(P), expected = 1;
+  uint32_t d = L >= 1 ? 1u << (L - 1) : 0;
+  uint32_t last_ignore = (uint32_t)__builtin_ctz((unsigned)P);
+  uint32_t ignore = (~((uint32_t)P >> last_ignore) | 1u) << last_ignore;
+  for (int i = 0; i < L; i++) {
+    int excl = (d & ignore) == d;
+    for (int r = 0; r < P; r++) {
+      int to = (int)((r + (int)d) % P), from = (int)((r - (int)d + P) % P);
+      for (int t = 0; t < expected - excl; t++) {
+        int sd = (r - 2 * t * (int)d + P) % P, rd = (r - (2 * t + 1) * (int)d + P) % P;
+        b_send_t(&c->b, r, to, BLK(r, sd), count * esz, sd);
+        b_recv_t(&c->b, r, from, BLK(r, rd), count * esz, rd);
+      }
+    }
+    deliver(c, rets);
+    d >>= 1;
+    expected = (expected << 1) - excl;
+  }
+}
+
+/* get_indexes / get_indexes_aux, libbine_utils.h:142-161 */
+static void idx_aux(int rank, int step, int n, int P, int *bm) {
+  for (int s = step; s < n; s++) { int p = orc_pi(rank, s, P); bm[p] = 1; idx_aux(p, s + 1, n, P, bm); }
+}
+static void get_indexes(int rank, int step, int n, int P, int *bm) {
+  if (step >= n) return;
+  int p = orc_pi(rank, step, P); bm[p] = 1; idx_aux(p, step + 1, n, P, bm);
+}
+
+/* allgather_bine_block_by_block, :410-490 (tag = block) */
+static void ag_bine_bbb(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets) {
+  int P = c->P; size_t esz = c->esz;
+  int steps = log_2(P);
+  if (!is_pow2(P) || steps < 1) { for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG; return; }
+  for (int r = 0; r < P; r++)
+    if (!inpl && (rets[r] = cpy(S[r], BLK(r, r), count, esz))) return;
+  int *sb = (int *)malloc(sizeof(int) * (size_t)P), *rb = (int *)malloc(sizeof(int) * (size_t)P);
+  for (int step = steps - 1; step >= 0; step--) {
+    for (int r = 0; r < P; r++) {
+      int remote = orc_pi(r, step, P);
+      memset(sb, 0, sizeof(int) * (size_t)P); memset(rb, 0, sizeof(int) * (size_t)P);
+      get_indexes(r, step, steps, P, rb);
+      get_indexes(remote, step, steps, P, sb);
+      for (int b = 0; b < P; b++) {
+        if (sb[b]) b_send_t(&c->b, r, remote, BLK(r, b), count * esz, b);
+        if (rb[b]) b_recv_t(&c->b, r, remote, BLK(r, b), count * esz, b);
+      }
+    }
+    deliver(c, rets);
+  }
+  free(sb); free(rb);
+}
+
+/* allgather_bine_block_by_block_any_even, :492-561 (always copies sbuf) */
+static void ag_bine_bbb_any_even(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets) {
+  int P = c->P; size_t esz = c->esz;
+  if (inpl) { for (int r = 0; r < P; r++) rets[r] = ORC_ASSERT; return; }   /* memcpy from MPI_IN_PLACE */
+  for (int r = 0; r < P; r++) if (count) memcpy(BLK(r, r), S[r], count * esz);
+  int inv = (int)(1u << ((unsigned)(log_2(P) - 1) & 31u)), step = 0;
+  while (inv > 0) {
+    for (int r = 0; r < P; r++) {
+      int d = nb2b((uint32_t)((inv << 1) - 1));
+      int partner = r % 2 == 0 ? mod(r + d, P) : mod(r - d, P);
+      for (int b = 1; b < P; b++) {
+        int k = 31 - __builtin_clz(orc_get_nu((uint32_t)b, (uint32_t)P));
+        if (k != step) continue;
+        int btr, bts;
+        if (r % 2 == 0) { btr = mod(b + r, P); bts = mod(partner - b, P); }
+        else { btr = mod(r - b, P); bts = mod(b + partner, P); }
+        b_send(&c->b, r, bts != partner ? partner : -1, BLK(r, bts), count * esz);
+        b_recv(&c->b, r, btr != r ? partner : -1, BLK(r, btr), count * esz);
+      }
+    }
+    deliver(c, rets);
+    inv >>= 1; step++;
+  }
+}
+
+/* reorder_blocks, libbine_utils.h:438-479: new[i] = old[perm[i]] */
+static void reorder(char *buf, size_t bb, const int *perm, int P) {
+  char *t = (char *)malloc(bb * (size_t)P);
+  memcpy(t, buf, bb * (size_t)P);
+  for (int i = 0; i < P; i++) memcpy(buf + (size_t)i * bb, t + (size_t)perm[i] * bb, bb);
+  free(t);
+}
+
+/* allgather_bine_permute_static (:563-640) and _send_static (:642-723) */
+static void ag_bine_static(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets, int permute) {
+  int P = c->P; size_t esz = c->esz;
+  int steps = log_2(P);
+  if (!is_pow2(P) || steps < 1 || steps > 8) { for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG; return; }
+  int *perm = (int *)malloc(sizeof(int) * (size_t)P);
+  int *st = (int *)malloc(sizeof(int) * (size_t)P * (size_t)steps), *rt = (int *)malloc(sizeof(int) * (size_t)P * (size_t)steps);
+  orc_static_tables(P, perm, st, rt);
+  if (permute) {
+    for (int r = 0; r < P; r++)
+      if (!inpl && (rets[r] = cpy(S[r], BLK(r, rt[r * steps + steps - 1]), count, esz))) goto out;
+  } else {
+    for (int r = 0; r < P; r++) {                                    /* :680-696 */
+      if (perm[r] != r) {
+        int to = -1;
+        for (int j = 0; j < P; j++) if (perm[j] == r) { to = j; break; }
+        b_send(&c->b, r, to, S[r], count * esz);
+        b_recv(&c->b, r, perm[r], BLK(r, perm[r]), count * esz);
+      } else if ((rets[r] = cpy(S[r], BLK(r, perm[r]), count, esz))) goto out;
+    }
+    deliver(c, rets);
+  }
+  size_t sc = count;
+  for (int step = steps - 1; step >= 0; step--) {                    /* :613-626 */
+    for (int r = 0; r < P; r++) {
+      int remote = orc_pi(r, step, P);
+      b_send(&c->b, r, remote, BLK(r, rt[r * steps + step]), sc * esz);
+      b_recv(&c->b, r, remote, BLK(r, st[r * steps + step]), sc * esz);
+    }
+    deliver(c, rets);
+    sc *= 2;
+  }
+  if (permute) for (int r = 0; r < P; r++) reorder(R[r], count * esz, perm, P);
+out:
+  free(perm); free(st); free(rt);
+}
+
+/* get_sender_rec, libbine_utils.h:585-594: x with remap_rank(x) == rank */
+static int sender_rec(int P, int rank) {
+  int x = rank;
+  for (;;) { int m = (int)orc_remap_rank((uint32_t)P, (uint32_t)x); if (m == rank) return x; x = m; }
+}
+
+/* allgather_bine_permute_remap (:725-809) and _send_remap (:811-890) */
+static void ag_bine_remap(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets, int permute) {
+  int P = c->P; size_t esz = c->esz;
+  int steps = log_2(P);
+  if (!is_pow2(P) || steps < 1 || steps > 8) { for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG; return; }
+  int *remap = (int *)malloc(sizeof(int) * (size_t)P), *sbl = (int *)malloc(sizeof(int) * (size_t)P);
+  for (int r = 0; r < P; r++) remap[r] = (int)orc_remap_rank((uint32_t)P, (uint32_t)r);
+  if (permute) {
+    for (int r = 0; r < P; r++)
+      if (!inpl && (rets[r] = cpy(S[r], BLK(r, remap[r]), count, esz))) goto out;
+  } else {
+    for (int r = 0; r < P; r++) {                                    /* :840-853 */
+      if (remap[r] != r) {
+        b_send(&c->b, r, sender_rec(P, r), S[r], count * esz);
+        b_recv(&c->b, r, remap[r], BLK(r, remap[r]), count * esz);
+      } else if ((rets[r] = cpy(S[r], BLK(r, remap[r]), count, esz))) goto out;
+    }
+    deliver(c, rets);
+  }
+  for (int r = 0; r < P; r++) sbl[r] = remap[r];
+  int d = 1;
+  for (int step = steps - 1; step >= 0; step--) {                    /* :776-795 */
+    for (int r = 0; r < P; r++) {
+      int remote = orc_pi(r, step, P), vr = remap[r], vrem = remap[remote];
+      int rb = vr < vrem ? sbl[r] + d : sbl[r] - d;
+      b_send(&c->b, r, remote, BLK(r, sbl[r]), (size_t)d * count * esz);
+      b_recv(&c->b, r, remote, BLK(r, rb), (size_t)d * count * esz);
+      if (!(vr < vrem)) sbl[r] -= d;
+    }
+    deliver(c, rets);
+    d <<= 1;
+  }
+  if (permute) for (int r = 0; r < P; r++) reorder(R[r], count * esz, remap, P);
+out:
+  free(remap); free(sbl);
+}
+
+/* allgather_bine_2_blocks (:892-997, extra wrap-around message with tag 1)
+ * and _2_blocks_dtype (:999-1106, one message packed by MPI_Type_indexed:
+ * wrapped head first, then the main run) */
+static void ag_bine_2_blocks(ctx_t *c, size_t count, char **S, char **R, int inpl, int *rets, int dtype_variant) {
+  int P = c->P; size_t esz = c->esz;
+  int steps = log_2(P);
+  if (!is_pow2(P) || steps < 1) { for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG; return; }
+  for (int r = 0; r < P; r++)
+    if (!inpl && (rets[r] = cpy(S[r], BLK(r, r), count, esz))) return;
+  int *first = (int *)malloc(sizeof(int) * (size_t)P);
+  int *ri = (int *)malloc(sizeof(int) * (size_t)P), *xr = (int *)malloc(sizeof(int) * (size_t)P);
+  char **stage = alloc_ranks(P, (size_t)P * count * esz);
+  for (int r = 0; r < P; r++) first[r] = r;
+  int mask = 1;
+  for (int step = 0; step < steps; step++) {
+    for (int r = 0; r < P; r++) {
+      int remote = orc_pi(r, step, P), si = first[r], rix;
+      if ((step & 1) == (r & 1)) rix = (si + mask + P) % P;
+      else { rix = (si - mask + P) % P; first[r] = rix; }
+      int xrv = rix + mask > P ? rix + mask - P : 0, xsd = si + mask > P ? si + mask - P : 0;
+      int rcn = mask - xrv, scn = mask - xsd;
+      ri[r] = rix; xr[r] = xrv;
+      if (!dtype_variant) {
+        if (xrv) b_recv_t(&c->b, r, remote, BLK(r, 0), (size_t)xrv * count * esz, 1);
+        if (xsd) b_send_t(&c->b, r, remote, BLK(r, 0), (size_t)xsd * count * esz, 1);
+        b_send(&c->b, r, remote, BLK(r, si), (size_t)scn * count * esz);
+        b_recv(&c->b, r, remote, BLK(r, rix), (size_t)rcn * count * esz);
+      } else {
+        char *pk = (char *)malloc((size_t)mask * count * esz + 1);
+        memcpy(pk, BLK(r, 0), (size_t)xsd * count * esz);
+        memcpy(pk + (size_t)xsd * count * esz, BLK(r, si), (size_t)scn * count * esz);
+        b_send(&c->b, r, remote, pk, (size_t)mask * count * esz);
+        free(pk);
+        b_recv(&c->b, r, remote, stage[r], (size_t)mask * count * esz);
+      }
+    }
+    deliver(c, rets);
+    if (dtype_variant)
+      for (int r = 0; r < P; r++) {
+        memcpy(BLK(r, 0), stage[r], (size_t)xr[r] * count * esz);
+        memcpy(BLK(r, ri[r]), stage[r] + (size_t)xr[r] * count * esz, (size_t)(mask - xr[r]) * count * esz);
+      }
+    mask <<= 1;
+  }
+  free(first); free(ri); free(xr); free_ranks(stage, P);
+}
+#undef BLK
+
+int orc_allgather(const char *algo, int P, size_t count, int dtype, int in_place,
+                  const void *const *sbufs, void *const *rbufs, int *rets) {
+  if (P < 1 || !orc_dtype_size(dtype)) return -1;
+  ctx_t c; memset(&c, 0, sizeof c);
+  c.P = P; c.dtype = dtype; c.esz = orc_dtype_size(dtype);
+  char **S = (char **)sbufs, **R = (char **)rbufs;
+  for (int r = 0; r < P; r++) rets[r] = ORC_OK;
+  int known = 1, ip = in_place != 0;
+  if (!strcmp(algo, "recursivedoubling")) ag_recursivedoubling(&c, count, S, R, ip, rets);
+  else if (!strcmp(algo, "k_bruck")) ag_k_bruck(&c, count, S, R, ip, rets);
+  else if (!strcmp(algo, "ring")) ag_ring(&c, count, S, R, ip, rets);
+  else if (!strcmp(algo, "sparbit")) ag_sparbit(&c, count, S, R, ip, rets);
+  else if (!strcmp(algo, "bine_block_by_block")) ag_bine_bbb(&c, count, S, R, ip, rets);
+  else if (!strcmp(algo, "bine_block_by_block_any_even")) ag_bine_bbb_any_even(&c, count, S, R, ip, rets);
+  else if (!strcmp(algo, "bine_permute_static")) ag_bine_static(&c, count, S, R, ip, rets, 1);
+  else if (!strcmp(algo, "bine_send_static")) ag_bine_static(&c, count, S, R, ip, rets, 0);
+  else if (!strcmp(algo, "bine_permute_remap")) ag_bine_remap(&c, count, S, R, ip, rets, 1);
+  else if (!strcmp(algo, "bine_send_remap")) ag_bine_remap(&c, count, S, R, ip, rets, 0);
+  else if (!strcmp(algo, "bine_2_blocks")) ag_bine_2_blocks(&c, count, S, R, ip, rets, 0);
+  else if (!strcmp(algo, "bine_2_blocks_dtype")) ag_bine_2_blocks(&c, count, S, R, ip, rets, 1);
   else known = 0;
   if (c.dead) for (int r = 0; r < P; r++) if (rets[r] == ORC_OK) rets[r] = c.dead;
   b_free(&c.b);

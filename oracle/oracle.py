@@ -52,6 +52,7 @@ def lib():
                                     sz, ctypes.c_int, vp, vp, vp]
         L.orc_reduce_scatter.argtypes = [ctypes.c_char_p, ctypes.c_int, vp, ctypes.c_int,
                                          ctypes.c_int, vp, vp, vp]
+        L.orc_allgather.argtypes = [ctypes.c_char_p, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int, vp, vp, vp]
         L.orc_reduce.argtypes = [ctypes.c_char_p, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, vp, vp, vp]
         _lib = L
@@ -125,6 +126,23 @@ def reduce(algo, sbufs, dtype, op="sum", root=0):
                         _ptrs(sbufs), _ptrs(rbufs), rets.ctypes.data):
         raise ValueError(algo)
     return rbufs[root], rets.tolist()
+
+
+def allgather(algo, sbufs, dtype, in_place_rbufs=None):
+    """sbufs[r]: rank r's count elements; returns (rbufs (P*count each), rets).
+    in_place_rbufs: MPI_IN_PLACE -- these P*count buffers already hold each
+    rank's block where the algorithm expects it (copied, not modified)."""
+    P = len(sbufs)
+    n = sbufs[0].size
+    if in_place_rbufs is not None:
+        rbufs = [np.array(b, dtype=NP_DTYPES[dtype]).copy() for b in in_place_rbufs]
+    else:
+        rbufs = [np.zeros(P * n, dtype=NP_DTYPES[dtype]) for _ in range(P)]
+    rets = np.zeros(P, np.int32)
+    if lib().orc_allgather(algo.encode(), P, n, DTYPES[dtype], int(in_place_rbufs is not None),
+                           _ptrs(sbufs), _ptrs(rbufs), rets.ctypes.data):
+        raise ValueError(algo)
+    return rbufs, rets.tolist()
 
 
 def rs_rcounts(N: int, P: int, kind: str = "even"):

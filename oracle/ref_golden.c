@@ -15,7 +15,9 @@
  *
  * usage: ref_golden <outdir> <coll> <algo> <op> <segsize> <rcounts_kind>
  *                   <seed_base> <dtype,dtype,...> <N,N,...>
- *   coll         allreduce | reduce_scatter | reduce | fill (dump the inputs)
+ *   coll         allreduce | reduce_scatter | reduce | allgather | fill (dump the inputs)
+ *                allgather: N = elements per rank (scount = rcount, same type,
+ *                pico_core_utils.c:511-514), rbuf = P * N zeroed elements
  *   rcounts_kind even   -> rcounts[i] = N / P  (pico_core_utils.c:535-536)
  *                ragged -> rcounts[i] = N / P + (i % 3)   (exercises displs)
  */
@@ -30,6 +32,7 @@
 typedef int (*ar_fn)(const void *, void *, size_t, MPI_Datatype, MPI_Op, MPI_Comm);
 typedef int (*rs_fn)(const void *, void *, const int *, MPI_Datatype, MPI_Op, MPI_Comm);
 typedef int (*rd_fn)(const void *, void *, size_t, MPI_Datatype, MPI_Op, int, MPI_Comm);
+typedef int (*ag_fn)(const void *, size_t, MPI_Datatype, void *, size_t, MPI_Datatype, MPI_Comm);
 
 static ar_fn pick_allreduce(const char *a) {
   if (!strcmp(a, "recursivedoubling")) return allreduce_recursivedoubling;
@@ -59,6 +62,22 @@ static rs_fn pick_reduce_scatter(const char *a) {
 static rd_fn pick_reduce(const char *a) {
   if (!strcmp(a, "bine_lat")) return reduce_bine_lat;
   if (!strcmp(a, "bine_bdw")) return reduce_bine_bdw;
+  return NULL;
+}
+
+static ag_fn pick_allgather(const char *a) {
+  if (!strcmp(a, "recursivedoubling")) return allgather_recursivedoubling;
+  if (!strcmp(a, "k_bruck")) return allgather_k_bruck;
+  if (!strcmp(a, "ring")) return allgather_ring;
+  if (!strcmp(a, "sparbit")) return allgather_sparbit;
+  if (!strcmp(a, "bine_block_by_block")) return allgather_bine_block_by_block;
+  if (!strcmp(a, "bine_block_by_block_any_even")) return allgather_bine_block_by_block_any_even;
+  if (!strcmp(a, "bine_permute_static")) return allgather_bine_permute_static;
+  if (!strcmp(a, "bine_send_static")) return allgather_bine_send_static;
+  if (!strcmp(a, "bine_permute_remap")) return allgather_bine_permute_remap;
+  if (!strcmp(a, "bine_send_remap")) return allgather_bine_send_remap;
+  if (!strcmp(a, "bine_2_blocks")) return allgather_bine_2_blocks;
+  if (!strcmp(a, "bine_2_blocks_dtype")) return allgather_bine_2_blocks_dtype;
   return NULL;
 }
 
@@ -135,8 +154,9 @@ int main(int argc, char **argv) {
         }
         outn = (size_t)rcounts[rank];
       }
+      if (!strcmp(coll, "allgather")) outn = N * (size_t)P;
       void *sbuf = malloc(total * esz + 16);
-      void *rbuf = calloc(total * esz + 16, 1);
+      void *rbuf = calloc(outn * esz + total * esz + 16, 1);
       fill(sbuf, dts[d], total, seed_base + (unsigned)rank);
       int ret = -12345;
       if (!strcmp(coll, "fill")) {           /* pins the input generator itself */
@@ -150,6 +170,10 @@ int main(int argc, char **argv) {
         rs_fn f = pick_reduce_scatter(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
         ret = f(sbuf, rbuf, rcounts, dt, op, MPI_COMM_WORLD);
+      } else if (!strcmp(coll, "allgather")) {
+        ag_fn f = pick_allgather(algo);
+        if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
+        ret = f(sbuf, N, dt, rbuf, N, dt, MPI_COMM_WORLD);
       } else if (!strcmp(coll, "reduce")) {
         rd_fn f = pick_reduce(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);

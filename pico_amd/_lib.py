@@ -30,6 +30,10 @@ ALGOS = {
                        "bine_permute_remap": 22, "bine_block_by_block": 23,
                        "bine_block_by_block_any_even": 24},
     "reduce": {"bine_lat": 32, "bine_bdw": 33},
+    "allgather": {"recursivedoubling": 48, "k_bruck": 49, "ring": 50, "sparbit": 51,
+                  "bine_block_by_block": 52, "bine_block_by_block_any_even": 53,
+                  "bine_permute_static": 54, "bine_send_static": 55, "bine_permute_remap": 56,
+                  "bine_send_remap": 57, "bine_2_blocks": 58, "bine_2_blocks_dtype": 59},
 }
 IN_PLACE = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)
 UNIQUE_ID_BYTES = 128
@@ -96,6 +100,8 @@ def lib():
         "bine_allreduce": ([vp, i, vp, vp, sz, i, i, sz, vp], i),
         "bine_reduce_scatter": ([vp, i, vp, vp, vp, i, i, vp], i),
         "bine_reduce": ([vp, i, vp, vp, sz, i, i, i, vp], i),
+        "bine_allgather": ([vp, i, vp, vp, sz, i, vp], i),
+        "bine_loopback_run_allgather": ([vp, i, i, vp, vp, sz, i, vp], i),
         "bine_loopback_run_allreduce": ([vp, i, i, vp, vp, sz, i, i, sz, vp], i),
         "bine_loopback_run_reduce_scatter": ([vp, i, i, vp, vp, vp, i, i, vp], i),
         "bine_loopback_run_reduce": ([vp, i, i, vp, vp, sz, i, i, i, vp], i),

@@ -272,6 +272,20 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
     return ops, bool(cj.value), int(fw.value)
 
 
+def allgather(algo, sbuf, rbuf, count: int, dtype, comm: Comm, stream=None) -> None:
+    """count = elements per rank; rbuf holds comm.size * count elements."""
+    check(lib().bine_allgather(comm.handle, _algo("allgather", algo), _ptr(sbuf), _ptr(rbuf), count,
+                               _dtype(dtype, rbuf), _stream(stream, comm)), f"allgather_{algo}")
+
+
+def loopback_allgather(comms, algo, sbufs, rbufs, count, dtype):
+    st = (ctypes.c_int * len(comms))()
+    hs = (ctypes.c_void_p * len(comms))(*[c.handle.value for c in comms])
+    rc = lib().bine_loopback_run_allgather(hs, len(comms), _algo("allgather", algo), _ptrs(sbufs), _ptrs(rbufs),
+                                           count, _dtype(dtype, rbufs[0]), st)
+    return rc, list(st)
+
+
 # ---- libbine-named entry points (include/libbine.h:30-78) --------------------------
 
 def _mk_ar(name):
@@ -298,6 +312,14 @@ def _mk_rd(name):
     return f
 
 
+def _mk_ag(name):
+    def f(sbuf, rbuf, count, dtype, comm, stream=None):
+        allgather(name, sbuf, rbuf, count, dtype, comm, stream=stream)
+    f.__name__ = "allgather_" + name
+    f.__doc__ = f"allgather_{name} (libbine_allgather.c) on MI355X."
+    return f
+
+
 ENTRY_POINTS = {}
 for _n in ALGOS["allreduce"]:
     ENTRY_POINTS["allreduce_" + _n] = _mk_ar(_n)
@@ -305,8 +327,10 @@ for _n in ALGOS["reduce_scatter"]:
     ENTRY_POINTS["reduce_scatter_" + _n] = _mk_rs(_n)
 for _n in ALGOS["reduce"]:
     ENTRY_POINTS["reduce_" + _n] = _mk_rd(_n)
+for _n in ALGOS["allgather"]:
+    ENTRY_POINTS["allgather_" + _n] = _mk_ag(_n)
 globals().update(ENTRY_POINTS)
 
 __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
-           "loopback_reduce_scatter", "loopback_reduce", "plan"] + list(ENTRY_POINTS)
+           "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather"] + list(ENTRY_POINTS)

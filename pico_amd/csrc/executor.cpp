@@ -458,6 +458,20 @@ static const struct { int algo; const char *coll, *name, *selector; } kAlgos[] =
     {BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN, "reduce_scatter", "bine_block_by_block_any_even", "bine_block_by_block_any_even"},
     {BINE_RD_BINE_LAT, "reduce", "bine_lat", "bine_lat_over"},
     {BINE_RD_BINE_BDW, "reduce", "bine_bdw", "bine_bdw_over"},
+    // pico_core_utils.c:125-140
+    {BINE_AG_K_BRUCK, "allgather", "k_bruck", "k_bruck_over"},
+    {BINE_AG_RECURSIVEDOUBLING, "allgather", "recursivedoubling", "recursive_doubling_over"},
+    {BINE_AG_RING, "allgather", "ring", "ring_over"},
+    {BINE_AG_SPARBIT, "allgather", "sparbit", "sparbit_over"},
+    {BINE_AG_BINE_BLOCK_BY_BLOCK_ANY_EVEN, "allgather", "bine_block_by_block_any_even",
+     "bine_block_by_block_over_any_even"},
+    {BINE_AG_BINE_BLOCK_BY_BLOCK, "allgather", "bine_block_by_block", "bine_block_by_block_over"},
+    {BINE_AG_BINE_PERMUTE_STATIC, "allgather", "bine_permute_static", "bine_permute_static_over"},
+    {BINE_AG_BINE_SEND_STATIC, "allgather", "bine_send_static", "bine_send_static_over"},
+    {BINE_AG_BINE_PERMUTE_REMAP, "allgather", "bine_permute_remap", "bine_permute_remap_over"},
+    {BINE_AG_BINE_SEND_REMAP, "allgather", "bine_send_remap", "bine_send_remap_over"},
+    {BINE_AG_BINE_2_BLOCKS, "allgather", "bine_2_blocks", "bine_2_blocks_over"},
+    {BINE_AG_BINE_2_BLOCKS_DTYPE, "allgather", "bine_2_blocks_dtype", "bine_2_blocks_dtype_over"},
 };
 
 int bine_algo_from_name(const char *coll, const char *name) {
@@ -605,6 +619,14 @@ int bine_reduce(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t co
   return run_collective(c, a, sbuf, rbuf, dtype, op, default_chunk_bytes(), stream);
 }
 
+int bine_allgather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, void *stream) {
+  if (algo < BINE_AG_RECURSIVEDOUBLING || algo > BINE_AG_BINE_2_BLOCKS_DTYPE) return BINE_ERR_UNSUPPORTED;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  return run_collective(c, a, sbuf, rbuf, dtype, BINE_SUM, default_chunk_bytes(), stream);
+}
+
 // ---- loopback drivers --------------------------------------------------------
 
 int bine_loopback_run_allreduce(bine_comm_t *comms, int n, int algo, const void *const *sbufs,
@@ -629,6 +651,14 @@ int bine_loopback_run_reduce(bine_comm_t *comms, int n, int algo, const void *co
   return run_threads(comms, n, statuses, [&](int r) {
     (void)hipSetDevice(comms[r]->device);
     return bine_reduce(comms[r], algo, sbufs[r], rbufs[r], count, dtype, op, root, nullptr);
+  });
+}
+
+int bine_loopback_run_allgather(bine_comm_t *comms, int n, int algo, const void *const *sbufs, void *const *rbufs,
+                                size_t count, int dtype, int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_allgather(comms[r], algo, sbufs[r], rbufs[r], count, dtype, nullptr);
   });
 }
 

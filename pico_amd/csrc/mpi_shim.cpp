@@ -240,11 +240,31 @@ int do_reduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype
   });
 }
 
+// allgather family: pure data movement, so it runs on bytes whatever the type
+int do_allgather(int algo, const void *sbuf, size_t scount, MPI_Datatype sdtype, void *rbuf, size_t rcount,
+                 MPI_Datatype rdtype, MPI_Comm comm) {
+  int rsz = 0, ssz = 0;
+  if (MPI_Type_size(rdtype, &rsz) != MPI_SUCCESS || rsz <= 0) return MPI_ERR_TYPE;
+  const size_t bytes = rcount * (size_t)rsz;
+  if (sbuf != MPI_IN_PLACE) {
+    if (MPI_Type_size(sdtype, &ssz) != MPI_SUCCESS || ssz <= 0) return MPI_ERR_TYPE;
+    if (scount * (size_t)ssz != bytes) return MPI_ERR_ARG;  // unequal block sizes: not supported
+  }
+  if (bytes == 0) return MPI_SUCCESS;
+  Entry *e;
+  int rc = get_entry(comm, &e);
+  if (rc) return rc;
+  return with_buffers(e, sbuf, bytes, rbuf, bytes * (size_t)e->size, false, [&](const void *s, void *r, void *st) {
+    return bine_allgather(e->comm, algo, s, r, bytes, BINE_UINT8, st);
+  });
+}
+
 int unsupported(const char *name) {
   static std::once_flag once;
   std::call_once(once, [&] {
     fprintf(stderr, "libbine(amd): %s is outside the reduce family this library provides "
-                    "(allreduce / reduce_scatter / reduce); returning MPI_ERR_UNSUPPORTED_OPERATION\n", name);
+                    "(allreduce / reduce_scatter / reduce / allgather); returning "
+                    "MPI_ERR_UNSUPPORTED_OPERATION\n", name);
   });
   return MPI_ERR_UNSUPPORTED_OPERATION;
 }
@@ -283,18 +303,22 @@ int reduce_bine_bdw(BINE_REDUCE_ARGS) { return do_reduce(BINE_RD_BINE_BDW, sbuf,
 
 #define NA(fn, args) \
   int fn(args) { return unsupported(#fn); }
-NA(allgather_k_bruck, BINE_ALLGATHER_ARGS)
-NA(allgather_recursivedoubling, BINE_ALLGATHER_ARGS)
-NA(allgather_ring, BINE_ALLGATHER_ARGS)
-NA(allgather_sparbit, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_block_by_block, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_block_by_block_any_even, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_permute_static, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_send_static, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_permute_remap, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_send_remap, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_2_blocks, BINE_ALLGATHER_ARGS)
-NA(allgather_bine_2_blocks_dtype, BINE_ALLGATHER_ARGS)
+#define AG(fn, id) \
+  int fn(BINE_ALLGATHER_ARGS) { return do_allgather(id, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm); }
+AG(allgather_k_bruck, BINE_AG_K_BRUCK)
+AG(allgather_recursivedoubling, BINE_AG_RECURSIVEDOUBLING)
+AG(allgather_ring, BINE_AG_RING)
+AG(allgather_sparbit, BINE_AG_SPARBIT)
+AG(allgather_bine_block_by_block, BINE_AG_BINE_BLOCK_BY_BLOCK)
+AG(allgather_bine_block_by_block_any_even, BINE_AG_BINE_BLOCK_BY_BLOCK_ANY_EVEN)
+AG(allgather_bine_permute_static, BINE_AG_BINE_PERMUTE_STATIC)
+AG(allgather_bine_send_static, BINE_AG_BINE_SEND_STATIC)
+AG(allgather_bine_permute_remap, BINE_AG_BINE_PERMUTE_REMAP)
+AG(allgather_bine_send_remap, BINE_AG_BINE_SEND_REMAP)
+AG(allgather_bine_2_blocks, BINE_AG_BINE_2_BLOCKS)
+AG(allgather_bine_2_blocks_dtype, BINE_AG_BINE_2_BLOCKS_DTYPE)
+#undef AG
+
 NA(alltoall_bine, BINE_ALLGATHER_ARGS)
 NA(bcast_scatter_allgather, BINE_BCAST_ARGS)
 NA(bcast_bine_lat, BINE_BCAST_ARGS)

@@ -913,6 +913,278 @@ void rd_bine_bdw(Builder &b, const PlanArgs &a) {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// allgather -- libbine_allgather.c (pure data movement)
+// ---------------------------------------------------------------------------
+// count = elements per rank; rbuf holds P blocks of `count`.  Every variant
+// writes each block straight to its final place: the permute variants' closing
+// reorder_blocks (:628, :797) is folded into the placement of every message
+// (a message of consecutive blocks of the reference's layout becomes one run
+// per maximal stretch that stays consecutive in the final layout; both ends
+// split identically because they see the same block numbers).
+
+namespace {
+
+// messages of one exchange, as (peer, first block, blocks), merged where the
+// next message continues the previous one on the same peer
+struct Msgs {
+  struct M { int peer; int blk; int n; };
+  std::vector<M> s, r;
+  static void add(std::vector<M> &v, int peer, int blk, int n) {
+    if (n <= 0 || peer < 0) return;
+    if (!v.empty() && v.back().peer == peer && v.back().blk + v.back().n == blk) { v.back().n += n; return; }
+    v.push_back({peer, blk, n});
+  }
+  void send(int peer, int blk, int n) { add(s, peer, blk, n); }
+  void recv(int peer, int blk, int n) { add(r, peer, blk, n); }
+  // blocks [blk, blk + n) of a ring of P blocks (wrapping past P)
+  void send_wrap(int peer, int blk, int n, int P) {
+    const int a = std::min(n, P - blk);
+    send(peer, blk, a);
+    send(peer, 0, n - a);
+  }
+  void recv_wrap(int peer, int blk, int n, int P) {
+    const int a = std::min(n, P - blk);
+    recv(peer, blk, a);
+    recv(peer, 0, n - a);
+  }
+  // blocks [lo, lo + n) of a layout whose block j sits at final block pos[j]
+  void send_mapped(int peer, int lo, int n, const std::vector<int> &pos) {
+    for (int j = lo; j < lo + n; j++) send(peer, pos[(size_t)j], 1);
+  }
+  void recv_mapped(int peer, int lo, int n, const std::vector<int> &pos) {
+    for (int j = lo; j < lo + n; j++) recv(peer, pos[(size_t)j], 1);
+  }
+  void flush(Builder &b, uint64_t count) {
+    for (auto &m : s) b.send(m.peer, RB, (uint64_t)m.blk * count, (uint64_t)m.n * count);
+    for (auto &m : r) b.recv(m.peer, RB, (uint64_t)m.blk * count, (uint64_t)m.n * count);
+    b.end();
+    s.clear();
+    r.clear();
+  }
+};
+
+// own block into place (COPY_BUFF_DIFF_DT of sbuf)
+void ag_own(Builder &b, const PlanArgs &a, int blk) {
+  if (!a.in_place) b.copy(SB, 0, RB, (uint64_t)blk * a.count, a.count);
+}
+
+}  // namespace
+
+// allgather_recursivedoubling, :18-86 (non-power-of-two: the reference returns
+// MPI_SUCCESS without doing anything, :31-34 -- reported as an error here)
+void ag_recursivedoubling(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  if (!is_pow2(P)) { b.fail(BINE_ERR_ARG); return; }
+  ag_own(b, a, r);
+  Msgs m;
+  int sbl = r;
+  for (int d = 1; d < P; d <<= 1) {
+    const int remote = r ^ d;
+    m.send(remote, sbl, d);
+    if (r < remote) m.recv(remote, sbl + d, d);
+    else { m.recv(remote, sbl - d, d); sbl -= d; }
+    m.flush(b, a.count);
+  }
+}
+
+// allgather_k_bruck, radix 2, :88-211.  The reference gathers into a rotated
+// layout (block i = rank r+i) and rotates at the end (:185-196); here block i of
+// that layout is written at its final place (r+i) mod P from the start.
+void ag_k_bruck(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  ag_own(b, a, r);  // in place: the reference moves rbuf[r] to rotated slot 0 = final slot r
+  Msgs m;
+  for (int d = 1; d < P; d *= 2) {
+    const int rc = d <= P / 2 ? d : std::min(d, P - d);
+    m.recv_wrap((r + d) % P, (r + d) % P, rc, P);
+    m.send_wrap((r - d + P) % P, r, rc, P);
+    m.flush(b, a.count);
+  }
+}
+
+// allgather_ring, :213-270
+void ag_ring(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  ag_own(b, a, r);
+  Msgs m;
+  for (int i = 0; i < P - 1; i++) {
+    m.send((r + 1) % P, (r - i + P) % P, 1);
+    m.recv((r - 1 + P) % P, (r - i - 1 + P) % P, 1);
+    m.flush(b, a.count);
+  }
+}
+
+// allgather_sparbit, :327-408 (one message per block, in transfer order)
+void ag_sparbit(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  ag_own(b, a, r);
+  const int L = log2_ceil(P);
+  uint32_t d = L >= 1 ? 1u << (L - 1) : 0;
+  const uint32_t last_ignore = (uint32_t)__builtin_ctz((unsigned)P);
+  const uint32_t ignore = (~((uint32_t)P >> last_ignore) | 1u) << last_ignore;
+  int expected = 1;
+  Msgs m;
+  for (int i = 0; i < L; i++) {
+    const int excl = (d & ignore) == d;
+    const int to = (r + (int)d) % P, from = (r - (int)d + P) % P;
+    for (int t = 0; t < expected - excl; t++) {
+      m.s.push_back({to, (r - 2 * t * (int)d + P) % P, 1});        // no merging: one
+      m.r.push_back({from, (r - (2 * t + 1) * (int)d + P) % P, 1});  // message per tag
+    }
+    m.flush(b, a.count);
+    d >>= 1;
+    expected = (expected << 1) - excl;
+  }
+}
+
+// get_indexes, libbine_utils.h:142-161
+static void tree_blocks(int rank, int step, int n, int P, std::vector<char> &bm) {
+  for (int s = step; s < n; s++) {
+    const int p = pi(rank, s, P);
+    bm[(size_t)p] = 1;
+    tree_blocks(p, s + 1, n, P, bm);
+  }
+}
+
+// allgather_bine_block_by_block, :410-490
+void ag_bine_bbb(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (!is_pow2(P) || steps < 1) { b.fail(BINE_ERR_ARG); return; }
+  ag_own(b, a, r);
+  Msgs m;
+  std::vector<char> sb((size_t)P), rb((size_t)P);
+  for (int step = steps - 1; step >= 0; step--) {
+    const int remote = pi(r, step, P);
+    std::fill(sb.begin(), sb.end(), 0);
+    std::fill(rb.begin(), rb.end(), 0);
+    rb[(size_t)pi(r, step, P)] = 1;
+    tree_blocks(pi(r, step, P), step + 1, steps, P, rb);
+    sb[(size_t)pi(remote, step, P)] = 1;
+    tree_blocks(pi(remote, step, P), step + 1, steps, P, sb);
+    for (int blk = 0; blk < P; blk++) {
+      if (sb[(size_t)blk]) m.send(remote, blk, 1);
+      if (rb[(size_t)blk]) m.recv(remote, blk, 1);
+    }
+    m.flush(b, a.count);
+  }
+}
+
+// allgather_bine_block_by_block_any_even, :492-561 (memcpy from sbuf even
+// in place -> in place is an error here)
+void ag_bine_bbb_any_even(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  if (a.in_place || (P > 1 && P % 2)) { b.fail(BINE_ERR_ARG); return; }
+  ag_own(b, a, r);
+  int inv = (int)(1u << ((unsigned)(log2_ceil(P) - 1) & 31u)), step = 0;
+  Msgs m;
+  while (inv > 0) {
+    const int partner = nb_partner(r, inv, P);
+    for (int blk = 1; blk < P; blk++) {
+      const int k = 31 - __builtin_clz(get_nu((uint32_t)blk, (uint32_t)P));
+      if (k != step) continue;
+      int btr, bts;
+      if (r % 2 == 0) { btr = pmod(blk + r, P); bts = pmod(partner - blk, P); }
+      else { btr = pmod(r - blk, P); bts = pmod(blk + partner, P); }
+      if (bts != partner) m.send(partner, bts, 1);
+      if (btr != r) m.recv(partner, btr, 1);
+    }
+    m.flush(b, a.count);
+    inv >>= 1;
+    step++;
+  }
+}
+
+// allgather_bine_permute_static (:563-640) and _send_static (:642-723).  Static
+// tables: recv[r][s] = perm[r] & ~(w-1), send[r][s] = recv[pi(r,s)][s], w = P >> (s+1).
+void ag_bine_static(Builder &b, const PlanArgs &a, bool permute) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (!is_pow2(P) || steps < 1 || steps > 8) { b.fail(BINE_ERR_ARG); return; }
+  if (!permute && a.in_place) { b.fail(BINE_ERR_ARG); return; }  // Sendrecv from MPI_IN_PLACE
+  std::vector<int> perm, pos((size_t)P);
+  static_perm(P, perm);
+  // permute: the reference's block j ends up at final block perm^-1(j); send
+  // variant: its layout is already final
+  for (int j = 0; j < P; j++) pos[(size_t)(permute ? perm[(size_t)j] : j)] = j;
+  auto recv_start = [&](int rank, int s) { const int w = P >> (s + 1); return perm[(size_t)rank] & ~(w - 1); };
+  if (permute) {
+    if (a.in_place) b.copy(RB, (uint64_t)perm[(size_t)r] * a.count, RB, (uint64_t)r * a.count, a.count);
+    else ag_own(b, a, r);
+  } else {
+    int to = 0;
+    for (int j = 0; j < P; j++)
+      if (perm[(size_t)j] == r) to = j;
+    b.send(to, SB, 0, a.count);
+    b.recv(perm[(size_t)r], RB, (uint64_t)perm[(size_t)r] * a.count, a.count);
+    b.end();
+  }
+  Msgs m;
+  int w = 1;
+  for (int step = steps - 1; step >= 0; step--) {
+    const int remote = pi(r, step, P);
+    m.send_mapped(remote, recv_start(r, step), w, pos);
+    m.recv_mapped(remote, recv_start(remote, step), w, pos);
+    m.flush(b, a.count);
+    w *= 2;
+  }
+}
+
+// allgather_bine_permute_remap (:725-809) and _send_remap (:811-890)
+void ag_bine_remap(Builder &b, const PlanArgs &a, bool permute) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (!is_pow2(P) || steps < 1 || steps > 8) { b.fail(BINE_ERR_ARG); return; }
+  if (!permute && a.in_place) { b.fail(BINE_ERR_ARG); return; }
+  std::vector<int> remap((size_t)P), pos((size_t)P);
+  for (int j = 0; j < P; j++) remap[(size_t)j] = (int)remap_rank((uint32_t)P, (uint32_t)j);
+  for (int j = 0; j < P; j++) pos[(size_t)(permute ? remap[(size_t)j] : j)] = j;
+  const int vr = remap[(size_t)r];
+  if (permute) {
+    if (a.in_place) b.copy(RB, (uint64_t)vr * a.count, RB, (uint64_t)r * a.count, a.count);
+    else ag_own(b, a, r);
+  } else {
+    int to = 0;  // get_sender_rec: the rank whose remap is r
+    for (int j = 0; j < P; j++)
+      if (remap[(size_t)j] == r) to = j;
+    b.send(to, SB, 0, a.count);
+    b.recv(vr, RB, (uint64_t)vr * a.count, a.count);
+    b.end();
+  }
+  Msgs m;
+  int d = 1, sbl = vr;
+  for (int step = steps - 1; step >= 0; step--) {
+    const int remote = pi(r, step, P), vrem = remap[(size_t)remote];
+    m.send_mapped(remote, sbl, d, pos);
+    if (vr < vrem) m.recv_mapped(remote, sbl + d, d, pos);
+    else { m.recv_mapped(remote, sbl - d, d, pos); sbl -= d; }
+    m.flush(b, a.count);
+    d <<= 1;
+  }
+}
+
+// allgather_bine_2_blocks (:892-997; wrap-around part as its own message,
+// posted first at both ends) and _2_blocks_dtype (:999-1106; the same bytes
+// packed by MPI_Type_indexed -- wrapped head, then main run)
+void ag_bine_2_blocks(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (!is_pow2(P) || steps < 1) { b.fail(BINE_ERR_ARG); return; }
+  ag_own(b, a, r);
+  Msgs m;
+  int mask = 1, first = r;
+  for (int step = 0; step < steps; step++) {
+    const int remote = pi(r, step, P), si = first;
+    int ri;
+    if ((step & 1) == (r & 1)) ri = (si + mask + P) % P;
+    else { ri = (si - mask + P) % P; first = ri; }
+    const int xr = ri + mask > P ? ri + mask - P : 0, xs = si + mask > P ? si + mask - P : 0;
+    m.s.push_back({remote, 0, xs});
+    m.r.push_back({remote, 0, xr});
+    m.s.push_back({remote, si, mask - xs});
+    m.r.push_back({remote, ri, mask - xr});
+    m.flush(b, a.count);
+    mask <<= 1;
+  }
+}
+
 Plan make_plan(const PlanArgs &a) {
   Builder b(a.rank);
   if (a.P < 1 || a.rank < 0 || a.rank >= a.P || a.esz == 0) { b.fail(BINE_ERR_ARG); return b.p; }
@@ -939,6 +1211,18 @@ Plan make_plan(const PlanArgs &a) {
     case BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN: rs_bine_bbb_any_even(b, a); break;
     case BINE_RD_BINE_LAT: rd_bine_lat(b, a); break;
     case BINE_RD_BINE_BDW: rd_bine_bdw(b, a); break;
+    case BINE_AG_RECURSIVEDOUBLING: ag_recursivedoubling(b, a); break;
+    case BINE_AG_K_BRUCK: ag_k_bruck(b, a); break;
+    case BINE_AG_RING: ag_ring(b, a); break;
+    case BINE_AG_SPARBIT: ag_sparbit(b, a); break;
+    case BINE_AG_BINE_BLOCK_BY_BLOCK: ag_bine_bbb(b, a); break;
+    case BINE_AG_BINE_BLOCK_BY_BLOCK_ANY_EVEN: ag_bine_bbb_any_even(b, a); break;
+    case BINE_AG_BINE_PERMUTE_STATIC: ag_bine_static(b, a, true); break;
+    case BINE_AG_BINE_SEND_STATIC: ag_bine_static(b, a, false); break;
+    case BINE_AG_BINE_PERMUTE_REMAP: ag_bine_remap(b, a, true); break;
+    case BINE_AG_BINE_SEND_REMAP: ag_bine_remap(b, a, false); break;
+    case BINE_AG_BINE_2_BLOCKS:
+    case BINE_AG_BINE_2_BLOCKS_DTYPE: ag_bine_2_blocks(b, a); break;
     default: b.fail(BINE_ERR_UNSUPPORTED); break;
   }
   if (!b.pend_send.empty() || !b.pend_recv.empty()) b.end();

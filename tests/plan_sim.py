@@ -56,14 +56,20 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             prims, stage = scheduled_prims(coll, algo, P, r, chunk_bytes, relay=relay, count=count, rcounts=rcounts, root=root,
                                     esz=esz, segsize=segsize, in_place=in_place)
         plans.append(prims)
-        if rbufs is not None:
+        if coll == "allgather":
+            # in place: rbufs[r] already holds the rank's block where the
+            # algorithm expects it (P * count elements)
+            rb = np.array(rbufs[r]).copy() if in_place else np.zeros(P * count, O.NP_DTYPES[dtype])
+            sb = np.zeros(0, O.NP_DTYPES[dtype]) if in_place else sbufs[r].copy()
+        elif rbufs is not None:
             rb = rbufs[r]
         elif coll == "reduce_scatter":
             rb = np.zeros(max(rcounts[r], 1), O.NP_DTYPES[dtype])
         else:
             rb = np.zeros(max(count, 1), O.NP_DTYPES[dtype])
-        sb = sbufs[r].copy()
-        if in_place:
+        if coll != "allgather":
+            sb = sbufs[r].copy()
+        if in_place and coll != "allgather":
             if coll == "reduce_scatter":
                 rb = sbufs[r].copy()
             else:
@@ -155,6 +161,8 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         rb = bufs[r][RB]
         if coll == "reduce_scatter":
             outs.append(rb[:rcounts[r]])
+        elif coll == "allgather":
+            outs.append(rb[:P * count])
         else:
             outs.append(rb[:count])
     return outs

@@ -33,6 +33,12 @@ CASES = [
     ("reduce_scatter", "recursive_distance_doubling", "float", 64),
     ("reduce", "bine_bdw", "float", 1000),
     ("reduce", "bine_lat", "float", 1000),
+    ("allgather", "bine_permute_remap", "float", 100),
+    ("allgather", "bine_send_static", "int8", 33),
+    ("allgather", "bine_2_blocks", "float", 10),
+    ("allgather", "k_bruck", "double", 7),
+    ("allgather", "sparbit", "float", 5),
+    ("allgather", "bine_block_by_block", "float", 9),
 ]
 
 
@@ -59,14 +65,16 @@ def _worker(rank, P, port, q):
         rc = [n // P] * P if coll == "reduce_scatter" else None
         total = sum(rc) if rc else n
         sb = O.inputs(dtype, total, P)
-        if coll == "allreduce":
+        if coll == "allgather":
+            want = O.allgather(algo, sb, dtype)[0][rank]
+        elif coll == "allreduce":
             want = O.allreduce(algo, sb, dtype, segsize=64)[0][rank]
         elif coll == "reduce_scatter":
             want = O.reduce_scatter(algo, sb, rc, dtype)[0][rank]
         else:
             want = O.reduce(algo, sb, dtype)[0] if rank == 0 else None
         prims, tmp = pico_amd.plan(coll, algo, P, rank, count=n, rcounts=rc, esz=esz, segsize=64)
-        out_n = rc[rank] if rc else n
+        out_n = rc[rank] if rc else (P * n if coll == "allgather" else n)
         bufs = [sb[rank].copy(), np.zeros(max(out_n, 1), npdt)] + [np.zeros(int(t) + 1, npdt) for t in tmp]
 
         def v(b, off, cnt):

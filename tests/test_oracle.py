@@ -1,8 +1,9 @@
 """The CPU restatement (oracle/) pinned against the real reference.
 
 * every golden vector captured from the reference's own libbine
-  (tools/make_golden.py; 3,300+ cases over 19 algorithms, 7 dtypes, 4 ops,
-  P = 1, 2, 3, 4, 6, 8) must be reproduced bit-for-bit, return codes included;
+  (tools/make_golden.py; reduce family: 3,300+ cases over 19 algorithms,
+  7 dtypes, 4 ops, P = 1, 2, 3, 4, 6, 8; allgather family: 12 algorithms,
+  P = 1 ... 8 and 16) must be reproduced bit-for-bit, return codes included;
 * the input generator must reproduce pico_core's (fill cases);
 * the regenerated static tables and remap_rank must equal the reference's
   literal tables (digests in tests/golden/tables.json, the source itself when
@@ -30,6 +31,9 @@ def _run(c, ref_bugs=True):
         rc = G.rcounts(c)
         sb = O.inputs(dt, sum(rc), P, c["seed_base"])
         return O.reduce_scatter(c["algo"], sb, rc, dt, c["op"])
+    if c["coll"] == "allgather":
+        sb = O.inputs(dt, N, P, c["seed_base"])
+        return O.allgather(c["algo"], sb, dt)
     sb = O.inputs(dt, N, P, c["seed_base"])
     o, rets = O.reduce(c["algo"], sb, dt, c["op"])
     return [o] + [np.zeros(0)] * (P - 1), rets

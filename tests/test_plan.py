@@ -138,3 +138,75 @@ def test_remap_plan_shape():
     assert [p["count"] for p in sends[:3]] == [1 << 19, 1 << 18, 1 << 17]
     assert tmp[0] == 1 << 19
     assert all(p["flags"] == 1 for p in prims[:9])             # RS steps are pipelined
+
+
+# ---- allgather family -----------------------------------
+
+AG = list(pico_amd.ALGOS["allgather"])
+AG_BINE_POW2 = {"bine_block_by_block", "bine_permute_static", "bine_send_static", "bine_permute_remap",
+                "bine_send_remap", "bine_2_blocks", "bine_2_blocks_dtype"}
+
+
+def _ok_ag(algo, P):
+    if algo in AG_BINE_POW2 and (P & (P - 1) or P == 1):
+        return False  # MPI_ERR_ARG in the reference (:421-425 and siblings)
+    if algo == "recursivedoubling" and P & (P - 1):
+        return False  # the reference returns success without gathering (:31-34)
+    if algo == "bine_block_by_block_any_even" and P % 2 and P > 1:
+        return False
+    return True
+
+
+@pytest.mark.parametrize("algo", AG)
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 8, 16])
+@pytest.mark.parametrize("dtype", ["float", "int8"])
+def test_allgather_plans_match_oracle(algo, P, dtype):
+    if not _ok_ag(algo, P):
+        with pytest.raises(pico_amd.BineError):
+            pico_amd.plan("allgather", algo, P, 0, count=13)
+        return
+    for n in (1, 3, 64, 1000):
+        sb = O.inputs(dtype, n, P)
+        exp, rets = O.allgather(algo, sb, dtype)
+        assert all(x == 0 for x in rets)
+        got = plan_sim.run("allgather", algo, sb, dtype)
+        for r in range(P):
+            assert np.array_equal(got[r], exp[r]), (algo, P, n, r)
+
+
+@pytest.mark.parametrize("algo", [a for a in AG if a not in ("bine_send_static", "bine_send_remap",
+                                                              "bine_block_by_block_any_even")])
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_allgather_in_place_follows_reference(algo, P):
+    """MPI_IN_PLACE: the oracle's restatement of each in-place path, with the
+    rank's block placed where that path expects it (block r, or perm[r] /
+    remap[r] for the permute variants)."""
+    n = 7
+    sb = O.inputs("float", n, P)
+    perm = O.static_tables(P)[0] if algo == "bine_permute_static" else None
+    pre = []
+    for r in range(P):
+        b = np.zeros(P * n, np.float32)
+        slot = r
+        if algo == "bine_permute_static":
+            slot = perm[r]
+        elif algo == "bine_permute_remap":
+            slot = O.remap_rank(P, r)
+        b[slot * n:(slot + 1) * n] = sb[r]
+        pre.append(b)
+    exp, rets = O.allgather(algo, sb, "float", in_place_rbufs=pre)
+    assert all(x == 0 for x in rets)
+    got = plan_sim.run("allgather", algo, sb, "float", in_place=True, rbufs=pre)
+    for r in range(P):
+        assert np.array_equal(got[r], exp[r]), (algo, P, r)
+        assert np.array_equal(exp[r], np.concatenate(sb))  # and it is the allgather
+
+
+def test_allgather_permute_variants_land_blocks_in_place():
+    """the permute variants' closing reorder is folded into message placement:
+    no COPY after the first one, messages split only where blocks stop being
+    consecutive in the final layout"""
+    for algo in ("bine_permute_remap", "bine_permute_static"):
+        prims, _ = pico_amd.plan("allgather", algo, 8, 3, count=100)
+        assert [p["type"] for p in prims].count("COPY") == 1
+        assert prims[0]["type"] == "COPY"

@@ -27,6 +27,7 @@ AR = ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented", "bine_lat
 RS = ["bine_permute_remap", "bine_send_remap", "bine_static", "bine_block_by_block", "bine_block_by_block_any_even",
       "ring", "butterfly", "recursivehalving", "recursive_distance_doubling"]
 RD = ["bine_bdw", "bine_lat"]
+AG = list(pico_amd.ALGOS["allgather"])
 
 
 def _regions(p, in_place):
@@ -101,6 +102,8 @@ def _cases():
             yield "reduce_scatter", a, P
         for a in RD:
             yield "reduce", a, P
+        for a in AG:
+            yield "allgather", a, P
 
 
 @pytest.mark.parametrize("chunk", [0, 64, 4096])
@@ -112,6 +115,8 @@ def test_schedules_race_free(chunk, in_place):
             kw = dict(count=1003, esz=4, segsize=128, in_place=in_place)
             if coll == "reduce_scatter":
                 kw = dict(rcounts=[37 + (i % 3) for i in range(P)], esz=4, in_place=in_place)
+            if coll == "allgather":
+                kw = dict(count=101, esz=4, in_place=in_place)
             try:
                 ops, cj, fw = pico_amd.schedule(coll, algo, P, rank, chunk_bytes=chunk, **kw)
             except pico_amd.BineError:
@@ -137,10 +142,16 @@ def test_chunking_overlaps_steps():
     ("reduce_scatter", "bine_permute_remap", 8), ("reduce_scatter", "bine_static", 4),
     ("reduce_scatter", "ring", 3), ("reduce_scatter", "recursivehalving", 8),
     ("reduce", "bine_bdw", 8),
+    ("allgather", "bine_permute_remap", 8), ("allgather", "bine_send_static", 8), ("allgather", "ring", 5),
+    ("allgather", "k_bruck", 6), ("allgather", "bine_2_blocks", 8), ("allgather", "recursivedoubling", 4),
+    ("allgather", "sparbit", 6),
 ])
 @pytest.mark.parametrize("chunk", [16, 200])
 def test_chunked_schedule_matches_oracle(coll, algo, P, chunk):
     dtype = "float"
+    if coll == "allgather":
+        assert _run_relay(coll, algo, P, chunk, 0)
+        return
     if coll == "reduce_scatter":
         rc = [29 + 3 * (i % 2) for i in range(P)]
         sb = O.inputs(dtype, sum(rc), P)
@@ -171,11 +182,19 @@ RELAY_CASES = [
     ("reduce_scatter", "bine_static", 8), ("reduce_scatter", "recursivehalving", 8), ("reduce_scatter", "ring", 6),
     ("reduce_scatter", "butterfly", 8),
     ("reduce", "bine_bdw", 8),
+    ("allgather", "bine_permute_remap", 8), ("allgather", "bine_send_static", 8), ("allgather", "ring", 5),
+    ("allgather", "k_bruck", 6), ("allgather", "bine_2_blocks", 8), ("allgather", "recursivedoubling", 4),
+    ("allgather", "sparbit", 6),
 ]
 
 
 def _run_relay(coll, algo, P, chunk, relay, n=997):
     dtype = "float"
+    if coll == "allgather":
+        sb = O.inputs(dtype, n // P + 1, P)
+        want = O.allgather(algo, sb, dtype)[0]
+        got = plan_sim.run(coll, algo, sb, dtype, chunk_bytes=chunk, relay=relay)
+        return all(np.array_equal(got[r], want[r]) for r in range(P))
     if coll == "reduce_scatter":
         rc = [n // P + (i % 2) for i in range(P)]
         sb = O.inputs(dtype, sum(rc), P)
@@ -204,6 +223,8 @@ def test_relay_schedules_race_free(coll, algo, P):
         kw = dict(count=4099, esz=4, segsize=512)
         if coll == "reduce_scatter":
             kw = dict(rcounts=[500 + (i % 3) for i in range(P)], esz=4)
+        if coll == "allgather":
+            kw = dict(count=513, esz=4)
         for chunk in (0, 1024):
             ops, cj, fw = pico_amd.schedule(coll, algo, P, rank, chunk_bytes=chunk, relay_min_bytes=8, **kw)
             check_race_free(ops, cj, fw, False)

@@ -87,10 +87,38 @@ def run_case(P, coll, algo, op, segsize, rk, dtypes, ns, timeout=120):
     return recs
 
 
+AG_ALGOS = ["recursivedoubling", "k_bruck", "ring", "sparbit", "bine_block_by_block",
+            "bine_block_by_block_any_even", "bine_permute_static", "bine_send_static",
+            "bine_permute_remap", "bine_send_remap", "bine_2_blocks", "bine_2_blocks_dtype"]
+
+
+def allgather_jobs():
+    """the allgather family, N = elements per rank"""
+    jobs = []
+    for P in (1, 2, 3, 4, 5, 6, 8):
+        for a in AG_ALGOS:
+            jobs.append((P, "allgather", a, "sum", 0, "even", ["float", "int64", "int8"], [1, 2, 7, 64, 333, 4099],
+                         True))
+    jobs.append((16, "allgather", "bine_permute_remap", "sum", 0, "even", ["float"], [5, 1000], True))
+    jobs.append((16, "allgather", "bine_send_static", "sum", 0, "even", ["float"], [5, 1000], True))
+    jobs.append((16, "allgather", "sparbit", "sum", 0, "even", ["float"], [5], True))
+    jobs.append((16, "allgather", "bine_2_blocks", "sum", 0, "even", ["float"], [5], True))
+    return jobs
+
+
 def main():
     if not os.path.exists(BIN):
         sys.exit("build the reference first: make -C oracle ref")
     os.makedirs(OUT, exist_ok=True)
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if only:
+        # regenerate one collective's cases, keep everything else as it is
+        old = json.load(open(os.path.join(OUT, "index.json")))["cases"]
+        prev = dict(np.load(os.path.join(OUT, "outputs.npz")))
+        index = [c for c in old if c["coll"] != only]
+        arrays = {k: v for k, v in prev.items() if not k.startswith(only + ".")}
+        jobs = {"allgather": allgather_jobs}[only]()
+        return capture(jobs, index, arrays)
     jobs = []  # (P, coll, algo, op, segsize, rk, dtypes, ns, store_small)
     # input generator pin
     jobs.append((8, "fill", "-", "sum", 0, "even", ALL_DT, [64], True))
@@ -127,10 +155,15 @@ def main():
         jobs.append((8, "allreduce", a, "sum", seg, "even", ["float"], [1000003], False))
     jobs.append((8, "reduce_scatter", "bine_permute_remap", "sum", 0, "even", ["float"], [8 * 131072 + 8 * 3], False))
     jobs.append((8, "allreduce", "bine_bdw_remap", "sum", 0, "even", ["double", "int64"], [262147], False))
+    jobs += allgather_jobs()
+    capture(jobs, [], {})
 
-    index, arrays = [], {}
+
+def capture(jobs, index, arrays):
     for (P, coll, algo, op, seg, rk, dts, ns, store) in jobs:
-        recs = run_case(P, coll, algo, op, seg, rk, dts, ns)
+        # the reference hangs on some shapes (e.g. odd P in the any_even
+        # variants): a short limit, then the cases are re-run one by one
+        recs = run_case(P, coll, algo, op, seg, rk, dts, ns, timeout=60 if coll == "allgather" else 120)
         if any(r[2] is None for r in recs):
             # one crashing case (e.g. the static variant's tmp_buf overflow,
             # libbine_allreduce.c:724 vs :749-765) kills the whole mpiexec:
@@ -138,7 +171,8 @@ def main():
             fixed = []
             for rec in recs:
                 if rec[2] is None:
-                    rec = run_case(P, coll, algo, op, seg, rk, [rec[0]], [rec[1]])[0]
+                    rec = run_case(P, coll, algo, op, seg, rk, [rec[0]], [rec[1]],
+                                   timeout=20 if coll == "allgather" else 120)[0]
                 fixed.append(rec)
             recs = fixed
         for dt, n, rets, outs, failed in recs:
