@@ -119,10 +119,10 @@ def bench_c2(steps: int, warmup: int):
     }
 
 
-def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup):
-    """max-over-ranks ms per allreduce and wall seconds of `steps` timed calls"""
+def _timed(torch, dist, comm, stream, call, steps, warmup):
+    """max-over-ranks ms per call() and wall seconds of `steps` timed calls"""
     for _ in range(warmup):
-        pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
+        call()
     torch.cuda.synchronize()
     comm.synchronize()
     dist.barrier()
@@ -131,7 +131,7 @@ def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(steps):
-        pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
+        call()
     e1.record(stream)
     torch.cuda.synchronize()
     comm.synchronize()
@@ -142,10 +142,50 @@ def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream
     return float(t[0]), float(t[1])
 
 
+def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup):
+    return _timed(torch, dist, comm, stream,
+                  lambda: pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream),
+                  steps, warmup)
+
+
+def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev):
+    """BASELINE configs C4 and C5 with the transport chosen for C3 (reported
+    beside the headline; a few steps each)"""
+    out = {}
+    # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
+    n = 268_435_456
+    sb = torch.empty(n, dtype=torch.float32, device=dev)
+    rb = torch.empty(n // world, dtype=torch.float32, device=dev)
+    pico_amd.fill_pico(sb, n, "float", 77 + rank)
+    rc = [n // world] * world
+    ms, _ = _timed(torch, dist, comm, stream,
+                   lambda: pico_amd.reduce_scatter("bine_permute_remap", sb, rb, rc, "float", "sum", comm,
+                                                   stream=stream), 5, 2)
+    S = n * 4
+    out["C4_reduce_scatter_bine_permute_remap_f32_1GiB"] = {
+        "ms": round(ms, 4), "busbw_per_rank_GBs": round((world - 1) / world * S / (ms * 1e-3) / 1e9, 2)}
+    del sb, rb
+    # C5: allreduce_bine_bdw_remap fp64 / int64 SUM, 256 MiB per rank
+    n = 33_554_432
+    for dt, tdt in (("double", torch.float64), ("int64", torch.int64)):
+        sb = torch.empty(n, dtype=tdt, device=dev)
+        rb = torch.empty(n, dtype=tdt, device=dev)
+        pico_amd.fill_pico(sb, n, dt, 99 + rank)
+        ms, _ = _timed(torch, dist, comm, stream,
+                       lambda: pico_amd.allreduce("bine_bdw_remap", sb, rb, n, dt, "sum", comm, stream=stream), 5, 2)
+        S = n * 8
+        out[f"C5_allreduce_bine_bdw_remap_{dt}_256MiB"] = {
+            "ms": round(ms, 4), "algbw_per_rank_GBs": round(S / (ms * 1e-3) / 1e9, 2),
+            "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2)}
+        del sb, rb
+    torch.cuda.empty_cache()
+    return out
+
+
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
 
 
-def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str):
+def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True):
     import torch
     import torch.distributed as dist
     import pico_amd
@@ -180,6 +220,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str):
         chosen = modes[0] if world > 2 else 0
     comm.set_relay(chosen)
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
+    extra = _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
@@ -201,7 +242,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str):
                        "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
                        "transport": "relay" if chosen else "direct", "relay_min_bytes": chosen,
                        "transport_trials_ms": {("relay" if m else "direct"): round(v, 4) for m, v in trials.items()},
-                       "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers},
+                       "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
+                       "other_baseline_configs": extra},
             "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
                          "traffic": egress,
@@ -224,10 +266,11 @@ def main():
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
     ap.add_argument("--relay", default="auto", help="auto | off | <min relayed part bytes> (N > 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay)
+        res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay, not args.no_extras)
         if res is not None:
             print(json.dumps(res), flush=True)
         return

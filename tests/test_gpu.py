@@ -8,6 +8,7 @@ in-process peer copies); the RCCL transport is exercised at P = 1 here and at
 P = 2..8 by the driver's multi-GPU bench.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -20,6 +21,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 import pico_amd  # noqa: E402
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALL_DT = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64", "float", "double"]
 STATUS_OF_MPI = {12: 1, 51: 2}   # MPI_ERR_ARG -> BINE_ERR_ARG, MPI_ERR_SIZE -> BINE_ERR_SIZE
 
@@ -300,3 +302,27 @@ def test_rccl_single_rank(dev):
         assert ei.value.status == 1
     finally:
         c.destroy()
+
+
+# ---- pico_core-compatible device-resident driver ----------
+
+@pytest.mark.parametrize("coll,algo,dtype", [("ALLREDUCE", "bine_bdw_remap_over", "float"),
+                                             ("REDUCE_SCATTER", "bine_permute_remap_over", "int64"),
+                                             ("ALLGATHER", "bine_permute_remap_over", "double"),
+                                             ("REDUCE", "bine_bdw_over", "int32")])
+def test_pico_amd_core_writes_pico_core_csv(dev, tmp_path, coll, algo, dtype):
+    """pico_amd_core: pico_core's CLI / env / ground-truth check / CSV layout,
+    buffers in HBM, calls through libbine.so's libbine.h symbols."""
+    import subprocess
+    exe = os.path.join(ROOT, "pico_amd", "lib", "pico_amd_core")
+    env = dict(os.environ, COLLECTIVE_TYPE=coll, OUTPUT_DIR=str(tmp_path), DATA_DIR=str(tmp_path),
+               OUTPUT_LEVEL="all", LOCATION="local", SEGMENTED="no", PICO_SEED="1234",
+               PATH="/opt/conda/bin:" + os.environ.get("PATH", ""))
+    p = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "1", exe, "1048576", "5", algo, dtype], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    csv = tmp_path / f"1048576_{algo}_{dtype}.csv"
+    lines = csv.read_text().splitlines()
+    assert lines[0] == "highest,rank0" and len(lines) == 6
+    assert all(int(x.split(",")[0]) > 0 for x in lines[1:])
+    assert (tmp_path / "alloc_1_GPU.csv").read_text().startswith("MPI_Rank,allocation\n0,")
