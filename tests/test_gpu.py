@@ -308,11 +308,12 @@ def test_rccl_single_rank(dev):
 
 @pytest.mark.parametrize("coll,algo,dtype", [("ALLREDUCE", "bine_bdw_remap_over", "float"),
                                              ("REDUCE_SCATTER", "bine_permute_remap_over", "int64"),
-                                             ("ALLGATHER", "bine_permute_remap_over", "double"),
+                                             ("ALLGATHER", "k_bruck_over", "double"),
                                              ("REDUCE", "bine_bdw_over", "int32")])
 def test_pico_amd_core_writes_pico_core_csv(dev, tmp_path, coll, algo, dtype):
     """pico_amd_core: pico_core's CLI / env / ground-truth check / CSV layout,
-    buffers in HBM, calls through libbine.so's libbine.h symbols."""
+    buffers in HBM, calls through libbine.so's libbine.h symbols.  One rank
+    (the Bine allgathers return MPI_ERR_ARG at P = 1, like the reference)."""
     import subprocess
     exe = os.path.join(ROOT, "pico_amd", "lib", "pico_amd_core")
     env = dict(os.environ, COLLECTIVE_TYPE=coll, OUTPUT_DIR=str(tmp_path), DATA_DIR=str(tmp_path),
@@ -326,3 +327,25 @@ def test_pico_amd_core_writes_pico_core_csv(dev, tmp_path, coll, algo, dtype):
     assert lines[0] == "highest,rank0" and len(lines) == 6
     assert all(int(x.split(",")[0]) > 0 for x in lines[1:])
     assert (tmp_path / "alloc_1_GPU.csv").read_text().startswith("MPI_Rank,allocation\n0,")
+
+
+@pytest.mark.parametrize("relay", [0, 64], ids=["direct", "relay"])
+@pytest.mark.parametrize("P", [2, 4, 6, 8])
+def test_allgather_family_matches_oracle(dev, P, relay):
+    """all 12 allgather algorithms, device path vs the oracle's restatement of
+    the reference (golden-pinned on the CPU side), incl. 1-byte elements"""
+    bad = []
+    for algo in pico_amd.ALGOS["allgather"]:
+        for dt, n in (("float", 1), ("int8", 333), ("double", 4099)):
+            sb = O.inputs(dt, n, P)
+            want, rets = O.allgather(algo, sb, dt)
+            outs, st = run_loopback("allgather", algo, sb, dt, relay=relay)
+            if any(rets) or (algo == "recursivedoubling" and P & (P - 1)):
+                if not any(st):
+                    bad.append((algo, dt, n, "expected an error", rets))
+                continue
+            if any(st):
+                bad.append((algo, dt, n, "status", st))
+            elif any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                bad.append((algo, dt, n, "data"))
+    assert not bad, bad[:8]
