@@ -1071,10 +1071,11 @@ void ag_bine_bbb(Builder &b, const PlanArgs &a) {
 }
 
 // allgather_bine_block_by_block_any_even, :492-561 (memcpy from sbuf even
-// in place -> in place is an error here)
+// in place -> in place is an error here; odd P, P = 1 included, hangs or
+// crashes in the reference -> error)
 void ag_bine_bbb_any_even(Builder &b, const PlanArgs &a) {
   const int P = a.P, r = a.rank;
-  if (a.in_place || (P > 1 && P % 2)) { b.fail(BINE_ERR_ARG); return; }
+  if (a.in_place || P % 2) { b.fail(BINE_ERR_ARG); return; }
   ag_own(b, a, r);
   int inv = (int)(1u << ((unsigned)(log2_ceil(P) - 1) & 31u)), step = 0;
   Msgs m;

@@ -152,8 +152,8 @@ def _ok_ag(algo, P):
         return False  # MPI_ERR_ARG in the reference (:421-425 and siblings)
     if algo == "recursivedoubling" and P & (P - 1):
         return False  # the reference returns success without gathering (:31-34)
-    if algo == "bine_block_by_block_any_even" and P % 2 and P > 1:
-        return False
+    if algo == "bine_block_by_block_any_even" and P % 2:
+        return False  # hangs (odd P > 1) or crashes (P = 1) in the reference
     return True
 
 
