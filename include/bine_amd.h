@@ -11,8 +11,10 @@
  *
  * Device pointers only: the buffers passed here must live in the memory of the
  * communicator's device.  Operations are stream-ordered: they are enqueued on
- * `stream` (NULL = the communicator's own stream) and return once enqueued;
- * bine_comm_synchronize() or a synchronize on `stream` waits for completion.
+ * `stream` (a hipStream_t; NULL = the HIP null stream, as in HIP and RCCL --
+ * pass bine_comm_stream() for the communicator's own) and return once
+ * enqueued; a synchronize on `stream` (or bine_comm_synchronize) waits for
+ * completion, exchanges included.
  */
 #ifndef BINE_AMD_H
 #define BINE_AMD_H

@@ -190,6 +190,8 @@ struct bine_comm {
   void *tmp[4] = {nullptr, nullptr, nullptr, nullptr};  // TMP0..2, STAGE
   size_t tmp_bytes[4] = {0, 0, 0, 0};
   size_t relay_min_bytes = 0;  // relay mode: smallest relayed part (0: off)
+  hipStream_t last_user = nullptr;  // caller's stream of the latest collective
+  bool used_user = false;
   std::vector<hipEvent_t> ev;
   size_t ev_next = 0;
   std::map<std::string, std::pair<bine::Plan, bine::Schedule>> plans;
@@ -375,7 +377,9 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   const Plan &plan = it->second.first;
   const Schedule &sc = it->second.second;
   if (plan.status != BINE_SUCCESS) return plan.status;
-  hipStream_t K = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t K = (hipStream_t)stream;  // NULL = the HIP null stream, as in every HIP / RCCL API
+  c->last_user = K;
+  c->used_user = true;
   const uint64_t need[4] = {plan.tmp_elems[0], plan.tmp_elems[1], plan.tmp_elems[2], sc.stage_elems};
   int rc = ensure_workspace(c, need, a.esz, K);
   if (rc) return rc;
@@ -554,6 +558,7 @@ int bine_comm_synchronize(bine_comm_t c) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipStreamSynchronize(c->cstream));
+  if (c->used_user) HIP_TRY(hipStreamSynchronize(c->last_user));
   if (c->hub && c->hub->mismatches.load()) {
     set_err("loopback: %d send/recv size mismatches", c->hub->mismatches.load());
     return BINE_ERR_INTERNAL;
@@ -634,7 +639,7 @@ int bine_loopback_run_allreduce(bine_comm_t *comms, int n, int algo, const void 
                                 int *statuses) {
   return run_threads(comms, n, statuses, [&](int r) {
     (void)hipSetDevice(comms[r]->device);
-    return bine_allreduce(comms[r], algo, sbufs[r], rbufs[r], count, dtype, op, segsize, nullptr);
+    return bine_allreduce(comms[r], algo, sbufs[r], rbufs[r], count, dtype, op, segsize, comms[r]->stream);  // one stream per virtual rank
   });
 }
 
@@ -642,7 +647,7 @@ int bine_loopback_run_reduce_scatter(bine_comm_t *comms, int n, int algo, const 
                                      void *const *rbufs, const int *rcounts, int dtype, int op, int *statuses) {
   return run_threads(comms, n, statuses, [&](int r) {
     (void)hipSetDevice(comms[r]->device);
-    return bine_reduce_scatter(comms[r], algo, sbufs[r], rbufs[r], rcounts, dtype, op, nullptr);
+    return bine_reduce_scatter(comms[r], algo, sbufs[r], rbufs[r], rcounts, dtype, op, comms[r]->stream);  // one stream per virtual rank
   });
 }
 
@@ -650,7 +655,7 @@ int bine_loopback_run_reduce(bine_comm_t *comms, int n, int algo, const void *co
                              size_t count, int dtype, int op, int root, int *statuses) {
   return run_threads(comms, n, statuses, [&](int r) {
     (void)hipSetDevice(comms[r]->device);
-    return bine_reduce(comms[r], algo, sbufs[r], rbufs[r], count, dtype, op, root, nullptr);
+    return bine_reduce(comms[r], algo, sbufs[r], rbufs[r], count, dtype, op, root, comms[r]->stream);  // one stream per virtual rank
   });
 }
 
@@ -658,7 +663,7 @@ int bine_loopback_run_allgather(bine_comm_t *comms, int n, int algo, const void 
                                 size_t count, int dtype, int *statuses) {
   return run_threads(comms, n, statuses, [&](int r) {
     (void)hipSetDevice(comms[r]->device);
-    return bine_allgather(comms[r], algo, sbufs[r], rbufs[r], count, dtype, nullptr);
+    return bine_allgather(comms[r], algo, sbufs[r], rbufs[r], count, dtype, comms[r]->stream);  // one stream per virtual rank
   });
 }
 
