@@ -206,30 +206,43 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     pico_amd.fill_pico(sbuf, nelem, "float", 1234 + rank)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
-    # transport: direct (one peer per step, the literal Bine schedule) or the
-    # multi-link relay of the same schedule (identical results); "auto" times
-    # both briefly and keeps the faster -- all ranks see the same max timings
-    modes = {"off": [0], "auto": [0, RELAY_MIN_BYTES]}.get(relay, None) or [int(relay)]
+    # transport: direct (one peer per step, the literal Bine schedule), the
+    # multi-link relay of the same schedule (identical results), or multi-tree
+    # (P-1 relabelled instances over edge-disjoint pairings; integer results
+    # identical, fp within rounding).  "auto" times each briefly (max over
+    # ranks, so every rank picks the same) and keeps the fastest.
+    modes = {"off": ["direct"], "auto": ["direct", "relay", "trees"], "relay": ["relay"],
+             "trees": ["trees"]}.get(relay, ["direct"])
+    if world <= 2:
+        modes = ["direct"]
+    if world not in (4, 8):
+        modes = [m for m in modes if m != "trees"] or ["direct"]
+
+    def use(m):
+        comm.set_relay(RELAY_MIN_BYTES if m == "relay" else 0)
+        comm.set_trees(m == "trees")
+
     trials = {}
-    if len(modes) > 1 and world > 2:
+    if len(modes) > 1:
         for m in modes:
-            comm.set_relay(m)
+            use(m)
             trials[m] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
         chosen = min(trials, key=trials.get)
     else:
-        chosen = modes[0] if world > 2 else 0
-    comm.set_relay(chosen)
+        chosen = modes[0]
+    use(chosen)
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
     extra = _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
     # bytes this rank puts on xGMI per allreduce (from the executed schedule)
-    ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4,
-                                  chunk_bytes=16 << 20, relay_min_bytes=chosen)
+    ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4, chunk_bytes=16 << 20,
+                                  relay_min_bytes=RELAY_MIN_BYTES if chosen == "relay" else 0,
+                                  trees=chosen == "trees")
     egress = 4 * sum(p["count"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND")
     peers = len({p["peer"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND"})
-    link_peak = XGMI_LINK_GBS * (7 if chosen else 1)
+    link_peak = XGMI_LINK_GBS * (min(7, world - 1) if chosen != "direct" else 1)
     out = None
     if rank == 0:
         out = {
@@ -240,15 +253,16 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             "config": {"workload": f"C3: allreduce_{algo} fp32 {S // MIB} MiB/rank over RCCL P2P (xGMI), "
                                    f"{world} x MI355X", "value_definition": "N * S / t (whole job)",
                        "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
-                       "transport": "relay" if chosen else "direct", "relay_min_bytes": chosen,
-                       "transport_trials_ms": {("relay" if m else "direct"): round(v, 4) for m, v in trials.items()},
+                       "transport": chosen,
+                       "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
+                       "transport_trials_ms": {m: round(v, 4) for m, v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": extra},
             "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
                          "traffic": egress,
                          "note": "achieved = this rank's xGMI egress bytes (schedule) / t; peak = "
-                                 + ("7 links x 153 GB/s (relay keeps all links busy)" if chosen else
+                                 + ("N-1 links x 153 GB/s (all peers used every step)" if chosen != "direct" else
                                     "one 153 GB/s link (direct Bine: one peer per step)")},
             "wall_s": round(wall, 4),
         }
@@ -264,7 +278,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--algo", default="bine_bdw_remap")
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
-    ap.add_argument("--relay", default="auto", help="auto | off | <min relayed part bytes> (N > 2)")
+    ap.add_argument("--relay", default="auto", help="transport at N > 2: auto | off (direct) | relay | trees")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=10.0)

@@ -151,6 +151,16 @@ int bine_comm_synchronize(bine_comm_t comm);
  * every rank of the communicator must use the same setting. */
 int bine_comm_set_relay(bine_comm_t comm, size_t min_part_bytes);
 
+/* Multi-tree mode for allreduce at P = 4 and 8: the buffer is cut into P-1
+ * slices and the algorithm runs once per slice with the ranks relabelled so
+ * that at every step the P-1 instances use P-1 edge-disjoint pairings -- all
+ * links of the node, one hop each.  Integer results are identical to the
+ * reference; floating-point results equal the reference's schedule applied to
+ * relabelled ranks (a different association order: within rounding of the
+ * reference, not bit-identical).  Off by default (BINE_TREES=1 turns it on);
+ * collective: every rank must use the same setting. */
+int bine_comm_set_trees(bine_comm_t comm, int on);
+
 /* ---- collectives (device pointers, stream-ordered) ------------------------- */
 /* allreduce_* (libbine.h:30-37).  `segsize` plays bine_allreduce_segsize
  * (libbine.h:28) for BINE_AR_BINE_BDW_REMAP_SEGMENTED and is the pipelining
@@ -228,9 +238,10 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
  * stream this op waits for (-1: none).  PIPELINE exchanges appear cut into
  * `chunk_bytes` pieces (0: uncut).  *c_join = 1 if the comm stream first waits
  * for the caller's prior work; *final_wait = op the caller's stream waits for
- * at the end (-1: none); *stage_elems = relay staging workspace (elements).
+ * at the end (-1: none); workspace[4] = elements of TMP0, TMP1, TMP2 and the
+ * relay staging buffer the schedule uses.
  * relay_min_bytes > 0 selects relay mode as
- * bine_comm_set_relay does.  Returns the number of entries (may exceed cap) or
+ * bine_comm_set_relay does, trees = 1 multi-tree mode as bine_comm_set_trees.  Returns the number of entries (may exceed cap) or
  * -status. */
 typedef struct {
   int32_t op;
@@ -241,8 +252,8 @@ typedef struct {
 
 int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root,
                            size_t esz, size_t segsize, int in_place, size_t chunk_bytes,
-                           size_t relay_min_bytes, bine_sched_entry_t *out, int64_t cap, int *c_join,
-                           int64_t *final_wait, uint64_t *stage_elems);
+                           size_t relay_min_bytes, int trees, bine_sched_entry_t *out, int64_t cap,
+                           int *c_join, int64_t *final_wait, uint64_t *workspace);
 
 #ifdef __cplusplus
 }

@@ -108,8 +108,9 @@ def lib():
         "bine_plan": ([i, i, i, sz, vp, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(u64)],
                       ctypes.c_int64),
         "bine_comm_set_relay": ([vp, sz], i),
-        "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
-                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(u64)], ctypes.c_int64),
+        "bine_comm_set_trees": ([vp, i], i),
+        "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
+                                ctypes.POINTER(ctypes.c_int64), vp], ctypes.c_int64),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

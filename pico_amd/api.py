@@ -129,6 +129,10 @@ class Comm:
     def synchronize(self) -> None:
         check(lib().bine_comm_synchronize(self.handle), "bine_comm_synchronize")
 
+    def set_trees(self, on: bool) -> None:
+        """Multi-tree mode (allreduce, P = 4 / 8); collective."""
+        check(lib().bine_comm_set_trees(self.handle, int(on)), "bine_comm_set_trees")
+
     def set_relay(self, min_part_bytes: int) -> None:
         """Multi-link relay for permutation steps (0 = off); collective."""
         check(lib().bine_comm_set_relay(self.handle, min_part_bytes), "bine_comm_set_relay")
@@ -246,19 +250,19 @@ def plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, 
 
 def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, root: int = 0,
              esz: int = 4, segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0,
-             relay_min_bytes: int = 0, info: bool = False):
+             relay_min_bytes: int = 0, info: bool = False, trees: bool = False):
     """The executor's two-stream issue schedule of rank `rank` (host only).
     Returns (ops, c_join, final_wait); ops[i] = {"xchg", "wait", "prims"}.
-    With info=True a 4th item: {"stage_elems": relay staging workspace}."""
+    With info=True a 4th item: {"tmp_elems": [TMP0..2], "stage_elems": relay staging}."""
     a = _algo(coll, algo)
     rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
-    cj, fw, se = ctypes.c_int(), ctypes.c_int64(), ctypes.c_uint64()
-    args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes, relay_min_bytes)
-    n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw), ctypes.byref(se))
+    cj, fw, ws = ctypes.c_int(), ctypes.c_int64(), (ctypes.c_uint64 * 4)()
+    args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes, relay_min_bytes, int(trees))
+    n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw), ws)
     if n < 0:
         raise BineError(int(-n), f"schedule {coll}_{algo}")
     arr = (_lib.SchedEntry * max(int(n), 1))()
-    lib().bine_plan_schedule(*args, arr, n, ctypes.byref(cj), ctypes.byref(fw), ctypes.byref(se))
+    lib().bine_plan_schedule(*args, arr, n, ctypes.byref(cj), ctypes.byref(fw), ws)
     ops = []
     for k in range(int(n)):
         e = arr[k]
@@ -268,7 +272,8 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
             ops.append({"xchg": bool(e.xchg), "wait": int(e.wait), "prims": []})
         ops[-1]["prims"].append(p)
     if info:
-        return ops, bool(cj.value), int(fw.value), {"stage_elems": int(se.value)}
+        return ops, bool(cj.value), int(fw.value), {"tmp_elems": [int(x) for x in ws[:3]],
+                                                     "stage_elems": int(ws[3])}
     return ops, bool(cj.value), int(fw.value)
 
 

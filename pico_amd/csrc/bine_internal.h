@@ -34,6 +34,12 @@ struct PlanArgs {
 
 Plan make_plan(const PlanArgs &a);
 
+// multi-tree mode (trees.cpp): P-1 relabelled instances on P-1 slices; status
+// BINE_ERR_UNSUPPORTED when not applicable (only allreduce, P = 4 or 8)
+int tree_count(int P);
+const int *tree_relabel(int P, int k);  // virtual -> physical rank of instance k
+Plan make_tree_plan(const PlanArgs &a);
+
 // schedule math (libbine_utils.h restated for the planner)
 int pi(int rank, int step, int P);
 uint32_t remap_rank(uint32_t P, uint32_t rank);

@@ -190,6 +190,7 @@ struct bine_comm {
   void *tmp[4] = {nullptr, nullptr, nullptr, nullptr};  // TMP0..2, STAGE
   size_t tmp_bytes[4] = {0, 0, 0, 0};
   size_t relay_min_bytes = 0;  // relay mode: smallest relayed part (0: off)
+  bool trees = false;          // multi-tree mode (allreduce, P = 4 / 8)
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
   std::vector<hipEvent_t> ev;
@@ -212,6 +213,7 @@ static int comm_setup(bine_comm *c) {
   c->ev.resize(1024);
   for (auto &e : c->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (const char *e = getenv("BINE_RELAY_MIN_BYTES")) c->relay_min_bytes = (size_t)strtoull(e, nullptr, 10);
+  if (const char *e = getenv("BINE_TREES")) c->trees = atoi(e) != 0;
   return BINE_SUCCESS;
 }
 
@@ -335,8 +337,9 @@ static std::string plan_key(const PlanArgs &a) {
 }
 
 // own plan + issue schedule; relay mode needs every rank's plan
-static void build(const PlanArgs &a, size_t ch, size_t relay_min_bytes, Plan &plan, Schedule &sc) {
-  plan = make_plan(a);
+static void build(const PlanArgs &a, size_t ch, size_t relay_min_bytes, bool trees, Plan &plan, Schedule &sc) {
+  if (trees) plan = make_tree_plan(a);
+  if (!trees || plan.status == BINE_ERR_UNSUPPORTED) plan = make_plan(a);
   if (plan.status != BINE_SUCCESS) return;
   SchedCfg cfg;
   cfg.chunk = ch;
@@ -367,11 +370,12 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   a.esz = bine_dtype_size(dtype);
   a.in_place = sbuf == BINE_IN_PLACE;
   const size_t ch = chunk_elems(chunk_bytes, a.esz);
-  const std::string key = plan_key(a) + "|" + std::to_string(ch) + "|" + std::to_string(c->relay_min_bytes);
+  const std::string key = plan_key(a) + "|" + std::to_string(ch) + "|" + std::to_string(c->relay_min_bytes) +
+                          (c->trees ? "|T" : "");
   auto it = c->plans.find(key);
   if (it == c->plans.end()) {
     std::pair<Plan, Schedule> v;
-    build(a, ch, c->relay_min_bytes, v.first, v.second);
+    build(a, ch, c->relay_min_bytes, c->trees, v.first, v.second);
     it = c->plans.emplace(key, std::move(v)).first;
   }
   const Plan &plan = it->second.first;
@@ -696,14 +700,14 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
 }
 
 int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
-                           size_t segsize, int in_place, size_t chunk_bytes, size_t relay_min_bytes,
+                           size_t segsize, int in_place, size_t chunk_bytes, size_t relay_min_bytes, int trees,
                            bine_sched_entry_t *out, int64_t cap, int *c_join, int64_t *final_wait,
-                           uint64_t *stage_elems) {
+                           uint64_t *workspace) {
   if (!esz) return -(int64_t)BINE_ERR_ARG;
   PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
   Plan p;
   Schedule sc;
-  build(a, chunk_elems(chunk_bytes, esz), relay_min_bytes, p, sc);
+  build(a, chunk_elems(chunk_bytes, esz), relay_min_bytes, trees != 0, p, sc);
   if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
   int64_t n = 0;
   for (size_t i = 0; i < sc.ops.size(); i++)
@@ -713,8 +717,18 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
     }
   if (c_join) *c_join = sc.c_join ? 1 : 0;
   if (final_wait) *final_wait = sc.final_wait;
-  if (stage_elems) *stage_elems = sc.stage_elems;
+  if (workspace) {
+    for (int t = 0; t < 3; t++) workspace[t] = p.tmp_elems[t];
+    workspace[3] = sc.stage_elems;
+  }
   return n;
+}
+
+int bine_comm_set_trees(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->trees = on != 0;
+  return BINE_SUCCESS;
 }
 
 int bine_comm_set_relay(bine_comm_t c, size_t min_part_bytes) {

@@ -191,45 +191,68 @@ void emit_relay(const std::vector<Perm> &steps, int r, size_t ch, size_t relay_m
       ops.push_back({false, {slice(*q, k * cht, std::min<uint64_t>(cht, q->count - k * cht))}, -1});
 }
 
-// chunked (or whole) exchange group g of `pl`, plus the pipelined reduction
-// that follows it when `pipe`
-void emit_direct(const Plan &pl, std::pair<size_t, size_t> g, bool pipe, size_t ch, std::vector<SOp> &ops) {
+// Pipelined pairs of an exchange group: the group is n {send, recv} pairs
+// (n = 1 normally; one per instance in multi-tree plans), each flagged
+// PIPELINE, followed by n pipelined REDUCE / REDUCE3, the i-th consuming the
+// i-th pair's receive element for element (the planner's contract for the
+// flag).  Returns n, 0 if the group is not of that shape.
+size_t pipe_pairs(const Plan &pl, std::pair<size_t, size_t> g) {
   const auto &pr = pl.prims;
-  if (!pipe) {
+  const size_t m = g.second - g.first;
+  if (m == 0 || m % 2) return 0;
+  const size_t n = m / 2;
+  if (g.second + n > pr.size()) return 0;
+  for (size_t i = 0; i < n; i++) {
+    const Prim &x = pr[g.first + 2 * i], &y = pr[g.first + 2 * i + 1];
+    if (x.type == y.type || !(x.flags & BINE_PRIM_PIPELINE) || !(y.flags & BINE_PRIM_PIPELINE)) return 0;
+    const Prim &q = pr[g.second + i];
+    // (the flags alone decide: both ends of a pair must cut it the same way)
+    if (!(q.flags & BINE_PRIM_PIPELINE) || (q.type != BINE_PRIM_REDUCE && q.type != BINE_PRIM_REDUCE3)) return 0;
+  }
+  return n;
+}
+
+// chunked (or whole) exchange group g of `pl`; with n pipelined pairs the
+// reductions that follow are cut along with it (all pairs advance together,
+// one chunk of every pair per exchange)
+void emit_direct(const Plan &pl, std::pair<size_t, size_t> g, size_t n, size_t ch, std::vector<SOp> &ops) {
+  const auto &pr = pl.prims;
+  if (!n || !ch) {
     ops.push_back({true, std::vector<Prim>(pr.begin() + (long)g.first, pr.begin() + (long)g.second), -1});
     return;
   }
-  const Prim &S = pr[g.first].type == BINE_PRIM_SEND ? pr[g.first] : pr[g.first + 1];
-  const Prim &R = pr[g.first].type == BINE_PRIM_RECV ? pr[g.first] : pr[g.first + 1];
-  const Prim &Q = pr[g.second];
-  // both ends derive the chunk count from the same two sizes (my send is the
-  // peer's receive and vice versa), so the k-th groups pair up
-  const uint64_t nch = std::max((S.count + ch - 1) / ch, (R.count + ch - 1) / ch);
-  for (uint64_t k = 0; k < nch; k++) {
+  // both ends of a pair derive its chunk count from the same two sizes (my
+  // send is the peer's receive and vice versa), so the k-th groups pair up
+  std::vector<const Prim *> S(n), R(n), Q(n);
+  uint64_t rounds = 0;
+  for (size_t i = 0; i < n; i++) {
+    const Prim &x = pr[g.first + 2 * i], &y = pr[g.first + 2 * i + 1];
+    S[i] = x.type == BINE_PRIM_SEND ? &x : &y;
+    R[i] = x.type == BINE_PRIM_RECV ? &x : &y;
+    Q[i] = &pr[g.second + i];
+    rounds = std::max(rounds, std::max((S[i]->count + ch - 1) / ch, (R[i]->count + ch - 1) / ch));
+  }
+  for (uint64_t k = 0; k < rounds; k++) {
     const uint64_t o = k * ch;
     SOp x{true, {}, -1};
-    if (o < S.count) {
-      Prim a = S;
-      a.src_off += o;
-      a.count = std::min<uint64_t>(ch, S.count - o);
-      x.prims.push_back(a);
+    for (size_t i = 0; i < n; i++) {
+      if (o < S[i]->count) {
+        Prim a = *S[i];
+        a.src_off += o;
+        a.count = std::min<uint64_t>(ch, S[i]->count - o);
+        x.prims.push_back(a);
+      }
+      if (o < R[i]->count) {
+        Prim a = *R[i];
+        a.dst_off += o;
+        a.count = std::min<uint64_t>(ch, R[i]->count - o);
+        x.prims.push_back(a);
+      }
     }
-    if (o < R.count) {
-      Prim a = R;
-      a.dst_off += o;
-      a.count = std::min<uint64_t>(ch, R.count - o);
-      x.prims.push_back(a);
-    }
-    ops.push_back(x);
-    if (o < Q.count) ops.push_back({false, {slice(Q, o, std::min<uint64_t>(ch, Q.count - o))}, -1});
+    if (!x.prims.empty()) ops.push_back(x);
+    for (size_t i = 0; i < n; i++)
+      if (o < Q[i]->count) ops.push_back({false, {slice(*Q[i], o, std::min<uint64_t>(ch, Q[i]->count - o))}, -1});
   }
-}
-
-bool pipelined(const Plan &pl, std::pair<size_t, size_t> g, size_t ch) {
-  const auto &pr = pl.prims;
-  return ch && (pr[g.first].flags & BINE_PRIM_PIPELINE) && g.second - g.first == 2 && g.second < pr.size() &&
-         (pr[g.second].flags & BINE_PRIM_PIPELINE) &&
-         (pr[g.second].type == BINE_PRIM_REDUCE || pr[g.second].type == BINE_PRIM_REDUCE3);
 }
 
 }  // namespace
@@ -291,7 +314,7 @@ void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, con
       continue;
     }
     const auto g = mg[t];
-    const bool pipe = pipelined(plan, g, ch);
+    const size_t npipe = pipe_pairs(plan, g);
     if (!perm[t].empty()) {
       const bool qpipe = (pr[g.first].flags & BINE_PRIM_PIPELINE) && g.second < pr.size() &&
                          (pr[g.second].flags & BINE_PRIM_PIPELINE) &&
@@ -300,8 +323,8 @@ void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, con
       out.relayed_steps++;
       i = g.second + (qpipe ? 1 : 0);
     } else {
-      emit_direct(plan, g, pipe, ch, out.ops);
-      i = g.second + (pipe ? 1 : 0);
+      emit_direct(plan, g, npipe, ch, out.ops);
+      i = g.second + (ch ? npipe : 0);
     }
     t++;
   }

@@ -27,22 +27,22 @@ class PlanError(AssertionError):
     pass
 
 
-def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, **kw):
+def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, **kw):
     """The executor's issue schedule (pico_amd.schedule) flattened back into a
     primitive list in issue order, one exchange group per op."""
     ops, _, _, info = pico_amd.schedule(coll, algo, P, r, chunk_bytes=chunk_bytes, relay_min_bytes=relay,
-                                        info=True, **kw)
+                                        info=True, trees=trees, **kw)
     out = []
     for i, o in enumerate(ops):
         for p in o["prims"]:
             q = dict(p)
             q["group"] = i
             out.append(q)
-    return out, info["stage_elems"]
+    return out, info
 
 
 def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_place=False,
-        rbufs=None, chunk_bytes=None, relay=0):
+        rbufs=None, chunk_bytes=None, relay=0, trees=False):
     """chunk_bytes != None: run the executor's chunked issue schedule instead of
     the plan itself (same semantics when ops run in issue order)."""
     P = len(sbufs)
@@ -53,7 +53,7 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         prims, tmp = pico_amd.plan(coll, algo, P, r, count=count, rcounts=rcounts, root=root, esz=esz,
                                    segsize=segsize, in_place=in_place)
         if chunk_bytes is not None:
-            prims, stage = scheduled_prims(coll, algo, P, r, chunk_bytes, relay=relay, count=count, rcounts=rcounts, root=root,
+            prims, info = scheduled_prims(coll, algo, P, r, chunk_bytes, relay=relay, trees=trees, count=count, rcounts=rcounts, root=root,
                                     esz=esz, segsize=segsize, in_place=in_place)
         plans.append(prims)
         if coll == "allgather":
@@ -75,9 +75,11 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             else:
                 rb = sbufs[r].copy()
             sb = rb
+        if chunk_bytes is not None:
+            tmp = info["tmp_elems"]  # the schedule's own plan (multi-tree plans differ)
         tbufs = [np.zeros(max(int(t), 1) + 16, O.NP_DTYPES[dtype]) for t in tmp]
         # relay staging (BINE_BUF_STAGE), exactly as large as the executor allocates
-        tbufs.append(np.zeros(stage if chunk_bytes is not None else 0, O.NP_DTYPES[dtype]))
+        tbufs.append(np.zeros(info["stage_elems"] if chunk_bytes is not None else 0, O.NP_DTYPES[dtype]))
         bufs.append([sb, rb] + tbufs)
     pc = [0] * P
     sendq = collections.defaultdict(collections.deque)  # (src, dst) -> [(rank, idx)]

@@ -349,3 +349,34 @@ def test_allgather_family_matches_oracle(dev, P, relay):
             elif any(sha(o) != sha(w) for o, w in zip(outs, want)):
                 bad.append((algo, dt, n, "data"))
     assert not bad, bad[:8]
+
+
+# ---- multi-tree mode ------------------------------------------------------------
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_multi_tree_allreduce_on_device(dev, P):
+    """tree mode on the device: bit-exact vs the relabelled oracle for fp32 /
+    fp64, and vs the reference's golden vectors for integers"""
+    import test_trees as TT
+    bad = []
+    try:
+        for c in comms(P):
+            c.set_trees(True)
+        for algo in ("bine_bdw_remap", "bine_bdw_static", "ring", "bine_lat"):
+            for dt, n in (("float", 100003), ("double", 4099), ("int32", 65537)):
+                sb = O.inputs(dt, n, P)
+                want = TT.relabelled_oracle(algo, sb, dt)
+                outs, st = run_loopback("allreduce", algo, sb, dt)
+                if any(st) or any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                    bad.append((algo, dt, n, st))
+        for c in G.select(coll="allreduce", algo="bine_bdw_remap", P=P, op="sum"):
+            if c["dtype"] not in ("int32", "int64", "int8", "int16", "uint8") or c["status"] != "ok":
+                continue
+            sb = O.inputs(c["dtype"], c["N"], P, c["seed_base"])
+            outs, st = run_loopback("allreduce", "bine_bdw_remap", sb, c["dtype"])
+            if any(st) or G.check_rank_outputs(c, outs):
+                bad.append((c["id"], st))
+    finally:
+        for c in comms(P):
+            c.set_trees(False)
+    assert not bad, bad[:8]
