@@ -224,34 +224,39 @@ void emit_direct(const Plan &pl, std::pair<size_t, size_t> g, size_t n, size_t c
   // both ends of a pair derive its chunk count from the same two sizes (my
   // send is the peer's receive and vice versa), so the k-th groups pair up
   std::vector<const Prim *> S(n), R(n), Q(n);
+  std::vector<uint64_t> cs(n);  // per pair: `ch` rebalanced so its chunks come out even
   uint64_t rounds = 0;
   for (size_t i = 0; i < n; i++) {
     const Prim &x = pr[g.first + 2 * i], &y = pr[g.first + 2 * i + 1];
     S[i] = x.type == BINE_PRIM_SEND ? &x : &y;
     R[i] = x.type == BINE_PRIM_RECV ? &x : &y;
     Q[i] = &pr[g.second + i];
-    rounds = std::max(rounds, std::max((S[i]->count + ch - 1) / ch, (R[i]->count + ch - 1) / ch));
+    const uint64_t m = std::max(S[i]->count, R[i]->count), k = (m + ch - 1) / ch;
+    cs[i] = k ? std::min<uint64_t>(ch, ((m + k - 1) / k + 15) / 16 * 16) : ch;
+    rounds = std::max(rounds, std::max((S[i]->count + cs[i] - 1) / cs[i], (R[i]->count + cs[i] - 1) / cs[i]));
   }
   for (uint64_t k = 0; k < rounds; k++) {
-    const uint64_t o = k * ch;
     SOp x{true, {}, -1};
     for (size_t i = 0; i < n; i++) {
+      const uint64_t o = k * cs[i], c = cs[i];
       if (o < S[i]->count) {
         Prim a = *S[i];
         a.src_off += o;
-        a.count = std::min<uint64_t>(ch, S[i]->count - o);
+        a.count = std::min<uint64_t>(c, S[i]->count - o);
         x.prims.push_back(a);
       }
       if (o < R[i]->count) {
         Prim a = *R[i];
         a.dst_off += o;
-        a.count = std::min<uint64_t>(ch, R[i]->count - o);
+        a.count = std::min<uint64_t>(c, R[i]->count - o);
         x.prims.push_back(a);
       }
     }
     if (!x.prims.empty()) ops.push_back(x);
-    for (size_t i = 0; i < n; i++)
-      if (o < Q[i]->count) ops.push_back({false, {slice(*Q[i], o, std::min<uint64_t>(ch, Q[i]->count - o))}, -1});
+    for (size_t i = 0; i < n; i++) {
+      const uint64_t o = k * cs[i];
+      if (o < Q[i]->count) ops.push_back({false, {slice(*Q[i], o, std::min<uint64_t>(cs[i], Q[i]->count - o))}, -1});
+    }
   }
 }
 
