@@ -6,7 +6,7 @@ so each rank claims a different host id (NCCL_HOSTID) and RCCL connects them
 over its socket network transport on the loopback interface.  This validates
 the executor's RCCL path (grouping, stream/event hand-offs, chunked pipeline,
 exact counts) with real multi-process RCCL; it says nothing about xGMI speed.
-usage: python tools/rccl_1gpu_multirank.py [P] [relay_min_bytes]
+usage: python tools/rccl_1gpu_multirank.py [P] [relay_min_bytes] [trees 0|1]
 """
 import os
 import sys
@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(rank, P, port, q, relay=0):
+def worker(rank, P, port, q, relay=0, trees=0):
     os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
@@ -29,12 +29,18 @@ def worker(rank, P, port, q, relay=0):
     dist.init_process_group("gloo")
     comm = pico_amd.Comm.from_torch_distributed(0)
     comm.set_relay(relay)
+    comm.set_trees(bool(trees))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     ok = True
     for algo, n, seg in (("bine_bdw_remap", 100003, 0), ("bine_bdw_remap", 100003, 4096),
                          ("bine_bdw_static", 4099, 0), ("ring", 4099, 0), ("bine_lat", 333, 0),
                          ("bine_bdw_remap_segmented", 5000, 64), ("bine_block_by_block_any_even", 4099, 0)):
         sb = O.inputs("float", n, P)
-        want, _ = O.allreduce(algo, sb, "float", segsize=seg)
+        if trees and P in (4, 8) and n >= 64 * (P - 1):
+            import test_trees
+            want = test_trees.relabelled_oracle(algo, sb, "float", segsize=seg)
+        else:
+            want, _ = O.allreduce(algo, sb, "float", segsize=seg)
         s = torch.from_numpy(sb[rank]).cuda()
         r = torch.zeros_like(s)
         pico_amd.allreduce(algo, s, r, n, "float", "sum", comm, segsize=seg)
@@ -42,7 +48,7 @@ def worker(rank, P, port, q, relay=0):
         comm.synchronize()
         same = np.array_equal(r.cpu().numpy(), want[rank])
         ok &= same
-        print(f"rank {rank} {algo} n={n} seg={seg} relay={relay}: {'ok' if same else 'MISMATCH'}", flush=True)
+        print(f"rank {rank} {algo} n={n} seg={seg} relay={relay} trees={trees}: {'ok' if same else 'MISMATCH'}", flush=True)
     rc = [4096] * P
     sb = O.inputs("float", sum(rc), P)
     want, _ = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
@@ -62,9 +68,10 @@ if __name__ == "__main__":
     import multiprocessing as mp
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     relay = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    trees = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, P, 29555, q, relay)) for r in range(P)]
+    ps = [ctx.Process(target=worker, args=(r, P, 29555, q, relay, trees)) for r in range(P)]
     for p in ps:
         p.start()
     for p in ps:
