@@ -728,6 +728,11 @@ void rs_bine_remap(Builder &b, const PlanArgs &a, bool permute) {
   const int P = a.P, r = a.rank;
   const auto &rc = a.rcounts;
   if (!is_pow2(P)) { b.fail(BINE_ERR_ARG); return; }  // the reference hangs
+  // permute: block i moves into the slot of block remap(i) (:1008-1011) --
+  // defined only for equal blocks (the reference overruns its buffers otherwise)
+  if (permute)
+    for (int x : rc)
+      if (x != rc[0]) { b.fail(BINE_ERR_ARG); return; }
   Displs ds(rc);
   const uint64_t count = ds.total;
   const int src = a.in_place ? RB : SB;

@@ -6,7 +6,8 @@
 //
 // Instance k: virtual rank v (a rank of the reference's schedule) is played by
 // physical rank sigma_k[v]; its input is that rank's slice k, so each slice is
-// a valid allreduce of all ranks' data.  The reduction tree of a slice is the
+// a valid allreduce of all ranks' data (reduce_scatter permute_remap: see
+// Mapper below).  The reduction tree of a slice is the
 // reference's tree over relabelled ranks: integer results are identical to the
 // reference (wrapping SUM/PROD, MAX, MIN are associative and commutative);
 // floating-point results differ from the reference only by association order
@@ -69,21 +70,50 @@ int tree_count(int P) { return (P == 4 || P == 8) ? P - 1 : 1; }
 
 const int *tree_relabel(int P, int k) { return relabel(P, k); }
 
+// One instance's plan mapped onto the physical buffers.  Allreduce: slice k is
+// the element range [off, off + len) of sbuf and rbuf.  Reduce-scatter
+// (permute_remap): slice k is sub-range k of every rank's block; the
+// instance's virtual block u is physical block sigma_k[u] (its input is read
+// block by block by the algorithm's own initial permutation copy, so the
+// relabelling costs no extra pass), its output is sub-range k of the own block.
+struct Mapper {
+  int kind = 0;                       // 0 allreduce, 1 reduce_scatter
+  uint64_t off = 0;                   // allreduce: slice offset
+  std::vector<uint64_t> vdisp, vcnt;  // reduce_scatter: virtual block layout
+  std::vector<uint64_t> pstart;       // reduce_scatter: physical start of virtual block u
+  uint64_t rb_off = 0;                // reduce_scatter: offset in the own output block
+  bool ok = true;
+  uint64_t sbuf(uint64_t x, uint64_t n) {
+    if (kind == 0) return x + off;
+    size_t u = (size_t)(std::upper_bound(vdisp.begin(), vdisp.end(), x) - vdisp.begin()) - 1;
+    if (x + n > vdisp[u] + vcnt[u]) ok = false;  // must stay inside one block
+    return pstart[u] + (x - vdisp[u]);
+  }
+  uint64_t rbuf(uint64_t x) { return kind == 0 ? x + off : x + rb_off; }
+};
+
 Plan make_tree_plan(const PlanArgs &a) {
   Plan out;
   const int P = a.P, T = tree_count(P);
   const bool allreduce = a.algo >= BINE_AR_RECURSIVEDOUBLING && a.algo <= BINE_AR_BINE_BLOCK_BY_BLOCK_ANY_EVEN;
-  if (T < 2 || !allreduce || a.count < (uint64_t)T * kAlign) {
+  const bool rs = a.algo == BINE_RS_BINE_PERMUTE_REMAP && !a.in_place && (int)a.rcounts.size() == P;
+  bool fit = T >= 2 && (allreduce || rs);
+  if (fit && allreduce) fit = a.count >= (uint64_t)T * kAlign;
+  if (fit && rs)
+    for (int c : a.rcounts) fit = fit && (uint64_t)c >= (uint64_t)T * kAlign;
+  if (!fit) {
     out.status = BINE_ERR_UNSUPPORTED;
     return out;
   }
-  // slice k: [off[k], off[k] + len[k])
-  std::vector<uint64_t> off((size_t)T), len((size_t)T);
-  const uint64_t base = a.count / (uint64_t)T / kAlign * kAlign;
-  for (int k = 0; k < T; k++) {
-    off[(size_t)k] = (uint64_t)k * base;
-    len[(size_t)k] = k == T - 1 ? a.count - (uint64_t)k * base : base;
-  }
+  // slice k of n elements: [k * base, ...), the last one takes the remainder
+  auto slice_of = [&](uint64_t n, int k, uint64_t &o, uint64_t &l) {
+    const uint64_t base = n / (uint64_t)T / kAlign * kAlign;
+    o = (uint64_t)k * base;
+    l = k == T - 1 ? n - o : base;
+  };
+  std::vector<uint64_t> pdisp((size_t)P + 1, 0);
+  if (rs)
+    for (int j = 0; j < P; j++) pdisp[(size_t)j + 1] = pdisp[(size_t)j] + (uint64_t)a.rcounts[(size_t)j];
   std::vector<std::vector<Seg>> segs((size_t)T);
   uint64_t tbase[3] = {0, 0, 0};
   for (int k = 0; k < T; k++) {
@@ -92,18 +122,46 @@ Plan make_tree_plan(const PlanArgs &a) {
     while (sig[v] != a.rank) v++;
     PlanArgs b = a;
     b.rank = v;
-    b.count = len[(size_t)k];
+    Mapper m;
+    if (allreduce) {
+      uint64_t l;
+      slice_of(a.count, k, m.off, l);
+      b.count = l;
+    } else {
+      m.kind = 1;
+      m.vdisp.resize((size_t)P);
+      m.vcnt.resize((size_t)P);
+      m.pstart.resize((size_t)P);
+      uint64_t acc = 0;
+      for (int u = 0; u < P; u++) {
+        const int j = sig[u];
+        uint64_t o, l;
+        slice_of((uint64_t)a.rcounts[(size_t)j], k, o, l);
+        b.rcounts[(size_t)u] = (int)l;
+        m.vdisp[(size_t)u] = acc;
+        m.vcnt[(size_t)u] = l;
+        m.pstart[(size_t)u] = pdisp[(size_t)j] + o;
+        acc += l;
+      }
+      uint64_t l;
+      slice_of((uint64_t)a.rcounts[(size_t)a.rank], k, m.rb_off, l);
+    }
     Plan pk = make_plan(b);
     if (pk.status != BINE_SUCCESS) return pk;
     for (auto &x : pk.prims) {
       if (x.type == BINE_PRIM_SEND || x.type == BINE_PRIM_RECV) x.peer = sig[x.peer];
       auto shift = [&](int32_t buf, uint64_t &o) {
-        if (buf == BINE_BUF_SBUF || buf == BINE_BUF_RBUF) o += off[(size_t)k];
+        if (buf == BINE_BUF_SBUF) o = m.sbuf(o, x.count);
+        else if (buf == BINE_BUF_RBUF) o = m.rbuf(o);
         else if (buf >= BINE_BUF_TMP0 && buf <= BINE_BUF_TMP2) o += tbase[buf - BINE_BUF_TMP0];
       };
-      shift(x.src_buf, x.src_off);
-      shift(x.dst_buf, x.dst_off);
+      if (x.type != BINE_PRIM_RECV) shift(x.src_buf, x.src_off);
+      if (x.type != BINE_PRIM_SEND) shift(x.dst_buf, x.dst_off);
       if (x.type == BINE_PRIM_REDUCE3) shift(x.aux_buf, x.aux_off);
+    }
+    if (!m.ok) {
+      out.status = BINE_ERR_UNSUPPORTED;
+      return out;
     }
     for (int t = 0; t < 3; t++) tbase[t] += pk.tmp_elems[t];
     segs[(size_t)k] = segments(pk);
@@ -113,16 +171,16 @@ Plan make_tree_plan(const PlanArgs &a) {
   // exchange holding all instances' group g (the pipelined reductions that
   // follow a group stay in instance order, matching the pairs' order)
   size_t nseg = 0;
-  for (const auto &s : segs) nseg = std::max(nseg, s.size());
+  for (const auto &sg : segs) nseg = std::max(nseg, sg.size());
   int gid = 0;
   for (size_t g = 0; g < nseg; g++) {
-    for (const auto &s : segs)
-      if (g < s.size())
-        for (const auto &x : s[g].pre) out.prims.push_back(x);
+    for (const auto &sg : segs)
+      if (g < sg.size())
+        for (const auto &x : sg[g].pre) out.prims.push_back(x);
     bool any = false;
-    for (const auto &s : segs)
-      if (g < s.size())
-        for (auto x : s[g].group) {
+    for (const auto &sg : segs)
+      if (g < sg.size())
+        for (auto x : sg[g].group) {
           x.group = gid;
           out.prims.push_back(x);
           any = true;

@@ -210,3 +210,12 @@ def test_allgather_permute_variants_land_blocks_in_place():
         prims, _ = pico_amd.plan("allgather", algo, 8, 3, count=100)
         assert [p["type"] for p in prims].count("COPY") == 1
         assert prims[0]["type"] == "COPY"
+
+
+def test_permute_remap_needs_equal_blocks():
+    """reduce_scatter_bine_permute_remap moves block i into block remap(i)'s slot
+    (libbine_reduce_scatter.c:1008-1011): the reference overruns its buffers on
+    unequal blocks; here that is MPI_ERR_ARG"""
+    with pytest.raises(pico_amd.BineError) as ei:
+        pico_amd.plan("reduce_scatter", "bine_permute_remap", 4, 0, rcounts=[4, 5, 4, 4])
+    assert ei.value.status == 1

@@ -114,7 +114,8 @@ def test_schedules_race_free(chunk, in_place):
         for rank in range(P):
             kw = dict(count=1003, esz=4, segsize=128, in_place=in_place)
             if coll == "reduce_scatter":
-                kw = dict(rcounts=[37 + (i % 3) for i in range(P)], esz=4, in_place=in_place)
+                kw = dict(rcounts=[37 + (i % 3) * (algo != "bine_permute_remap") for i in range(P)], esz=4,
+                          in_place=in_place)
             if coll == "allgather":
                 kw = dict(count=101, esz=4, in_place=in_place)
             try:
@@ -153,7 +154,7 @@ def test_chunked_schedule_matches_oracle(coll, algo, P, chunk):
         assert _run_relay(coll, algo, P, chunk, 0)
         return
     if coll == "reduce_scatter":
-        rc = [29 + 3 * (i % 2) for i in range(P)]
+        rc = [29 + 3 * (i % 2) * (algo != "bine_permute_remap") for i in range(P)]  # permute: equal blocks
         sb = O.inputs(dtype, sum(rc), P)
         want = O.reduce_scatter(algo, sb, rc, dtype)[0]
         got = plan_sim.run(coll, algo, sb, dtype, rcounts=rc, chunk_bytes=chunk)
@@ -196,7 +197,7 @@ def _run_relay(coll, algo, P, chunk, relay, n=997):
         got = plan_sim.run(coll, algo, sb, dtype, chunk_bytes=chunk, relay=relay)
         return all(np.array_equal(got[r], want[r]) for r in range(P))
     if coll == "reduce_scatter":
-        rc = [n // P + (i % 2) for i in range(P)]
+        rc = [n // P + (i % 2) * (algo != "bine_permute_remap") for i in range(P)]
         sb = O.inputs(dtype, sum(rc), P)
         want = O.reduce_scatter(algo, sb, rc, dtype)[0]
         got = plan_sim.run(coll, algo, sb, dtype, rcounts=rc, chunk_bytes=chunk, relay=relay)
@@ -222,7 +223,7 @@ def test_relay_schedules_race_free(coll, algo, P):
     for rank in range(P):
         kw = dict(count=4099, esz=4, segsize=512)
         if coll == "reduce_scatter":
-            kw = dict(rcounts=[500 + (i % 3) for i in range(P)], esz=4)
+            kw = dict(rcounts=[500 + (i % 3) * (algo != "bine_permute_remap") for i in range(P)], esz=4)
         if coll == "allgather":
             kw = dict(count=513, esz=4)
         for chunk in (0, 1024):

@@ -115,3 +115,58 @@ def test_small_counts_and_other_sizes_fall_back():
     a, _, _ = pico_amd.schedule("allreduce", "bine_bdw_remap", 16, 0, count=1 << 16, trees=True)
     b, _, _ = pico_amd.schedule("allreduce", "bine_bdw_remap", 16, 0, count=1 << 16)
     assert a == b
+
+
+def relabelled_rs_oracle(sb, rc, dtype):
+    """multi-tree reduce_scatter_bine_permute_remap: instance k reduces
+    sub-range k of every block, virtual block u = physical block sigma_k[u]"""
+    P = len(sb)
+    T = P - 1
+    disp = np.concatenate([[0], np.cumsum(rc)])
+    out = [np.zeros(rc[r], sb[0].dtype) for r in range(P)]
+
+    def sl(n, k):
+        base = n // T // 64 * 64
+        return k * base, (n - k * base) if k == T - 1 else base
+
+    for k in range(T):
+        sig = RELABEL[P][k]
+        vr = [sl(rc[sig[u]], k)[1] for u in range(P)]
+        virt = []
+        for v in range(P):
+            parts = []
+            for u in range(P):
+                j = sig[u]
+                o, ln = sl(rc[j], k)
+                parts.append(sb[sig[v]][disp[j] + o:disp[j] + o + ln])
+            virt.append(np.ascontiguousarray(np.concatenate(parts)))
+        res, rets = O.reduce_scatter("bine_permute_remap", virt, vr, dtype)
+        assert not any(rets)
+        for v in range(P):
+            r = sig[v]
+            o, ln = sl(rc[r], k)
+            out[r][o:o + ln] = res[v]
+    return out
+
+
+@pytest.mark.parametrize("P", [4, 8])
+@pytest.mark.parametrize("chunk", [0, 1024])
+def test_tree_reduce_scatter_matches_relabelled_oracle(P, chunk):
+    rc = [64 * (P - 1) * 2 + 5] * P  # permute_remap needs equal blocks
+    for dtype in ("float", "int32"):
+        sb = O.inputs(dtype, sum(rc), P)
+        want = relabelled_rs_oracle(sb, rc, dtype)
+        got = plan_sim.run("reduce_scatter", "bine_permute_remap", sb, dtype, rcounts=rc, chunk_bytes=chunk,
+                           trees=True)
+        for r in range(P):
+            assert np.array_equal(got[r], want[r]), (P, dtype, r)
+        ref, _ = O.reduce_scatter("bine_permute_remap", sb, rc, dtype)
+        if dtype == "int32":
+            assert all(np.array_equal(g, w) for g, w in zip(got, ref))
+        else:
+            assert max(float(np.max(np.abs(g - w))) for g, w in zip(got, ref)) <= P * 1e-4
+        for r in range(P):
+            ops, cj, fw = pico_amd.schedule("reduce_scatter", "bine_permute_remap", P, r, rcounts=rc, esz=4,
+                                            chunk_bytes=chunk, trees=True)
+            check_race_free(ops, cj, fw, False)
+            assert len({p["peer"] for o in ops if o["xchg"] for p in o["prims"]}) == P - 1
