@@ -380,3 +380,21 @@ def test_multi_tree_allreduce_on_device(dev, P):
         for c in comms(P):
             c.set_trees(False)
     assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_multi_tree_reduce_scatter_on_device(dev, P):
+    import test_trees as TT
+    rc = [(1 << 15) + 3] * P
+    try:
+        for c in comms(P):
+            c.set_trees(True)
+        for dt in ("float", "int64"):
+            sb = O.inputs(dt, sum(rc), P)
+            want = TT.relabelled_rs_oracle(sb, rc, dt)
+            outs, st = run_loopback("reduce_scatter", "bine_permute_remap", sb, dt, rcounts=rc)
+            assert not any(st)
+            assert all(sha(o) == sha(w) for o, w in zip(outs, want)), dt
+    finally:
+        for c in comms(P):
+            c.set_trees(False)
