@@ -119,6 +119,10 @@ int bine_reduce3(const void *a, const void *b, void *out, size_t count, int dtyp
 /* pico_core's input distribution (pico_core_utils.c:902-923) generated on the
  * device: element i of buffer `seed` equals what glibc rand_r(&seed) would
  * produce for pico_core (LCG jump-ahead, bit-exact). */
+/* n (1..8) independent reductions out[k] = b[k] (op) a[k] in one launch
+ * (BINE_ERR_ARG if some window's operands are not co-aligned mod 16 B). */
+int bine_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out,
+                      const size_t *count, int dtype, int op, void *stream);
 int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
 /* Order-independent 64-bit digest of a buffer: sum over i of
  * mix64(bits(x[i]) + i * 0x9E3779B97F4A7C15) mod 2^64 (bits zero-extended).

@@ -101,6 +101,7 @@ def lib():
         "bine_reduce_scatter": ([vp, i, vp, vp, vp, i, i, vp], i),
         "bine_reduce": ([vp, i, vp, vp, sz, i, i, i, vp], i),
         "bine_allgather": ([vp, i, vp, vp, sz, i, vp], i),
+        "bine_reduce_batch": ([i, vp, vp, vp, vp, i, i, vp], i),
         "bine_loopback_run_allgather": ([vp, i, i, vp, vp, sz, i, vp], i),
         "bine_loopback_run_allreduce": ([vp, i, i, vp, vp, sz, i, i, sz, vp], i),
         "bine_loopback_run_reduce_scatter": ([vp, i, i, vp, vp, vp, i, i, vp], i),

@@ -277,6 +277,15 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
     return ops, bool(cj.value), int(fw.value)
 
 
+def reduce_batch(ins, inouts, counts, dtype, op: str = "sum", stream=None) -> int:
+    """inouts[k][:counts[k]] = inouts[k] (op) ins[k], all windows in one launch.
+    Returns the status (BINE_ERR_ARG = 1 when windows are not co-aligned)."""
+    n = len(ins)
+    c = (ctypes.c_size_t * n)(*counts)
+    b = _ptrs(inouts)
+    return lib().bine_reduce_batch(n, _ptrs(ins), b, b, c, _dtype(dtype, inouts[0]), OPS[op], _stream(stream, None))
+
+
 def allgather(algo, sbuf, rbuf, count: int, dtype, comm: Comm, stream=None) -> None:
     """count = elements per rank; rbuf holds comm.size * count elements."""
     check(lib().bine_allgather(comm.handle, _algo("allgather", algo), _ptr(sbuf), _ptr(rbuf), count,
@@ -338,4 +347,4 @@ globals().update(ENTRY_POINTS)
 
 __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
-           "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather"] + list(ENTRY_POINTS)
+           "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "reduce_batch"] + list(ENTRY_POINTS)

@@ -84,6 +84,11 @@ void make_schedule(const Plan &plan, size_t chunk, bool in_place, Schedule &out)
 // ---- kernels (kernels.hip) ----------------------------------------------------
 int launch_reduce(const void *a, const void *b, void *out, size_t count, int dtype, int op,
                   void *stream);   // out = b (op) a
+// up to kMaxBatch windows in one launch; BINE_ERR_ARG if a window is not
+// co-aligned mod 16 B (then launch them one by one)
+constexpr int kMaxBatch = 8;
+int launch_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out, const size_t *count,
+                        int dtype, int op, void *stream);
 int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
 int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
 

@@ -266,6 +266,43 @@ static size_t default_chunk_bytes() {
 // Issue a schedule (make_schedule): exchanges on the comm stream C, local
 // primitives on the caller's stream K, one event per op, and a cross-stream
 // wait only where the schedule names one.
+// the local primitives of one op: several reductions go out as one batched
+// launch (multi-tree rounds), anything else one launch / copy each
+template <typename Ptr>
+static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op, size_t esz, hipStream_t K) {
+  const size_t n = prims.size();
+  bool batch = n >= 2 && n <= (size_t)kMaxBatch;
+  for (const Prim &p : prims) batch = batch && (p.type == BINE_PRIM_REDUCE || p.type == BINE_PRIM_REDUCE3);
+  if (batch) {
+    const void *a[kMaxBatch], *b[kMaxBatch];
+    void *out[kMaxBatch];
+    size_t cnt[kMaxBatch];
+    for (size_t i = 0; i < n; i++) {
+      const Prim &p = prims[i];
+      a[i] = ptr(p.src_buf, p.src_off);
+      b[i] = p.type == BINE_PRIM_REDUCE ? ptr(p.dst_buf, p.dst_off) : ptr(p.aux_buf, p.aux_off);
+      out[i] = ptr(p.dst_buf, p.dst_off);
+      cnt[i] = p.count;
+    }
+    const int rc = launch_reduce_batch((int)n, a, b, out, cnt, dtype, op, K);
+    if (rc != BINE_ERR_ARG) return rc;  // ERR_ARG: not co-aligned, one by one below
+  }
+  for (const Prim &p : prims) {
+    int rc = BINE_SUCCESS;
+    if (p.type == BINE_PRIM_REDUCE)
+      rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.dst_buf, p.dst_off), ptr(p.dst_buf, p.dst_off), p.count,
+                         dtype, op, K);
+    else if (p.type == BINE_PRIM_REDUCE3)
+      rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count,
+                         dtype, op, K);
+    else
+      HIP_TRY(hipMemcpyAsync(ptr(p.dst_buf, p.dst_off), ptr(p.src_buf, p.src_off), p.count * esz,
+                             hipMemcpyDeviceToDevice, K));
+    if (rc) return rc;
+  }
+  return BINE_SUCCESS;
+}
+
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
                    hipStream_t K) {
   char *base[6];
@@ -298,16 +335,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       rc = c->tx->exchange(sends, recvs, C);
       if (rc) return rc;
     } else {
-      const Prim &p = o.prims[0];
-      if (p.type == BINE_PRIM_REDUCE)
-        rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.dst_buf, p.dst_off), ptr(p.dst_buf, p.dst_off), p.count,
-                           dtype, op, K);
-      else if (p.type == BINE_PRIM_REDUCE3)
-        rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count,
-                           dtype, op, K);
-      else
-        HIP_TRY(hipMemcpyAsync(ptr(p.dst_buf, p.dst_off), ptr(p.src_buf, p.src_off), p.count * esz,
-                               hipMemcpyDeviceToDevice, K));
+      rc = run_local(o.prims, ptr, dtype, op, esz, K);
       if (rc) { set_err("local primitive failed (%s)", bine_status_string(rc)); return rc; }
     }
     // an event of the pool may be re-recorded by a later op once the pool
@@ -504,6 +532,11 @@ int bine_reduce_local(const void *in, void *inout, size_t count, int dtype, int 
 
 int bine_reduce3(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream) {
   return launch_reduce(a, b, out, count, dtype, op, stream);
+}
+
+int bine_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out, const size_t *count,
+                      int dtype, int op, void *stream) {
+  return launch_reduce_batch(n, a, b, out, count, dtype, op, stream);
 }
 
 int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream) {

@@ -253,10 +253,13 @@ void emit_direct(const Plan &pl, std::pair<size_t, size_t> g, size_t n, size_t c
       }
     }
     if (!x.prims.empty()) ops.push_back(x);
+    // this round's chunk reductions of every pair: one op (one batched launch)
+    SOp q{false, {}, -1};
     for (size_t i = 0; i < n; i++) {
       const uint64_t o = k * cs[i];
-      if (o < Q[i]->count) ops.push_back({false, {slice(*Q[i], o, std::min<uint64_t>(cs[i], Q[i]->count - o))}, -1});
+      if (o < Q[i]->count) q.prims.push_back(slice(*Q[i], o, std::min<uint64_t>(cs[i], Q[i]->count - o)));
     }
+    if (!q.prims.empty()) ops.push_back(q);
   }
 }
 

@@ -232,6 +232,118 @@ int launch_reduce(const void *a, const void *b, void *out, size_t count, int dty
 }
 
 // ----------------------------------------------------------------------------
+// batched reduction: up to kMaxBatch independent windows in one launch (the
+// P-1 per-instance chunk reductions of a multi-tree round).  The grid is the
+// concatenation of every window's tiles; a workgroup finds its window by a
+// scan over at most 8 tile offsets.  Windows must be co-aligned mod 16 B
+// (the caller falls back to one launch per window otherwise).
+
+struct BatchWin {
+  const void *a, *b;
+  void *out;
+  uint64_t head, nvec, n, tile0;
+};
+struct Batch {
+  int nwin;
+  BatchWin w[kMaxBatch];
+};
+
+template <typename T, int OP, int U, int NT>
+__global__ __launch_bounds__(kBlock) void k_reduce_batch(Batch bt) {
+  constexpr size_t V = 16 / sizeof(T);
+  const uint64_t t = blockIdx.x;
+  int k = 0;
+  while (k + 1 < bt.nwin && t >= bt.w[k + 1].tile0) k++;
+  const BatchWin &w = bt.w[k];
+  const T *a = (const T *)w.a, *b = (const T *)w.b;
+  T *out = (T *)w.out;
+  if (t == w.tile0) {  // head and tail of this window
+    for (size_t i = threadIdx.x; i < w.head; i += kBlock) out[i] = apply<T, OP>(b[i], a[i]);
+    for (size_t i = w.head + w.nvec * V + threadIdx.x; i < w.n; i += kBlock) out[i] = apply<T, OP>(b[i], a[i]);
+  }
+  const u32x4 *va = reinterpret_cast<const u32x4 *>(a + w.head);
+  const u32x4 *vb = reinterpret_cast<const u32x4 *>(b + w.head);
+  u32x4 *vo = reinterpret_cast<u32x4 *>(out + w.head);
+  const size_t base = (size_t)(t - w.tile0) * kBlock * U + threadIdx.x;
+  if (base + (U - 1) * (size_t)kBlock < w.nvec) {
+    u32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      x[u] = ld<NT & 1>(va + base + (size_t)u * kBlock);
+      y[u] = ld<NT & 2>(vb + base + (size_t)u * kBlock);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) vo[base + (size_t)u * kBlock] = apply16<T, OP>(y[u], x[u]);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * kBlock;
+      if (i < w.nvec) vo[i] = apply16<T, OP>(vb[i], va[i]);
+    }
+  }
+}
+
+template <typename T, int OP>
+static hipError_t batch_t(int n, const void *const *a, const void *const *b, void *const *out,
+                          const size_t *count, hipStream_t st) {
+  constexpr int U = kDefaultUnroll;
+  constexpr size_t V = 16 / sizeof(T);
+  Batch bt;
+  bt.nwin = n;
+  uint64_t tiles = 0;
+  for (int k = 0; k < n; k++) {
+    const uintptr_t ao = (uintptr_t)a[k], bo = (uintptr_t)b[k], oo = (uintptr_t)out[k];
+    if (((ao ^ oo) & 15) || ((bo ^ oo) & 15) || (oo % sizeof(T))) return hipErrorInvalidValue;
+    BatchWin &w = bt.w[k];
+    w.a = a[k];
+    w.b = b[k];
+    w.out = out[k];
+    w.n = count[k];
+    w.head = std::min<uint64_t>(((16 - (oo & 15)) & 15) / sizeof(T), w.n);
+    w.nvec = (w.n - w.head) / V;
+    w.tile0 = tiles;
+    tiles += std::max<uint64_t>(1, (w.nvec + (uint64_t)kBlock * U - 1) / ((uint64_t)kBlock * U));
+  }
+  hipLaunchKernelGGL((k_reduce_batch<T, OP, U, kDefaultNT>), dim3((unsigned)tiles), dim3(kBlock), 0, st, bt);
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t batch_op(int n, const void *const *a, const void *const *b, void *const *out, const size_t *c,
+                           int op, hipStream_t st) {
+  switch (op) {
+    case BINE_SUM: return batch_t<T, BINE_SUM>(n, a, b, out, c, st);
+    case BINE_PROD: return batch_t<T, BINE_PROD>(n, a, b, out, c, st);
+    case BINE_MAX: return batch_t<T, BINE_MAX>(n, a, b, out, c, st);
+    case BINE_MIN: return batch_t<T, BINE_MIN>(n, a, b, out, c, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int launch_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out, const size_t *count,
+                        int dtype, int op, void *stream) {
+  if (n < 1 || n > kMaxBatch) return BINE_ERR_ARG;
+  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case BINE_INT8: e = batch_op<int8_t>(n, a, b, out, count, op, st); break;
+    case BINE_UINT8: e = batch_op<uint8_t>(n, a, b, out, count, op, st); break;
+    case BINE_INT16: e = batch_op<int16_t>(n, a, b, out, count, op, st); break;
+    case BINE_UINT16: e = batch_op<uint16_t>(n, a, b, out, count, op, st); break;
+    case BINE_INT32: e = batch_op<int32_t>(n, a, b, out, count, op, st); break;
+    case BINE_UINT32: e = batch_op<uint32_t>(n, a, b, out, count, op, st); break;
+    case BINE_INT64: e = batch_op<int64_t>(n, a, b, out, count, op, st); break;
+    case BINE_UINT64: e = batch_op<uint64_t>(n, a, b, out, count, op, st); break;
+    case BINE_FLOAT: e = batch_op<float>(n, a, b, out, count, op, st); break;
+    case BINE_DOUBLE: e = batch_op<double>(n, a, b, out, count, op, st); break;
+    default: return BINE_ERR_UNSUPPORTED;
+  }
+  if (e == hipErrorInvalidValue) return BINE_ERR_ARG;  // not co-aligned: caller falls back
+  return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
 // pico_core input generator (glibc rand_r, LCG jump-ahead)
 // ----------------------------------------------------------------------------
 

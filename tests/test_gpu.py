@@ -398,3 +398,37 @@ def test_multi_tree_reduce_scatter_on_device(dev, P):
     finally:
         for c in comms(P):
             c.set_trees(False)
+
+
+@pytest.mark.parametrize("dtype", ["float", "double", "int8", "int64"])
+def test_reduce_batch_matches_per_window(dev, dtype):
+    """batched launch (multi-tree rounds): windows of different sizes and 16-B
+    phases, heads and tails, vs the oracle's MPI_Reduce_local per window"""
+    npdt = O.NP_DTYPES[dtype]
+    esz = np.dtype(npdt).itemsize
+    sizes = [1, 7, 4097, 100003, 65536, 3, 12345, 1 << 18][: 8]
+    ins, ios, host_in, host_io = [], [], [], []
+    for k, n in enumerate(sizes):
+        a = O.fill(dtype, n, 100 + k)
+        b = O.fill(dtype, n, 200 + k)
+        shift = (k * esz) % 16  # same phase for both operands of a window
+
+        def placed(x):
+            raw = torch.from_numpy(np.ascontiguousarray(x).view(np.uint8).copy())
+            t = torch.zeros(raw.numel() + shift + 16, dtype=torch.uint8, device="cuda:0")
+            t[shift:shift + raw.numel()] = raw.to("cuda:0")
+            return t[shift:]
+        ins.append(placed(a))
+        ios.append(placed(b))
+        host_in.append(a)
+        host_io.append(b.copy())
+    assert pico_amd.reduce_batch(ins, ios, sizes, dtype) == 0
+    torch.cuda.synchronize()
+    for k, n in enumerate(sizes):
+        O.reduce_local(host_in[k], host_io[k], dtype)
+        assert sha(from_dev(ios[k], dtype, n)) == sha(host_io[k]), k
+    # not co-aligned -> ERR_ARG (the executor then launches window by window)
+    a = to_dev(O.fill(dtype, 64, 1), pad=16)
+    b = to_dev(O.fill(dtype, 64, 2), pad=16)
+    if esz < 16:
+        assert pico_amd.reduce_batch([a[esz:], a], [b, b], [32, 32], dtype) == 1
