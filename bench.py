@@ -52,7 +52,72 @@ def _pmc_traffic(kernel_prefix: str):
         return None
 
 
+REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+
+def _ref_bench(np_: int, args, timeout: float):
+    """Run oracle/_ref/ref_bench (the real reference libbine + MPICH, built from
+    the reference sources by `make -C oracle ref`) under mpiexec as a child
+    process; its JSON line, or None."""
+    import subprocess
+    env = dict(os.environ)
+    env["PATH"] = "/opt/conda/bin:" + env.get("PATH", "")
+    r = subprocess.run([MPIEXEC, "-n", str(np_), REF_BENCH] + [str(a) for a in args], env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        return None
+    for line in r.stdout.splitlines():
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
+
+
 def cpu_baseline_c2(budget_s: float = 10.0):
+    """CPU baseline of the C2 workload on the box's host cores.
+
+    kind "reference": the reference's own arithmetic -- MPICH 3.3.2's
+    MPI_Reduce_local, which libbine calls per step (libbine_allreduce.c:888) --
+    timed by oracle/_ref/ref_bench on one core for ~budget_s, plus CPU libbine
+    allreduce_bine_bdw_remap at the C3 shape (256 MiB/rank fp32) for P = 2, 4, 8
+    host ranks (one per core), the figure the north star asks to report beside
+    the GPU numbers.  Falls back to the oracle's restatement (kind "port") when
+    the reference build is absent (oracle/_ref is built only where
+    /root/reference is mounted)."""
+    if os.path.exists(REF_BENCH) and os.path.exists(MPIEXEC):
+        try:
+            rl = _ref_bench(1, ["reduce_local", C2_ELEMS, budget_s], budget_s + 60)
+        except Exception:
+            rl = None
+        if rl:
+            per = rl["s_per_call"]
+            out = {"value": round(3 * C2_ELEMS * 4 / per / 1e9, 3), "unit": "GB/s", "cores": 1,
+                   "kind": "reference",
+                   "sample": f"MPICH 3.3.2 MPI_Reduce_local fp32 SUM (libbine's arithmetic), 64 MiB, "
+                             f"{rl['calls']} calls in {rl['seconds']:.1f} s on one host core "
+                             f"({per * 1e3:.2f} ms/call), oracle/_ref/ref_bench"}
+            c3 = {}
+            for p in (2, 4, 8):
+                try:
+                    ar = _ref_bench(p, ["allreduce", "bine_bdw_remap", C3_ELEMS, 5], 120)
+                except Exception:
+                    ar = None
+                if ar and ar.get("rc") == 0:
+                    t = ar["median_s"]
+                    S = C3_ELEMS * 4
+                    c3[f"P{p}"] = {"ms": round(t * 1e3, 2), "algbw_per_rank_GBs": round(S / t / 1e9, 3),
+                                   "busbw_per_rank_GBs": round(2 * (p - 1) / p * S / t / 1e9, 3),
+                                   "cores": p}
+            if c3:
+                out["libbine_allreduce_bine_bdw_remap_c3"] = c3
+                out["libbine_sample"] = ("real libbine allreduce_bine_bdw_remap fp32 256 MiB/rank, P host ranks "
+                                         "(mpiexec, one per core), 5 iterations, max over ranks, median after "
+                                         "dropping the first 20 %")
+            return out
+    return cpu_baseline_c2_port(budget_s)
+
+
+def cpu_baseline_c2_port(budget_s: float = 10.0):
     """The oracle's MPI_Reduce_local (MPICH semantics, one host core) on the C2
     workload, bounded to ~budget_s of CPU time."""
     import numpy as np

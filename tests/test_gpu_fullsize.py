@@ -1,0 +1,173 @@
+"""GPU parity at BASELINE.json's full sizes.
+
+Eight virtual ranks on one MI355X (loopback transport, the same planner and
+executor as RCCL), inputs generated on the device by k_fill_pico (bit-identical
+to pico_core's host generator, tests/test_gpu.py), default 16 MiB pipelining
+chunks -- i.e. the exact schedules bench.py times.
+
+* C3 fp32 allreduce 256 MiB/rank: every rank's output digest equals the
+  oracle's (the CPU restatement pinned by the reference's vectors) computed on
+  the host at full size -- bit-exact, tolerance 0 ulp; direct, relay and
+  multi-tree transports (trees: vs the relabelled oracle).
+* C5 int64 allreduce 256 MiB/rank: exact vs the element-wise wrapped int64 sum
+  (integer SUM is associative, so any correct schedule gives these bits); fp64
+  vs the oracle's digests.
+* C4 fp32 reduce_scatter 1 GiB/rank: integer-valued fp32 inputs (sums of eight
+  values < 2^24 are exact in any association order), so every block can be
+  checked bit-exact against a device-side sum at full size; the association
+  order itself is pinned against the oracle at smaller sizes in test_gpu.py.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import pico_amd  # noqa: E402
+
+P = 8
+C3_N = 67_108_864
+C4_N = 268_435_456
+C5_N = 33_554_432
+
+
+def _mix64(x):
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def host_checksum(a: np.ndarray) -> int:
+    """k_checksum's digest on the host, computed in slabs to bound memory"""
+    bits_t = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize]
+    raw = a.view(bits_t)
+    tot = np.uint64(0)
+    slab = 1 << 22
+    with np.errstate(over="ignore"):
+        for s in range(0, a.size, slab):
+            bits = raw[s:s + slab].astype(np.uint64)
+            idx = np.arange(s, s + bits.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+            tot = tot + _mix64(bits + idx).sum(dtype=np.uint64)
+    return int(tot)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def comms(dev):
+    cs = pico_amd.Comm.loopback(P, 0)
+    yield cs
+    for c in cs:
+        c.destroy()
+    torch.cuda.empty_cache()
+
+
+def _mode(cs, mode):
+    for c in cs:
+        c.set_relay(256 << 10 if mode == "relay" else 0)  # bench.py RELAY_MIN_BYTES
+        c.set_trees(mode == "trees")
+
+
+def _device_inputs(dtype, tdt, n):
+    bufs = [torch.empty(n, dtype=tdt, device="cuda:0") for _ in range(P)]
+    for r, b in enumerate(bufs):
+        pico_amd.fill_pico(b, n, dtype, 1234 + r)
+    torch.cuda.synchronize()
+    return bufs
+
+
+def test_fill_checksum_consistency_fullsize(dev):
+    """the device generator + digest agree with the host at the C3 size"""
+    t = torch.empty(C3_N, dtype=torch.float32, device="cuda:0")
+    pico_amd.fill_pico(t, C3_N, "float", 1234)
+    assert pico_amd.checksum(t, C3_N, "float") == host_checksum(O.fill("float", C3_N, 1234))
+
+
+@pytest.fixture(scope="module")
+def c3_oracle():
+    sb = O.inputs("float", C3_N, P)
+    want, rets = O.allreduce("bine_bdw_remap", sb, "float")
+    assert not any(rets)
+    return sb, [host_checksum(w) for w in want]
+
+
+@pytest.mark.parametrize("mode", ["direct", "relay", "trees"])
+def test_c3_allreduce_fullsize(dev, comms, c3_oracle, mode):
+    sb_host, digests = c3_oracle
+    assert len(set(digests)) == 1  # allreduce: every rank holds the same bits
+    if mode == "trees":
+        import test_trees as TT
+        want = TT.relabelled_oracle("bine_bdw_remap", sb_host, "float")
+        expect = [host_checksum(w) for w in want]
+    else:
+        expect = digests
+    sb = _device_inputs("float", torch.float32, C3_N)
+    rb = [torch.empty(C3_N, dtype=torch.float32, device="cuda:0") for _ in range(P)]
+    _mode(comms, mode)
+    try:
+        rc, st = pico_amd.loopback_allreduce(comms, "bine_bdw_remap", sb, rb, C3_N, "float")
+        assert rc == 0 and not any(st), st
+        got = [pico_amd.checksum(b, C3_N, "float") for b in rb]
+    finally:
+        _mode(comms, "direct")
+    assert got == expect
+
+
+@pytest.mark.parametrize("mode", ["direct", "relay", "trees"])
+def test_c5_int64_allreduce_fullsize(dev, comms, mode):
+    sb = _device_inputs("int64", torch.int64, C5_N)
+    want = sb[0].clone()
+    for b in sb[1:]:
+        want.add_(b)  # two's-complement wrap, same as MPICH's int64 SUM
+    rb = [torch.empty(C5_N, dtype=torch.int64, device="cuda:0") for _ in range(P)]
+    _mode(comms, mode)
+    try:
+        rc, st = pico_amd.loopback_allreduce(comms, "bine_bdw_remap", sb, rb, C5_N, "int64")
+        assert rc == 0 and not any(st), st
+        torch.cuda.synchronize()
+        assert all(torch.equal(b, want) for b in rb)
+    finally:
+        _mode(comms, "direct")
+
+
+def test_c5_double_allreduce_fullsize(dev, comms):
+    sb_host = O.inputs("double", C5_N, P)
+    want, rets = O.allreduce("bine_bdw_remap", sb_host, "double")
+    assert not any(rets)
+    expect = host_checksum(want[0])
+    del sb_host, want
+    sb = _device_inputs("double", torch.float64, C5_N)
+    rb = [torch.empty(C5_N, dtype=torch.float64, device="cuda:0") for _ in range(P)]
+    rc, st = pico_amd.loopback_allreduce(comms, "bine_bdw_remap", sb, rb, C5_N, "double")
+    assert rc == 0 and not any(st), st
+    assert [pico_amd.checksum(b, C5_N, "double") for b in rb] == [expect] * P
+
+
+@pytest.mark.parametrize("mode", ["direct", "relay", "trees"])
+def test_c4_reduce_scatter_fullsize(dev, comms, mode):
+    per = C4_N // P
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(4)
+    sb = [torch.randint(0, 1 << 20, (C4_N,), generator=g, device="cuda:0", dtype=torch.int32).float()
+          for _ in range(P)]
+    rb = [torch.empty(per, dtype=torch.float32, device="cuda:0") for _ in range(P)]
+    _mode(comms, mode)
+    try:
+        rc, st = pico_amd.loopback_reduce_scatter(comms, "bine_permute_remap", sb, rb, [per] * P, "float")
+        assert rc == 0 and not any(st), st
+        torch.cuda.synchronize()
+    finally:
+        _mode(comms, "direct")
+    for r in range(P):
+        want = sb[0][r * per:(r + 1) * per].clone()
+        for b in sb[1:]:
+            want.add_(b[r * per:(r + 1) * per])
+        assert torch.equal(rb[r], want), r
+    del sb, rb
+    torch.cuda.empty_cache()
