@@ -157,6 +157,9 @@ def test_c4_reduce_scatter_fullsize(dev, comms, mode):
     sb = [torch.randint(0, 1 << 20, (C4_N,), generator=g, device="cuda:0", dtype=torch.int32).float()
           for _ in range(P)]
     rb = [torch.empty(per, dtype=torch.float32, device="cuda:0") for _ in range(P)]
+    # the loopback drivers run on the communicators' own (non-blocking) streams:
+    # torch's generator kernels must be finished before they start
+    torch.cuda.synchronize()
     _mode(comms, mode)
     try:
         rc, st = pico_amd.loopback_reduce_scatter(comms, "bine_permute_remap", sb, rb, [per] * P, "float")
