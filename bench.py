@@ -13,9 +13,12 @@ N > 1 (torch.distributed.run, one process per GPU): BASELINE config C3,
 allreduce_bine_bdw_remap fp32 256 MiB per rank over RCCL P2P / xGMI.
 value = whole-job algorithmic throughput = N * 256 MiB / t; per-rank busbw
 2 (N-1)/N * S / t and algbw S / t are reported beside it.  The transport is
-either the literal Bine schedule (one peer per step) or its multi-link relay
-(same schedule, parts routed over two hops through the other ranks, identical
-results); --relay auto (default) times both briefly and keeps the faster.
+the literal Bine schedule (one peer per step), its multi-link relay (same
+schedule, parts routed over two hops through the other ranks, identical
+results) or multi-tree mode (N = 4, 8: P-1 relabelled instances over
+edge-disjoint pairings; integers identical, fp within rounding); --relay auto
+(default) times every transport x pipelining chunk (4 / 16 / 64 MiB) briefly
+and keeps the fastest.
 
 Timing: W untimed warm-up steps, then K steps between a barrier +
 device synchronize on both sides, HIP events on the stream the kernels run on,
@@ -248,9 +251,11 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev):
 
 
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
+CHUNK_TRIALS = (4 << 20, 16 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 
 
-def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True):
+def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
+                    chunk_mib: int = 0):
     import torch
     import torch.distributed as dist
     import pico_amd
@@ -283,26 +288,36 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     if world not in (4, 8):
         modes = [m for m in modes if m != "trees"] or ["direct"]
 
-    def use(m):
+    chunks = [chunk_mib << 20] if chunk_mib else list(CHUNK_TRIALS)
+
+    def use(cfg):
+        m, ch = cfg
         comm.set_relay(RELAY_MIN_BYTES if m == "relay" else 0)
         comm.set_trees(m == "trees")
+        comm.set_chunk(ch)
 
+    # every (transport, pipelining chunk) pair is timed briefly on this
+    # hardware (max over ranks, so every rank picks the same) and the fastest
+    # is kept: measured, not guessed -- none of them changes the schedule's
+    # reduction order except "trees" (reported below)
+    cands = [(m, ch) for m in modes for ch in chunks]
     trials = {}
-    if len(modes) > 1:
-        for m in modes:
-            use(m)
-            trials[m] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
-        chosen = min(trials, key=trials.get)
+    if len(cands) > 1:
+        for cfg in cands:
+            use(cfg)
+            trials[cfg] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
+        best = min(trials, key=trials.get)
     else:
-        chosen = modes[0]
-    use(chosen)
+        best = cands[0]
+    use(best)
+    chosen, chunk = best
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
     extra = _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
     # bytes this rank puts on xGMI per allreduce (from the executed schedule)
-    ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4, chunk_bytes=16 << 20,
+    ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4, chunk_bytes=chunk,
                                   relay_min_bytes=RELAY_MIN_BYTES if chosen == "relay" else 0,
                                   trees=chosen == "trees")
     egress = 4 * sum(p["count"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND")
@@ -320,7 +335,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
                        "transport": chosen,
                        "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
-                       "transport_trials_ms": {m: round(v, 4) for m, v in trials.items()},
+                       "chunk_bytes": chunk,
+                       "transport_trials_ms": {f"{m}/{ch >> 20}MiB": round(v, 4) for (m, ch), v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": extra},
             "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
@@ -344,12 +360,14 @@ def main():
     ap.add_argument("--algo", default="bine_bdw_remap")
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
     ap.add_argument("--relay", default="auto", help="transport at N > 2: auto | off (direct) | relay | trees")
+    ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/16/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay, not args.no_extras)
+        res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay, not args.no_extras,
+                              args.chunk_mib)
         if res is not None:
             print(json.dumps(res), flush=True)
         return

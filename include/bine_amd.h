@@ -165,6 +165,15 @@ int bine_comm_set_relay(bine_comm_t comm, size_t min_part_bytes);
  * collective: every rank must use the same setting. */
 int bine_comm_set_trees(bine_comm_t comm, int on);
 
+/* Pipelining chunk of this communicator's exchanges, in bytes: every step
+ * whose received block feeds a reduction is cut into chunks of this size so
+ * that chunk k+1's transfer overlaps chunk k's reduction (the device form of
+ * the segmented variant's Irecv/Reduce_local loop, libbine_allreduce.c:
+ * 1218-1253).  0 = the default (16 MiB, or BINE_CHUNK_BYTES).  Never changes a
+ * result bit.  A nonzero `segsize` argument of bine_allreduce still wins for
+ * that call.  Collective: every rank must use the same setting. */
+int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
+
 /* ---- collectives (device pointers, stream-ordered) ------------------------- */
 /* allreduce_* (libbine.h:30-37).  `segsize` plays bine_allreduce_segsize
  * (libbine.h:28) for BINE_AR_BINE_BDW_REMAP_SEGMENTED and is the pipelining

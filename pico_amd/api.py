@@ -133,6 +133,10 @@ class Comm:
         """Multi-tree mode (allreduce, P = 4 / 8); collective."""
         check(lib().bine_comm_set_trees(self.handle, int(on)), "bine_comm_set_trees")
 
+    def set_chunk(self, nbytes: int) -> None:
+        """Pipelining chunk in bytes (0 = default 16 MiB); never changes a bit; collective."""
+        check(lib().bine_comm_set_chunk(self.handle, nbytes), "bine_comm_set_chunk")
+
     def set_relay(self, min_part_bytes: int) -> None:
         """Multi-link relay for permutation steps (0 = off); collective."""
         check(lib().bine_comm_set_relay(self.handle, min_part_bytes), "bine_comm_set_relay")

@@ -191,6 +191,7 @@ struct bine_comm {
   size_t tmp_bytes[4] = {0, 0, 0, 0};
   size_t relay_min_bytes = 0;  // relay mode: smallest relayed part (0: off)
   bool trees = false;          // multi-tree mode (allreduce, P = 4 / 8)
+  size_t chunk_bytes = 0;      // pipelining chunk (0: default_chunk_bytes())
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
   std::vector<hipEvent_t> ev;
@@ -386,12 +387,16 @@ static void build(const PlanArgs &a, size_t ch, size_t relay_min_bytes, bool tre
   }
 }
 
+// chunk_bytes == kCommChunk: the communicator's setting (bine_comm_set_chunk)
+constexpr size_t kCommChunk = ~(size_t)0;
+
 static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbuf, int dtype, int op,
                           size_t chunk_bytes, void *stream) {
   if (!c) return BINE_ERR_ARG;
   if (dtype < 0 || dtype >= BINE_NUM_DTYPES) return BINE_ERR_UNSUPPORTED;
   if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
   std::lock_guard<std::mutex> g(c->mu);
+  if (chunk_bytes == kCommChunk) chunk_bytes = c->chunk_bytes ? c->chunk_bytes : default_chunk_bytes();
   HIP_TRY(hipSetDevice(c->device));
   a.P = c->size;
   a.rank = c->rank;
@@ -631,7 +636,7 @@ int bine_allreduce(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t
   a.count = count;
   a.segsize = segsize;
   // segmented: the reference's segment is the pipelining chunk (0 = one chunk)
-  size_t chunk = algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? segsize : (segsize ? segsize : default_chunk_bytes());
+  size_t chunk = algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? segsize : (segsize ? segsize : kCommChunk);
   return run_collective(c, a, sbuf, rbuf, dtype, op, chunk, stream);
 }
 
@@ -642,7 +647,7 @@ int bine_reduce_scatter(bine_comm_t c, int algo, const void *sbuf, void *rbuf, c
   PlanArgs a;
   a.algo = algo;
   a.rcounts.assign(rcounts, rcounts + c->size);
-  return run_collective(c, a, sbuf, rbuf, dtype, op, default_chunk_bytes(), stream);
+  return run_collective(c, a, sbuf, rbuf, dtype, op, kCommChunk, stream);
 }
 
 int bine_reduce(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int op, int root,
@@ -658,7 +663,7 @@ int bine_reduce(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t co
   } else if (sbuf == BINE_IN_PLACE) {
     return BINE_ERR_ARG;
   }
-  return run_collective(c, a, sbuf, rbuf, dtype, op, default_chunk_bytes(), stream);
+  return run_collective(c, a, sbuf, rbuf, dtype, op, kCommChunk, stream);
 }
 
 int bine_allgather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, void *stream) {
@@ -666,7 +671,7 @@ int bine_allgather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t
   PlanArgs a;
   a.algo = algo;
   a.count = count;
-  return run_collective(c, a, sbuf, rbuf, dtype, BINE_SUM, default_chunk_bytes(), stream);
+  return run_collective(c, a, sbuf, rbuf, dtype, BINE_SUM, kCommChunk, stream);
 }
 
 // ---- loopback drivers --------------------------------------------------------
@@ -761,6 +766,13 @@ int bine_comm_set_trees(bine_comm_t c, int on) {
   if (!c) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->trees = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_chunk(bine_comm_t c, size_t bytes) {
+  if (!c) return BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->chunk_bytes = bytes;
   return BINE_SUCCESS;
 }
 

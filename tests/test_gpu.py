@@ -261,6 +261,30 @@ def test_pipelined_chunks_bit_exact(dev, chunk):
     assert all(sha(o) == sha(w) for o, w in zip(outs, want))
 
 
+@pytest.mark.parametrize("chunk", [256, 65536, 4 << 20])
+def test_comm_chunk_setting_bit_exact(dev, chunk):
+    """bine_comm_set_chunk (the bench's chunk trials) re-cuts every pipelined
+    step of every collective; results stay the reference's"""
+    P, per = 8, 40009
+    rc = [per] * P
+    sb = O.inputs("float", per * P, P)
+    want_rs, _ = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
+    want_ar, _ = O.allreduce("bine_bdw_static", sb, "float")
+    try:
+        for c in comms(P):
+            c.set_chunk(chunk)
+        outs, st = run_loopback("reduce_scatter", "bine_permute_remap", sb, "float", rcounts=rc)
+        assert not any(st)
+        assert all(sha(o) == sha(w) for o, w in zip(outs, want_rs))
+        outs, st = run_loopback("allreduce", "bine_bdw_static", sb, "float", relay=4096)
+        assert not any(st)
+        assert all(sha(o) == sha(w) for o, w in zip(outs, want_ar))
+    finally:
+        for c in comms(P):
+            c.set_chunk(0)
+            c.set_relay(0)
+
+
 @pytest.mark.parametrize("algo", list(pico_amd.ALGOS["allreduce"]))
 def test_in_place_allreduce(dev, algo):
     P = 4
