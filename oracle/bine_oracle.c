@@ -1091,6 +1091,16 @@ static int nb_partner(int r, int mask, int P) {
 /* reduce_scatter_bine_send_remap (:906-983) and _permute_remap (:985-1063) */
 static void rs_bine_remap(ctx_t *c, const int *rc, char **S, char **R, int *rets, int permute) {
   int P = c->P; size_t esz = c->esz;
+  if (permute)
+    for (int i = 1; i < P; i++)
+      if (rc[i] != rc[0]) {
+        /* unequal blocks: the reference copies block i into block remap(i)'s
+         * slot with block i's size (:1008-1011) and overruns its buffers --
+         * undefined behaviour, no vector exists.  Reported as MPI_ERR_ARG, the
+         * status the device path returns (deviations). */
+        for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG;
+        return;
+      }
   int *displs = (int *)malloc(sizeof(int) * (size_t)P), count = 0;
   for (int i = 0; i < P; i++) { displs[i] = count; count += rc[i]; }
   char **tmp = alloc_ranks(P, (size_t)count * esz), **res = alloc_ranks(P, (size_t)count * esz);

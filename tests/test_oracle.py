@@ -138,3 +138,14 @@ def test_reduce_local_semantics():
     x = np.array([127, -128], np.int8); y = np.array([1, -1], np.int8)
     O.reduce_local(x, y, "int8", "sum")
     assert y.tolist() == [-128, 127]          # wrap-around, no UB
+
+
+def test_permute_remap_unequal_blocks_is_err_arg():
+    """the reference overruns its buffers on unequal rcounts (UB, no vector);
+    the oracle reports MPI_ERR_ARG like the device path instead of corrupting
+    its heap"""
+    for P in (4, 8):
+        rc = [10 + (i % 3) for i in range(P)]
+        sb = O.inputs("float", sum(rc), P)
+        _, rets = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
+        assert rets == [O.ERR_ARG] * P

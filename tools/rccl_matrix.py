@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Every algorithm of every family through the RCCL transport, P real processes
+sharing ONE GPU, against the oracle (the CPU restatement pinned by the
+reference's golden vectors).
+
+Like tools/rccl_1gpu_multirank.py, each rank claims its own NCCL_HOSTID so RCCL
+accepts P ranks on one device and connects them over its socket transport on
+`lo`: this checks the executor's RCCL path (group matching, exact counts,
+stream / event hand-offs, chunked pipelines, relay routes) in real processes;
+it says nothing about xGMI speed.
+
+For each transport setting (direct; small pipelining chunks; multi-link relay)
+it runs all 8 allreduce, 9 reduce_scatter, 2 reduce and 12 allgather
+algorithms on fp32 / int64 / int8 at odd sizes, and checks outputs bit for bit
+and error statuses against the oracle's return codes.
+usage: python tools/rccl_matrix.py [P]   (exit 0 = every rank, every case ok)
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CASES = (("float", 4099), ("int64", 1001), ("int8", 333))
+SETTINGS = (("direct", 0, 0), ("chunk4KiB", 0, 4096), ("relay", 64, 1024))
+
+
+def worker(rank, P, port, q):
+    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import pico_amd
+    from oracle import oracle as O
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    comm = pico_amd.Comm.from_torch_distributed(0)
+    npdt = O.NP_DTYPES
+    bad, n_ok = [], 0
+
+    def dev(a):
+        t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
+        return t if t.numel() else torch.zeros(16, dtype=torch.uint8, device="cuda:0")
+
+    def host(t, dt, n):
+        return t[: n * np.dtype(npdt[dt]).itemsize].cpu().numpy().view(npdt[dt]).copy()
+
+    def run(tag, want_rc, want, call, out, dt, n):
+        nonlocal n_ok
+        try:
+            call()
+            torch.cuda.synchronize()
+            comm.synchronize()
+            rc = 0
+        except pico_amd.BineError:
+            rc = 1
+        if want_rc != 0:
+            if rc == 0:
+                bad.append((tag, "expected an error"))
+            else:
+                n_ok += 1
+            return
+        if rc != 0:
+            bad.append((tag, "error"))
+        elif want is not None and not np.array_equal(host(out, dt, n), want):
+            bad.append((tag, "data"))
+        else:
+            n_ok += 1
+
+    for sname, relay, chunk in SETTINGS:
+        comm.set_relay(relay)
+        comm.set_chunk(chunk)
+        for dt, n in CASES:
+            esz = np.dtype(npdt[dt]).itemsize
+            sb = O.inputs(dt, n, P)
+            for algo in pico_amd.ALGOS["allreduce"]:
+                want, rets = O.allreduce(algo, sb, dt, segsize=256)
+                r = torch.zeros(n * esz + 16, dtype=torch.uint8, device="cuda:0")
+                s = dev(sb[rank])
+                run(f"{sname} allreduce_{algo} {dt} n={n}", rets[rank], want[rank],
+                    lambda: pico_amd.allreduce(algo, s, r, n, dt, "sum", comm, segsize=256), r, dt, n)
+            rc = [n // P + (i % 3) for i in range(P)]
+            sbr = O.inputs(dt, sum(rc), P)
+            for algo in pico_amd.ALGOS["reduce_scatter"]:
+                want, rets = O.reduce_scatter(algo, sbr, rc, dt)
+                r = torch.zeros(rc[rank] * esz + 16, dtype=torch.uint8, device="cuda:0")
+                s = dev(sbr[rank])
+                run(f"{sname} reduce_scatter_{algo} {dt} ragged", rets[rank], want[rank],
+                    lambda: pico_amd.reduce_scatter(algo, s, r, rc, dt, "sum", comm), r, dt, rc[rank])
+            for algo in pico_amd.ALGOS["reduce"]:
+                want, rets = O.reduce(algo, sb, dt)
+                r = torch.zeros(n * esz + 16, dtype=torch.uint8, device="cuda:0")
+                s = dev(sb[rank])
+                run(f"{sname} reduce_{algo} {dt}", rets[rank], want if rank == 0 else None,
+                    lambda: pico_amd.reduce(algo, s, r if rank == 0 else None, n, dt, "sum", 0, comm), r, dt, n)
+            for algo in pico_amd.ALGOS["allgather"]:
+                want, rets = O.allgather(algo, sb, dt)
+                r = torch.zeros(P * n * esz + 16, dtype=torch.uint8, device="cuda:0")
+                s = dev(sb[rank])
+                run(f"{sname} allgather_{algo} {dt}", rets[rank], want[rank],
+                    lambda: pico_amd.allgather(algo, s, r, n, dt, comm), r, dt, P * n)
+        print(f"rank {rank} {sname}: {n_ok} ok, {len(bad)} bad so far", flush=True)
+    for b in bad[:20]:
+        print(f"rank {rank} MISMATCH {b}", flush=True)
+    comm.destroy()
+    dist.destroy_process_group()
+    q.put((rank, n_ok, len(bad)))
+
+
+if __name__ == "__main__":
+    import multiprocessing as mp
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=worker, args=(r, P, 29577, q)) for r in range(P)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(600)
+    res = [q.get() for _ in range(sum(1 for p in ps if p.exitcode == 0))]
+    print("RESULT P=%d" % P, sorted(res), "exitcodes", [p.exitcode for p in ps], flush=True)
+    sys.exit(0 if len(res) == P and all(b == 0 for _, _, b in res) else 1)
