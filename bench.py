@@ -250,6 +250,32 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev):
     return out
 
 
+def _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, per_peer=32 << 20):
+    """RCCL P2P calibration of this node through the same transport the
+    collectives use (bine_exchange = one ncclGroupStart/End): (a) one peer,
+    rank r <-> r^1 both ways; (b) all P-1 peers at once (what relay / trees
+    modes do per step).  GB/s per rank and direction, max-over-ranks time."""
+    out = {"bytes_per_peer": per_peer}
+    sb = torch.empty(per_peer * (world - 1), dtype=torch.uint8, device=dev)
+    rb = torch.empty(per_peer * (world - 1), dtype=torch.uint8, device=dev)
+    sb.fill_(rank & 0xFF)
+    torch.cuda.synchronize()
+    if world % 2 == 0:
+        peer = rank ^ 1
+        ms, _ = _timed(torch, dist, comm, stream,
+                       lambda: pico_amd.exchange(comm, [(peer, sb, per_peer)], [(peer, rb, per_peer)], stream=stream),
+                       10, 3)
+        out["one_peer_GBs"] = round(per_peer / (ms * 1e-3) / 1e9, 2)
+    peers = [p for p in range(world) if p != rank]
+    sends = [(p, sb[i * per_peer:], per_peer) for i, p in enumerate(peers)]
+    recvs = [(p, rb[i * per_peer:], per_peer) for i, p in enumerate(peers)]
+    ms, _ = _timed(torch, dist, comm, stream, lambda: pico_amd.exchange(comm, sends, recvs, stream=stream), 10, 3)
+    out["all_peers_egress_GBs"] = round(len(peers) * per_peer / (ms * 1e-3) / 1e9, 2)
+    del sb, rb
+    torch.cuda.empty_cache()
+    return out
+
+
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
 CHUNK_TRIALS = (4 << 20, 16 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 
@@ -313,6 +339,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     chosen, chunk = best
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
     extra = _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
+    probe = _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
@@ -338,7 +365,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "chunk_bytes": chunk,
                        "transport_trials_ms": {f"{m}/{ch >> 20}MiB": round(v, 4) for (m, ch), v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
-                       "other_baseline_configs": extra},
+                       "other_baseline_configs": extra,
+                       "rccl_p2p_probe": probe},
             "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
                          "traffic": egress,
@@ -347,6 +375,11 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                                     "one 153 GB/s link (direct Bine: one peer per step)")},
             "wall_s": round(wall, 4),
         }
+        # the same egress against what RCCL P2P itself moves on this node
+        ceil = probe.get("one_peer_GBs" if chosen == "direct" else "all_peers_egress_GBs")
+        if ceil:
+            out["roofline"]["rccl_p2p_ceiling_GBs"] = ceil
+            out["roofline"]["frac_of_rccl_p2p"] = round(egress / (ms * 1e-3) / 1e9 / ceil, 4)
     comm.destroy()
     dist.destroy_process_group()
     return out

@@ -195,6 +195,18 @@ int bine_reduce(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t
 int bine_allgather(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count,
                    int dtype, void *stream);
 
+/* One group of point-to-point transfers on the communicator's transport (RCCL:
+ * ncclSend / ncclRecv inside one ncclGroupStart/End) -- the MPI_Sendrecv /
+ * Isend+Irecv+Waitall building block of every libbine schedule
+ * (e.g. libbine_allreduce.c:866-870), exposed for link calibration
+ * (bench.py's RCCL P2P probe) and tests.  Byte counts; receives must match the
+ * peers' sends in count and posting order.  Stream-ordered like the
+ * collectives (runs after the caller's prior work on `stream`, which waits for
+ * it).  RCCL communicators only (loopback: BINE_ERR_UNSUPPORTED). */
+int bine_exchange(bine_comm_t comm, int nsend, const int *send_peers, const void *const *sbufs,
+                  const size_t *sbytes, int nrecv, const int *recv_peers, void *const *rbufs,
+                  const size_t *rbytes, void *stream);
+
 /* ---- loopback drivers: run one collective on all virtual ranks ---------------
  * (one host thread per rank; returns the first non-success status) */
 int bine_loopback_run_allreduce(bine_comm_t *comms, int nranks, int algo,

@@ -290,6 +290,20 @@ def reduce_batch(ins, inouts, counts, dtype, op: str = "sum", stream=None) -> in
     return lib().bine_reduce_batch(n, _ptrs(ins), b, b, c, _dtype(dtype, inouts[0]), OPS[op], _stream(stream, None))
 
 
+def exchange(comm: Comm, sends=(), recvs=(), stream=None) -> None:
+    """One group of P2P transfers (bine_exchange): sends / recvs are
+    (peer, buffer, nbytes) triples; receives match the peers' sends in size
+    and posting order."""
+    ns, nr = len(sends), len(recvs)
+    sp = (ctypes.c_int * max(ns, 1))(*[p for p, _, _ in sends])
+    sb = (ctypes.c_void_p * max(ns, 1))(*[_ptr(b) for _, b, _ in sends])
+    sz = (ctypes.c_size_t * max(ns, 1))(*[n for _, _, n in sends])
+    rp = (ctypes.c_int * max(nr, 1))(*[p for p, _, _ in recvs])
+    rb = (ctypes.c_void_p * max(nr, 1))(*[_ptr(b) for _, b, _ in recvs])
+    rz = (ctypes.c_size_t * max(nr, 1))(*[n for _, _, n in recvs])
+    check(lib().bine_exchange(comm.handle, ns, sp, sb, sz, nr, rp, rb, rz, _stream(stream, comm)), "exchange")
+
+
 def allgather(algo, sbuf, rbuf, count: int, dtype, comm: Comm, stream=None) -> None:
     """count = elements per rank; rbuf holds comm.size * count elements."""
     check(lib().bine_allgather(comm.handle, _algo("allgather", algo), _ptr(sbuf), _ptr(rbuf), count,
@@ -351,4 +365,5 @@ globals().update(ENTRY_POINTS)
 
 __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
-           "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "reduce_batch"] + list(ENTRY_POINTS)
+           "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "reduce_batch",
+           "exchange"] + list(ENTRY_POINTS)

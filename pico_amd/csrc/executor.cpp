@@ -674,6 +674,31 @@ int bine_allgather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t
   return run_collective(c, a, sbuf, rbuf, dtype, BINE_SUM, kCommChunk, stream);
 }
 
+int bine_exchange(bine_comm_t c, int nsend, const int *send_peers, const void *const *sbufs, const size_t *sbytes,
+                  int nrecv, const int *recv_peers, void *const *rbufs, const size_t *rbytes, void *stream) {
+  if (!c || nsend < 0 || nrecv < 0) return BINE_ERR_ARG;
+  if (c->hub) return BINE_ERR_UNSUPPORTED;  // loopback: exchanges block on the host (drivers only)
+  std::lock_guard<std::mutex> g(c->mu);
+  std::vector<XSend> xs;
+  std::vector<XRecv> xr;
+  for (int i = 0; i < nsend; i++) {
+    if (send_peers[i] < 0 || send_peers[i] >= c->size) return BINE_ERR_ARG;
+    if (sbytes[i]) xs.push_back({send_peers[i], sbufs[i], sbytes[i]});
+  }
+  for (int i = 0; i < nrecv; i++) {
+    if (recv_peers[i] < 0 || recv_peers[i] >= c->size) return BINE_ERR_ARG;
+    if (rbytes[i]) xr.push_back({recv_peers[i], rbufs[i], rbytes[i]});
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t K = (hipStream_t)stream;
+  c->last_user = K;
+  c->used_user = true;
+  int rc = stream_join(c, c->cstream, K);
+  if (rc) return rc;
+  if ((rc = c->tx->exchange(xs, xr, c->cstream))) return rc;
+  return stream_join(c, K, c->cstream);
+}
+
 // ---- loopback drivers --------------------------------------------------------
 
 int bine_loopback_run_allreduce(bine_comm_t *comms, int n, int algo, const void *const *sbufs,

@@ -103,6 +103,22 @@ def worker(rank, P, port, q):
                 run(f"{sname} allgather_{algo} {dt}", rets[rank], want[rank],
                     lambda: pico_amd.allgather(algo, s, r, n, dt, comm), r, dt, P * n)
         print(f"rank {rank} {sname}: {n_ok} ok, {len(bad)} bad so far", flush=True)
+    # the raw P2P primitive (bine_exchange): ring shift, then all peers at once
+    nb = 100003
+    mine = torch.full((nb,), rank + 1, dtype=torch.uint8, device="cuda:0")
+    got = torch.zeros(nb, dtype=torch.uint8, device="cuda:0")
+    pico_amd.exchange(comm, [((rank + 1) % P, mine, nb)], [((rank - 1) % P, got, nb)])
+    torch.cuda.synchronize()
+    ok = bool((got == (rank - 1) % P + 1).all())
+    peers = [p for p in range(P) if p != rank]
+    allr = torch.zeros(len(peers) * nb, dtype=torch.uint8, device="cuda:0")
+    pico_amd.exchange(comm, [(p, mine, nb) for p in peers], [(p, allr[i * nb:], nb) for i, p in enumerate(peers)])
+    torch.cuda.synchronize()
+    ok &= all(bool((allr[i * nb:(i + 1) * nb] == p + 1).all()) for i, p in enumerate(peers))
+    if ok:
+        n_ok += 1
+    else:
+        bad.append(("exchange", "data"))
     for b in bad[:20]:
         print(f"rank {rank} MISMATCH {b}", flush=True)
     comm.destroy()
