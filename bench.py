@@ -307,34 +307,49 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # (P-1 relabelled instances over edge-disjoint pairings; integer results
     # identical, fp within rounding).  "auto" times each briefly (max over
     # ranks, so every rank picks the same) and keeps the fastest.
-    modes = {"off": ["direct"], "auto": ["direct", "relay", "trees"], "relay": ["relay"],
-             "trees": ["trees"]}.get(relay, ["direct"])
+    # transports: "direct" = the literal Bine schedule (one peer per step);
+    # "relay" = the same schedule with permutation steps routed over all links
+    # (two hops); "+flat" = the allgather phase as one all-peers exchange
+    # (one hop on every link); "trees" = P-1 relabelled instances over
+    # edge-disjoint pairings.  All but "trees" are bit-identical to the reference.
+    modes = {"off": ["direct"], "auto": ["direct", "flat", "relay", "relay+flat", "trees"],
+             "relay": ["relay"], "trees": ["trees"], "flat": ["flat"], "relay+flat": ["relay+flat"]
+             }.get(relay, ["direct"])
     if world <= 2:
-        modes = ["direct"]
+        modes = [m for m in modes if "relay" not in m] or ["direct"]
     if world not in (4, 8):
         modes = [m for m in modes if m != "trees"] or ["direct"]
-
+    if world & (world - 1):
+        modes = [m for m in modes if "flat" not in m] or ["direct"]
     chunks = [chunk_mib << 20] if chunk_mib else list(CHUNK_TRIALS)
 
     def use(cfg):
         m, ch = cfg
-        comm.set_relay(RELAY_MIN_BYTES if m == "relay" else 0)
+        comm.set_relay(RELAY_MIN_BYTES if "relay" in m else 0)
         comm.set_trees(m == "trees")
+        comm.set_flat_ag("flat" in m)
         comm.set_chunk(ch)
 
-    # every (transport, pipelining chunk) pair is timed briefly on this
-    # hardware (max over ranks, so every rank picks the same) and the fastest
-    # is kept: measured, not guessed -- none of them changes the schedule's
-    # reduction order except "trees" (reported below)
-    cands = [(m, ch) for m in modes for ch in chunks]
+    # measured, not guessed: each transport is timed briefly on this hardware
+    # (max over ranks, so every rank picks the same), then the pipelining chunk
+    # for the fastest one; the fastest pair is kept
     trials = {}
-    if len(cands) > 1:
-        for cfg in cands:
-            use(cfg)
-            trials[cfg] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
+
+    def trial(cfg):
+        use(cfg)
+        trials[cfg] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
+
+    mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
+    if len(modes) > 1 or len(chunks) > 1:
+        for m in modes:
+            trial((m, mid))
+        m_best = min((c for c in trials if c[1] == mid), key=trials.get)[0]
+        for ch in chunks:
+            if (m_best, ch) not in trials:
+                trial((m_best, ch))
         best = min(trials, key=trials.get)
     else:
-        best = cands[0]
+        best = (modes[0], chunks[0])
     use(best)
     chosen, chunk = best
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
@@ -345,11 +360,23 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
     # bytes this rank puts on xGMI per allreduce (from the executed schedule)
     ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4, chunk_bytes=chunk,
-                                  relay_min_bytes=RELAY_MIN_BYTES if chosen == "relay" else 0,
-                                  trees=chosen == "trees")
+                                  relay_min_bytes=RELAY_MIN_BYTES if "relay" in chosen else 0,
+                                  trees=chosen == "trees", flat_ag="flat" in chosen)
     egress = 4 * sum(p["count"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND")
     peers = len({p["peer"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND"})
-    link_peak = XGMI_LINK_GBS * (min(7, world - 1) if chosen != "direct" else 1)
+    # schedule-aware link roofline: exchange ops run one after another, the
+    # links of one op in parallel, so at B GB/s per link the schedule needs at
+    # least L / B, L = sum over ops of the busiest link's bytes; peak = the
+    # egress rate that bound allows (one link: 153; all 7 links: 1071)
+    L = 0
+    for o in ops:
+        if o["xchg"]:
+            lk = {}
+            for p in o["prims"]:
+                if p["type"] in ("SEND", "RECV"):
+                    lk[(p["type"], p["peer"])] = lk.get((p["type"], p["peer"]), 0) + 4 * p["count"]
+            L += max(lk.values())
+    link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
     out = None
     if rank == 0:
         out = {
@@ -370,16 +397,20 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
                          "traffic": egress,
-                         "note": "achieved = this rank's xGMI egress bytes (schedule) / t; peak = "
-                                 + ("N-1 links x 153 GB/s (all peers used every step)" if chosen != "direct" else
-                                    "one 153 GB/s link (direct Bine: one peer per step)")},
+                         "link_time_bytes": L,
+                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / t; peak = "
+                                 "153 GB/s per link x egress / link_time_bytes (sum over exchange ops of the "
+                                 "busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
+                                 "to 7 x 153 when every step loads all links"},
             "wall_s": round(wall, 4),
         }
         # the same egress against what RCCL P2P itself moves on this node
-        ceil = probe.get("one_peer_GBs" if chosen == "direct" else "all_peers_egress_GBs")
-        if ceil:
-            out["roofline"]["rccl_p2p_ceiling_GBs"] = ceil
-            out["roofline"]["frac_of_rccl_p2p"] = round(egress / (ms * 1e-3) / 1e9 / ceil, 4)
+        # the same schedule bound with RCCL's own measured P2P rate per link
+        one = probe.get("one_peer_GBs")
+        if one and L:
+            t_rccl = L / (one * 1e9)
+            out["roofline"]["rccl_p2p_one_link_GBs"] = one
+            out["roofline"]["frac_of_rccl_p2p_bound"] = round(t_rccl / (ms * 1e-3), 4)
     comm.destroy()
     dist.destroy_process_group()
     return out
@@ -392,7 +423,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--algo", default="bine_bdw_remap")
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
-    ap.add_argument("--relay", default="auto", help="transport at N > 2: auto | off (direct) | relay | trees")
+    ap.add_argument("--relay", default="auto",
+                    help="transport at N > 1: auto | off (direct) | flat | relay | relay+flat | trees")
     ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/16/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")

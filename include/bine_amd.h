@@ -174,6 +174,16 @@ int bine_comm_set_trees(bine_comm_t comm, int on);
  * that call.  Collective: every rank must use the same setting. */
 int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
 
+/* Flat allgather phase for allreduce_bine_bdw_remap / _static /
+ * _remap_segmented at power-of-two P: after the Bine reduce-scatter (unchanged,
+ * so every reduction sees the reference's operands in the reference's order)
+ * every rank sends its reduced block to all other ranks in ONE exchange,
+ * instead of the log2(P) mirrored steps (libbine_allreduce.c:779-809,
+ * :898-906).  On a fully connected node that is one hop on every link at once.
+ * Pure data movement: results identical bit for bit.  Off by default (the
+ * literal schedule; BINE_FLAT_AG=1 turns it on); collective. */
+int bine_comm_set_flat_ag(bine_comm_t comm, int on);
+
 /* ---- collectives (device pointers, stream-ordered) ------------------------- */
 /* allreduce_* (libbine.h:30-37).  `segsize` plays bine_allreduce_segsize
  * (libbine.h:28) for BINE_AR_BINE_BDW_REMAP_SEGMENTED and is the pipelining
@@ -265,8 +275,9 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
  * for the caller's prior work; *final_wait = op the caller's stream waits for
  * at the end (-1: none); workspace[4] = elements of TMP0, TMP1, TMP2 and the
  * relay staging buffer the schedule uses.
- * relay_min_bytes > 0 selects relay mode as
- * bine_comm_set_relay does, trees = 1 multi-tree mode as bine_comm_set_trees.  Returns the number of entries (may exceed cap) or
+ * relay_min_bytes > 0 selects relay mode as bine_comm_set_relay does; `mode`
+ * bit 0 = multi-tree mode (bine_comm_set_trees), bit 1 = flat allgather
+ * (bine_comm_set_flat_ag).  Returns the number of entries (may exceed cap) or
  * -status. */
 typedef struct {
   int32_t op;
@@ -277,7 +288,7 @@ typedef struct {
 
 int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root,
                            size_t esz, size_t segsize, int in_place, size_t chunk_bytes,
-                           size_t relay_min_bytes, int trees, bine_sched_entry_t *out, int64_t cap,
+                           size_t relay_min_bytes, int mode, bine_sched_entry_t *out, int64_t cap,
                            int *c_join, int64_t *final_wait, uint64_t *workspace);
 
 #ifdef __cplusplus

@@ -111,6 +111,7 @@ def lib():
         "bine_comm_set_relay": ([vp, sz], i),
         "bine_comm_set_trees": ([vp, i], i),
         "bine_comm_set_chunk": ([vp, sz], i),
+        "bine_comm_set_flat_ag": ([vp, i], i),
         "bine_exchange": ([vp, i, vp, vp, vp, i, vp, vp, vp, vp], i),
         "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int64), vp], ctypes.c_int64),

@@ -133,6 +133,11 @@ class Comm:
         """Multi-tree mode (allreduce, P = 4 / 8); collective."""
         check(lib().bine_comm_set_trees(self.handle, int(on)), "bine_comm_set_trees")
 
+    def set_flat_ag(self, on: bool) -> None:
+        """Allreduce (remap / static, power-of-two P): one all-peers allgather
+        exchange after the Bine reduce-scatter; bit-identical; collective."""
+        check(lib().bine_comm_set_flat_ag(self.handle, int(on)), "bine_comm_set_flat_ag")
+
     def set_chunk(self, nbytes: int) -> None:
         """Pipelining chunk in bytes (0 = default 16 MiB); never changes a bit; collective."""
         check(lib().bine_comm_set_chunk(self.handle, nbytes), "bine_comm_set_chunk")
@@ -254,14 +259,15 @@ def plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, 
 
 def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, root: int = 0,
              esz: int = 4, segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0,
-             relay_min_bytes: int = 0, info: bool = False, trees: bool = False):
+             relay_min_bytes: int = 0, info: bool = False, trees: bool = False, flat_ag: bool = False):
     """The executor's two-stream issue schedule of rank `rank` (host only).
     Returns (ops, c_join, final_wait); ops[i] = {"xchg", "wait", "prims"}.
     With info=True a 4th item: {"tmp_elems": [TMP0..2], "stage_elems": relay staging}."""
     a = _algo(coll, algo)
     rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
     cj, fw, ws = ctypes.c_int(), ctypes.c_int64(), (ctypes.c_uint64 * 4)()
-    args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes, relay_min_bytes, int(trees))
+    args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes, relay_min_bytes,
+            int(trees) | (2 if flat_ag else 0))
     n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw), ws)
     if n < 0:
         raise BineError(int(-n), f"schedule {coll}_{algo}")

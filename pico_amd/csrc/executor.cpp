@@ -192,6 +192,7 @@ struct bine_comm {
   size_t relay_min_bytes = 0;  // relay mode: smallest relayed part (0: off)
   bool trees = false;          // multi-tree mode (allreduce, P = 4 / 8)
   size_t chunk_bytes = 0;      // pipelining chunk (0: default_chunk_bytes())
+  bool flat_ag = false;        // allreduce: one-step all-peers allgather phase
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
   std::vector<hipEvent_t> ev;
@@ -215,6 +216,7 @@ static int comm_setup(bine_comm *c) {
   for (auto &e : c->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (const char *e = getenv("BINE_RELAY_MIN_BYTES")) c->relay_min_bytes = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_TREES")) c->trees = atoi(e) != 0;
+  if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) != 0;
   return BINE_SUCCESS;
 }
 
@@ -359,7 +361,8 @@ static size_t chunk_elems(size_t chunk_bytes, size_t esz) {
 static std::string plan_key(const PlanArgs &a) {
   std::string k;
   char buf[160];
-  snprintf(buf, sizeof buf, "%d|%zu|%zu|%zu|%d|%d|", a.algo, a.count, a.esz, a.segsize, (int)a.in_place, a.root);
+  snprintf(buf, sizeof buf, "%d|%zu|%zu|%zu|%d|%d|%d|", a.algo, a.count, a.esz, a.segsize, (int)a.in_place, a.root,
+           (int)a.flat_ag);
   k = buf;
   for (int x : a.rcounts) { k += std::to_string(x); k += ','; }
   return k;
@@ -402,6 +405,7 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   a.rank = c->rank;
   a.esz = bine_dtype_size(dtype);
   a.in_place = sbuf == BINE_IN_PLACE;
+  a.flat_ag = c->flat_ag;
   const size_t ch = chunk_elems(chunk_bytes, a.esz);
   const std::string key = plan_key(a) + "|" + std::to_string(ch) + "|" + std::to_string(c->relay_min_bytes) +
                           (c->trees ? "|T" : "");
@@ -763,14 +767,15 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
 }
 
 int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
-                           size_t segsize, int in_place, size_t chunk_bytes, size_t relay_min_bytes, int trees,
+                           size_t segsize, int in_place, size_t chunk_bytes, size_t relay_min_bytes, int mode,
                            bine_sched_entry_t *out, int64_t cap, int *c_join, int64_t *final_wait,
                            uint64_t *workspace) {
   if (!esz) return -(int64_t)BINE_ERR_ARG;
   PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
+  a.flat_ag = (mode & 2) != 0;
   Plan p;
   Schedule sc;
-  build(a, chunk_elems(chunk_bytes, esz), relay_min_bytes, trees != 0, p, sc);
+  build(a, chunk_elems(chunk_bytes, esz), relay_min_bytes, (mode & 1) != 0, p, sc);
   if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
   int64_t n = 0;
   for (size_t i = 0; i < sc.ops.size(); i++)
@@ -791,6 +796,13 @@ int bine_comm_set_trees(bine_comm_t c, int on) {
   if (!c) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->trees = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_flat_ag(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->flat_ag = on != 0;
   return BINE_SUCCESS;
 }
 

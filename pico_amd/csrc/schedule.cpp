@@ -380,11 +380,36 @@ void ar_bine_bdw_static(Builder &b, const PlanArgs &a) {
     if (elide && s == 0) b.reduce3(T0, 0, SB, bl.off(rb), RB, bl.off(rb), bl.wcnt(rb, w), PIPE);
     else b.reduce(T0, 0, RB, bl.off(rb), bl.wcnt(rb, w), PIPE);
   }
+  if (a.flat_ag) {  // rank x owns block perm[x] after the reduce-scatter
+    for (int x = 0; x < P; x++)
+      if (x != r) b.send(x, RB, bl.off(perm[(size_t)r]), bl.wcnt(perm[(size_t)r], 1));
+    for (int x = 0; x < P; x++)
+      if (x != r) b.recv(x, RB, bl.off(perm[(size_t)x]), bl.wcnt(perm[(size_t)x], 1));
+    b.end();
+    return;
+  }
   for (int s = steps - 1; s >= 0; s--) {
     const int dest = pi(r, s, P), sb = recv_start(dest, s), rb = recv_start(r, s);
     b.send(dest, RB, bl.off(rb), bl.wcnt(rb, w)); b.recv(dest, RB, bl.off(sb), bl.wcnt(sb, w)); b.end();
     w <<= 1;
   }
+}
+
+// the window rank x of P (power of two) owns after the remap reduce-scatter of
+// n elements: the halving recurrence of libbine_allreduce.c:866-885 for x
+static void remap_owned(int P, int x, uint64_t n, uint64_t *off, uint64_t *cnt) {
+  const int steps = log2_ceil(P);
+  const uint32_t vx = remap_rank((uint32_t)P, (uint32_t)x);
+  uint64_t w = n, o = 0;
+  for (int s = 0; s < steps; s++) {
+    const uint32_t vd = remap_rank((uint32_t)P, (uint32_t)pi(x, s, P));
+    uint64_t rc;
+    if (vx < vd) rc = w / 2;  // lower half kept at offset o
+    else { rc = w - w / 2; o += w / 2; }
+    w = rc;
+  }
+  *off = o;
+  *cnt = w;
 }
 
 // allreduce_bine_bdw_remap (:820-923) and allreduce_bine_bdw_remap_segmented
@@ -444,8 +469,20 @@ void ar_bine_remap(Builder &b, const PlanArgs &a, bool segmented) {
       else b.reduce(T0, 0, RB, ri[s], rc[s], PIPE);
       if (s + 1 < steps) { ri[s + 1] = ri[s]; si[s + 1] = ri[s]; w = rc[s]; }
     }
-    for (int s = steps - 1; s >= 0; s--) {
-      b.send(dst[s], RB, ri[s], rc[s]); b.recv(dst[s], RB, si[s], sc[s]); b.end();
+    if (a.flat_ag && pw2 && steps >= 1) {
+      for (int x = 0; x < P; x++)
+        if (x != r) b.send(x, RB, ri[steps - 1], rc[steps - 1]);
+      for (int x = 0; x < P; x++) {
+        if (x == r) continue;
+        uint64_t o, c;
+        remap_owned(P, x, n, &o, &c);
+        b.recv(x, RB, o, c);
+      }
+      b.end();
+    } else {
+      for (int s = steps - 1; s >= 0; s--) {
+        b.send(dst[s], RB, ri[s], rc[s]); b.recv(dst[s], RB, si[s], sc[s]); b.end();
+      }
     }
   }
   if (r < 2 * extra) {

@@ -121,6 +121,7 @@ Plan make_tree_plan(const PlanArgs &a) {
     int v = 0;
     while (sig[v] != a.rank) v++;
     PlanArgs b = a;
+    b.flat_ag = false;  // instances keep their own (mirrored) allgather
     b.rank = v;
     Mapper m;
     if (allreduce) {

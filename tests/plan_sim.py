@@ -27,11 +27,11 @@ class PlanError(AssertionError):
     pass
 
 
-def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, **kw):
+def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, flat_ag=False, **kw):
     """The executor's issue schedule (pico_amd.schedule) flattened back into a
     primitive list in issue order, one exchange group per op."""
     ops, _, _, info = pico_amd.schedule(coll, algo, P, r, chunk_bytes=chunk_bytes, relay_min_bytes=relay,
-                                        info=True, trees=trees, **kw)
+                                        info=True, trees=trees, flat_ag=flat_ag, **kw)
     out = []
     for i, o in enumerate(ops):
         for p in o["prims"]:
@@ -42,7 +42,7 @@ def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, **kw):
 
 
 def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_place=False,
-        rbufs=None, chunk_bytes=None, relay=0, trees=False):
+        rbufs=None, chunk_bytes=None, relay=0, trees=False, flat_ag=False):
     """chunk_bytes != None: run the executor's chunked issue schedule instead of
     the plan itself (same semantics when ops run in issue order)."""
     P = len(sbufs)
@@ -53,7 +53,8 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         prims, tmp = pico_amd.plan(coll, algo, P, r, count=count, rcounts=rcounts, root=root, esz=esz,
                                    segsize=segsize, in_place=in_place)
         if chunk_bytes is not None:
-            prims, info = scheduled_prims(coll, algo, P, r, chunk_bytes, relay=relay, trees=trees, count=count, rcounts=rcounts, root=root,
+            prims, info = scheduled_prims(coll, algo, P, r, chunk_bytes, relay=relay, trees=trees, flat_ag=flat_ag,
+                                          count=count, rcounts=rcounts, root=root,
                                     esz=esz, segsize=segsize, in_place=in_place)
         plans.append(prims)
         if coll == "allgather":

@@ -285,6 +285,31 @@ def test_comm_chunk_setting_bit_exact(dev, chunk):
             c.set_relay(0)
 
 
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_flat_allgather_bit_exact(dev, P):
+    """flat allgather phase (one all-peers exchange after the Bine
+    reduce-scatter), alone and with the relayed reduce-scatter: the reference's
+    bits, in and out of place"""
+    bad = []
+    try:
+        for c in comms(P):
+            c.set_flat_ag(True)
+        for algo in ("bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented"):
+            for dt, n in (("float", 100003), ("int64", 4099), ("double", 7)):
+                sb = O.inputs(dt, n, P)
+                want, _ = O.allreduce(algo, sb, dt, segsize=4096)
+                for relay in (0, 4096):
+                    for ip in (False, True):
+                        outs, st = run_loopback("allreduce", algo, sb, dt, segsize=4096, relay=relay, in_place=ip)
+                        if any(st) or any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                            bad.append((algo, dt, relay, ip, st))
+    finally:
+        for c in comms(P):
+            c.set_flat_ag(False)
+            c.set_relay(0)
+    assert not bad, bad[:8]
+
+
 @pytest.mark.parametrize("algo", list(pico_amd.ALGOS["allreduce"]))
 def test_in_place_allreduce(dev, algo):
     P = 4

@@ -70,8 +70,9 @@ def comms(dev):
 
 def _mode(cs, mode):
     for c in cs:
-        c.set_relay(256 << 10 if mode == "relay" else 0)  # bench.py RELAY_MIN_BYTES
+        c.set_relay(256 << 10 if "relay" in mode else 0)  # bench.py RELAY_MIN_BYTES
         c.set_trees(mode == "trees")
+        c.set_flat_ag("flat" in mode)
 
 
 def _device_inputs(dtype, tdt, n):
@@ -97,7 +98,7 @@ def c3_oracle():
     return sb, [host_checksum(w) for w in want]
 
 
-@pytest.mark.parametrize("mode", ["direct", "relay", "trees"])
+@pytest.mark.parametrize("mode", ["direct", "relay", "trees", "flat", "relay+flat"])
 def test_c3_allreduce_fullsize(dev, comms, c3_oracle, mode):
     sb_host, digests = c3_oracle
     assert len(set(digests)) == 1  # allreduce: every rank holds the same bits

@@ -269,3 +269,89 @@ def test_relay_off_for_non_permutation_steps():
     multi = [i for i, o in enumerate(a) if o["xchg"] and len(o["prims"]) > 2]
     assert multi and a[:max(multi) + 1] == b[:max(multi) + 1]
     assert len(b) > len(a)
+
+
+# ---- flat allgather phase ------------------------------------------------------
+
+FLAT_AG = ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented"]
+
+
+@pytest.mark.parametrize("algo", FLAT_AG)
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+@pytest.mark.parametrize("chunk,relay", [(0, 0), (256, 0), (256, 4)])
+def test_flat_allgather_matches_oracle(algo, P, chunk, relay):
+    """one all-peers exchange replaces the mirrored allgather: bit-identical to
+    the reference (the reduce-scatter and its reduction order are untouched)"""
+    for dtype, n in (("float", 997), ("int64", 64 * P + 5), ("double", 3)):
+        sb = O.inputs(dtype, n, P)
+        want, rets = O.allreduce(algo, sb, dtype, segsize=256)
+        for in_place in (False, True):
+            got = plan_sim.run("allreduce", algo, sb, dtype, segsize=256, chunk_bytes=chunk, relay=relay,
+                               flat_ag=True, in_place=in_place)
+            for r in range(P):
+                assert np.array_equal(got[r], want[r]), (algo, P, dtype, in_place, r)
+
+
+@pytest.mark.parametrize("algo", FLAT_AG)
+@pytest.mark.parametrize("P", [4, 8])
+def test_flat_allgather_schedule_race_free_and_one_step(algo, P):
+    for rank in range(P):
+        for in_place in (False, True):
+            ops, cj, fw = pico_amd.schedule("allreduce", algo, P, rank, count=4099, esz=4, chunk_bytes=1024,
+                                            segsize=256, in_place=in_place, flat_ag=True)
+            check_race_free(ops, cj, fw, in_place)
+            # the allgather phase is the last exchange: one group, all P-1 peers
+            last = [o for o in ops if o["xchg"]][-1]
+            assert {p["peer"] for p in last["prims"] if p["type"] == "SEND"} == set(range(P)) - {rank}
+            assert {p["peer"] for p in last["prims"] if p["type"] == "RECV"} == set(range(P)) - {rank}
+
+
+def test_flat_allgather_not_applied_where_it_does_not_fit():
+    """non-power-of-two segmented (folded ranks) and multi-tree instances keep
+    their own allgather; other algorithms ignore the flag"""
+    P = 6
+    sb = O.inputs("float", 1001, P)
+    want, _ = O.allreduce("bine_bdw_remap_segmented", sb, "float", segsize=256)
+    got = plan_sim.run("allreduce", "bine_bdw_remap_segmented", sb, "float", segsize=256, chunk_bytes=0, flat_ag=True)
+    assert all(np.array_equal(g, w) for g, w in zip(got, want))
+    for algo in ("ring", "bine_lat", "rabenseifner"):
+        a = pico_amd.schedule("allreduce", algo, 8, 3, count=4099, esz=4, chunk_bytes=1024)
+        b = pico_amd.schedule("allreduce", algo, 8, 3, count=4099, esz=4, chunk_bytes=1024, flat_ag=True)
+        assert a == b
+
+
+def _link_time(coll, algo, P, **kw):
+    """link-time model of a schedule: exchange ops run one after another on the
+    comm stream, the links of one op in parallel -> sum over ops of the busiest
+    directed link's bytes (max over ranks, op by op)"""
+    per_rank = []
+    for r in range(P):
+        ops, _, _ = pico_amd.schedule(coll, algo, P, r, **kw)
+        t = []
+        for o in ops:
+            if not o["xchg"]:
+                continue
+            link = {}
+            for p in o["prims"]:
+                if p["type"] in ("SEND", "RECV"):
+                    k = (p["type"], p["peer"])
+                    link[k] = link.get(k, 0) + p["count"]
+            t.append(max(link.values()))
+        per_rank.append(t)
+    return sum(max(ts) for ts in zip(*per_rank))
+
+
+def test_flat_allgather_link_time_model():
+    """P = 8, remap: in units of S/link the literal schedule takes 1.75 (RS 0.875
+    + AG 0.875); the flat allgather costs 0.125 instead of 0.875 -> 1.0; with
+    the relayed reduce-scatter (0.21875) 0.34375 instead of relay's 0.4375"""
+    n = 1 << 20
+    kw = dict(count=n, esz=4, chunk_bytes=1 << 16)
+    direct = _link_time("allreduce", "bine_bdw_remap", 8, **kw)
+    flat = _link_time("allreduce", "bine_bdw_remap", 8, flat_ag=True, **kw)
+    relay = _link_time("allreduce", "bine_bdw_remap", 8, relay_min_bytes=1024, **kw)
+    relay_flat = _link_time("allreduce", "bine_bdw_remap", 8, relay_min_bytes=1024, flat_ag=True, **kw)
+    assert abs(direct / n - 1.75) < 0.01
+    assert abs(flat / n - 1.0) < 0.01
+    assert abs(relay / n - 0.4375) < 0.02
+    assert abs(relay_flat / n - 0.34375) < 0.02

@@ -9,7 +9,8 @@ accepts P ranks on one device and connects them over its socket transport on
 stream / event hand-offs, chunked pipelines, relay routes) in real processes;
 it says nothing about xGMI speed.
 
-For each transport setting (direct; small pipelining chunks; multi-link relay)
+For each transport setting (direct; small pipelining chunks; multi-link relay;
+relay + flat allgather)
 it runs all 8 allreduce, 9 reduce_scatter, 2 reduce and 12 allgather
 algorithms on fp32 / int64 / int8 at odd sizes, and checks outputs bit for bit
 and error statuses against the oracle's return codes.
@@ -22,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CASES = (("float", 4099), ("int64", 1001), ("int8", 333))
-SETTINGS = (("direct", 0, 0), ("chunk4KiB", 0, 4096), ("relay", 64, 1024))
+SETTINGS = (("direct", 0, 0, 0), ("chunk4KiB", 0, 4096, 0), ("relay", 64, 1024, 0), ("relay+flat", 64, 1024, 1))
 
 
 def worker(rank, P, port, q):
@@ -70,9 +71,10 @@ def worker(rank, P, port, q):
         else:
             n_ok += 1
 
-    for sname, relay, chunk in SETTINGS:
+    for sname, relay, chunk, flat in SETTINGS:
         comm.set_relay(relay)
         comm.set_chunk(chunk)
+        comm.set_flat_ag(bool(flat))
         for dt, n in CASES:
             esz = np.dtype(npdt[dt]).itemsize
             sb = O.inputs(dt, n, P)
