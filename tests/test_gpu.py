@@ -4,8 +4,9 @@ schedule fixes the per-element association order, and the kernels reproduce
 MPICH's IEEE arithmetic (fp32/fp64 tolerance used: 0 ulp).
 
 Multi-rank cases run on ONE GPU through the loopback transport (virtual ranks,
-in-process peer copies); the RCCL transport is exercised at P = 1 here and at
-P = 2..8 by the driver's multi-GPU bench.
+in-process peer copies); the RCCL transport is exercised at P = 1 here, in
+real processes by tests/test_gpu_rccl.py, and over xGMI by the driver's
+multi-GPU bench.
 """
 import hashlib
 import os
