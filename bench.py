@@ -188,7 +188,9 @@ def bench_c2(steps: int, warmup: int):
 
 
 def _timed(torch, dist, comm, stream, call, steps, warmup):
-    """max-over-ranks ms per call() and wall seconds of `steps` timed calls"""
+    """max-over-ranks ms per call() and wall seconds of `steps` timed calls;
+    _timed.issue_ms = max-over-ranks host time per call spent enqueueing (a
+    value close to the ms per call means the host, not the GPU, set the pace)"""
     for _ in range(warmup):
         call()
     torch.cuda.synchronize()
@@ -200,13 +202,15 @@ def _timed(torch, dist, comm, stream, call, steps, warmup):
     e0.record(stream)
     for _ in range(steps):
         call()
+    issue = time.perf_counter() - t0
     e1.record(stream)
     torch.cuda.synchronize()
     comm.synchronize()
     wall = time.perf_counter() - t0
     dist.barrier()
-    t = torch.tensor([e0.elapsed_time(e1) / steps, wall], dtype=torch.float64)
+    t = torch.tensor([e0.elapsed_time(e1) / steps, wall, issue * 1e3 / steps], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    _timed.issue_ms = float(t[2])
     return float(t[0]), float(t[1])
 
 
@@ -353,6 +357,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     use(best)
     chosen, chunk = best
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
+    issue_ms = _timed.issue_ms
     extra = _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     probe = _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     S = nelem * 4
@@ -390,6 +395,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "transport": chosen,
                        "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
                        "chunk_bytes": chunk,
+                       "host_issue_ms_per_step": round(issue_ms, 4),
                        "transport_trials_ms": {f"{m}/{ch >> 20}MiB": round(v, 4) for (m, ch), v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": extra,

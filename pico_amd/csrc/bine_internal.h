@@ -73,6 +73,7 @@ struct Schedule {
   int64_t final_wait = -1;    // op of the comm stream the caller's stream waits for at the end
   uint64_t stage_elems = 0;   // BINE_BUF_STAGE workspace (relay mode)
   int relayed_steps = 0;
+  std::vector<char> signals;  // op i is waited on (by an op's `wait` or final_wait): record its event
 };
 
 struct SchedCfg {

@@ -220,6 +220,12 @@ static int comm_setup(bine_comm *c) {
   return BINE_SUCCESS;
 }
 
+// BINE_TRACE=1: one stderr line per issued op (debugging the issue sequence)
+static bool trace_on() {
+  static const bool on = getenv("BINE_TRACE") && atoi(getenv("BINE_TRACE")) != 0;
+  return on;
+}
+
 static hipEvent_t next_event(bine_comm *c) {
   hipEvent_t e = c->ev[c->ev_next];
   c->ev_next = (c->ev_next + 1) % c->ev.size();
@@ -241,6 +247,7 @@ static int ensure_workspace(bine_comm *c, const uint64_t *elems, size_t esz, hip
   // old buffers may still be read by enqueued work
   HIP_TRY(hipStreamSynchronize(user));
   HIP_TRY(hipStreamSynchronize(c->cstream));
+
   for (int t = 0; t < 4; t++) {
     const size_t need = elems[t] * esz;
     if (need <= c->tmp_bytes[t]) continue;
@@ -326,6 +333,9 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   for (size_t i = 0; i < sc.ops.size(); i++) {
     const SOp &o = sc.ops[i];
     hipStream_t st = o.xchg ? C : K;
+    if (trace_on())
+      fprintf(stderr, "bine[%d] op %zu/%zu %s wait %lld prims %zu\n", c->rank, i, sc.ops.size(),
+              o.xchg ? "xchg" : "local", (long long)o.wait, o.prims.size());
     if (o.wait >= 0) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
     int rc = BINE_SUCCESS;
     if (o.xchg) {
@@ -342,9 +352,12 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       if (rc) { set_err("local primitive failed (%s)", bine_status_string(rc)); return rc; }
     }
     // an event of the pool may be re-recorded by a later op once the pool
-    // wraps: any later record only delays a waiter, never lets it run early
-    evs[i] = next_event(c);
-    HIP_TRY(hipEventRecord(evs[i], st));
+    // wraps: any later record only delays a waiter, never lets it run early.
+    // Ops nothing waits for record no event (host cost per op).
+    if (sc.signals[i]) {
+      evs[i] = next_event(c);
+      HIP_TRY(hipEventRecord(evs[i], st));
+    }
   }
   if (sc.final_wait >= 0) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
   return BINE_SUCCESS;

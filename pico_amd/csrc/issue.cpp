@@ -401,6 +401,11 @@ void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, con
       if (j > waited[0]) out.final_wait = j;
       break;
     }
+  // only ops something waits for need an event recorded after them
+  out.signals.assign(out.ops.size(), 0);
+  for (const auto &o : out.ops)
+    if (o.wait >= 0) out.signals[(size_t)o.wait] = 1;
+  if (out.final_wait >= 0) out.signals[(size_t)out.final_wait] = 1;
 }
 
 }  // namespace bine

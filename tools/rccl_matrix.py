@@ -10,12 +10,14 @@ stream / event hand-offs, chunked pipelines, relay routes) in real processes;
 it says nothing about xGMI speed.
 
 For each transport setting (direct; small pipelining chunks; multi-link relay;
-relay + flat allgather)
+relay + flat allgather; the same on a non-default caller stream with every
+collective run twice, the second time into a zeroed output)
 it runs all 8 allreduce, 9 reduce_scatter, 2 reduce and 12 allgather
 algorithms on fp32 / int64 / int8 at odd sizes, and checks outputs bit for bit
 and error statuses against the oracle's return codes.
 usage: python tools/rccl_matrix.py [P]   (exit 0 = every rank, every case ok)
 """
+import contextlib
 import os
 import sys
 
@@ -23,7 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CASES = (("float", 4099), ("int64", 1001), ("int8", 333))
-SETTINGS = (("direct", 0, 0, 0), ("chunk4KiB", 0, 4096, 0), ("relay", 64, 1024, 0), ("relay+flat", 64, 1024, 1))
+# (name, relay_min_bytes, chunk_bytes, flat allgather, run each collective twice on a side stream)
+SETTINGS = (("direct", 0, 0, 0, 0), ("chunk4KiB", 0, 4096, 0, 0), ("relay", 64, 1024, 0, 0),
+            ("relay+flat", 64, 1024, 1, 0), ("side-stream x2", 64, 1024, 1, 1))
 
 
 def worker(rank, P, port, q):
@@ -55,6 +59,11 @@ def worker(rank, P, port, q):
             call()
             torch.cuda.synchronize()
             comm.synchronize()
+            if twice:  # second call into a zeroed output (plan / schedule cache reuse)
+                out.zero_()
+                call()
+                torch.cuda.synchronize()
+                comm.synchronize()
             rc = 0
         except pico_amd.BineError:
             rc = 1
@@ -71,10 +80,13 @@ def worker(rank, P, port, q):
         else:
             n_ok += 1
 
-    for sname, relay, chunk, flat in SETTINGS:
+    side = torch.cuda.Stream()
+    for sname, relay, chunk, flat, twice in SETTINGS:
         comm.set_relay(relay)
         comm.set_chunk(chunk)
         comm.set_flat_ag(bool(flat))
+        ctx = torch.cuda.stream(side) if twice else contextlib.nullcontext()
+        ctx.__enter__()
         for dt, n in CASES:
             esz = np.dtype(npdt[dt]).itemsize
             sb = O.inputs(dt, n, P)
@@ -104,6 +116,7 @@ def worker(rank, P, port, q):
                 s = dev(sb[rank])
                 run(f"{sname} allgather_{algo} {dt}", rets[rank], want[rank],
                     lambda: pico_amd.allgather(algo, s, r, n, dt, comm), r, dt, P * n)
+        ctx.__exit__(None, None, None)
         print(f"rank {rank} {sname}: {n_ok} ok, {len(bad)} bad so far", flush=True)
     # the raw P2P primitive (bine_exchange): ring shift, then all peers at once
     nb = 100003
