@@ -482,3 +482,52 @@ def test_reduce_batch_matches_per_window(dev, dtype):
     b = to_dev(O.fill(dtype, 64, 2), pad=16)
     if esz < 16:
         assert pico_amd.reduce_batch([a[esz:], a], [b, b], [32, 32], dtype) == 1
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_known_answer_debug_inputs(dev, P):
+    """pico_core's DEBUG known-answer mode (pico_core.c:82-95,
+    debug_sbuf_generator pico_core_utils.c:1095-1126): rank r sends 10^r in
+    every element, so every allreduce element is sum(10^r) -- for every
+    allreduce algorithm, every transport, int32 and int64"""
+    n = 10007
+    bad = []
+    for dt, npdt in (("int32", np.int32), ("int64", np.int64)):
+        sb = [np.full(n, 10 ** r, npdt) for r in range(P)]
+        want = np.full(n, sum(10 ** r for r in range(P)), npdt)
+        for algo in pico_amd.ALGOS["allreduce"]:
+            for mode in ("direct", "relay", "flat", "trees"):
+                try:
+                    for c in comms(P):
+                        c.set_trees(mode == "trees")
+                        c.set_flat_ag(mode == "flat")
+                    outs, st = run_loopback("allreduce", algo, sb, dt, segsize=256,
+                                            relay=64 if mode == "relay" else 0)
+                finally:
+                    for c in comms(P):
+                        c.set_trees(False)
+                        c.set_flat_ag(False)
+                if any(st) or any(not np.array_equal(o, want) for o in outs):
+                    bad.append((dt, algo, mode, st))
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_trees_within_pico_core_tolerance(dev, P):
+    """multi-tree mode changes the fp association order: its results must stay
+    within pico_core's ground-truth tolerance against an exact (fp64) sum --
+    P * 1e-4 absolute for float, P * 1e-13 for double (pico_core_utils.c:967-988)"""
+    n = 65537
+    try:
+        for c in comms(P):
+            c.set_trees(True)
+        for dt, tol in (("float", P * 1e-4), ("double", P * 1e-13)):
+            sb = O.inputs(dt, n, P)
+            exact = np.sum(np.stack([x.astype(np.float64) for x in sb]), axis=0)
+            outs, st = run_loopback("allreduce", "bine_bdw_remap", sb, dt)
+            assert not any(st)
+            for o in outs:
+                assert np.max(np.abs(o.astype(np.float64) - exact)) <= tol, dt
+    finally:
+        for c in comms(P):
+            c.set_trees(False)
