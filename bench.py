@@ -111,6 +111,13 @@ def cpu_baseline_c2(budget_s: float = 10.0):
                     c3[f"P{p}"] = {"ms": round(t * 1e3, 2), "algbw_per_rank_GBs": round(S / t / 1e9, 3),
                                    "busbw_per_rank_GBs": round(2 * (p - 1) / p * S / t / 1e9, 3),
                                    "cores": p}
+            try:  # C1: the reference's own configuration, 1 MiB/rank fp32, P = 4
+                c1 = _ref_bench(4, ["allreduce", "bine_bdw_remap", 262_144, 200], 120)
+            except Exception:
+                c1 = None
+            if c1 and c1.get("rc") == 0:
+                out["libbine_allreduce_bine_bdw_remap_c1_P4"] = {"us": round(c1["median_s"] * 1e6, 2), "cores": 4,
+                                                                  "iterations": 200}
             if c3:
                 out["libbine_allreduce_bine_bdw_remap_c3"] = c3
                 out["libbine_sample"] = ("real libbine allreduce_bine_bdw_remap fp32 256 MiB/rank, P host ranks "
@@ -221,9 +228,23 @@ def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream
 
 
 def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev):
-    """BASELINE configs C4 and C5 with the transport chosen for C3 (reported
-    beside the headline; a few steps each)"""
+    """BASELINE configs C1, C4 and C5 with the transport chosen for C3
+    (reported beside the headline; a few steps each)"""
     out = {}
+    # C1 shape on the GPUs: fp32 allreduce 1 MiB per rank (the reference's own
+    # CPU configuration: libbine bine_bdw_remap_over 381.9 us at P = 4 through
+    # pico_core, BASELINE.md section 2) -- latency-bound, so the literal
+    # schedule and the latency-optimal Bine variant are both timed
+    n1 = 262_144
+    sb = torch.empty(n1, dtype=torch.float32, device=dev)
+    rb = torch.empty(n1, dtype=torch.float32, device=dev)
+    pico_amd.fill_pico(sb, n1, "float", 55 + rank)
+    for algo in ("bine_bdw_remap", "bine_lat"):
+        ms, _ = _timed(torch, dist, comm, stream,
+                       lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream), 50, 10)
+        out[f"C1_allreduce_{algo}_f32_1MiB"] = {"us": round(ms * 1e3, 2),
+                                                "algbw_per_rank_GBs": round(n1 * 4 / (ms * 1e-3) / 1e9, 2)}
+    del sb, rb
     # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
     n = 268_435_456
     sb = torch.empty(n, dtype=torch.float32, device=dev)
