@@ -86,9 +86,15 @@ struct RcclTransport final : Transport {
   }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
     NCCL_TRY(ncclGroupStart());
-    for (const auto &x : s) NCCL_TRY(ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, comm, st));
-    for (const auto &x : r) NCCL_TRY(ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, comm, st));
-    NCCL_TRY(ncclGroupEnd());
+    // the group is always closed, also when posting an operation failed
+    ncclResult_t r0 = ncclSuccess;
+    for (const auto &x : s)
+      if (r0 == ncclSuccess) r0 = ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, comm, st);
+    for (const auto &x : r)
+      if (r0 == ncclSuccess) r0 = ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, comm, st);
+    const ncclResult_t r1 = ncclGroupEnd();
+    NCCL_TRY(r0);
+    NCCL_TRY(r1);
     return BINE_SUCCESS;
   }
 };
@@ -202,6 +208,17 @@ struct bine_comm {
   std::vector<bine::XSend> xs;
   std::vector<bine::XRecv> xr;
   std::mutex mu;
+  // releases whatever was set up (also after a failed init); the caller has
+  // drained the streams (bine_comm_destroy) or never used them (init errors)
+  ~bine_comm() {
+    (void)hipSetDevice(device);
+    tx.reset();
+    for (int t = 0; t < 4; t++)
+      if (tmp[t]) (void)hipFree(tmp[t]);
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (cstream) (void)hipStreamDestroy(cstream);
+  }
 };
 
 namespace bine {
@@ -604,7 +621,13 @@ int bine_comm_init_loopback(bine_comm_t *comms, int nranks, int device) {
     c->size = nranks;
     c->device = device;
     int rc = comm_setup(c.get());
-    if (rc) return rc;
+    if (rc) {  // undo the ranks already set up
+      for (int k = 0; k < r; k++) {
+        delete comms[k];
+        comms[k] = nullptr;
+      }
+      return rc;
+    }
     c->hub = hub;
     c->tx = std::make_unique<LoopbackTransport>(hub, r);
     comms[r] = c.release();
@@ -630,12 +653,6 @@ int bine_comm_destroy(bine_comm_t c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->cstream);
-  c->tx.reset();
-  for (int t = 0; t < 4; t++)
-    if (c->tmp[t]) (void)hipFree(c->tmp[t]);
-  for (auto e : c->ev) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(c->stream);
-  (void)hipStreamDestroy(c->cstream);
   delete c;
   return BINE_SUCCESS;
 }
