@@ -175,7 +175,9 @@ int bine_comm_set_trees(bine_comm_t comm, int on);
 int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
 
 /* Flat allgather phase for allreduce_bine_bdw_remap / _static /
- * _remap_segmented at power-of-two P: after the Bine reduce-scatter (unchanged,
+ * _remap_segmented / allreduce_rabenseifner at power-of-two P (and a flat
+ * gather for reduce_bine_bdw: every rank sends its reduced block straight to
+ * the root): after the reduce-scatter (unchanged,
  * so every reduction sees the reference's operands in the reference's order)
  * every rank sends its reduced block to all other ranks in ONE exchange,
  * instead of the log2(P) mirrored steps (libbine_allreduce.c:779-809,

@@ -30,10 +30,11 @@ struct PlanArgs {
   size_t esz = 4;
   size_t segsize = 0;               // bytes; segmented variant's segment
   bool in_place = false;
-  // allreduce (remap / static, power-of-two P): replace the mirrored Bine
-  // allgather by one exchange in which every rank sends its reduced block to
-  // every other rank (one hop on every link of a fully connected node).  Pure
-  // data movement: result bits unchanged.
+  // allreduce (remap / static / rabenseifner, power-of-two P): replace the
+  // mirrored allgather by one exchange in which every rank sends its reduced
+  // block to every other rank (one hop on every link of a fully connected
+  // node); reduce_bine_bdw: the gather tree becomes one step into the root.
+  // Pure data movement: result bits unchanged.
   bool flat_ag = false;
 };
 

@@ -316,11 +316,34 @@ void ar_rabenseifner(Builder &b, const PlanArgs &a) {
       b.reduce(T0, ri[step], RB, ri[step], rc[step], PIPE);
       if (step + 1 < steps) { ri[step + 1] = ri[step]; si[step + 1] = ri[step]; w = rc[step]; step++; }
     }
-    step = steps - 1;
-    for (int mask = adj >> 1; mask > 0; mask >>= 1) {
-      int vdest = vrank ^ mask, dest = vdest < rem ? vdest * 2 : vdest + rem;
-      b.send(dest, RB, ri[step], rc[step]); b.recv(dest, RB, si[step], sc[step]); b.end();
-      step--;
+    if (a.flat_ag && rem == 0 && steps >= 1) {
+      // one all-peers exchange: rank x's block after the halving of :553-590
+      auto owned = [&](int x, uint64_t *off, uint64_t *cnt) {
+        uint64_t ww = n, o = 0;
+        for (int mask = 1; mask < adj; mask <<= 1) {
+          const int d = x ^ mask;
+          if (x < d) ww = ww / 2;
+          else { o += ww / 2; ww = ww - ww / 2; }
+        }
+        *off = o;
+        *cnt = ww;
+      };
+      for (int x = 0; x < P; x++)
+        if (x != r) b.send(x, RB, ri[steps - 1], rc[steps - 1]);
+      for (int x = 0; x < P; x++) {
+        if (x == r) continue;
+        uint64_t o, c;
+        owned(x, &o, &c);
+        b.recv(x, RB, o, c);
+      }
+      b.end();
+    } else {
+      step = steps - 1;
+      for (int mask = adj >> 1; mask > 0; mask >>= 1) {
+        int vdest = vrank ^ mask, dest = vdest < rem ? vdest * 2 : vdest + rem;
+        b.send(dest, RB, ri[step], rc[step]); b.recv(dest, RB, si[step], sc[step]); b.end();
+        step--;
+      }
     }
   }
   if (r < 2 * rem) {
@@ -940,6 +963,20 @@ void rd_bine_bdw(Builder &b, const PlanArgs &a) {
     b.send(partner, res, si[step], sc[step]); b.recv(partner, T0, ri[step], rc[step]); b.end(pipe);
     b.reduce(T0, ri[step], res, ri[step], rc[step], pipe);
     mask <<= 1; inv >>= 1; step++;
+  }
+  if (a.flat_ag && steps >= 1) {
+    // flat gather: every rank sends its reduced block straight to the root
+    // (pure data movement, same bytes as the binomial gather of :167-199)
+    if (r != 0) {
+      b.send(0, res, first(me), span(me, me));
+    } else {
+      for (int x = 1; x < P; x++) {
+        const int mx = (int)remap_rank((uint32_t)P, (uint32_t)x);
+        b.recv(x, res, first(mx), span(mx, mx));
+      }
+    }
+    b.end();
+    return;
   }
   mask >>= 1;
   inv = 1;

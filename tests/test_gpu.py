@@ -295,7 +295,13 @@ def test_flat_allgather_bit_exact(dev, P):
     try:
         for c in comms(P):
             c.set_flat_ag(True)
-        for algo in ("bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented"):
+        for dt, n in (("float", 100003), ("double", 4099)):  # flat gather of reduce_bine_bdw
+            sb = O.inputs(dt, n, P)
+            want, _ = O.reduce("bine_bdw", sb, dt)
+            outs, st = run_loopback("reduce", "bine_bdw", sb, dt)
+            if any(st) or sha(outs[0]) != sha(want):
+                bad.append(("reduce_bine_bdw", dt, st))
+        for algo in ("bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented", "rabenseifner"):
             for dt, n in (("float", 100003), ("int64", 4099), ("double", 7)):
                 sb = O.inputs(dt, n, P)
                 want, _ = O.allreduce(algo, sb, dt, segsize=4096)

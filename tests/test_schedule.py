@@ -273,7 +273,7 @@ def test_relay_off_for_non_permutation_steps():
 
 # ---- flat allgather phase ------------------------------------------------------
 
-FLAT_AG = ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented"]
+FLAT_AG = ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented", "rabenseifner"]
 
 
 @pytest.mark.parametrize("algo", FLAT_AG)
@@ -314,7 +314,11 @@ def test_flat_allgather_not_applied_where_it_does_not_fit():
     want, _ = O.allreduce("bine_bdw_remap_segmented", sb, "float", segsize=256)
     got = plan_sim.run("allreduce", "bine_bdw_remap_segmented", sb, "float", segsize=256, chunk_bytes=0, flat_ag=True)
     assert all(np.array_equal(g, w) for g, w in zip(got, want))
-    for algo in ("ring", "bine_lat", "rabenseifner"):
+    sb = O.inputs("float", 1001, P)
+    want, _ = O.allreduce("rabenseifner", sb, "float")
+    got = plan_sim.run("allreduce", "rabenseifner", sb, "float", chunk_bytes=0, flat_ag=True)
+    assert all(np.array_equal(g, w) for g, w in zip(got, want))
+    for algo in ("ring", "bine_lat", "recursivedoubling"):
         a = pico_amd.schedule("allreduce", algo, 8, 3, count=4099, esz=4, chunk_bytes=1024)
         b = pico_amd.schedule("allreduce", algo, 8, 3, count=4099, esz=4, chunk_bytes=1024, flat_ag=True)
         assert a == b
@@ -355,3 +359,20 @@ def test_flat_allgather_link_time_model():
     assert abs(flat / n - 1.0) < 0.01
     assert abs(relay / n - 0.4375) < 0.02
     assert abs(relay_flat / n - 0.34375) < 0.02
+
+
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+def test_flat_gather_reduce_bdw_matches_oracle(P):
+    """reduce_bine_bdw with the gather tree replaced by one step into the root:
+    the reference's bits at the root"""
+    for dtype, n in (("float", 997), ("int64", 64 * P + 5), ("double", 3)):
+        sb = O.inputs(dtype, n, P)
+        want, _ = O.reduce("bine_bdw", sb, dtype)
+        for in_place in (False, True):
+            got = plan_sim.run("reduce", "bine_bdw", sb, dtype, chunk_bytes=256, relay=4, flat_ag=True,
+                               in_place=in_place)
+            assert np.array_equal(got[0], want), (P, dtype, in_place)
+        for rank in range(P):
+            ops, cj, fw = pico_amd.schedule("reduce", "bine_bdw", P, rank, count=n, esz=8, chunk_bytes=256,
+                                            flat_ag=True)
+            check_race_free(ops, cj, fw, False)
