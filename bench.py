@@ -361,8 +361,17 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     trials = {}
 
     def trial(cfg):
+        # a setting the planner rejects fails identically on every rank before
+        # any transfer (plans are a pure function of the arguments): skip it
         use(cfg)
-        trials[cfg] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
+        try:
+            trials[cfg] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
+        except pico_amd.BineError as e:
+            if rank == 0:
+                print(f"bench: transport {cfg[0]} / chunk {cfg[1] >> 20} MiB skipped: {e}", file=sys.stderr)
+            torch.cuda.synchronize()
+            comm.synchronize()
+            trials[cfg] = float("inf")
 
     mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
     if len(modes) > 1 or len(chunks) > 1:
