@@ -198,6 +198,7 @@ struct bine_comm {
   size_t relay_min_bytes = 0;  // relay mode: smallest relayed part (0: off)
   bool trees = false;          // multi-tree mode (allreduce, P = 4 / 8)
   size_t chunk_bytes = 0;      // pipelining chunk (0: default_chunk_bytes())
+  size_t single_stream_bytes = 1 << 20;  // collectives up to this size run on the caller's stream only
   bool flat_ag = false;        // allreduce: one-step all-peers allgather phase
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
@@ -234,6 +235,7 @@ static int comm_setup(bine_comm *c) {
   if (const char *e = getenv("BINE_RELAY_MIN_BYTES")) c->relay_min_bytes = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_TREES")) c->trees = atoi(e) != 0;
   if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) != 0;
+  if (const char *e = getenv("BINE_SINGLE_STREAM_BYTES")) c->single_stream_bytes = (size_t)strtoull(e, nullptr, 10);
   return BINE_SUCCESS;
 }
 
@@ -330,16 +332,18 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
   return BINE_SUCCESS;
 }
 
+// single = true: every op on the caller's stream K in issue order (small
+// collectives: no overlap to win, so no cross-stream event edges to pay for)
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
-                   hipStream_t K) {
+                   hipStream_t K, bool single = false) {
   char *base[6];
   base[BINE_BUF_SBUF] = (char *)sbuf;
   base[BINE_BUF_RBUF] = (char *)rbuf;
   for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
   base[BINE_BUF_STAGE] = (char *)c->tmp[3];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
-  hipStream_t C = c->cstream;
-  if (sc.c_join) {
+  hipStream_t C = single ? K : c->cstream;
+  if (sc.c_join && !single) {
     int rc = stream_join(c, C, K);
     if (rc) return rc;
   }
@@ -353,7 +357,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     if (trace_on())
       fprintf(stderr, "bine[%d] op %zu/%zu %s wait %lld prims %zu\n", c->rank, i, sc.ops.size(),
               o.xchg ? "xchg" : "local", (long long)o.wait, o.prims.size());
-    if (o.wait >= 0) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
+    if (o.wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
     int rc = BINE_SUCCESS;
     if (o.xchg) {
       sends.clear();
@@ -371,12 +375,12 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     // an event of the pool may be re-recorded by a later op once the pool
     // wraps: any later record only delays a waiter, never lets it run early.
     // Ops nothing waits for record no event (host cost per op).
-    if (sc.signals[i]) {
+    if (sc.signals[i] && !single) {
       evs[i] = next_event(c);
       HIP_TRY(hipEventRecord(evs[i], st));
     }
   }
-  if (sc.final_wait >= 0) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
+  if (sc.final_wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
   return BINE_SUCCESS;
 }
 
@@ -454,7 +458,10 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   const uint64_t need[4] = {plan.tmp_elems[0], plan.tmp_elems[1], plan.tmp_elems[2], sc.stage_elems};
   int rc = ensure_workspace(c, need, a.esz, K);
   if (rc) return rc;
-  return execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K);
+  uint64_t bytes = (uint64_t)a.count;
+  for (int x : a.rcounts) bytes += (uint64_t)x;
+  bytes *= a.esz;
+  return execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, bytes <= c->single_stream_bytes);
 }
 
 }  // namespace bine
