@@ -178,6 +178,8 @@ def bench_c2(steps: int, warmup: int):
     alg_bytes = 3 * C2_ELEMS * 4
     gbs = alg_bytes / (ms * 1e-3) / 1e9
     traffic = _pmc_traffic("k_reduce")
+    del ins, ios
+    tree = _bench_tree_kernel(torch, pico_amd, dev, stream, steps, warmup)
     return {
         "metric": "device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X",
         "value": round(gbs, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
@@ -185,13 +187,54 @@ def bench_c2(steps: int, warmup: int):
         "dtype": "f32", "data": "synthetic (pico_core rand_r distribution, generated on device)",
         "config": {"workload": "C2: fp32 MPI_Reduce_local replacement kernel, inout=inout+in, 64 MiB "
                                "(16,777,216 elem), 1 MI355X, 4 rotating buffer sets",
-                   "value_definition": "HBM GB/s = 3*64MiB/t (BASELINE.md 3)"},
+                   "value_definition": "HBM GB/s = 3*64MiB/t (BASELINE.md 3)",
+                   "side_kernels": {"k_reduce_tree": tree}},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "kernel": "bine::k_reduce<float,SUM>", "algorithmic_bytes_per_launch": alg_bytes},
         "wall_s": round(wall, 4),
     }
+
+
+TREE_LEAVES, TREE_ELEMS = 8, 4_194_304   # flat reduce-scatter at C3, P = 8, 16 MiB chunks
+
+
+def _bench_tree_kernel(torch, pico_amd, dev, stream, steps, warmup):
+    """The flat reduce-scatter's fused tree kernel at its C3 shape (P = 8
+    leaves x 16 MiB chunk -> 16 MiB out; algorithmic bytes 9 x 16 MiB per
+    launch), 4 rotating sets (576 MiB, beyond the Infinity Cache), HIP events
+    on the launch stream."""
+    sets = 4
+    bufs = []
+    for k in range(sets):
+        leaves = [torch.empty(TREE_ELEMS, dtype=torch.float32, device=dev) for _ in range(TREE_LEAVES)]
+        for j, t in enumerate(leaves):
+            pico_amd.fill_pico(t, TREE_ELEMS, "float", 5000 + 16 * k + j)
+        bufs.append((leaves, torch.empty(TREE_ELEMS, dtype=torch.float32, device=dev)))
+    torch.cuda.synchronize()
+
+    def run(i):
+        leaves, out = bufs[i % sets]
+        rc = pico_amd.reduce_tree(leaves, out, TREE_ELEMS, "float", "sum", stream=stream)
+        assert rc == 0, rc
+    for i in range(warmup):
+        run(i)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for i in range(steps):
+        run(i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / steps * 1e3
+    alg = (TREE_LEAVES + 1) * TREE_ELEMS * 4
+    gbs = alg / (us * 1e-6) / 1e9
+    del bufs
+    torch.cuda.empty_cache()
+    return {"kernel": "bine::k_reduce_tree<float,SUM,8>", "leaves": TREE_LEAVES, "elems_per_leaf": TREE_ELEMS,
+            "us": round(us, 2), "algorithmic_bytes_per_launch": alg, "achieved_GBs": round(gbs, 1),
+            "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
 
 
 def _timed(torch, dist, comm, stream, call, steps, warmup):
@@ -336,9 +379,12 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # "relay" = the same schedule with permutation steps routed over all links
     # (two hops); "+flat" = the allgather phase as one all-peers exchange
     # (one hop on every link); "trees" = P-1 relabelled instances over
-    # edge-disjoint pairings.  All but "trees" are bit-identical to the reference.
-    modes = {"off": ["direct"], "auto": ["direct", "flat", "relay", "relay+flat", "trees"],
-             "relay": ["relay"], "trees": ["trees"], "flat": ["flat"], "relay+flat": ["relay+flat"]
+    # edge-disjoint pairings; "flatrs" = the reduce-scatter phase as one
+    # all-peers exchange whose owner evaluates the reference's reduction tree
+    # in one fused kernel.  All but "trees" are bit-identical to the reference.
+    modes = {"off": ["direct"], "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "trees"],
+             "relay": ["relay"], "trees": ["trees"], "flat": ["flat"], "relay+flat": ["relay+flat"],
+             "flatrs+flat": ["flatrs+flat"], "flatrs": ["flatrs"]
              }.get(relay, ["direct"])
     if world <= 2:
         modes = [m for m in modes if "relay" not in m] or ["direct"]
@@ -353,6 +399,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         comm.set_relay(RELAY_MIN_BYTES if "relay" in m else 0)
         comm.set_trees(m == "trees")
         comm.set_flat_ag("flat" in m)
+        comm.set_flat_rs("flatrs" in m)
         comm.set_chunk(ch)
 
     # measured, not guessed: each transport is timed briefly on this hardware
@@ -396,7 +443,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # bytes this rank puts on xGMI per allreduce (from the executed schedule)
     ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4, chunk_bytes=chunk,
                                   relay_min_bytes=RELAY_MIN_BYTES if "relay" in chosen else 0,
-                                  trees=chosen == "trees", flat_ag="flat" in chosen)
+                                  trees=chosen == "trees", flat_ag="flat" in chosen,
+                                  flat_rs="flatrs" in chosen)
     egress = 4 * sum(p["count"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND")
     peers = len({p["peer"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND"})
     # schedule-aware link roofline: exchange ops run one after another, the
@@ -460,7 +508,8 @@ def main():
     ap.add_argument("--algo", default="bine_bdw_remap")
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
     ap.add_argument("--relay", default="auto",
-                    help="transport at N > 1: auto | off (direct) | flat | relay | relay+flat | trees")
+                    help="transport at N > 1: auto | off (direct) | flat | relay | relay+flat | flatrs | "
+                         "flatrs+flat | trees")
     ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/16/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")

@@ -123,6 +123,13 @@ int bine_reduce3(const void *a, const void *b, void *out, size_t count, int dtyp
  * (BINE_ERR_ARG if some window's operands are not co-aligned mod 16 B). */
 int bine_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out,
                       const size_t *count, int dtype, int op, void *stream);
+/* The owner's side of the flat reduce-scatter (bine_comm_set_flat_rs): out =
+ * the binary reduction tree over `nleaves` (2, 4, 8 or 16) blocks given in tree
+ * order, evaluated level by level -- v[i] = v[i] (op) v[i + w] for w = 1, 2,
+ * 4, ... and i a multiple of 2w (v[i] the inout side) -- in one pass over the
+ * operands.  `out` may alias any leaf element for element. */
+int bine_reduce_tree(int nleaves, const void *const *leaves, void *out, size_t count, int dtype, int op,
+                     void *stream);
 int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
 /* Order-independent 64-bit digest of a buffer: sum over i of
  * mix64(bits(x[i]) + i * 0x9E3779B97F4A7C15) mod 2^64 (bits zero-extended).
@@ -186,6 +193,20 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
  * literal schedule; BINE_FLAT_AG=1 turns it on); collective. */
 int bine_comm_set_flat_ag(bine_comm_t comm, int on);
 
+/* Flat reduce-scatter phase for allreduce_bine_bdw_remap / _static /
+ * _remap_segmented, reduce_scatter_bine_permute_remap / _send_remap / _static
+ * and reduce_bine_bdw at power-of-two P <= 16: the log2(P) halving steps
+ * become ONE exchange in which every rank sends each block straight to the
+ * rank that computes it (one hop on every link at once), and that rank
+ * evaluates the reference's reduction tree for its block -- the same binary
+ * tree over the same P contributions, same association, same operand order
+ * (T(x,s) = T(x,s-1) (op) T(peer(x,s),s-1)) -- in one fused kernel
+ * (BINE_PRIM_REDUCE_TREE: reads P blocks, writes one).  Results identical bit
+ * for bit to the literal schedule.  Chunked like the other pipelined steps
+ * (the transfer of chunk k+1 overlaps the tree of chunk k).  Off by default
+ * (BINE_FLAT_RS=1 turns it on); collective. */
+int bine_comm_set_flat_rs(bine_comm_t comm, int on);
+
 /* ---- collectives (device pointers, stream-ordered) ------------------------- */
 /* allreduce_* (libbine.h:30-37).  `segsize` plays bine_allreduce_segsize
  * (libbine.h:28) for BINE_AR_BINE_BDW_REMAP_SEGMENTED and is the pipelining
@@ -237,7 +258,9 @@ int bine_loopback_run_allgather(bine_comm_t *comms, int nranks, int algo,
 /* ---- schedule introspection (host only, no GPU needed) ----------------------
  * A plan is the ordered list of primitives one rank executes. */
 typedef enum { BINE_PRIM_SEND = 1, BINE_PRIM_RECV = 2, BINE_PRIM_REDUCE = 3,
-               BINE_PRIM_REDUCE3 = 4, BINE_PRIM_COPY = 5 } bine_prim_type_t;
+               BINE_PRIM_REDUCE3 = 4, BINE_PRIM_COPY = 5,
+               BINE_PRIM_REDUCE_TREE = 6  /* flat reduce-scatter: see bine_comm_set_flat_rs */
+} bine_prim_type_t;
 typedef enum { BINE_BUF_SBUF = 0, BINE_BUF_RBUF = 1, BINE_BUF_TMP0 = 2, BINE_BUF_TMP1 = 3,
                BINE_BUF_TMP2 = 4,
                BINE_BUF_STAGE = 5  /* relay staging; appears in issue schedules only */
@@ -248,12 +271,14 @@ typedef enum { BINE_BUF_SBUF = 0, BINE_BUF_RBUF = 1, BINE_BUF_TMP0 = 2, BINE_BUF
 typedef struct {
   int32_t type;      /* bine_prim_type_t */
   int32_t group;     /* consecutive SEND/RECV with equal group form one exchange */
-  int32_t peer;      /* SEND/RECV peer rank */
+  int32_t peer;      /* SEND/RECV peer rank; REDUCE_TREE: number of leaves nl */
   int32_t flags;     /* BINE_PRIM_PIPELINE */
-  int32_t src_buf;   /* SEND: source; REDUCE/REDUCE3: `in` (a); COPY: source */
-  int32_t dst_buf;   /* RECV: destination; REDUCE: inout; REDUCE3: out; COPY: dest */
-  int32_t aux_buf;   /* REDUCE3: b */
-  int32_t pad_;
+  int32_t src_buf;   /* SEND: source; REDUCE/REDUCE3: `in` (a); COPY: source;
+                        REDUCE_TREE: the other nl-1 leaves, k-th at src_off + k*count */
+  int32_t dst_buf;   /* RECV: destination; REDUCE: inout; REDUCE3 / REDUCE_TREE: out; COPY: dest */
+  int32_t aux_buf;   /* REDUCE3: b; REDUCE_TREE: the rank's own leaf (position `pos`) */
+  int32_t pos;       /* REDUCE_TREE: tree position of the aux leaf (the staged leaves
+                        fill the other positions in order) */
   uint64_t src_off;  /* element offsets */
   uint64_t dst_off;
   uint64_t aux_off;
@@ -279,7 +304,7 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
  * relay staging buffer the schedule uses.
  * relay_min_bytes > 0 selects relay mode as bine_comm_set_relay does; `mode`
  * bit 0 = multi-tree mode (bine_comm_set_trees), bit 1 = flat allgather
- * (bine_comm_set_flat_ag).  Returns the number of entries (may exceed cap) or
+ * (bine_comm_set_flat_ag), bit 2 = flat reduce-scatter (bine_comm_set_flat_rs).  Returns the number of entries (may exceed cap) or
  * -status. */
 typedef struct {
   int32_t op;

@@ -42,7 +42,7 @@ UNIQUE_ID_BYTES = 128
 class Prim(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("group", ctypes.c_int32), ("peer", ctypes.c_int32),
                 ("flags", ctypes.c_int32), ("src_buf", ctypes.c_int32), ("dst_buf", ctypes.c_int32),
-                ("aux_buf", ctypes.c_int32), ("pad_", ctypes.c_int32), ("src_off", ctypes.c_uint64),
+                ("aux_buf", ctypes.c_int32), ("pos", ctypes.c_int32), ("src_off", ctypes.c_uint64),
                 ("dst_off", ctypes.c_uint64), ("aux_off", ctypes.c_uint64), ("count", ctypes.c_uint64)]
 
 
@@ -50,7 +50,7 @@ class SchedEntry(ctypes.Structure):
     _fields_ = [("op", ctypes.c_int32), ("xchg", ctypes.c_int32), ("wait", ctypes.c_int64), ("prim", Prim)]
 
 
-PRIM_NAMES = {1: "SEND", 2: "RECV", 3: "REDUCE", 4: "REDUCE3", 5: "COPY"}
+PRIM_NAMES = {1: "SEND", 2: "RECV", 3: "REDUCE", 4: "REDUCE3", 5: "COPY", 6: "REDUCE_TREE"}
 
 
 class BineError(RuntimeError):
@@ -102,6 +102,7 @@ def lib():
         "bine_reduce": ([vp, i, vp, vp, sz, i, i, i, vp], i),
         "bine_allgather": ([vp, i, vp, vp, sz, i, vp], i),
         "bine_reduce_batch": ([i, vp, vp, vp, vp, i, i, vp], i),
+        "bine_reduce_tree": ([i, vp, vp, ctypes.c_size_t, i, i, vp], i),
         "bine_loopback_run_allgather": ([vp, i, i, vp, vp, sz, i, vp], i),
         "bine_loopback_run_allreduce": ([vp, i, i, vp, vp, sz, i, i, sz, vp], i),
         "bine_loopback_run_reduce_scatter": ([vp, i, i, vp, vp, vp, i, i, vp], i),
@@ -112,6 +113,7 @@ def lib():
         "bine_comm_set_trees": ([vp, i], i),
         "bine_comm_set_chunk": ([vp, sz], i),
         "bine_comm_set_flat_ag": ([vp, i], i),
+        "bine_comm_set_flat_rs": ([vp, i], i),
         "bine_exchange": ([vp, i, vp, vp, vp, i, vp, vp, vp, vp], i),
         "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int64), vp], ctypes.c_int64),

@@ -138,6 +138,11 @@ class Comm:
         exchange after the Bine reduce-scatter; bit-identical; collective."""
         check(lib().bine_comm_set_flat_ag(self.handle, int(on)), "bine_comm_set_flat_ag")
 
+    def set_flat_rs(self, on: bool) -> None:
+        """Flat reduce-scatter phase (one all-peers exchange + the reference's
+        reduction tree in one kernel; bit-identical); collective."""
+        check(lib().bine_comm_set_flat_rs(self.handle, int(on)), "bine_comm_set_flat_rs")
+
     def set_chunk(self, nbytes: int) -> None:
         """Pipelining chunk in bytes (0 = default 16 MiB); never changes a bit; collective."""
         check(lib().bine_comm_set_chunk(self.handle, nbytes), "bine_comm_set_chunk")
@@ -251,7 +256,7 @@ def plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, 
         raise BineError(int(-n), f"plan {coll}_{algo}")
     arr = (_lib.Prim * max(int(n), 1))()
     lib().bine_plan(a, nranks, rank, count, rc, root, esz, segsize, int(in_place), arr, n, tmp)
-    prims = [{f: getattr(arr[k], f) for f, _ in _lib.Prim._fields_ if f != "pad_"} for k in range(int(n))]
+    prims = [{f: getattr(arr[k], f) for f, _ in _lib.Prim._fields_ } for k in range(int(n))]
     for p in prims:
         p["type"] = _lib.PRIM_NAMES[p["type"]]
     return prims, list(tmp)
@@ -259,7 +264,8 @@ def plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, 
 
 def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, root: int = 0,
              esz: int = 4, segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0,
-             relay_min_bytes: int = 0, info: bool = False, trees: bool = False, flat_ag: bool = False):
+             relay_min_bytes: int = 0, info: bool = False, trees: bool = False, flat_ag: bool = False,
+             flat_rs: bool = False):
     """The executor's two-stream issue schedule of rank `rank` (host only).
     Returns (ops, c_join, final_wait); ops[i] = {"xchg", "wait", "prims"}.
     With info=True a 4th item: {"tmp_elems": [TMP0..2], "stage_elems": relay staging}."""
@@ -267,7 +273,7 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
     rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
     cj, fw, ws = ctypes.c_int(), ctypes.c_int64(), (ctypes.c_uint64 * 4)()
     args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes, relay_min_bytes,
-            int(trees) | (2 if flat_ag else 0))
+            int(trees) | (2 if flat_ag else 0) | (4 if flat_rs else 0))
     n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw), ws)
     if n < 0:
         raise BineError(int(-n), f"schedule {coll}_{algo}")
@@ -276,7 +282,7 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
     ops = []
     for k in range(int(n)):
         e = arr[k]
-        p = {f: getattr(e.prim, f) for f, _ in _lib.Prim._fields_ if f != "pad_"}
+        p = {f: getattr(e.prim, f) for f, _ in _lib.Prim._fields_ }
         p["type"] = _lib.PRIM_NAMES[p["type"]]
         if not ops or e.op != len(ops) - 1:
             ops.append({"xchg": bool(e.xchg), "wait": int(e.wait), "prims": []})
@@ -294,6 +300,13 @@ def reduce_batch(ins, inouts, counts, dtype, op: str = "sum", stream=None) -> in
     c = (ctypes.c_size_t * n)(*counts)
     b = _ptrs(inouts)
     return lib().bine_reduce_batch(n, _ptrs(ins), b, b, c, _dtype(dtype, inouts[0]), OPS[op], _stream(stream, None))
+
+
+def reduce_tree(leaves, out, count: int, dtype, op: str = "sum", stream=None) -> int:
+    """out[:count] = the reduction tree over the leaf buffers (tree order,
+    len 2/4/8/16) in one launch (bine_reduce_tree).  Returns the status."""
+    return lib().bine_reduce_tree(len(leaves), _ptrs(leaves), _ptr(out), count, _dtype(dtype, out), OPS[op],
+                                  _stream(stream, None))
 
 
 def exchange(comm: Comm, sends=(), recvs=(), stream=None) -> None:
@@ -372,4 +385,4 @@ globals().update(ENTRY_POINTS)
 __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "reduce_batch",
-           "exchange"] + list(ENTRY_POINTS)
+           "exchange", "reduce_tree"] + list(ENTRY_POINTS)

@@ -36,6 +36,16 @@ struct PlanArgs {
   // node); reduce_bine_bdw: the gather tree becomes one step into the root.
   // Pure data movement: result bits unchanged.
   bool flat_ag = false;
+  // allreduce remap / static / segmented (power-of-two P), reduce_scatter
+  // bine_{permute,send}_remap / bine_static, reduce_bine_bdw, 2 <= P <= 16:
+  // replace the log2(P) reduce-scatter steps by one all-peers exchange in which
+  // every rank sends each block straight to the rank that computes it, which
+  // then evaluates the reference's reduction tree for that block over the P
+  // contributions in one REDUCE_TREE (same operands, same association, same
+  // operand order: result bits unchanged).  flat_chunk = pipelining chunk in
+  // elements (0: one chunk): chunk k's transfer overlaps chunk k-1's tree.
+  bool flat_rs = false;
+  size_t flat_chunk = 0;
 };
 
 Plan make_plan(const PlanArgs &a);
@@ -96,6 +106,11 @@ int launch_reduce(const void *a, const void *b, void *out, size_t count, int dty
 constexpr int kMaxBatch = 8;
 int launch_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out, const size_t *count,
                         int dtype, int op, void *stream);
+// out = the reduction tree over nl (2..kMaxLeaves, power of two) leaves in
+// tree order:
+// level by level (w = 1, 2, 4, ...) v[i] = v[i] (op) v[i + w] for i % 2w == 0
+constexpr int kMaxLeaves = 16;
+int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream);
 int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
 int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
 

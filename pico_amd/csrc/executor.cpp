@@ -200,6 +200,7 @@ struct bine_comm {
   size_t chunk_bytes = 0;      // pipelining chunk (0: default_chunk_bytes())
   size_t single_stream_bytes = 1 << 20;  // collectives up to this size run on the caller's stream only
   bool flat_ag = false;        // allreduce: one-step all-peers allgather phase
+  bool flat_rs = false;        // one-step all-peers reduce-scatter phase + tree kernel
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
   std::vector<hipEvent_t> ev;
@@ -235,6 +236,7 @@ static int comm_setup(bine_comm *c) {
   if (const char *e = getenv("BINE_RELAY_MIN_BYTES")) c->relay_min_bytes = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_TREES")) c->trees = atoi(e) != 0;
   if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) != 0;
+  if (const char *e = getenv("BINE_FLAT_RS")) c->flat_rs = atoi(e) != 0;
   if (const char *e = getenv("BINE_SINGLE_STREAM_BYTES")) c->single_stream_bytes = (size_t)strtoull(e, nullptr, 10);
   return BINE_SUCCESS;
 }
@@ -321,7 +323,14 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
     if (p.type == BINE_PRIM_REDUCE)
       rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.dst_buf, p.dst_off), ptr(p.dst_buf, p.dst_off), p.count,
                          dtype, op, K);
-    else if (p.type == BINE_PRIM_REDUCE3)
+    else if (p.type == BINE_PRIM_REDUCE_TREE) {
+      if (p.peer < 2 || p.peer > kMaxLeaves) return BINE_ERR_INTERNAL;
+      if (p.pos < 0 || p.pos >= p.peer) return BINE_ERR_INTERNAL;
+      const void *leaf[kMaxLeaves];
+      for (int j = 0, k = 0; j < p.peer; j++)
+        leaf[j] = j == p.pos ? ptr(p.aux_buf, p.aux_off) : ptr(p.src_buf, p.src_off + (uint64_t)k++ * p.count);
+      rc = launch_reduce_tree(p.peer, leaf, ptr(p.dst_buf, p.dst_off), p.count, dtype, op, K);
+    } else if (p.type == BINE_PRIM_REDUCE3)
       rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count,
                          dtype, op, K);
     else
@@ -395,15 +404,17 @@ static size_t chunk_elems(size_t chunk_bytes, size_t esz) {
 static std::string plan_key(const PlanArgs &a) {
   std::string k;
   char buf[160];
-  snprintf(buf, sizeof buf, "%d|%zu|%zu|%zu|%d|%d|%d|", a.algo, a.count, a.esz, a.segsize, (int)a.in_place, a.root,
-           (int)a.flat_ag);
+  snprintf(buf, sizeof buf, "%d|%zu|%zu|%zu|%d|%d|%d|%d|", a.algo, a.count, a.esz, a.segsize, (int)a.in_place, a.root,
+           (int)a.flat_ag, (int)a.flat_rs);
   k = buf;
   for (int x : a.rcounts) { k += std::to_string(x); k += ','; }
   return k;
 }
 
 // own plan + issue schedule; relay mode needs every rank's plan
-static void build(const PlanArgs &a, size_t ch, size_t relay_min_bytes, bool trees, Plan &plan, Schedule &sc) {
+static void build(const PlanArgs &args, size_t ch, size_t relay_min_bytes, bool trees, Plan &plan, Schedule &sc) {
+  PlanArgs a = args;
+  a.flat_chunk = ch;  // the flat reduce-scatter is chunked by the planner itself
   if (trees) plan = make_tree_plan(a);
   if (!trees || plan.status == BINE_ERR_UNSUPPORTED) plan = make_plan(a);
   if (plan.status != BINE_SUCCESS) return;
@@ -440,6 +451,7 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   a.esz = bine_dtype_size(dtype);
   a.in_place = sbuf == BINE_IN_PLACE;
   a.flat_ag = c->flat_ag;
+  a.flat_rs = c->flat_rs;
   const size_t ch = chunk_elems(chunk_bytes, a.esz);
   const std::string key = plan_key(a) + "|" + std::to_string(ch) + "|" + std::to_string(c->relay_min_bytes) +
                           (c->trees ? "|T" : "");
@@ -583,6 +595,12 @@ int bine_reduce3(const void *a, const void *b, void *out, size_t count, int dtyp
 int bine_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out, const size_t *count,
                       int dtype, int op, void *stream) {
   return launch_reduce_batch(n, a, b, out, count, dtype, op, stream);
+}
+
+int bine_reduce_tree(int nleaves, const void *const *leaves, void *out, size_t count, int dtype, int op,
+                     void *stream) {
+  if (!leaves || (!out && count)) return BINE_ERR_ARG;
+  return launch_reduce_tree(nleaves, leaves, out, count, dtype, op, stream);
 }
 
 int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream) {
@@ -810,6 +828,7 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
   if (!esz) return -(int64_t)BINE_ERR_ARG;
   PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
   a.flat_ag = (mode & 2) != 0;
+  a.flat_rs = (mode & 4) != 0;
   Plan p;
   Schedule sc;
   build(a, chunk_elems(chunk_bytes, esz), relay_min_bytes, (mode & 1) != 0, p, sc);
@@ -840,6 +859,13 @@ int bine_comm_set_flat_ag(bine_comm_t c, int on) {
   if (!c) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->flat_ag = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_flat_rs(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->flat_rs = on != 0;
   return BINE_SUCCESS;
 }
 

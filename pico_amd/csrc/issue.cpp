@@ -364,6 +364,11 @@ void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, con
           r.rd.push_back(reg(p.aux_buf, p.aux_off, p.count));
           r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
           break;
+        case BINE_PRIM_REDUCE_TREE:
+          r.rd.push_back(reg(p.aux_buf, p.aux_off, p.count));
+          r.rd.push_back(reg(p.src_buf, p.src_off, (uint64_t)(p.peer - 1) * p.count));
+          r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));
+          break;
         default:  // COPY
           r.rd.push_back(reg(p.src_buf, p.src_off, p.count));
           r.wr.push_back(reg(p.dst_buf, p.dst_off, p.count));

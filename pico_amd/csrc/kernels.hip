@@ -344,6 +344,149 @@ int launch_reduce_batch(int n, const void *const *a, const void *const *b, void 
 }
 
 // ----------------------------------------------------------------------------
+// tree reduction: the owner's side of the flat reduce-scatter phase.  One
+// launch evaluates the reference's whole reduction tree of a block from its P
+// contributions (leaf 0 = the rank's own input, leaves 1..P-1 = the received
+// blocks in tree order): HBM traffic (P + 1) * count * sizeof(T) instead of the
+// 3 (P - 1) * count * sizeof(T) of P - 1 pairwise passes.  Per lane U 16-B
+// vectors of every leaf in flight (NL * U loads), the tree evaluated in
+// registers level by level -- v[i] = v[i] (op) v[i + w], left = inout -- so
+// every element sees the reference's association and operand order.  Received
+// leaves are read once: non-temporal loads.
+
+struct TreeArgs {
+  const void *leaf[kMaxLeaves];
+  void *out;
+  uint64_t head, nvec, n;
+  int vec;  // 1: all operands co-aligned mod 16 B with `out`
+};
+
+template <typename T, int OP, int NL>
+__device__ __forceinline__ T tree_scalar(const TreeArgs &t, size_t i) {
+  T v[NL];
+#pragma unroll
+  for (int j = 0; j < NL; j++) v[j] = ((const T *)t.leaf[j])[i];
+#pragma unroll
+  for (int w = 1; w < NL; w <<= 1)
+#pragma unroll
+    for (int j = 0; j < NL; j += 2 * w) v[j] = apply<T, OP>(v[j], v[j + w]);
+  return v[0];
+}
+
+template <typename T, int OP, int NL, int U>
+__global__ __launch_bounds__(kBlock) void k_reduce_tree(TreeArgs t) {
+  constexpr size_t V = 16 / sizeof(T);
+  T *out = (T *)t.out;
+  if (!t.vec) {  // operands not co-aligned: scalar grid-stride
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < t.n; i += (size_t)gridDim.x * kBlock)
+      out[i] = tree_scalar<T, OP, NL>(t, i);
+    return;
+  }
+  if (blockIdx.x == 0) {
+    for (size_t i = threadIdx.x; i < t.head; i += kBlock) out[i] = tree_scalar<T, OP, NL>(t, i);
+    for (size_t i = t.head + t.nvec * V + threadIdx.x; i < t.n; i += kBlock) out[i] = tree_scalar<T, OP, NL>(t, i);
+  }
+  u32x4 *vo = reinterpret_cast<u32x4 *>(out + t.head);
+  const size_t tile = (size_t)kBlock * U;
+  for (size_t base = (size_t)blockIdx.x * tile + threadIdx.x; base < t.nvec; base += (size_t)gridDim.x * tile) {
+    u32x4 v[U][NL];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * kBlock;
+      if (i < t.nvec) {
+#pragma unroll
+        for (int j = 0; j < NL; j++) {
+          const u32x4 *p = reinterpret_cast<const u32x4 *>((const T *)t.leaf[j] + t.head) + i;
+          v[u][j] = j == 0 ? *p : __builtin_nontemporal_load(p);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * kBlock;
+      if (i < t.nvec) {
+#pragma unroll
+        for (int w = 1; w < NL; w <<= 1)
+#pragma unroll
+          for (int j = 0; j < NL; j += 2 * w) v[u][j] = apply16<T, OP>(v[u][j], v[u][j + w]);
+        vo[i] = v[u][0];
+      }
+    }
+  }
+}
+
+template <typename T, int OP, int NL>
+static hipError_t tree_nl(TreeArgs &t, hipStream_t st) {
+  constexpr int U = NL <= 4 ? 4 : NL == 8 ? 2 : 1;
+  size_t blocks;
+  if (t.vec) {
+    const size_t tiles = (t.nvec + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
+    blocks = tiles ? tiles : 1;
+  } else {
+    blocks = (t.n + kBlock * 4 - 1) / (kBlock * 4);
+    if (blocks > 2048) blocks = 2048;
+  }
+  if (blocks > 65536) blocks = 65536;  // grid-strided beyond
+  hipLaunchKernelGGL((k_reduce_tree<T, OP, NL, U>), dim3((unsigned)blocks), dim3(kBlock), 0, st, t);
+  return hipGetLastError();
+}
+
+template <typename T, int OP>
+static hipError_t tree_t(int nl, TreeArgs &t, hipStream_t st) {
+  switch (nl) {
+    case 2: return tree_nl<T, OP, 2>(t, st);
+    case 4: return tree_nl<T, OP, 4>(t, st);
+    case 8: return tree_nl<T, OP, 8>(t, st);
+    case 16: return tree_nl<T, OP, 16>(t, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <typename T>
+static hipError_t tree_op(int nl, TreeArgs &t, int op, hipStream_t st) {
+  constexpr size_t V = 16 / sizeof(T);
+  const uintptr_t oo = (uintptr_t)t.out;
+  bool co = (oo % sizeof(T)) == 0;
+  for (int j = 0; j < nl; j++) co = co && (((uintptr_t)t.leaf[j] ^ oo) & 15) == 0;
+  t.vec = co ? 1 : 0;
+  t.head = co ? std::min<uint64_t>(((16 - (oo & 15)) & 15) / sizeof(T), t.n) : t.n;
+  t.nvec = co ? (t.n - t.head) / V : 0;
+  switch (op) {
+    case BINE_SUM: return tree_t<T, BINE_SUM>(nl, t, st);
+    case BINE_PROD: return tree_t<T, BINE_PROD>(nl, t, st);
+    case BINE_MAX: return tree_t<T, BINE_MAX>(nl, t, st);
+    case BINE_MIN: return tree_t<T, BINE_MIN>(nl, t, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream) {
+  if (count == 0) return BINE_SUCCESS;
+  if (nl < 2 || nl > kMaxLeaves || (nl & (nl - 1))) return BINE_ERR_ARG;
+  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+  TreeArgs t{};
+  for (int j = 0; j < nl; j++) t.leaf[j] = leaf[j];
+  t.out = out;
+  t.n = count;
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case BINE_INT8: e = tree_op<int8_t>(nl, t, op, st); break;
+    case BINE_UINT8: e = tree_op<uint8_t>(nl, t, op, st); break;
+    case BINE_INT16: e = tree_op<int16_t>(nl, t, op, st); break;
+    case BINE_UINT16: e = tree_op<uint16_t>(nl, t, op, st); break;
+    case BINE_INT32: e = tree_op<int32_t>(nl, t, op, st); break;
+    case BINE_UINT32: e = tree_op<uint32_t>(nl, t, op, st); break;
+    case BINE_INT64: e = tree_op<int64_t>(nl, t, op, st); break;
+    case BINE_UINT64: e = tree_op<uint64_t>(nl, t, op, st); break;
+    case BINE_FLOAT: e = tree_op<float>(nl, t, op, st); break;
+    case BINE_DOUBLE: e = tree_op<double>(nl, t, op, st); break;
+    default: return BINE_ERR_UNSUPPORTED;
+  }
+  return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
 // pico_core input generator (glibc rand_r, LCG jump-ahead)
 // ----------------------------------------------------------------------------
 

@@ -195,6 +195,18 @@ struct Builder {
     x.src_buf = src; x.src_off = src_off; x.dst_buf = dst; x.dst_off = dst_off; x.count = n;
     p.prims.push_back(x);
   }
+  // out = tree over nl leaves: leaf `pos` at (own, own_off), the k-th of the
+  // others at (in, in_off + k * n)
+  void reduce_tree(int nl, int pos, int own, uint64_t own_off, int in, uint64_t in_off, int out, uint64_t out_off,
+                   uint64_t n) {
+    if (n == 0) return;
+    Prim x = mk(BINE_PRIM_REDUCE_TREE);
+    x.peer = nl;
+    x.pos = pos;
+    x.aux_buf = own; x.aux_off = own_off; x.src_buf = in; x.src_off = in_off;
+    x.dst_buf = out; x.dst_off = out_off; x.count = n;
+    p.prims.push_back(x);
+  }
   void tmp(int t, uint64_t n) {
     uint64_t &s = p.tmp_elems[t - T0];
     s = std::max(s, n);
@@ -204,6 +216,64 @@ struct Builder {
 
 // reduction "pipelined" only when the REDUCE directly follows its exchange
 constexpr bool PIPE = true;
+
+// ---------------------------------------------------------------------------
+// flat reduce-scatter phase (PlanArgs::flat_rs)
+// ---------------------------------------------------------------------------
+// In a halving reduce-scatter whose step s pairs rank r with peer(r, s), the
+// two partners share their window at every step and each keeps
+// acc = acc (op) received on its half (every MPI_Reduce_local call of these
+// schedules is reduce(received, own accumulator), e.g.
+// libbine_allreduce.c:888, libbine_reduce_scatter.c:1034).  So the block rank x
+// holds at the end is the binary tree
+//     T(x, -1) = input of x,   T(x, s) = T(x, s-1) (op) T(peer(x, s), s-1),
+// i.e. over the leaf order L(x, s) = L(x, s-1) ++ L(peer(x, s), s-1), combined
+// level by level, left operand = inout.  flat_leaves() returns L(x, steps-1).
+template <typename Peer>
+std::vector<int> flat_leaves(int P, int steps, int x, Peer peer) {
+  std::vector<std::vector<int>> L((size_t)P), N((size_t)P);
+  for (int r = 0; r < P; r++) L[(size_t)r] = {r};
+  for (int s = 0; s < steps; s++) {
+    for (int r = 0; r < P; r++) {
+      N[(size_t)r] = L[(size_t)r];
+      const auto &o = L[(size_t)peer(r, s)];
+      N[(size_t)r].insert(N[(size_t)r].end(), o.begin(), o.end());
+    }
+    L.swap(N);
+  }
+  return L[(size_t)x];
+}
+
+bool flat_rs_fits(const PlanArgs &a) { return a.flat_rs && a.P >= 2 && a.P <= kMaxLeaves && is_pow2(a.P); }
+
+// One all-peers exchange per chunk: this rank sends block x (boff[x], bcnt[x]
+// of buffer `src`) to rank x for every x != rank, receives its own block from
+// the P-1 others into TMP0 (chunk-major staging, leaf order), and reduces the
+// chunk with one REDUCE_TREE into (out, out_off).  `leaves` = the tree of the
+// block this rank computes (this rank's own contribution is one of them, not
+// necessarily the first: send_remap / static hand the block to another rank).
+void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &boff,
+             const std::vector<uint64_t> &bcnt, const std::vector<int> &leaves, int out, uint64_t out_off) {
+  const int P = a.P, r = a.rank;
+  uint64_t cmax = 0;
+  for (int x = 0; x < P; x++) cmax = std::max(cmax, bcnt[(size_t)x]);
+  const uint64_t mine = bcnt[(size_t)r];
+  const uint64_t ch = a.flat_chunk ? a.flat_chunk : std::max<uint64_t>(cmax, 1);
+  b.tmp(T0, (uint64_t)(P - 1) * mine);
+  for (uint64_t k = 0; k * ch < cmax; k++) {
+    const uint64_t o = k * ch;
+    for (int x = 0; x < P; x++)
+      if (x != r && o < bcnt[(size_t)x]) b.send(x, src, boff[(size_t)x] + o, std::min(ch, bcnt[(size_t)x] - o));
+    const uint64_t base = (uint64_t)(P - 1) * o, cl = o < mine ? std::min(ch, mine - o) : 0;
+    int pos = 0;
+    for (int j = 0, k = 0; j < P; j++) {
+      if (leaves[(size_t)j] == r) { pos = j; continue; }
+      b.recv(leaves[(size_t)j], T0, base + (uint64_t)k++ * cl, cl);
+    }
+    b.end();
+    b.reduce_tree(P, pos, src, boff[(size_t)r] + o, T0, base, out, out_off + o, cl);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // allreduce -- libbine_allreduce.c
@@ -395,7 +465,14 @@ void ar_bine_bdw_static(Builder &b, const PlanArgs &a) {
   b.tmp(T0, bl.wcnt(0, P / 2) + bl.early);
   const bool elide = !a.in_place;  // step 0 reads sbuf, writes rbuf
   int w = P;
-  for (int s = 0; s < steps; s++) {
+  if (flat_rs_fits(a)) {  // rank x computes block perm[x]
+    std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
+    for (int x = 0; x < P; x++) { boff[(size_t)x] = bl.off(perm[(size_t)x]); bcnt[(size_t)x] = bl.wcnt(perm[(size_t)x], 1); }
+    const auto leaves = flat_leaves(P, steps, r, [&](int x, int s) { return pi(x, s, P); });
+    flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, leaves, RB, boff[(size_t)r]);
+    w = 1;
+  }
+  for (int s = 0; s < steps && w > 1; s++) {
     w >>= 1;
     const int dest = pi(r, s, P), sb = recv_start(dest, s), rb = recv_start(r, s);
     const int sbuf = (elide && s == 0) ? SB : RB;
@@ -480,6 +557,7 @@ void ar_bine_remap(Builder &b, const PlanArgs &a, bool segmented) {
     std::vector<int> dst(steps + 1);
     uint64_t w = n;
     const uint32_t vrank = remap_rank((uint32_t)adj, (uint32_t)nr);
+    const bool flat = pw2 && flat_rs_fits(a);
     for (int s = 0; s < steps; s++) {
       const int vd = pi(nr, s, adj);
       dst[s] = pw2 ? vd : (vd < extra ? (vd << 1) + 1 : vd + extra);
@@ -487,10 +565,18 @@ void ar_bine_remap(Builder &b, const PlanArgs &a, bool segmented) {
       if (vrank < vdest) { rc[s] = w / 2; sc[s] = w - rc[s]; si[s] = ri[s] + rc[s]; }
       else { sc[s] = w / 2; rc[s] = w - sc[s]; ri[s] = si[s] + sc[s]; }
       const bool first = elide && s == 0;
-      b.send(dst[s], first ? SB : RB, si[s], sc[s]); b.recv(dst[s], T0, 0, rc[s]); b.end(PIPE);
-      if (first) b.reduce3(T0, 0, SB, ri[s], RB, ri[s], rc[s], PIPE);
-      else b.reduce(T0, 0, RB, ri[s], rc[s], PIPE);
+      if (!flat) {
+        b.send(dst[s], first ? SB : RB, si[s], sc[s]); b.recv(dst[s], T0, 0, rc[s]); b.end(PIPE);
+        if (first) b.reduce3(T0, 0, SB, ri[s], RB, ri[s], rc[s], PIPE);
+        else b.reduce(T0, 0, RB, ri[s], rc[s], PIPE);
+      }
       if (s + 1 < steps) { ri[s + 1] = ri[s]; si[s + 1] = ri[s]; w = rc[s]; }
+    }
+    if (flat && steps >= 1) {  // rank x computes the window remap_owned(x)
+      std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
+      for (int x = 0; x < P; x++) remap_owned(P, x, n, &boff[(size_t)x], &bcnt[(size_t)x]);
+      const auto leaves = flat_leaves(P, steps, r, [&](int x, int s) { return pi(x, s, P); });
+      flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, leaves, RB, ri[steps - 1]);
     }
     if (a.flat_ag && pw2 && steps >= 1) {
       for (int x = 0; x < P; x++)
@@ -574,6 +660,20 @@ struct Displs {
     }
   }
 };
+
+// flat reduce-scatter of the reduce_scatter variants: block y (displacement
+// d[y], rc[y] elements) goes to rank y; the result lands in rbuf, through TMP1
+// when in place (rbuf's own blocks are still being sent)
+void flat_rs_block(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &d, const std::vector<int> &rc,
+                   const std::vector<int> &leaves) {
+  std::vector<uint64_t> cnt(rc.size());
+  for (size_t i = 0; i < rc.size(); i++) cnt[i] = (uint64_t)rc[i];
+  const uint64_t mine = cnt[(size_t)a.rank];
+  if (!a.in_place) { flat_rs(b, a, src, d, cnt, leaves, RB, 0); return; }
+  b.tmp(T1, mine);
+  flat_rs(b, a, src, d, cnt, leaves, T1, 0);
+  b.copy(T1, 0, RB, 0, mine);
+}
 
 // reduce_scatter_recursivehalving, :15-257
 void rs_recursivehalving(Builder &b, const PlanArgs &a) {
@@ -762,6 +862,12 @@ void rs_bine_static(Builder &b, const PlanArgs &a) {
     return c;
   };
   const int src = a.in_place ? RB : SB;
+  if (flat_rs_fits(a)) {  // rank x computes block perm[x] and sends it to rank perm[x]
+    int tx = r;
+    for (int j = 0; j < P; j++) if (perm[(size_t)j] == r) { tx = j; break; }
+    flat_rs_block(b, a, src, ds.d, rc, flat_leaves(P, steps, tx, [&](int x, int s) { return pi(x, s, P); }));
+    return;
+  }
   b.tmp(T0, count); b.tmp(T1, count);  // recv_buf, result_buf
   b.copy(src, 0, T1, 0, count);
   int w = P >> 1;
@@ -796,6 +902,17 @@ void rs_bine_remap(Builder &b, const PlanArgs &a, bool permute) {
   Displs ds(rc);
   const uint64_t count = ds.total;
   const int src = a.in_place ? RB : SB;
+  if (flat_rs_fits(a)) {
+    // permute: rank x computes block x with tree T(x); send: rank x computes
+    // block remap(x) and sends it to rank remap(x), so rank y's block y has
+    // the tree of remap^-1(y)
+    int tx = r;
+    if (!permute)
+      for (int j = 0; j < P; j++) if ((int)remap_rank((uint32_t)P, (uint32_t)j) == r) { tx = j; break; }
+    const auto leaves = flat_leaves(P, log2_ceil(P), tx, [&](int x, int s) { return nb_partner(x, 1 << s, P); });
+    flat_rs_block(b, a, src, ds.d, rc, leaves);
+    return;
+  }
   b.tmp(T0, count); b.tmp(T1, count + ds.maxc);  // tmpbuf, resbuf
   if (!permute) b.copy(src, 0, T1, 0, count);
   else
@@ -942,9 +1059,10 @@ void rd_bine_bdw(Builder &b, const PlanArgs &a) {
   const int rem = (int)(n % (uint64_t)P);
   const int src = (a.in_place && r == 0) ? RB : SB;
   const int res = r == 0 ? RB : T1;
+  const bool flat = flat_rs_fits(a);
   b.tmp(T0, n);
   if (r != 0) b.tmp(T1, n);
-  b.copy(src, 0, res, 0, n);
+  if (!flat) b.copy(src, 0, res, 0, n);
   const int me = (int)remap_rank((uint32_t)P, (uint32_t)r);
   std::vector<uint64_t> ri(steps + 1), si(steps + 1), rc(steps + 1), sc(steps + 1);
   auto first = [&](int blk) { return cpr * (uint64_t)blk + (uint64_t)std::min(blk, rem); };
@@ -960,9 +1078,20 @@ void rd_bine_bdw(Builder &b, const PlanArgs &a) {
     si[step] = first(sbf); sc[step] = span(sbf, sbl);
     ri[step] = first(rbf); rc[step] = span(rbf, rbl);
     const bool pipe = sc[step] > 0 && rc[step] > 0;
-    b.send(partner, res, si[step], sc[step]); b.recv(partner, T0, ri[step], rc[step]); b.end(pipe);
-    b.reduce(T0, ri[step], res, ri[step], rc[step], pipe);
+    if (!flat) {
+      b.send(partner, res, si[step], sc[step]); b.recv(partner, T0, ri[step], rc[step]); b.end(pipe);
+      b.reduce(T0, ri[step], res, ri[step], rc[step], pipe);
+    }
     mask <<= 1; inv >>= 1; step++;
+  }
+  if (flat && steps >= 1) {  // rank x computes block remap(x)
+    std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
+    for (int x = 0; x < P; x++) {
+      const int mx = (int)remap_rank((uint32_t)P, (uint32_t)x);
+      boff[(size_t)x] = first(mx); bcnt[(size_t)x] = span(mx, mx);
+    }
+    const auto leaves = flat_leaves(P, steps, r, [&](int x, int s) { return nb_partner(x, 1 << s, P); });
+    flat_rs(b, a, src, boff, bcnt, leaves, res, boff[(size_t)r]);
   }
   if (a.flat_ag && steps >= 1) {
     // flat gather: every rank sends its reduced block straight to the root

@@ -122,6 +122,7 @@ Plan make_tree_plan(const PlanArgs &a) {
     while (sig[v] != a.rank) v++;
     PlanArgs b = a;
     b.flat_ag = false;  // instances keep their own (mirrored) allgather
+    b.flat_rs = false;  // and their own halving steps
     b.rank = v;
     Mapper m;
     if (allreduce) {

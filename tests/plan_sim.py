@@ -27,11 +27,11 @@ class PlanError(AssertionError):
     pass
 
 
-def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, flat_ag=False, **kw):
+def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, flat_ag=False, flat_rs=False, **kw):
     """The executor's issue schedule (pico_amd.schedule) flattened back into a
     primitive list in issue order, one exchange group per op."""
     ops, _, _, info = pico_amd.schedule(coll, algo, P, r, chunk_bytes=chunk_bytes, relay_min_bytes=relay,
-                                        info=True, trees=trees, flat_ag=flat_ag, **kw)
+                                        info=True, trees=trees, flat_ag=flat_ag, flat_rs=flat_rs, **kw)
     out = []
     for i, o in enumerate(ops):
         for p in o["prims"]:
@@ -42,7 +42,7 @@ def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, flat_ag
 
 
 def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_place=False,
-        rbufs=None, chunk_bytes=None, relay=0, trees=False, flat_ag=False):
+        rbufs=None, chunk_bytes=None, relay=0, trees=False, flat_ag=False, flat_rs=False):
     """chunk_bytes != None: run the executor's chunked issue schedule instead of
     the plan itself (same semantics when ops run in issue order)."""
     P = len(sbufs)
@@ -54,6 +54,7 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
                                    segsize=segsize, in_place=in_place)
         if chunk_bytes is not None:
             prims, info = scheduled_prims(coll, algo, P, r, chunk_bytes, relay=relay, trees=trees, flat_ag=flat_ag,
+                                          flat_rs=flat_rs,
                                           count=count, rcounts=rcounts, root=root,
                                     esz=esz, segsize=segsize, in_place=in_place)
         plans.append(prims)
@@ -107,6 +108,19 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             b = view(r, p["aux_buf"], p["aux_off"], n).copy()
             O.reduce_local(np.ascontiguousarray(view(r, p["src_buf"], p["src_off"], n)), b, dtype, op)
             view(r, p["dst_buf"], p["dst_off"], n)[:] = b
+        elif p["type"] == "REDUCE_TREE":
+            # leaf `pos` = aux, the k-th other leaf = src + k*n; level by level
+            # v[i] = v[i] (op) v[i+w], left operand = inout (MPI_Reduce_local(in=v[i+w], inout=v[i]))
+            nl, pos = p["peer"], p["pos"]
+            others = iter(range(nl - 1))
+            v = [view(r, p["aux_buf"], p["aux_off"], n).copy() if j == pos else
+                 view(r, p["src_buf"], p["src_off"] + next(others) * n, n).copy() for j in range(nl)]
+            w = 1
+            while w < nl:
+                for i in range(0, nl, 2 * w):
+                    O.reduce_local(np.ascontiguousarray(v[i + w]), v[i], dtype, op)
+                w *= 2
+            view(r, p["dst_buf"], p["dst_off"], n)[:] = v[0]
 
     def try_transfer(key):
         moved = False

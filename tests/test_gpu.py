@@ -317,6 +317,117 @@ def test_flat_allgather_bit_exact(dev, P):
     assert not bad, bad[:8]
 
 
+def _host_tree(leaves, dtype, op):
+    """the reduction tree on the host with the oracle's MPI_Reduce_local:
+    level by level v[i] = v[i] (op) v[i + w], v[i] = inout"""
+    v = [np.array(x).copy() for x in leaves]
+    w = 1
+    while w < len(v):
+        for i in range(0, len(v), 2 * w):
+            O.reduce_local(np.ascontiguousarray(v[i + w]), v[i], dtype, op)
+        w *= 2
+    return v[0]
+
+
+@pytest.mark.parametrize("nl", [2, 4, 8, 16])
+@pytest.mark.parametrize("dtype", ALL_DT)
+def test_reduce_tree_kernel_bit_exact(dev, nl, dtype):
+    """bine_reduce_tree (the flat reduce-scatter's fused kernel) vs the oracle's
+    pairwise MPI_Reduce_local tree: every op, vector body + head/tail, and
+    leaves not co-aligned mod 16 B (scalar path)"""
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for op in ("sum", "prod", "max", "min"):
+        for n, shift in ((100003, 0), (4096, 0), (3, 0), (5001, esz if esz < 16 else 0)):
+            host = [O.fill(dtype, n, 300 + j) for j in range(nl)]
+            want = _host_tree(host, dtype, op)
+            leaves = []
+            for j, h in enumerate(host):
+                t = to_dev(h, pad=16 + shift)
+                if shift and j % 2:  # odd leaves one element off the others' 16-B phase
+                    t2 = torch.zeros_like(t)
+                    t2[shift:shift + h.nbytes] = t[:h.nbytes]
+                    t = t2[shift:]
+                leaves.append(t)
+            out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
+            assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
+            torch.cuda.synchronize()
+            assert sha(from_dev(out, dtype, n)) == sha(want), (op, n, shift)
+
+
+def test_reduce_tree_special_values(dev):
+    """NaN / inf / -0 / denormals keep MPICH's operand-order semantics inside
+    the fused tree (the same selects and IEEE adds as the pairwise kernel):
+    bit-exact with one NaN encoding (as test_reduce_local_special_values);
+    when NaNs of both signs meet in one add the two ISAs may return either
+    input NaN, so with mixed-sign NaNs the check is value-level (NaN where
+    the host has NaN, bits elsewhere)"""
+    specials = [np.nan, np.inf, -np.inf, 0.0, -0.0, 1e-40, -1e-40, 1.0, -1.0, 3.4e38, -3.4e38]
+    rng = np.random.default_rng(7)
+    for mixed in (False, True):
+        vals = np.array(specials + ([-np.nan] if mixed else []), np.float32)
+        host = [rng.choice(vals, 4099).astype(np.float32) for _ in range(8)]
+        for op in ("sum", "prod", "max", "min"):
+            want = _host_tree(host, "float", op)
+            out = torch.zeros(4099 * 4 + 64, dtype=torch.uint8, device="cuda:0")
+            assert pico_amd.reduce_tree([to_dev(h) for h in host], out, 4099, "float", op) == 0
+            torch.cuda.synchronize()
+            got = from_dev(out, "float", 4099)
+            if not mixed:
+                assert sha(got) == sha(want), op
+            else:
+                nan = np.isnan(want)
+                assert np.array_equal(np.isnan(got), nan), op
+                assert got[~nan].tobytes() == want[~nan].tobytes(), op
+
+
+FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
+           ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
+           ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"), ("reduce", "bine_bdw")]
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_flat_reduce_scatter_bit_exact(dev, P):
+    """flat reduce-scatter phase (one all-peers exchange, one fused tree per
+    chunk) on the device: the reference's bits for every algorithm it applies
+    to, chunked and not, in and out of place, with the flat allgather too"""
+    bad = []
+    cs = comms(P)
+    try:
+        for c in cs:
+            c.set_flat_rs(True)
+        for coll, algo in FLAT_RS:
+            for dt, n in (("float", 100003), ("int64", 4099), ("double", 7)):
+                for chunk in (0, 4096):
+                    for flat_ag in (False, True):
+                        for c in cs:
+                            c.set_chunk(chunk)
+                            c.set_flat_ag(flat_ag)
+                        for ip in (False, True):
+                            if coll == "allreduce":
+                                sb = O.inputs(dt, n, P)
+                                want, _ = O.allreduce(algo, sb, dt, segsize=4096)
+                                outs, st = run_loopback(coll, algo, sb, dt, segsize=4096, in_place=ip)
+                            elif coll == "reduce_scatter":
+                                rc = [n // P + 1] * P if algo == "bine_permute_remap" else \
+                                    [n // P + (i % 3) for i in range(P)]
+                                sb = O.inputs(dt, sum(rc), P)
+                                want, _ = O.reduce_scatter(algo, sb, rc, dt)
+                                outs, st = run_loopback(coll, algo, sb, dt, rcounts=rc, in_place=ip)
+                            else:
+                                sb = O.inputs(dt, n, P)
+                                w, _ = O.reduce(algo, sb, dt)
+                                outs, st = run_loopback(coll, algo, sb, dt, in_place=ip)
+                                want, outs = [w], outs[:1]
+                            if any(st) or any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                                bad.append((coll, algo, dt, chunk, flat_ag, ip, st))
+    finally:
+        for c in cs:
+            c.set_flat_rs(False)
+            c.set_flat_ag(False)
+            c.set_chunk(0)
+    assert not bad, bad[:8]
+
+
 @pytest.mark.parametrize("algo", list(pico_amd.ALGOS["allreduce"]))
 def test_in_place_allreduce(dev, algo):
     P = 4

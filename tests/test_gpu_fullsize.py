@@ -73,6 +73,7 @@ def _mode(cs, mode):
         c.set_relay(256 << 10 if "relay" in mode else 0)  # bench.py RELAY_MIN_BYTES
         c.set_trees(mode == "trees")
         c.set_flat_ag("flat" in mode)
+        c.set_flat_rs("flatrs" in mode)
 
 
 def _device_inputs(dtype, tdt, n):
@@ -98,7 +99,7 @@ def c3_oracle():
     return sb, [host_checksum(w) for w in want]
 
 
-@pytest.mark.parametrize("mode", ["direct", "relay", "trees", "flat", "relay+flat"])
+@pytest.mark.parametrize("mode", ["direct", "relay", "trees", "flat", "relay+flat", "flatrs+flat"])
 def test_c3_allreduce_fullsize(dev, comms, c3_oracle, mode):
     sb_host, digests = c3_oracle
     assert len(set(digests)) == 1  # allreduce: every rank holds the same bits
@@ -120,7 +121,7 @@ def test_c3_allreduce_fullsize(dev, comms, c3_oracle, mode):
     assert got == expect
 
 
-@pytest.mark.parametrize("mode", ["direct", "relay", "trees"])
+@pytest.mark.parametrize("mode", ["direct", "relay", "trees", "flatrs+flat"])
 def test_c5_int64_allreduce_fullsize(dev, comms, mode):
     sb = _device_inputs("int64", torch.int64, C5_N)
     want = sb[0].clone()
@@ -150,7 +151,7 @@ def test_c5_double_allreduce_fullsize(dev, comms):
     assert [pico_amd.checksum(b, C5_N, "double") for b in rb] == [expect] * P
 
 
-@pytest.mark.parametrize("mode", ["direct", "relay", "trees"])
+@pytest.mark.parametrize("mode", ["direct", "relay", "trees", "flatrs"])
 def test_c4_reduce_scatter_fullsize(dev, comms, mode):
     per = C4_N // P
     g = torch.Generator(device="cuda:0")

@@ -1,6 +1,6 @@
 """The RCCL transport in real processes: every algorithm of every family
 (allreduce 8, reduce_scatter 9, reduce 2, allgather 12) x fp32 / int64 / int8
-x {direct, 4 KiB pipelining chunks, multi-link relay}, 4 ranks sharing the one
+x {direct, 4 KiB pipelining chunks, multi-link relay, flat phases}, 4 ranks sharing the one
 GPU of the test box (distinct NCCL_HOSTIDs, RCCL's socket transport), checked
 bit for bit against the oracle on every rank (tools/rccl_matrix.py).  The
 8-rank run of the same matrix is in profiles/r1_rccl_matrix_1gpu.txt."""
@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_rccl_matrix_4_ranks():
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_matrix.py"), "4"], env=env,
-                       capture_output=True, text=True, timeout=110)
+                       capture_output=True, text=True, timeout=150)
     tail = "\n".join(r.stdout.splitlines()[-12:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=4" in r.stdout

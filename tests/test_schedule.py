@@ -376,3 +376,89 @@ def test_flat_gather_reduce_bdw_matches_oracle(P):
             ops, cj, fw = pico_amd.schedule("reduce", "bine_bdw", P, rank, count=n, esz=8, chunk_bytes=256,
                                             flat_ag=True)
             check_race_free(ops, cj, fw, False)
+
+
+# ---- flat reduce-scatter phase ----------------------------------------------------
+
+FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
+           ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
+           ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"), ("reduce", "bine_bdw")]
+
+
+def _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag):
+    if coll == "allreduce":
+        sb = O.inputs(dtype, n, P)
+        want, _ = O.allreduce(algo, sb, dtype, op=op, segsize=256)
+        got = plan_sim.run(coll, algo, sb, dtype, op=op, segsize=256, chunk_bytes=chunk, flat_rs=True,
+                           flat_ag=flat_ag, in_place=in_place)
+        return all(np.array_equal(got[r], want[r]) for r in range(P))
+    if coll == "reduce_scatter":
+        rc = [n // P + 1] * P if algo == "bine_permute_remap" else [n // P + (i % 3) for i in range(P)]
+        sb = O.inputs(dtype, sum(rc), P)
+        want, _ = O.reduce_scatter(algo, sb, rc, dtype, op=op)
+        got = plan_sim.run(coll, algo, sb, dtype, op=op, rcounts=rc, chunk_bytes=chunk, flat_rs=True,
+                           in_place=in_place)
+        return all(np.array_equal(got[r], want[r]) for r in range(P))
+    sb = O.inputs(dtype, n, P)
+    want, _ = O.reduce(algo, sb, dtype, op=op)
+    got = plan_sim.run(coll, algo, sb, dtype, op=op, chunk_bytes=chunk, flat_rs=True, flat_ag=flat_ag,
+                       in_place=in_place)
+    return np.array_equal(got[0], want)
+
+
+@pytest.mark.parametrize("coll,algo", FLAT_RS)
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+def test_flat_reduce_scatter_matches_oracle(coll, algo, P):
+    """one all-peers exchange + the reference's reduction tree per block
+    (REDUCE_TREE) gives the reference's bits: fp and int, SUM / MAX / PROD,
+    ragged blocks, chunked, in place, with and without the flat allgather"""
+    for dtype, n, op in (("float", 997, "sum"), ("int64", 64 * P + 5, "sum"), ("double", 3, "sum"),
+                         ("float", 1001, "max"), ("int32", 515, "prod")):
+        for chunk in (0, 64):
+            for in_place in (False, True):
+                for flat_ag in ((False, True) if coll != "reduce_scatter" else (False,)):
+                    assert _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag), \
+                        (dtype, n, op, chunk, in_place, flat_ag)
+
+
+@pytest.mark.parametrize("coll,algo", FLAT_RS)
+@pytest.mark.parametrize("P", [4, 8])
+def test_flat_reduce_scatter_race_free_and_one_hop(coll, algo, P):
+    """race-free under chunking; every exchange of the reduce-scatter phase
+    talks to all P-1 peers; one REDUCE_TREE of P leaves per chunk"""
+    for rank in range(P):
+        for in_place in (False, True):
+            kw = dict(count=4099, esz=4, segsize=256)
+            if coll == "reduce_scatter":
+                kw = dict(rcounts=[513 + (i % 2) * (algo != "bine_permute_remap") for i in range(P)], esz=4)
+            ops, cj, fw = pico_amd.schedule(coll, algo, P, rank, chunk_bytes=1024, in_place=in_place, flat_rs=True,
+                                            **kw)
+            check_race_free(ops, cj, fw, in_place)
+            trees = [p for o in ops for p in o["prims"] if p["type"] == "REDUCE_TREE"]
+            assert trees and all(p["peer"] == P for p in trees)
+            assert not any(p["type"] in ("REDUCE", "REDUCE3") for o in ops for p in o["prims"])
+            first = [o for o in ops if o["xchg"]][0]
+            assert {p["peer"] for p in first["prims"] if p["type"] == "SEND"} == set(range(P)) - {rank}
+
+
+def test_flat_reduce_scatter_not_applied_where_it_does_not_fit():
+    """non-power-of-two P and the other algorithms keep their literal schedule"""
+    for coll, algo, P in (("allreduce", "bine_bdw_remap_segmented", 6), ("allreduce", "ring", 8),
+                          ("allreduce", "rabenseifner", 8), ("reduce_scatter", "ring", 8)):
+        kw = dict(rcounts=[100] * P) if coll == "reduce_scatter" else dict(count=4099)
+        a = pico_amd.schedule(coll, algo, P, 1, esz=4, chunk_bytes=1024, segsize=256, **kw)
+        b = pico_amd.schedule(coll, algo, P, 1, esz=4, chunk_bytes=1024, segsize=256, flat_rs=True, **kw)
+        assert a == b
+
+
+def test_flat_reduce_scatter_link_time_model():
+    """P = 8, remap allreduce in units of S / link: flat RS + flat AG = 0.125 +
+    0.125 = 0.25 -- the multi-tree mode's link time, but bit-identical to the
+    reference; C4's reduce-scatter 0.125 (vs 0.875 literal)"""
+    n = 1 << 20
+    kw = dict(count=n, esz=4, chunk_bytes=1 << 16)
+    assert abs(_link_time("allreduce", "bine_bdw_remap", 8, flat_rs=True, flat_ag=True, **kw) / n - 0.25) < 0.01
+    assert abs(_link_time("allreduce", "bine_bdw_remap", 8, flat_rs=True, **kw) / n - 1.0) < 0.01
+    rk = dict(rcounts=[n // 8] * 8, esz=4, chunk_bytes=1 << 16)
+    assert abs(_link_time("reduce_scatter", "bine_permute_remap", 8, **rk) / n - 0.875) < 0.01
+    assert abs(_link_time("reduce_scatter", "bine_permute_remap", 8, flat_rs=True, **rk) / n - 0.125) < 0.01

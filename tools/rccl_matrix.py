@@ -10,7 +10,7 @@ stream / event hand-offs, chunked pipelines, relay routes) in real processes;
 it says nothing about xGMI speed.
 
 For each transport setting (direct; small pipelining chunks; multi-link relay;
-relay + flat allgather; the same on a non-default caller stream with every
+relay + flat allgather; flat reduce-scatter + flat allgather; the same on a non-default caller stream with every
 collective run twice, the second time into a zeroed output)
 it runs all 8 allreduce, 9 reduce_scatter, 2 reduce and 12 allgather
 algorithms on fp32 / int64 / int8 at odd sizes, and checks outputs bit for bit
@@ -25,9 +25,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CASES = (("float", 4099), ("int64", 1001), ("int8", 333))
-# (name, relay_min_bytes, chunk_bytes, flat allgather, run each collective twice on a side stream)
+# (name, relay_min_bytes, chunk_bytes, flat phases (1: allgather, 2: reduce-scatter), run each
+# collective twice on a side stream)
 SETTINGS = (("direct", 0, 0, 0, 0), ("chunk4KiB", 0, 4096, 0, 0), ("relay", 64, 1024, 0, 0),
-            ("relay+flat", 64, 1024, 1, 0), ("side-stream x2", 64, 1024, 1, 1))
+            ("relay+flat", 64, 1024, 1, 0), ("flatrs+flat", 0, 1024, 3, 0), ("side-stream x2", 64, 1024, 1, 1))
 
 
 def worker(rank, P, port, q):
@@ -84,7 +85,8 @@ def worker(rank, P, port, q):
     for sname, relay, chunk, flat, twice in SETTINGS:
         comm.set_relay(relay)
         comm.set_chunk(chunk)
-        comm.set_flat_ag(bool(flat))
+        comm.set_flat_ag(bool(flat & 1))
+        comm.set_flat_rs(bool(flat & 2))
         ctx = torch.cuda.stream(side) if twice else contextlib.nullcontext()
         ctx.__enter__()
         for dt, n in CASES:
