@@ -373,61 +373,99 @@ __device__ __forceinline__ T tree_scalar(const TreeArgs &t, size_t i) {
   return v[0];
 }
 
-template <typename T, int OP, int NL, int U>
-__global__ __launch_bounds__(kBlock) void k_reduce_tree(TreeArgs t) {
+// Leaves are loaded and reduced in groups of G = min(NL, 8): positions
+// [8g, 8g + 8) form a complete subtree of the reference's tree (levels w = 1,
+// 2, 4), and the group results combine by the upper levels (w = 8) exactly
+// as the leaves would.  U vectors of each leaf per lane in flight (tree_nl).  One tile of kBlock * U vectors per workgroup, no
+// grid-stride loop, unguarded loads in every full tile (measured on MI355X,
+// tools/tree_variants.hip: a grid-strided form with a guard on every load ran
+// 31 us vs 24.5 us for 8 x 16 MiB).
+template <typename T, int OP, int NL, int U, bool GUARD>
+__device__ __forceinline__ void tree_tile(const u32x4 *const *lp, u32x4 *vo, size_t base, size_t nvec) {
+  constexpr int G = NL < 8 ? NL : 8, NG = NL / G;
+  u32x4 part[U][NG];
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    u32x4 v[U][G];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * kBlock;
+      if (!GUARD || i < nvec) {
+        // own leaf: plain load; received leaves: read once, non-temporal (two
+        // separate statements: a select between the two loads of one address
+        // is folded into one plain load)
+        if (g == 0) v[u][0] = lp[0][i];
+#pragma unroll
+        for (int j = g == 0 ? 1 : 0; j < G; j++) v[u][j] = __builtin_nontemporal_load(lp[g * G + j] + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int w = 1; w < G; w <<= 1)
+#pragma unroll
+        for (int j = 0; j < G; j += 2 * w) v[u][j] = apply16<T, OP>(v[u][j], v[u][j + w]);
+      part[u][g] = v[u][0];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+#pragma unroll
+    for (int w = 1; w < NG; w <<= 1)
+#pragma unroll
+      for (int g = 0; g < NG; g += 2 * w) part[u][g] = apply16<T, OP>(part[u][g], part[u][g + w]);
+    const size_t i = base + (size_t)u * kBlock;
+    if (!GUARD || i < nvec) vo[i] = part[u][0];
+  }
+}
+
+// elements before the 16-B aligned body and after its last vector (one
+// workgroup; launched only when there are any: keeping this code out of the
+// body kernel keeps its register count -- and occupancy -- at the body's own)
+template <typename T, int OP, int NL>
+__global__ __launch_bounds__(kBlock) void k_reduce_tree_edges(TreeArgs t) {
   constexpr size_t V = 16 / sizeof(T);
   T *out = (T *)t.out;
-  if (!t.vec) {  // operands not co-aligned: scalar grid-stride
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < t.n; i += (size_t)gridDim.x * kBlock)
-      out[i] = tree_scalar<T, OP, NL>(t, i);
-    return;
-  }
-  if (blockIdx.x == 0) {
-    for (size_t i = threadIdx.x; i < t.head; i += kBlock) out[i] = tree_scalar<T, OP, NL>(t, i);
-    for (size_t i = t.head + t.nvec * V + threadIdx.x; i < t.n; i += kBlock) out[i] = tree_scalar<T, OP, NL>(t, i);
-  }
+  for (size_t i = threadIdx.x; i < t.head; i += kBlock) out[i] = tree_scalar<T, OP, NL>(t, i);
+  for (size_t i = t.head + t.nvec * V + threadIdx.x; i < t.n; i += kBlock) out[i] = tree_scalar<T, OP, NL>(t, i);
+}
+
+template <typename T, int OP, int NL, int U>
+__global__ __launch_bounds__(kBlock) void k_reduce_tree(TreeArgs t) {
+  T *out = (T *)t.out;
+  // leaf base pointers into registers once (loading them from the kernel
+  // arguments inside guarded loads put an s_waitcnt in front of every load)
+  const u32x4 *lp[NL];
+#pragma unroll
+  for (int j = 0; j < NL; j++) lp[j] = reinterpret_cast<const u32x4 *>((const T *)t.leaf[j] + t.head);
   u32x4 *vo = reinterpret_cast<u32x4 *>(out + t.head);
-  const size_t tile = (size_t)kBlock * U;
-  for (size_t base = (size_t)blockIdx.x * tile + threadIdx.x; base < t.nvec; base += (size_t)gridDim.x * tile) {
-    u32x4 v[U][NL];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const size_t i = base + (size_t)u * kBlock;
-      if (i < t.nvec) {
-#pragma unroll
-        for (int j = 0; j < NL; j++) {
-          const u32x4 *p = reinterpret_cast<const u32x4 *>((const T *)t.leaf[j] + t.head) + i;
-          v[u][j] = j == 0 ? *p : __builtin_nontemporal_load(p);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const size_t i = base + (size_t)u * kBlock;
-      if (i < t.nvec) {
-#pragma unroll
-        for (int w = 1; w < NL; w <<= 1)
-#pragma unroll
-          for (int j = 0; j < NL; j += 2 * w) v[u][j] = apply16<T, OP>(v[u][j], v[u][j + w]);
-        vo[i] = v[u][0];
-      }
-    }
-  }
+  const size_t base = (size_t)blockIdx.x * kBlock * U + threadIdx.x;
+  if ((size_t)(blockIdx.x + 1) * kBlock * U <= t.nvec) tree_tile<T, OP, NL, U, false>(lp, vo, base, t.nvec);
+  else tree_tile<T, OP, NL, U, true>(lp, vo, base, t.nvec);
+}
+
+// operands not co-aligned mod 16 B: scalar grid-stride
+template <typename T, int OP, int NL>
+__global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeArgs t) {
+  T *out = (T *)t.out;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < t.n; i += (size_t)gridDim.x * kBlock)
+    out[i] = tree_scalar<T, OP, NL>(t, i);
 }
 
 template <typename T, int OP, int NL>
 static hipError_t tree_nl(TreeArgs &t, hipStream_t st) {
-  constexpr int U = NL <= 4 ? 4 : NL == 8 ? 2 : 1;
-  size_t blocks;
+  constexpr int U = NL == 2 ? 8 : NL <= 8 ? 4 : 2;  // tools/tree_variants.hip: <8,4> 25.2 us, <8,2> 26.5 us
   if (t.vec) {
+    constexpr size_t V = 16 / sizeof(T);
     const size_t tiles = (t.nvec + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    blocks = tiles ? tiles : 1;
+    if (tiles) hipLaunchKernelGGL((k_reduce_tree<T, OP, NL, U>), dim3((unsigned)tiles), dim3(kBlock), 0, st, t);
+    if (t.head || t.head + t.nvec * V < t.n)
+      hipLaunchKernelGGL((k_reduce_tree_edges<T, OP, NL>), dim3(1), dim3(kBlock), 0, st, t);
   } else {
-    blocks = (t.n + kBlock * 4 - 1) / (kBlock * 4);
+    size_t blocks = (t.n + kBlock * 4 - 1) / (kBlock * 4);
     if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL((k_reduce_tree_scalar<T, OP, NL>), dim3((unsigned)blocks), dim3(kBlock), 0, st, t);
   }
-  if (blocks > 65536) blocks = 65536;  // grid-strided beyond
-  hipLaunchKernelGGL((k_reduce_tree<T, OP, NL, U>), dim3((unsigned)blocks), dim3(kBlock), 0, st, t);
   return hipGetLastError();
 }
 
