@@ -270,6 +270,36 @@ def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream
                   steps, warmup)
 
 
+def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
+    """One extra collective (outside the timed region) with per-op timing
+    events (bine_comm_set_profile): where the time of this rank goes -- busy
+    time of the comm stream (exchanges) and of the compute stream (reductions),
+    their span, and the exchange ops' egress rates."""
+    comm.set_profile(True)
+    try:
+        pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
+        torch.cuda.synchronize()
+        comm.synchronize()
+        ops = comm.profile()
+    finally:
+        comm.set_profile(False)
+    if not ops:
+        return {}
+    span = max(o["start_ms"] + o["ms"] for o in ops)
+    xs = [o for o in ops if o["xchg"]]
+    ls = [o for o in ops if not o["xchg"]]
+    out = {"ops": len(ops), "span_ms": round(span, 4),
+           "exchange_busy_ms": round(sum(o["ms"] for o in xs), 4),
+           "local_busy_ms": round(sum(o["ms"] for o in ls), 4),
+           "exchanges": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4), "peers": o["nprims"],
+                          "egress_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 2) if o["ms"] > 0 else None}
+                         for o in xs[:24]],
+           "local": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4),
+                      "hbm_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 1) if o["ms"] > 0 else None}
+                     for o in ls[:24]]}
+    return out
+
+
 def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev):
     """BASELINE configs C1, C4 and C5 with the transport chosen for C3
     (reported beside the headline; a few steps each)"""
@@ -435,6 +465,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     chosen, chunk = best
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
     issue_ms = _timed.issue_ms
+    steps_prof = _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream)
     extra = _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     probe = _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
     S = nelem * 4
@@ -474,6 +505,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
                        "chunk_bytes": chunk,
                        "host_issue_ms_per_step": round(issue_ms, 4),
+                       "step_profile_rank0": steps_prof,
                        "transport_trials_ms": {f"{m}/{ch >> 20}MiB": round(v, 4) for (m, ch), v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": extra,

@@ -207,6 +207,26 @@ int bine_comm_set_flat_ag(bine_comm_t comm, int on);
  * (BINE_FLAT_RS=1 turns it on); collective. */
 int bine_comm_set_flat_rs(bine_comm_t comm, int on);
 
+/* Per-op device timing ("hipEvents per step"): with profiling on, every op
+ * of a collective's issue schedule -- an exchange group on the comm stream or
+ * a local primitive on the caller's stream -- is bracketed by two timing
+ * events on its stream (single-stream small collectives are not profiled).
+ * bine_comm_profile() waits for the latest collective's events and fills one
+ * entry per op: kind, primitives, bytes (exchange: bytes this rank sends;
+ * local: algorithmic HBM bytes), start relative to the first op's start and
+ * duration.  Returns the number of ops (may exceed cap) or -status.  Off by
+ * default (the events cost host time per op).  BINE_ROCTX=1 additionally
+ * brackets every collective and every issued op with a roctx range. */
+typedef struct {
+  int32_t xchg;
+  int32_t nprims;
+  uint64_t bytes;
+  float start_ms;
+  float ms;
+} bine_op_time_t;
+int bine_comm_set_profile(bine_comm_t comm, int on);
+int64_t bine_comm_profile(bine_comm_t comm, bine_op_time_t *out, int64_t cap);
+
 /* ---- collectives (device pointers, stream-ordered) ------------------------- */
 /* allreduce_* (libbine.h:30-37).  `segsize` plays bine_allreduce_segsize
  * (libbine.h:28) for BINE_AR_BINE_BDW_REMAP_SEGMENTED and is the pipelining

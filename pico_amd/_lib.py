@@ -50,6 +50,11 @@ class SchedEntry(ctypes.Structure):
     _fields_ = [("op", ctypes.c_int32), ("xchg", ctypes.c_int32), ("wait", ctypes.c_int64), ("prim", Prim)]
 
 
+class OpTime(ctypes.Structure):
+    _fields_ = [("xchg", ctypes.c_int32), ("nprims", ctypes.c_int32), ("bytes", ctypes.c_uint64),
+                ("start_ms", ctypes.c_float), ("ms", ctypes.c_float)]
+
+
 PRIM_NAMES = {1: "SEND", 2: "RECV", 3: "REDUCE", 4: "REDUCE3", 5: "COPY", 6: "REDUCE_TREE"}
 
 
@@ -114,6 +119,8 @@ def lib():
         "bine_comm_set_chunk": ([vp, sz], i),
         "bine_comm_set_flat_ag": ([vp, i], i),
         "bine_comm_set_flat_rs": ([vp, i], i),
+        "bine_comm_set_profile": ([vp, i], i),
+        "bine_comm_profile": ([vp, vp, ctypes.c_int64], ctypes.c_int64),
         "bine_exchange": ([vp, i, vp, vp, vp, i, vp, vp, vp, vp], i),
         "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int64), vp], ctypes.c_int64),

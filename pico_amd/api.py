@@ -143,6 +143,22 @@ class Comm:
         reduction tree in one kernel; bit-identical); collective."""
         check(lib().bine_comm_set_flat_rs(self.handle, int(on)), "bine_comm_set_flat_rs")
 
+    def set_profile(self, on: bool) -> None:
+        """Per-op device timing of the following collectives (bine_comm_set_profile)."""
+        check(lib().bine_comm_set_profile(self.handle, int(on)), "bine_comm_set_profile")
+
+    def profile(self):
+        """Per-op timing of the latest profiled collective: list of
+        {"xchg", "nprims", "bytes", "start_ms", "ms"} in issue order."""
+        n = lib().bine_comm_profile(self.handle, None, 0)
+        if n < 0:
+            raise BineError(int(-n), "bine_comm_profile")
+        arr = (_lib.OpTime * max(int(n), 1))()
+        n = lib().bine_comm_profile(self.handle, arr, n)
+        if n < 0:
+            raise BineError(int(-n), "bine_comm_profile")
+        return [{f: getattr(arr[k], f) for f, _ in _lib.OpTime._fields_} for k in range(int(n))]
+
     def set_chunk(self, nbytes: int) -> None:
         """Pipelining chunk in bytes (0 = default 16 MiB); never changes a bit; collective."""
         check(lib().bine_comm_set_chunk(self.handle, nbytes), "bine_comm_set_chunk")

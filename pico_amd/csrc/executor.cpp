@@ -17,6 +17,7 @@
 //   * workspace (TMP0..2), plans and their schedules are cached per communicator.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <atomic>
@@ -207,6 +208,11 @@ struct bine_comm {
   size_t ev_next = 0;
   std::map<std::string, std::pair<bine::Plan, bine::Schedule>> plans;
   std::vector<hipEvent_t> op_ev;  // scratch of execute()
+  // per-op device timing of the latest collective (bine_comm_set_profile)
+  bool profile = false;
+  struct OpTime { hipEvent_t a = nullptr, b = nullptr; int xchg = 0, nprims = 0; uint64_t bytes = 0; };
+  std::vector<OpTime> prof;
+  size_t prof_n = 0;
   std::vector<bine::XSend> xs;
   std::vector<bine::XRecv> xr;
   std::mutex mu;
@@ -218,6 +224,10 @@ struct bine_comm {
     for (int t = 0; t < 4; t++)
       if (tmp[t]) (void)hipFree(tmp[t]);
     for (auto e : ev) (void)hipEventDestroy(e);
+    for (auto &p : prof) {
+      if (p.a) (void)hipEventDestroy(p.a);
+      if (p.b) (void)hipEventDestroy(p.b);
+    }
     if (stream) (void)hipStreamDestroy(stream);
     if (cstream) (void)hipStreamDestroy(cstream);
   }
@@ -239,6 +249,13 @@ static int comm_setup(bine_comm *c) {
   if (const char *e = getenv("BINE_FLAT_RS")) c->flat_rs = atoi(e) != 0;
   if (const char *e = getenv("BINE_SINGLE_STREAM_BYTES")) c->single_stream_bytes = (size_t)strtoull(e, nullptr, 10);
   return BINE_SUCCESS;
+}
+
+// BINE_ROCTX=1: roctx ranges around every collective and every issued op
+// (host timeline of rocprofv3 --marker-trace)
+static bool roctx_on() {
+  static const bool on = getenv("BINE_ROCTX") && atoi(getenv("BINE_ROCTX")) != 0;
+  return on;
 }
 
 // BINE_TRACE=1: one stderr line per issued op (debugging the issue sequence)
@@ -358,6 +375,11 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   }
   std::vector<hipEvent_t> &evs = c->op_ev;
   evs.resize(sc.ops.size());
+  const bool prof = c->profile;
+  if (prof) {
+    if (c->prof.size() < sc.ops.size()) c->prof.resize(sc.ops.size());
+    c->prof_n = sc.ops.size();
+  }
   std::vector<XSend> &sends = c->xs;
   std::vector<XRecv> &recvs = c->xr;
   for (size_t i = 0; i < sc.ops.size(); i++) {
@@ -367,6 +389,26 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       fprintf(stderr, "bine[%d] op %zu/%zu %s wait %lld prims %zu\n", c->rank, i, sc.ops.size(),
               o.xchg ? "xchg" : "local", (long long)o.wait, o.prims.size());
     if (o.wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
+    if (roctx_on()) {
+      char lbl[64];
+      snprintf(lbl, sizeof lbl, "bine op %zu %s (%zu prims)", i, o.xchg ? "exchange" : "local", o.prims.size());
+      roctxRangePushA(lbl);
+    }
+    if (prof) {
+      auto &pt = c->prof[i];
+      if (!pt.a) HIP_TRY(hipEventCreate(&pt.a));
+      if (!pt.b) HIP_TRY(hipEventCreate(&pt.b));
+      pt.xchg = o.xchg ? 1 : 0;
+      pt.nprims = (int)o.prims.size();
+      pt.bytes = 0;
+      for (const Prim &x : o.prims) {  // exchanges: bytes sent; local ops: algorithmic HBM bytes
+        if (x.type == BINE_PRIM_SEND) pt.bytes += x.count * esz;
+        else if (x.type == BINE_PRIM_REDUCE || x.type == BINE_PRIM_REDUCE3) pt.bytes += 3 * x.count * esz;
+        else if (x.type == BINE_PRIM_REDUCE_TREE) pt.bytes += (uint64_t)(x.peer + 1) * x.count * esz;
+        else if (x.type == BINE_PRIM_COPY) pt.bytes += 2 * x.count * esz;
+      }
+      HIP_TRY(hipEventRecord(pt.a, st));
+    }
     int rc = BINE_SUCCESS;
     if (o.xchg) {
       sends.clear();
@@ -381,6 +423,8 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       rc = run_local(o.prims, ptr, dtype, op, esz, K);
       if (rc) { set_err("local primitive failed (%s)", bine_status_string(rc)); return rc; }
     }
+    if (prof) HIP_TRY(hipEventRecord(c->prof[i].b, st));
+    if (roctx_on()) roctxRangePop();
     // an event of the pool may be re-recorded by a later op once the pool
     // wraps: any later record only delays a waiter, never lets it run early.
     // Ops nothing waits for record no event (host cost per op).
@@ -473,7 +517,14 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   uint64_t bytes = (uint64_t)a.count;
   for (int x : a.rcounts) bytes += (uint64_t)x;
   bytes *= a.esz;
-  return execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, bytes <= c->single_stream_bytes);
+  if (roctx_on()) {
+    char lbl[96];
+    snprintf(lbl, sizeof lbl, "bine %s P=%d count=%zu", bine_algo_name(a.algo), a.P, a.count);
+    roctxRangePushA(lbl);
+  }
+  rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, bytes <= c->single_stream_bytes);
+  if (roctx_on()) roctxRangePop();
+  return rc;
 }
 
 }  // namespace bine
@@ -860,6 +911,30 @@ int bine_comm_set_flat_ag(bine_comm_t c, int on) {
   std::lock_guard<std::mutex> g(c->mu);
   c->flat_ag = on != 0;
   return BINE_SUCCESS;
+}
+
+int bine_comm_set_profile(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->profile = on != 0;
+  c->prof_n = 0;
+  return BINE_SUCCESS;
+}
+
+int64_t bine_comm_profile(bine_comm_t c, bine_op_time_t *out, int64_t cap) {
+  if (!c) return -(int64_t)BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->prof_n == 0) return 0;
+  hipEvent_t first = c->prof[0].a;
+  for (size_t i = 0; i < c->prof_n && (int64_t)i < cap; i++) {
+    auto &pt = c->prof[i];
+    if (hipEventSynchronize(pt.b) != hipSuccess) return -(int64_t)BINE_ERR_HIP;
+    float ms = 0.f, st = 0.f;
+    if (hipEventElapsedTime(&ms, pt.a, pt.b) != hipSuccess || hipEventElapsedTime(&st, first, pt.a) != hipSuccess)
+      return -(int64_t)BINE_ERR_HIP;
+    out[i] = {pt.xchg, pt.nprims, pt.bytes, st, ms};
+  }
+  return (int64_t)c->prof_n;
 }
 
 int bine_comm_set_flat_rs(bine_comm_t c, int on) {

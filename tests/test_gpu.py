@@ -428,6 +428,44 @@ def test_flat_reduce_scatter_bit_exact(dev, P):
     assert not bad, bad[:8]
 
 
+def test_per_op_profile(dev):
+    """bine_comm_set_profile: one timed entry per op of the issue schedule
+    (exchanges with their send bytes, local ops with algorithmic HBM bytes),
+    starts ordered within each stream; results unchanged"""
+    P, n = 4, 1 << 20
+    cs = comms(P)
+    sb = O.inputs("float", n, P)
+    want, _ = O.allreduce("bine_bdw_remap", sb, "float")
+    try:
+        for c in cs:
+            c.set_profile(True)
+            c.set_flat_rs(True)
+            c.set_flat_ag(True)
+            c.set_chunk(1 << 20)
+        outs, st = run_loopback("allreduce", "bine_bdw_remap", sb, "float")
+        assert not any(st) and all(sha(o) == sha(w) for o, w in zip(outs, want))
+        for r, c in enumerate(cs):
+            ops = c.profile()
+            sched, _, _ = pico_amd.schedule("allreduce", "bine_bdw_remap", P, r, count=n, esz=4, chunk_bytes=1 << 20,
+                                            flat_rs=True, flat_ag=True)
+            assert len(ops) == len(sched)
+            for o, s in zip(ops, sched):
+                assert o["xchg"] == s["xchg"] and o["nprims"] == len(s["prims"]) and o["ms"] >= 0
+                if s["xchg"]:
+                    assert o["bytes"] == 4 * sum(p["count"] for p in s["prims"] if p["type"] == "SEND")
+                else:
+                    assert o["bytes"] == sum((p["peer"] + 1) * p["count"] * 4 for p in s["prims"])
+            for kind in (0, 1):
+                starts = [o["start_ms"] for o in ops if o["xchg"] == kind]
+                assert starts == sorted(starts)
+    finally:
+        for c in cs:
+            c.set_profile(False)
+            c.set_flat_rs(False)
+            c.set_flat_ag(False)
+            c.set_chunk(0)
+
+
 @pytest.mark.parametrize("algo", list(pico_amd.ALGOS["allreduce"]))
 def test_in_place_allreduce(dev, algo):
     P = 4
