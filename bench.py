@@ -234,7 +234,7 @@ def _bench_tree_kernel(torch, pico_amd, dev, stream, steps, warmup):
     torch.cuda.empty_cache()
     return {"kernel": "bine::k_reduce_tree<float,SUM,8>", "leaves": TREE_LEAVES, "elems_per_leaf": TREE_ELEMS,
             "us": round(us, 2), "algorithmic_bytes_per_launch": alg, "achieved_GBs": round(gbs, 1),
-            "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+            "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_reduce_tree")}
 
 
 def _timed(torch, dist, comm, stream, call, steps, warmup):
