@@ -428,6 +428,40 @@ def test_flat_reduce_scatter_bit_exact(dev, P):
     assert not bad, bad[:8]
 
 
+@pytest.mark.parametrize("P", [8, 16])
+def test_flat_reduce_scatter_ops_and_dtypes(dev, P):
+    """flat reduce-scatter + flat allgather for every operator and the narrow
+    integer types (the tree kernel's 16-element-per-vector paths), P = 8 and
+    P = 16 (16 leaves: two 8-leaf groups), with blocks of 0 and 1 element"""
+    bad = []
+    cs = comms(P)
+    try:
+        for c in cs:
+            c.set_flat_rs(True)
+            c.set_flat_ag(True)
+            c.set_chunk(4096)
+        for dt in ("int8", "uint16", "int32", "float", "double"):
+            for op in ("sum", "prod", "max", "min"):
+                for n in (P // 2, 4099):
+                    sb = O.inputs(dt, n, P)
+                    want, _ = O.allreduce("bine_bdw_remap", sb, dt, op=op)
+                    outs, st = run_loopback("allreduce", "bine_bdw_remap", sb, dt, op=op)
+                    if any(st) or any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                        bad.append(("allreduce", dt, op, n, st))
+                rc = [3 + (i % 2) for i in range(P)]
+                sb = O.inputs(dt, sum(rc), P)
+                want, _ = O.reduce_scatter("bine_static", sb, rc, dt, op=op)
+                outs, st = run_loopback("reduce_scatter", "bine_static", sb, dt, op=op, rcounts=rc)
+                if any(st) or any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                    bad.append(("rs_static", dt, op, st))
+    finally:
+        for c in cs:
+            c.set_flat_rs(False)
+            c.set_flat_ag(False)
+            c.set_chunk(0)
+    assert not bad, bad[:8]
+
+
 def test_per_op_profile(dev):
     """bine_comm_set_profile: one timed entry per op of the issue schedule
     (exchanges with their send bytes, local ops with algorithmic HBM bytes),
