@@ -210,7 +210,8 @@ int bine_comm_set_flat_rs(bine_comm_t comm, int on);
 /* Per-op device timing ("hipEvents per step"): with profiling on, every op
  * of a collective's issue schedule -- an exchange group on the comm stream or
  * a local primitive on the caller's stream -- is bracketed by two timing
- * events on its stream (single-stream small collectives are not profiled).
+ * events on its stream (single-stream small collectives: all on the caller's
+ * stream).
  * bine_comm_profile() waits for the latest collective's events and fills one
  * entry per op: kind, primitives, bytes (exchange: bytes this rank sends;
  * local: algorithmic HBM bytes), start relative to the first op's start and
