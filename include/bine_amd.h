@@ -194,8 +194,8 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
 int bine_comm_set_flat_ag(bine_comm_t comm, int on);
 
 /* Flat reduce-scatter phase for allreduce_bine_bdw_remap / _static /
- * _remap_segmented, reduce_scatter_bine_permute_remap / _send_remap / _static
- * and reduce_bine_bdw at power-of-two P <= 16: the log2(P) halving steps
+ * _remap_segmented, reduce_scatter_bine_permute_remap / _send_remap / _static /
+ * _block_by_block and reduce_bine_bdw at power-of-two P <= 16: the log2(P) halving steps
  * become ONE exchange in which every rank sends each block straight to the
  * rank that computes it (one hop on every link at once), and that rank
  * evaluates the reference's reduction tree for its block -- the same binary
@@ -289,6 +289,8 @@ typedef enum { BINE_BUF_SBUF = 0, BINE_BUF_RBUF = 1, BINE_BUF_TMP0 = 2, BINE_BUF
 #define BINE_PRIM_PIPELINE 1  /* flags: exchange whose receive feeds the next
                                  REDUCE(3) element for element -- both may be
                                  split into chunks and overlapped */
+/* REDUCE_TREE: flags >> 8 = levels whose combine is v[i + w] (op) v[i] (the
+   right subtree is the inout side; block_by_block's last step) */
 typedef struct {
   int32_t type;      /* bine_prim_type_t */
   int32_t group;     /* consecutive SEND/RECV with equal group form one exchange */

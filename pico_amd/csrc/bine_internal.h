@@ -109,8 +109,10 @@ int launch_reduce_batch(int n, const void *const *a, const void *const *b, void 
 // out = the reduction tree over nl (2..kMaxLeaves, power of two) leaves in
 // tree order:
 // level by level (w = 1, 2, 4, ...) v[i] = v[i] (op) v[i + w] for i % 2w == 0
+// (v[i + w] (op) v[i] at the levels whose bit is set in `swap`)
 constexpr int kMaxLeaves = 16;
-int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream);
+int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream,
+                       unsigned swap = 0);
 int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
 int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
 

@@ -346,7 +346,8 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
       const void *leaf[kMaxLeaves];
       for (int j = 0, k = 0; j < p.peer; j++)
         leaf[j] = j == p.pos ? ptr(p.aux_buf, p.aux_off) : ptr(p.src_buf, p.src_off + (uint64_t)k++ * p.count);
-      rc = launch_reduce_tree(p.peer, leaf, ptr(p.dst_buf, p.dst_off), p.count, dtype, op, K);
+      rc = launch_reduce_tree(p.peer, leaf, ptr(p.dst_buf, p.dst_off), p.count, dtype, op, K,
+                              (unsigned)p.flags >> 8);
     } else if (p.type == BINE_PRIM_REDUCE3)
       rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count,
                          dtype, op, K);

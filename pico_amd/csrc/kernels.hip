@@ -358,18 +358,28 @@ struct TreeArgs {
   const void *leaf[kMaxLeaves];
   void *out;
   uint64_t head, nvec, n;
-  int vec;  // 1: all operands co-aligned mod 16 B with `out`
+  int vec;        // 1: all operands co-aligned mod 16 B with `out`
+  unsigned swap;  // bit l: level l combines v[i + w] (op) v[i] (the right side is inout)
 };
+
+// one level's combine; `sw` is wave-uniform (a scalar branch)
+template <typename T, int OP>
+__device__ __forceinline__ T comb(T l, T r, bool sw) { return sw ? apply<T, OP>(r, l) : apply<T, OP>(l, r); }
+template <typename T, int OP>
+__device__ __forceinline__ u32x4 comb16(u32x4 l, u32x4 r, bool sw) {
+  return sw ? apply16<T, OP>(r, l) : apply16<T, OP>(l, r);
+}
 
 template <typename T, int OP, int NL>
 __device__ __forceinline__ T tree_scalar(const TreeArgs &t, size_t i) {
   T v[NL];
 #pragma unroll
   for (int j = 0; j < NL; j++) v[j] = ((const T *)t.leaf[j])[i];
+  int lvl = 0;
 #pragma unroll
-  for (int w = 1; w < NL; w <<= 1)
+  for (int w = 1; w < NL; w <<= 1, lvl++)
 #pragma unroll
-    for (int j = 0; j < NL; j += 2 * w) v[j] = apply<T, OP>(v[j], v[j + w]);
+    for (int j = 0; j < NL; j += 2 * w) v[j] = comb<T, OP>(v[j], v[j + w], (t.swap >> lvl) & 1);
   return v[0];
 }
 
@@ -381,8 +391,9 @@ __device__ __forceinline__ T tree_scalar(const TreeArgs &t, size_t i) {
 // tools/tree_variants.hip: a grid-strided form with a guard on every load ran
 // 31 us vs 24.5 us for 8 x 16 MiB).
 template <typename T, int OP, int NL, int U, bool GUARD>
-__device__ __forceinline__ void tree_tile(const u32x4 *const *lp, u32x4 *vo, size_t base, size_t nvec) {
-  constexpr int G = NL < 8 ? NL : 8, NG = NL / G;
+__device__ __forceinline__ void tree_tile(const u32x4 *const *lp, u32x4 *vo, size_t base, size_t nvec,
+                                          unsigned swap) {
+  constexpr int G = NL < 8 ? NL : 8, NG = NL / G, LG = G == 2 ? 1 : G == 4 ? 2 : 3;
   u32x4 part[U][NG];
 #pragma unroll
   for (int g = 0; g < NG; g++) {
@@ -401,19 +412,21 @@ __device__ __forceinline__ void tree_tile(const u32x4 *const *lp, u32x4 *vo, siz
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
+      int lvl = 0;
 #pragma unroll
-      for (int w = 1; w < G; w <<= 1)
+      for (int w = 1; w < G; w <<= 1, lvl++)
 #pragma unroll
-        for (int j = 0; j < G; j += 2 * w) v[u][j] = apply16<T, OP>(v[u][j], v[u][j + w]);
+        for (int j = 0; j < G; j += 2 * w) v[u][j] = comb16<T, OP>(v[u][j], v[u][j + w], (swap >> lvl) & 1);
       part[u][g] = v[u][0];
     }
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
+    int lvl = LG;
 #pragma unroll
-    for (int w = 1; w < NG; w <<= 1)
+    for (int w = 1; w < NG; w <<= 1, lvl++)
 #pragma unroll
-      for (int g = 0; g < NG; g += 2 * w) part[u][g] = apply16<T, OP>(part[u][g], part[u][g + w]);
+      for (int g = 0; g < NG; g += 2 * w) part[u][g] = comb16<T, OP>(part[u][g], part[u][g + w], (swap >> lvl) & 1);
     const size_t i = base + (size_t)u * kBlock;
     if (!GUARD || i < nvec) vo[i] = part[u][0];
   }
@@ -440,8 +453,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree(TreeArgs t) {
   for (int j = 0; j < NL; j++) lp[j] = reinterpret_cast<const u32x4 *>((const T *)t.leaf[j] + t.head);
   u32x4 *vo = reinterpret_cast<u32x4 *>(out + t.head);
   const size_t base = (size_t)blockIdx.x * kBlock * U + threadIdx.x;
-  if ((size_t)(blockIdx.x + 1) * kBlock * U <= t.nvec) tree_tile<T, OP, NL, U, false>(lp, vo, base, t.nvec);
-  else tree_tile<T, OP, NL, U, true>(lp, vo, base, t.nvec);
+  if ((size_t)(blockIdx.x + 1) * kBlock * U <= t.nvec) tree_tile<T, OP, NL, U, false>(lp, vo, base, t.nvec, t.swap);
+  else tree_tile<T, OP, NL, U, true>(lp, vo, base, t.nvec, t.swap);
 }
 
 // operands not co-aligned mod 16 B: scalar grid-stride
@@ -498,7 +511,8 @@ static hipError_t tree_op(int nl, TreeArgs &t, int op, hipStream_t st) {
   }
 }
 
-int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream) {
+int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream,
+                       unsigned swap) {
   if (count == 0) return BINE_SUCCESS;
   if (nl < 2 || nl > kMaxLeaves || (nl & (nl - 1))) return BINE_ERR_ARG;
   if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
@@ -506,6 +520,7 @@ int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count,
   for (int j = 0; j < nl; j++) t.leaf[j] = leaf[j];
   t.out = out;
   t.n = count;
+  t.swap = swap;
   hipStream_t st = (hipStream_t)stream;
   hipError_t e;
   switch (dtype) {

@@ -198,11 +198,12 @@ struct Builder {
   // out = tree over nl leaves: leaf `pos` at (own, own_off), the k-th of the
   // others at (in, in_off + k * n)
   void reduce_tree(int nl, int pos, int own, uint64_t own_off, int in, uint64_t in_off, int out, uint64_t out_off,
-                   uint64_t n) {
+                   uint64_t n, unsigned swap = 0) {
     if (n == 0) return;
     Prim x = mk(BINE_PRIM_REDUCE_TREE);
     x.peer = nl;
     x.pos = pos;
+    x.flags = (int)(swap << 8);
     x.aux_buf = own; x.aux_off = own_off; x.src_buf = in; x.src_off = in_off;
     x.dst_buf = out; x.dst_off = out_off; x.count = n;
     p.prims.push_back(x);
@@ -253,7 +254,8 @@ bool flat_rs_fits(const PlanArgs &a) { return a.flat_rs && a.P >= 2 && a.P <= kM
 // block this rank computes (this rank's own contribution is one of them, not
 // necessarily the first: send_remap / static hand the block to another rank).
 void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &boff,
-             const std::vector<uint64_t> &bcnt, const std::vector<int> &leaves, int out, uint64_t out_off) {
+             const std::vector<uint64_t> &bcnt, const std::vector<int> &leaves, int out, uint64_t out_off,
+             unsigned swap = 0) {
   const int P = a.P, r = a.rank;
   uint64_t cmax = 0;
   for (int x = 0; x < P; x++) cmax = std::max(cmax, bcnt[(size_t)x]);
@@ -271,7 +273,7 @@ void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t>
       b.recv(leaves[(size_t)j], T0, base + (uint64_t)k++ * cl, cl);
     }
     b.end();
-    b.reduce_tree(P, pos, src, boff[(size_t)r] + o, T0, base, out, out_off + o, cl);
+    b.reduce_tree(P, pos, src, boff[(size_t)r] + o, T0, base, out, out_off + o, cl, swap);
   }
 }
 
@@ -665,13 +667,13 @@ struct Displs {
 // d[y], rc[y] elements) goes to rank y; the result lands in rbuf, through TMP1
 // when in place (rbuf's own blocks are still being sent)
 void flat_rs_block(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &d, const std::vector<int> &rc,
-                   const std::vector<int> &leaves) {
+                   const std::vector<int> &leaves, unsigned swap = 0) {
   std::vector<uint64_t> cnt(rc.size());
   for (size_t i = 0; i < rc.size(); i++) cnt[i] = (uint64_t)rc[i];
   const uint64_t mine = cnt[(size_t)a.rank];
-  if (!a.in_place) { flat_rs(b, a, src, d, cnt, leaves, RB, 0); return; }
+  if (!a.in_place) { flat_rs(b, a, src, d, cnt, leaves, RB, 0, swap); return; }
   b.tmp(T1, mine);
-  flat_rs(b, a, src, d, cnt, leaves, T1, 0);
+  flat_rs(b, a, src, d, cnt, leaves, T1, 0, swap);
   b.copy(T1, 0, RB, 0, mine);
 }
 
@@ -950,6 +952,15 @@ void rs_bine_bbb(Builder &b, const PlanArgs &a) {
   Displs ds(rc);
   const int src = a.in_place ? RB : SB;
   if (P == 1) { b.copy(src, 0, RB, 0, (uint64_t)rc[0]); return; }  // reference: rbuf untouched
+  if (flat_rs_fits(a)) {
+    // rank r ends with block r; every step reduces received into its own
+    // accumulator except the last, reduce(own, received) (:1143): the top
+    // level's operands are swapped
+    const int L = log2_ceil(P);
+    flat_rs_block(b, a, src, ds.d, rc, flat_leaves(P, L, r, [&](int x, int s) { return nb_partner(x, 1 << s, P); }),
+                  1u << (L - 1));
+    return;
+  }
   std::vector<int> invr((size_t)P);
   for (int i = 0; i < P; i++) invr[remap_rank((uint32_t)P, (uint32_t)i)] = i;
   b.tmp(T0, ds.total); b.tmp(T1, ds.total);  // tmpbuf, resbuf

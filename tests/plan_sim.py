@@ -115,11 +115,17 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             others = iter(range(nl - 1))
             v = [view(r, p["aux_buf"], p["aux_off"], n).copy() if j == pos else
                  view(r, p["src_buf"], p["src_off"] + next(others) * n, n).copy() for j in range(nl)]
-            w = 1
+            w, lvl, swap = 1, 0, p["flags"] >> 8
             while w < nl:
                 for i in range(0, nl, 2 * w):
-                    O.reduce_local(np.ascontiguousarray(v[i + w]), v[i], dtype, op)
+                    if (swap >> lvl) & 1:  # v[i+w] is the inout side
+                        t = v[i + w].copy()
+                        O.reduce_local(np.ascontiguousarray(v[i]), t, dtype, op)
+                        v[i] = t
+                    else:
+                        O.reduce_local(np.ascontiguousarray(v[i + w]), v[i], dtype, op)
                 w *= 2
+                lvl += 1
             view(r, p["dst_buf"], p["dst_off"], n)[:] = v[0]
 
     def try_transfer(key):

@@ -382,7 +382,8 @@ def test_reduce_tree_special_values(dev):
 
 FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
-           ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"), ("reduce", "bine_bdw")]
+           ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"),
+           ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw")]
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])
@@ -460,6 +461,32 @@ def test_flat_reduce_scatter_ops_and_dtypes(dev, P):
             c.set_flat_ag(False)
             c.set_chunk(0)
     assert not bad, bad[:8]
+
+
+def test_flat_block_by_block_swapped_level_on_device(dev):
+    """the tree kernel's swapped top level (block_by_block's last step reduces
+    (own, received)) with signed zeros and NaNs under MAX / MIN: the
+    reference's bits"""
+    P = 8
+    rng = np.random.default_rng(3)
+    vals = np.array([0.0, -0.0, np.nan, 1.0, -1.0], np.float32)
+    rc = [4099 + (i % 2) for i in range(P)]
+    sb = [rng.choice(vals, sum(rc)).astype(np.float32) for _ in range(P)]
+    cs = comms(P)
+    try:
+        for c in cs:
+            c.set_flat_rs(True)
+        for op in ("max", "min", "sum"):
+            want, _ = O.reduce_scatter("bine_block_by_block", sb, rc, "float", op=op)
+            outs, st = run_loopback("reduce_scatter", "bine_block_by_block", sb, "float", op=op, rcounts=rc)
+            assert not any(st)
+            if op == "sum":  # NaN payloads of mixed-sign NaN sums: value-level (see test_reduce_tree_special_values)
+                assert all(np.array_equal(np.isnan(o), np.isnan(w)) for o, w in zip(outs, want))
+            else:
+                assert all(o.tobytes() == w.tobytes() for o, w in zip(outs, want)), op
+    finally:
+        for c in cs:
+            c.set_flat_rs(False)
 
 
 def test_per_op_profile(dev):

@@ -44,6 +44,9 @@ def _regions(p, in_place):
     if t == "REDUCE3":
         return [reg(p["src_buf"], p["src_off"], n), reg(p["aux_buf"], p["aux_off"], n)], \
             [reg(p["dst_buf"], p["dst_off"], n)]
+    if t == "REDUCE_TREE":  # own leaf at aux, the nl-1 others back to back at src
+        return [reg(p["aux_buf"], p["aux_off"], n), reg(p["src_buf"], p["src_off"], (p["peer"] - 1) * n)], \
+            [reg(p["dst_buf"], p["dst_off"], n)]
     return [reg(p["src_buf"], p["src_off"], n)], [reg(p["dst_buf"], p["dst_off"], n)]
 
 
@@ -382,7 +385,8 @@ def test_flat_gather_reduce_bdw_matches_oracle(P):
 
 FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
-           ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"), ("reduce", "bine_bdw")]
+           ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"),
+           ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw")]
 
 
 def _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag):
@@ -462,3 +466,36 @@ def test_flat_reduce_scatter_link_time_model():
     rk = dict(rcounts=[n // 8] * 8, esz=4, chunk_bytes=1 << 16)
     assert abs(_link_time("reduce_scatter", "bine_permute_remap", 8, **rk) / n - 0.875) < 0.01
     assert abs(_link_time("reduce_scatter", "bine_permute_remap", 8, flat_rs=True, **rk) / n - 0.125) < 0.01
+
+
+def test_flat_block_by_block_keeps_the_swapped_last_step():
+    """reduce_scatter_bine_block_by_block reduces (own, received) at its last
+    step (libbine_reduce_scatter.c:1143), the other steps (received, own): the
+    flat tree swaps its top level.  With signed zeros and NaNs MAX / MIN see
+    the difference -- the flat schedule matches the reference, and the same
+    schedule with the swap bit cleared does not (negative control)"""
+    P = 8
+    rng = np.random.default_rng(3)
+    vals = np.array([0.0, -0.0, np.nan, 1.0, -1.0], np.float32)
+    rc = [5 + (i % 2) for i in range(P)]
+    sb = [rng.choice(vals, sum(rc)).astype(np.float32) for _ in range(P)]
+    orig = plan_sim.scheduled_prims
+
+    def unswapped(*a, **k):
+        prims, info = orig(*a, **k)
+        for p in prims:
+            if p["type"] == "REDUCE_TREE":
+                p["flags"] &= 0xFF
+        return prims, info
+    for op in ("max", "min"):
+        want, _ = O.reduce_scatter("bine_block_by_block", sb, rc, "float", op=op)
+        got = plan_sim.run("reduce_scatter", "bine_block_by_block", sb, "float", op=op, rcounts=rc, chunk_bytes=0,
+                           flat_rs=True)
+        assert all(g.tobytes() == w.tobytes() for g, w in zip(got, want)), op
+        plan_sim.scheduled_prims = unswapped
+        try:
+            bad = plan_sim.run("reduce_scatter", "bine_block_by_block", sb, "float", op=op, rcounts=rc,
+                               chunk_bytes=0, flat_rs=True)
+        finally:
+            plan_sim.scheduled_prims = orig
+        assert not all(g.tobytes() == w.tobytes() for g, w in zip(bad, want)), op
