@@ -360,7 +360,19 @@ void ar_rabenseifner(Builder &b, const PlanArgs &a) {
   const uint64_t n = a.count;
   const int steps = floor_log2(P), adj = 1 << steps, rem = P - adj;
   b.tmp(T0, n);
-  if (!a.in_place) b.copy(SB, 0, RB, 0, n);
+  // rank x's block after the halving of :553-590 (power-of-two P)
+  auto owned = [&](int x, uint64_t *off, uint64_t *cnt) {
+    uint64_t ww = n, o = 0;
+    for (int mask = 1; mask < adj; mask <<= 1) {
+      const int d = x ^ mask;
+      if (x < d) ww = ww / 2;
+      else { o += ww / 2; ww = ww - ww / 2; }
+    }
+    *off = o;
+    *cnt = ww;
+  };
+  const bool flat = rem == 0 && flat_rs_fits(a);
+  if (!a.in_place && !flat) b.copy(SB, 0, RB, 0, n);
   const uint64_t lh = n / 2, rh = n - lh;
   int vrank;
   if (r < 2 * rem) {
@@ -384,22 +396,20 @@ void ar_rabenseifner(Builder &b, const PlanArgs &a) {
       int vdest = vrank ^ mask, dest = vdest < rem ? vdest * 2 : vdest + rem;
       if (r < dest) { rc[step] = w / 2; sc[step] = w - rc[step]; si[step] = ri[step] + rc[step]; }
       else { sc[step] = w / 2; rc[step] = w - sc[step]; ri[step] = si[step] + sc[step]; }
-      b.send(dest, RB, si[step], sc[step]); b.recv(dest, T0, ri[step], rc[step]); b.end(PIPE);
-      b.reduce(T0, ri[step], RB, ri[step], rc[step], PIPE);
+      if (!flat) {
+        b.send(dest, RB, si[step], sc[step]); b.recv(dest, T0, ri[step], rc[step]); b.end(PIPE);
+        b.reduce(T0, ri[step], RB, ri[step], rc[step], PIPE);
+      }
       if (step + 1 < steps) { ri[step + 1] = ri[step]; si[step + 1] = ri[step]; w = rc[step]; step++; }
     }
+    if (flat && steps >= 1) {  // partners x ^ 2^s, acc = acc (op) received
+      std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
+      for (int x = 0; x < P; x++) owned(x, &boff[(size_t)x], &bcnt[(size_t)x]);
+      flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, flat_leaves(P, steps, r, [](int x, int s) { return x ^ (1 << s); }),
+              RB, boff[(size_t)r]);
+    }
     if (a.flat_ag && rem == 0 && steps >= 1) {
-      // one all-peers exchange: rank x's block after the halving of :553-590
-      auto owned = [&](int x, uint64_t *off, uint64_t *cnt) {
-        uint64_t ww = n, o = 0;
-        for (int mask = 1; mask < adj; mask <<= 1) {
-          const int d = x ^ mask;
-          if (x < d) ww = ww / 2;
-          else { o += ww / 2; ww = ww - ww / 2; }
-        }
-        *off = o;
-        *cnt = ww;
-      };
+      // one all-peers exchange: rank x's block after the halving
       for (int x = 0; x < P; x++)
         if (x != r) b.send(x, RB, ri[steps - 1], rc[steps - 1]);
       for (int x = 0; x < P; x++) {
@@ -685,6 +695,11 @@ void rs_recursivehalving(Builder &b, const PlanArgs &a) {
   const uint64_t count = ds.total;
   if (!count) return;
   const int src = a.in_place ? RB : SB;
+  if (is_pow2(P) && flat_rs_fits(a)) {  // rank r ends with block r; partners r ^ (P >> (s + 1))
+    flat_rs_block(b, a, src, ds.d, rc,
+                  flat_leaves(P, log2_ceil(P), r, [P](int x, int s) { return x ^ (P >> (s + 1)); }));
+    return;
+  }
   b.tmp(T0, count); b.tmp(T1, count);  // recv_buf, result_buf
   b.copy(src, 0, T1, 0, count);
   const int tsz = next_pow2(P) >> 1, rem = P - tsz;

@@ -386,7 +386,8 @@ def test_flat_gather_reduce_bdw_matches_oracle(P):
 FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
            ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"),
-           ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw")]
+           ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw"),
+           ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving")]
 
 
 def _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag):
@@ -448,7 +449,8 @@ def test_flat_reduce_scatter_race_free_and_one_hop(coll, algo, P):
 def test_flat_reduce_scatter_not_applied_where_it_does_not_fit():
     """non-power-of-two P and the other algorithms keep their literal schedule"""
     for coll, algo, P in (("allreduce", "bine_bdw_remap_segmented", 6), ("allreduce", "ring", 8),
-                          ("allreduce", "rabenseifner", 8), ("reduce_scatter", "ring", 8)):
+                          ("allreduce", "rabenseifner", 6), ("reduce_scatter", "recursivehalving", 6),
+                          ("reduce_scatter", "ring", 8)):
         kw = dict(rcounts=[100] * P) if coll == "reduce_scatter" else dict(count=4099)
         a = pico_amd.schedule(coll, algo, P, 1, esz=4, chunk_bytes=1024, segsize=256, **kw)
         b = pico_amd.schedule(coll, algo, P, 1, esz=4, chunk_bytes=1024, segsize=256, flat_rs=True, **kw)
