@@ -267,10 +267,10 @@ void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t>
     for (int x = 0; x < P; x++)
       if (x != r && o < bcnt[(size_t)x]) b.send(x, src, boff[(size_t)x] + o, std::min(ch, bcnt[(size_t)x] - o));
     const uint64_t base = (uint64_t)(P - 1) * o, cl = o < mine ? std::min(ch, mine - o) : 0;
-    int pos = 0;
-    for (int j = 0, k = 0; j < P; j++) {
+    int pos = 0, slot = 0;
+    for (int j = 0; j < P; j++) {
       if (leaves[(size_t)j] == r) { pos = j; continue; }
-      b.recv(leaves[(size_t)j], T0, base + (uint64_t)k++ * cl, cl);
+      b.recv(leaves[(size_t)j], T0, base + (uint64_t)slot++ * cl, cl);
     }
     b.end();
     b.reduce_tree(P, pos, src, boff[(size_t)r] + o, T0, base, out, out_off + o, cl, swap);
