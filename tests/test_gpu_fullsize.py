@@ -138,17 +138,27 @@ def test_c5_int64_allreduce_fullsize(dev, comms, mode):
         _mode(comms, "direct")
 
 
-def test_c5_double_allreduce_fullsize(dev, comms):
+@pytest.fixture(scope="module")
+def c5_double_digest():
     sb_host = O.inputs("double", C5_N, P)
     want, rets = O.allreduce("bine_bdw_remap", sb_host, "double")
     assert not any(rets)
-    expect = host_checksum(want[0])
-    del sb_host, want
+    return host_checksum(want[0])
+
+
+@pytest.mark.parametrize("mode", ["direct", "flatrs+flat"])
+def test_c5_double_allreduce_fullsize(dev, comms, c5_double_digest, mode):
+    expect = c5_double_digest
     sb = _device_inputs("double", torch.float64, C5_N)
     rb = [torch.empty(C5_N, dtype=torch.float64, device="cuda:0") for _ in range(P)]
-    rc, st = pico_amd.loopback_allreduce(comms, "bine_bdw_remap", sb, rb, C5_N, "double")
-    assert rc == 0 and not any(st), st
-    assert [pico_amd.checksum(b, C5_N, "double") for b in rb] == [expect] * P
+    _mode(comms, mode)
+    try:
+        rc, st = pico_amd.loopback_allreduce(comms, "bine_bdw_remap", sb, rb, C5_N, "double")
+        assert rc == 0 and not any(st), st
+        got = [pico_amd.checksum(b, C5_N, "double") for b in rb]
+    finally:
+        _mode(comms, "direct")
+    assert got == [expect] * P
 
 
 @pytest.mark.parametrize("mode", ["direct", "relay", "trees", "flatrs"])
