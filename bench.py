@@ -270,6 +270,18 @@ def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream
                   steps, warmup)
 
 
+def _side(rank, what, fn):
+    """a side measurement beside the headline: its failure (a library error,
+    symmetric on every rank since plans are a pure function of the arguments)
+    is reported in the JSON line instead of ending the run"""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 -- reported, not swallowed
+        if rank == 0:
+            print(f"bench: {what} skipped: {e}", file=sys.stderr)
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
     """One extra collective (outside the timed region) with per-op timing
     events (bine_comm_set_profile): where the time of this rank goes -- busy
@@ -465,9 +477,12 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     chosen, chunk = best
     ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
     issue_ms = _timed.issue_ms
-    steps_prof = _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream)
-    extra = _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
-    probe = _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev) if extras else {}
+    steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
+                                                                      stream))
+    extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
+        if extras else {}
+    probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
+        if extras else {}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
