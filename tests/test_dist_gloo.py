@@ -40,6 +40,17 @@ CASES = [
     ("allgather", "sparbit", "float", 5),
     ("allgather", "bine_block_by_block", "float", 9),
 ]
+# the flat reduce-scatter + flat allgather phases (one all-peers exchange per
+# phase, REDUCE_TREE on the owner), executed from the issue schedule
+FLAT_CASES = [
+    ("allreduce", "bine_bdw_remap", "float", 1001),
+    ("allreduce", "bine_bdw_static", "double", 999),
+    ("allreduce", "rabenseifner", "int64", 1000),
+    ("reduce_scatter", "bine_permute_remap", "float", 64),
+    ("reduce_scatter", "bine_static", "float", 64),
+    ("reduce_scatter", "bine_block_by_block", "float", 64),
+    ("reduce", "bine_bdw", "double", 1000),
+]
 
 
 def _free_port():
@@ -59,7 +70,7 @@ def _worker(rank, P, port, q):
     from oracle import oracle as O
     dist.init_process_group("gloo", rank=rank, world_size=P, init_method=f"tcp://127.0.0.1:{port}")
     bad = []
-    for coll, algo, dtype, n in CASES:
+    for flat, (coll, algo, dtype, n) in [(False, c) for c in CASES] + [(True, c) for c in FLAT_CASES]:
         npdt = O.NP_DTYPES[dtype]
         esz = np.dtype(npdt).itemsize
         rc = [n // P] * P if coll == "reduce_scatter" else None
@@ -73,7 +84,13 @@ def _worker(rank, P, port, q):
             want = O.reduce_scatter(algo, sb, rc, dtype)[0][rank]
         else:
             want = O.reduce(algo, sb, dtype)[0] if rank == 0 else None
-        prims, tmp = pico_amd.plan(coll, algo, P, rank, count=n, rcounts=rc, esz=esz, segsize=64)
+        if not flat:
+            prims, tmp = pico_amd.plan(coll, algo, P, rank, count=n, rcounts=rc, esz=esz, segsize=64)
+        else:  # the executor's issue schedule, one exchange group per op
+            ops, _, _, info = pico_amd.schedule(coll, algo, P, rank, count=n, rcounts=rc, esz=esz, segsize=64,
+                                                chunk_bytes=128, flat_rs=True, flat_ag=True, info=True)
+            prims = [dict(x, group=k) for k, o in enumerate(ops) for x in o["prims"]]
+            tmp = info["tmp_elems"]
         out_n = rc[rank] if rc else (P * n if coll == "allgather" else n)
         bufs = [sb[rank].copy(), np.zeros(max(out_n, 1), npdt)] + [np.zeros(int(t) + 1, npdt) for t in tmp]
 
@@ -101,6 +118,20 @@ def _worker(rank, P, port, q):
             cnt = p["count"]
             if p["type"] == "COPY":
                 v(p["dst_buf"], p["dst_off"], cnt)[:] = v(p["src_buf"], p["src_off"], cnt).copy()
+            elif p["type"] == "REDUCE_TREE":  # level by level, left = inout (bit 8+l: swapped)
+                nl, pos, swap = p["peer"], p["pos"], p["flags"] >> 8
+                others = iter(range(nl - 1))
+                vv = [v(p["aux_buf"], p["aux_off"], cnt).copy() if j == pos else
+                      v(p["src_buf"], p["src_off"] + next(others) * cnt, cnt).copy() for j in range(nl)]
+                w, lvl = 1, 0
+                while w < nl:
+                    for k in range(0, nl, 2 * w):
+                        inout, inp = (vv[k + w], vv[k]) if (swap >> lvl) & 1 else (vv[k], vv[k + w])
+                        io = inout.copy()
+                        O.reduce_local(np.ascontiguousarray(inp), io, dtype)
+                        vv[k] = io
+                    w, lvl = w * 2, lvl + 1
+                v(p["dst_buf"], p["dst_off"], cnt)[:] = vv[0]
             elif p["type"] == "REDUCE":
                 io = v(p["dst_buf"], p["dst_off"], cnt)
                 tmpio = io.copy()
@@ -112,7 +143,7 @@ def _worker(rank, P, port, q):
                 v(p["dst_buf"], p["dst_off"], cnt)[:] = b
             i += 1
         if want is not None and not np.array_equal(bufs[1][:out_n], want):
-            bad.append((coll, algo))
+            bad.append((coll, algo, "flat" if flat else "literal"))
         dist.barrier()
     dist.destroy_process_group()
     q.put((rank, bad))
