@@ -1059,6 +1059,21 @@ void rd_bine_lat(Builder &b, const PlanArgs &a) {
   if (!is_pow2(P)) { b.fail(BINE_ERR_SIZE); return; }
   const int src = (a.in_place && r == root) ? RB : SB;
   const int acc = r == root ? RB : T1;
+  // partner of rank x at step s (mask 2^s) in the negabinary binomial tree
+  auto partner_of = [&](int x, int s) {
+    const int bx = (int)to_nb(pmod(x - root, P));
+    return pmod(from_nb((uint32_t)(bx ^ ((2 << s) - 1))) + root, P);
+  };
+  if (flat_rs_fits(a)) {
+    // every subtree root that sends at step s has received at every step
+    // before (binomial tree), so the root's result is the tree T(root) of the
+    // flat reduce-scatter with these partners: every rank sends its whole
+    // vector straight to the root (one hop each) and the root evaluates it
+    std::vector<uint64_t> boff((size_t)P, 0), bcnt((size_t)P, 0);
+    bcnt[(size_t)root] = n;
+    flat_rs(b, a, src, boff, bcnt, flat_leaves(P, log2_ceil(P), root, partner_of), RB, 0);
+    return;
+  }
   b.tmp(T0, n);
   if (r != root) b.tmp(T1, n);
   b.copy(src, 0, acc, 0, n);

@@ -387,7 +387,7 @@ FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
            ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"),
            ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw"),
-           ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving")]
+           ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving"), ("reduce", "bine_lat")]
 
 
 def _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag):
@@ -440,10 +440,15 @@ def test_flat_reduce_scatter_race_free_and_one_hop(coll, algo, P):
                                             **kw)
             check_race_free(ops, cj, fw, in_place)
             trees = [p for o in ops for p in o["prims"] if p["type"] == "REDUCE_TREE"]
-            assert trees and all(p["peer"] == P for p in trees)
+            assert all(p["peer"] == P for p in trees)
+            assert trees or (algo == "bine_lat" and rank != 0)  # reduce_bine_lat: the tree is the root's
             assert not any(p["type"] in ("REDUCE", "REDUCE3") for o in ops for p in o["prims"])
             first = [o for o in ops if o["xchg"]][0]
-            assert {p["peer"] for p in first["prims"] if p["type"] == "SEND"} == set(range(P)) - {rank}
+            sends = {p["peer"] for p in first["prims"] if p["type"] == "SEND"}
+            if algo == "bine_lat":  # reduce_bine_lat: every rank straight to the root
+                assert sends == ({0} if rank else set())
+            else:
+                assert sends == set(range(P)) - {rank}
 
 
 def test_flat_reduce_scatter_not_applied_where_it_does_not_fit():
