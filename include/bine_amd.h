@@ -197,7 +197,9 @@ int bine_comm_set_flat_ag(bine_comm_t comm, int on);
  * _remap_segmented / allreduce_rabenseifner, reduce_scatter_bine_permute_remap /
  * _send_remap / _static / _block_by_block / reduce_scatter_recursivehalving and
  * reduce_bine_bdw / reduce_bine_lat (every rank's vector straight to the root,
- * the root evaluates the binomial tree) at power-of-two P <= 16: the log2(P) halving steps
+ * the root evaluates the binomial tree) and allreduce_bine_lat (one-shot: every
+ * rank's vector to every other, each rank evaluates its own recursive-doubling
+ * tree) at power-of-two P <= 16: the log2(P) halving steps
  * become ONE exchange in which every rank sends each block straight to the
  * rank that computes it (one hop on every link at once), and that rank
  * evaluates the reference's reduction tree for its block -- the same binary

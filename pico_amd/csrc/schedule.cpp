@@ -440,6 +440,15 @@ void ar_bine_lat(Builder &b, const PlanArgs &a) {
   const uint64_t n = a.count;
   const int src = a.in_place ? RB : SB;
   if (P == 1) { b.copy(src, 0, RB, 0, n); return; }
+  if (flat_rs_fits(a)) {
+    // recursive doubling with acc = acc (op) received at every step: rank x's
+    // result is the tree T(x) over the partners pi -- a different association
+    // on every rank, as in the reference.  One-shot form: every rank sends its
+    // whole vector to every other (one hop each) and evaluates its own tree.
+    std::vector<uint64_t> boff((size_t)P, 0), bcnt((size_t)P, n);
+    flat_rs(b, a, src, boff, bcnt, flat_leaves(P, log2_ceil(P), r, [P](int x, int s) { return pi(x, s, P); }), RB, 0);
+    return;
+  }
   b.tmp(T0, n);
   b.copy(src, 0, T0, 0, n);
   int tsend = T0;

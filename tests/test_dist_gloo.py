@@ -51,6 +51,7 @@ FLAT_CASES = [
     ("reduce_scatter", "bine_block_by_block", "float", 64),
     ("reduce", "bine_bdw", "double", 1000),
     ("reduce", "bine_lat", "float", 1000),
+    ("allreduce", "bine_lat", "double", 1000),
 ]
 
 

@@ -384,7 +384,8 @@ FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
            ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"),
            ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw"),
-           ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving"), ("reduce", "bine_lat")]
+           ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving"), ("reduce", "bine_lat"),
+           ("allreduce", "bine_lat")]
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])

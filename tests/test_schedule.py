@@ -387,7 +387,8 @@ FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("allreduce", "bine_bdw_remap_segmented"), ("reduce_scatter", "bine_permute_remap"),
            ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"),
            ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw"),
-           ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving"), ("reduce", "bine_lat")]
+           ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving"), ("reduce", "bine_lat"),
+           ("allreduce", "bine_lat")]
 
 
 def _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag):
@@ -441,11 +442,11 @@ def test_flat_reduce_scatter_race_free_and_one_hop(coll, algo, P):
             check_race_free(ops, cj, fw, in_place)
             trees = [p for o in ops for p in o["prims"] if p["type"] == "REDUCE_TREE"]
             assert all(p["peer"] == P for p in trees)
-            assert trees or (algo == "bine_lat" and rank != 0)  # reduce_bine_lat: the tree is the root's
+            assert trees or ((coll, algo) == ("reduce", "bine_lat") and rank != 0)  # the root's tree
             assert not any(p["type"] in ("REDUCE", "REDUCE3") for o in ops for p in o["prims"])
             first = [o for o in ops if o["xchg"]][0]
             sends = {p["peer"] for p in first["prims"] if p["type"] == "SEND"}
-            if algo == "bine_lat":  # reduce_bine_lat: every rank straight to the root
+            if (coll, algo) == ("reduce", "bine_lat"):  # every rank straight to the root
                 assert sends == ({0} if rank else set())
             else:
                 assert sends == set(range(P)) - {rank}
