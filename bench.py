@@ -15,9 +15,12 @@ value = whole-job algorithmic throughput = N * 256 MiB / t; per-rank busbw
 2 (N-1)/N * S / t and algbw S / t are reported beside it.  The transport is
 the literal Bine schedule (one peer per step), its multi-link relay (same
 schedule, parts routed over two hops through the other ranks, identical
-results) or multi-tree mode (N = 4, 8: P-1 relabelled instances over
-edge-disjoint pairings; integers identical, fp within rounding); --relay auto
-(default) times every transport x pipelining chunk (4 / 16 / 64 MiB) briefly
+results), the flat phases (the allgather and/or the reduce-scatter as one
+all-peers exchange, the reference's reduction tree evaluated by one fused
+kernel; identical results) or multi-tree mode (N = 4, 8: P-1 relabelled
+instances over edge-disjoint pairings; integers identical, fp within
+rounding); --relay auto
+(default) times every transport x pipelining chunk (4 / 8 / 16 / 32 / 64 MiB) briefly
 and keeps the fastest.
 
 Timing: W untimed warm-up steps, then K steps between a barrier +
@@ -387,7 +390,7 @@ def _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, per_peer=3
 
 
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
-CHUNK_TRIALS = (4 << 20, 16 << 20, 64 << 20)   # pipelining chunks tried at N > 1
+CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 
 
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
@@ -557,7 +560,7 @@ def main():
     ap.add_argument("--relay", default="auto",
                     help="transport at N > 1: auto | off (direct) | flat | relay | relay+flat | flatrs | "
                          "flatrs+flat | trees")
-    ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/16/64 MiB)")
+    ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/8/16/32/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
