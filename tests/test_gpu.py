@@ -597,6 +597,33 @@ def test_pico_amd_core_writes_pico_core_csv(dev, tmp_path, coll, algo, dtype):
     assert (tmp_path / "alloc_1_GPU.csv").read_text().startswith("MPI_Rank,allocation\n0,")
 
 
+PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
+
+
+@pytest.mark.skipif(not os.path.exists(PICO_CORE), reason="reference pico_core not built (integration/Makefile)")
+@pytest.mark.parametrize("np_,coll,algo,dtype,flat", [
+    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", False),
+    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", True),
+    (2, "ALLREDUCE", "bine_lat_over", "double", True),
+    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "int64", True),
+    (2, "REDUCE", "bine_bdw_over", "float", False),
+])
+def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat):
+    """the reference's UNCHANGED pico_core (integration/Makefile links it against
+    libbine.so) drives the GPU path through the libbine.h symbols and checks
+    every result against MPICH's own PMPI_* collective (pico_core_utils.c:
+    553-610), aborting on a mismatch; 2 ranks share the GPU through RCCL's
+    socket transport (distinct NCCL_HOSTIDs), optionally with the flat phases"""
+    import subprocess
+    env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
+    if flat:
+        env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
+    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, "1048576",
+                        "5", algo, dtype], env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
+    assert "Last Iter Time" in p.stdout
+
+
 @pytest.mark.parametrize("relay", [0, 64], ids=["direct", "relay"])
 @pytest.mark.parametrize("P", [2, 4, 6, 8])
 def test_allgather_family_matches_oracle(dev, P, relay):
