@@ -501,6 +501,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # least L / B, L = sum over ops of the busiest link's bytes; peak = the
     # egress rate that bound allows (one link: 153; all 7 links: 1071)
     L = 0
+    op_links = []  # per exchange op: (busiest directed link's bytes, peers it talks to)
     for o in ops:
         if o["xchg"]:
             lk = {}
@@ -508,6 +509,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                 if p["type"] in ("SEND", "RECV"):
                     lk[(p["type"], p["peer"])] = lk.get((p["type"], p["peer"]), 0) + 4 * p["count"]
             L += max(lk.values())
+            op_links.append((max(lk.values()), len({p["peer"] for p in o["prims"]})))
     link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
     out = None
     if rank == 0:
@@ -540,10 +542,15 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         }
         # the same egress against what RCCL P2P itself moves on this node
         # the same schedule bound with RCCL's own measured P2P rate per link
-        one = probe.get("one_peer_GBs")
+        # per exchange op: its busiest link at what RCCL moves per link in that
+        # pattern -- the one-peer rate for a one-peer op, the all-peers egress
+        # rate / (P - 1) when the op talks to several peers at once
+        one, allp = probe.get("one_peer_GBs"), probe.get("all_peers_egress_GBs")
         if one and L:
-            t_rccl = L / (one * 1e9)
+            per_link_all = min(one, allp / (world - 1)) if allp else one
+            t_rccl = sum(b / ((one if npeers <= 1 else per_link_all) * 1e9) for b, npeers in op_links)
             out["roofline"]["rccl_p2p_one_link_GBs"] = one
+            out["roofline"]["rccl_p2p_per_link_all_peers_GBs"] = round(per_link_all, 2)
             out["roofline"]["frac_of_rccl_p2p_bound"] = round(t_rccl / (ms * 1e-3), 4)
     comm.destroy()
     dist.destroy_process_group()
