@@ -189,8 +189,10 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
  * every rank sends its reduced block to all other ranks in ONE exchange,
  * instead of the log2(P) mirrored steps (libbine_allreduce.c:779-809,
  * :898-906).  On a fully connected node that is one hop on every link at once.
- * Pure data movement: results identical bit for bit.  Off by default (the
- * literal schedule; BINE_FLAT_AG=1 turns it on); collective. */
+ * The allgather family (out of place) becomes one all-peers exchange after
+ * its own plan has decided the status.  Pure data movement: results
+ * identical bit for bit.  Off by default (the literal schedule;
+ * BINE_FLAT_AG=1 turns it on); collective. */
 int bine_comm_set_flat_ag(bine_comm_t comm, int on);
 
 /* Flat reduce-scatter phase for allreduce_bine_bdw_remap / _static /

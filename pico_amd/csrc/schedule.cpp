@@ -1485,6 +1485,22 @@ Plan make_plan(const PlanArgs &a) {
     default: b.fail(BINE_ERR_UNSUPPORTED); break;
   }
   if (!b.pend_send.empty() || !b.pend_recv.empty()) b.end();
+  // flat allgather for the allgather family (out of place): the algorithm's
+  // own plan decides the status (the reference's error returns stay); a
+  // successful one is replaced by one all-peers exchange that places every
+  // block where the algorithm leaves it (rank order) -- pure data movement
+  const bool ag = a.algo >= BINE_AG_RECURSIVEDOUBLING && a.algo <= BINE_AG_BINE_2_BLOCKS_DTYPE;
+  if (ag && a.flat_ag && !a.in_place && a.P >= 2 && b.p.status == BINE_SUCCESS) {
+    Builder f(a.rank);
+    const uint64_t n = a.count;
+    f.copy(SB, 0, RB, (uint64_t)a.rank * n, n);
+    for (int x = 0; x < a.P; x++)
+      if (x != a.rank) f.send(x, SB, 0, n);
+    for (int x = 0; x < a.P; x++)
+      if (x != a.rank) f.recv(x, RB, (uint64_t)x * n, n);
+    f.end();
+    return f.p;
+  }
   return b.p;
 }
 

@@ -624,12 +624,17 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat)
     assert "Last Iter Time" in p.stdout
 
 
-@pytest.mark.parametrize("relay", [0, 64], ids=["direct", "relay"])
+@pytest.mark.parametrize("relay", [0, 64, "flat"], ids=["direct", "relay", "flat"])
 @pytest.mark.parametrize("P", [2, 4, 6, 8])
 def test_allgather_family_matches_oracle(dev, P, relay):
     """all 12 allgather algorithms, device path vs the oracle's restatement of
-    the reference (golden-pinned on the CPU side), incl. 1-byte elements"""
+    the reference (golden-pinned on the CPU side), incl. 1-byte elements;
+    "flat": every algorithm as one all-peers exchange"""
     bad = []
+    flat = relay == "flat"
+    relay = 0 if flat else relay
+    for c in comms(P):
+        c.set_flat_ag(flat)
     for algo in pico_amd.ALGOS["allgather"]:
         for dt, n in (("float", 1), ("int8", 333), ("double", 4099)):
             sb = O.inputs(dt, n, P)
@@ -643,6 +648,8 @@ def test_allgather_family_matches_oracle(dev, P, relay):
                 bad.append((algo, dt, n, "status", st))
             elif any(sha(o) != sha(w) for o, w in zip(outs, want)):
                 bad.append((algo, dt, n, "data"))
+    for c in comms(P):
+        c.set_flat_ag(False)
     assert not bad, bad[:8]
 
 

@@ -507,3 +507,27 @@ def test_flat_block_by_block_keeps_the_swapped_last_step():
         finally:
             plan_sim.scheduled_prims = orig
         assert not all(g.tobytes() == w.tobytes() for g, w in zip(bad, want)), op
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 6, 8, 16])
+def test_flat_allgather_family(P):
+    """allgather family with the flat flag: the algorithm's own plan decides
+    the status, a successful one becomes one all-peers exchange -- the
+    reference's blocks in the reference's places; in place keeps the literal
+    algorithm (each has its own in-place input layout)"""
+    for algo in AG:
+        for dt, n in (("float", 7), ("int8", 33), ("double", 1)):
+            sb = O.inputs(dt, n, P)
+            try:
+                lit = plan_sim.run("allgather", algo, sb, dt, chunk_bytes=64)
+            except pico_amd.BineError as e:
+                with pytest.raises(pico_amd.BineError) as f:
+                    plan_sim.run("allgather", algo, sb, dt, chunk_bytes=64, flat_ag=True)
+                assert f.value.status == e.status
+                continue
+            got = plan_sim.run("allgather", algo, sb, dt, chunk_bytes=64, flat_ag=True)
+            want, _ = O.allgather(algo, sb, dt)
+            assert all(np.array_equal(g, w) for g, w in zip(got, want)), (algo, dt)
+            assert all(np.array_equal(g, w) for g, w in zip(lit, want)), (algo, dt)
+            ops, _, _ = pico_amd.schedule("allgather", algo, P, 1, count=n, esz=4, chunk_bytes=64, flat_ag=True)
+            assert len([o for o in ops if o["xchg"]]) == 1
