@@ -1,0 +1,15 @@
+"""bench.py's transport choice (host logic only): the fastest transport, but a
+bit-exact one over multi-tree mode unless trees wins by more than 3 %."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def test_prefer_bit_exact_transport():
+    assert bench._prefer_exact({"direct": 10.0, "trees": 5.0, "flatrs+flat": 5.1}) == "flatrs+flat"
+    assert bench._prefer_exact({"direct": 10.0, "trees": 5.0, "flatrs+flat": 6.0}) == "trees"
+    assert bench._prefer_exact({"direct": 3.0, "trees": 5.0}) == "direct"
+    assert bench._prefer_exact({"trees": 5.0}) == "trees"
+    assert bench._prefer_exact({"relay": 4.0, "flat": 4.5}) == "relay"
