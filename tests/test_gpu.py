@@ -354,6 +354,28 @@ def test_reduce_tree_kernel_bit_exact(dev, nl, dtype):
             assert sha(from_dev(out, dtype, n)) == sha(want), (op, n, shift)
 
 
+@pytest.mark.parametrize("dtype", ["int8", "int16", "float", "double"])
+def test_reduce_tree_unaligned_but_coaligned(dev, dtype):
+    """every leaf and the output start at the same offset past a 16-B boundary:
+    the vector body plus the head / tail edges launch"""
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for nl in (2, 8, 16):
+        for shift in range(1, 16 // esz):
+            n = 4099
+            host = [O.fill(dtype, n, 700 + j) for j in range(nl)]
+            want = _host_tree(host, dtype, "sum")
+            leaves = []
+            for h in host:
+                t = torch.zeros(h.nbytes + 64, dtype=torch.uint8, device="cuda:0")
+                t[shift * esz:shift * esz + h.nbytes] = torch.from_numpy(h.view(np.uint8).copy()).to("cuda:0")
+                leaves.append(t[shift * esz:])
+            out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
+            o = out[shift * esz:]
+            assert pico_amd.reduce_tree(leaves, o, n, dtype, "sum") == 0
+            torch.cuda.synchronize()
+            assert sha(from_dev(out, dtype, n, shift * esz)) == sha(want), (nl, shift)
+
+
 def test_reduce_tree_special_values(dev):
     """NaN / inf / -0 / denormals keep MPICH's operand-order semantics inside
     the fused tree (the same selects and IEEE adds as the pairwise kernel):
