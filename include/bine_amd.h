@@ -195,13 +195,15 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
  * BINE_FLAT_AG=1 turns it on); collective. */
 int bine_comm_set_flat_ag(bine_comm_t comm, int on);
 
-/* Flat reduce-scatter phase for allreduce_bine_bdw_remap / _static /
- * _remap_segmented / allreduce_rabenseifner, reduce_scatter_bine_permute_remap /
- * _send_remap / _static / _block_by_block / reduce_scatter_recursivehalving and
- * reduce_bine_bdw / reduce_bine_lat (every rank's vector straight to the root,
- * the root evaluates the binomial tree) and allreduce_bine_lat (one-shot: every
- * rank's vector to every other, each rank evaluates its own recursive-doubling
- * tree) at power-of-two P <= 16: the log2(P) halving steps
+/* Flat reduce-scatter phase for every reduce-family algorithm but the two
+ * rings, at power-of-two P <= 16: allreduce_bine_bdw_remap / _static /
+ * _remap_segmented / _block_by_block_any_even / allreduce_rabenseifner,
+ * reduce_scatter_bine_permute_remap / _send_remap / _static / _block_by_block /
+ * _block_by_block_any_even / _recursivehalving / _recursive_distance_doubling /
+ * _butterfly, reduce_bine_bdw, reduce_bine_lat (every rank's vector straight to
+ * the root, the root evaluates the binomial tree), allreduce_bine_lat and
+ * allreduce_recursivedoubling (one-shot: every rank's vector to every other,
+ * each rank evaluates its own recursive-doubling tree): the log2(P) halving steps
  * become ONE exchange in which every rank sends each block straight to the
  * rank that computes it (one hop on every link at once), and that rank
  * evaluates the reference's reduction tree for its block -- the same binary

@@ -230,19 +230,26 @@ constexpr bool PIPE = true;
 //     T(x, -1) = input of x,   T(x, s) = T(x, s-1) (op) T(peer(x, s), s-1),
 // i.e. over the leaf order L(x, s) = L(x, s-1) ++ L(peer(x, s), s-1), combined
 // level by level, left operand = inout.  flat_leaves() returns L(x, steps-1).
-template <typename Peer>
-std::vector<int> flat_leaves(int P, int steps, int x, Peer peer) {
+// own_first(r, s) = false puts the partner's subtree on the inout side of
+// rank r's step-s combine (schedules whose operand order depends on the ranks).
+template <typename Peer, typename OwnFirst>
+std::vector<int> flat_leaves(int P, int steps, int x, Peer peer, OwnFirst own_first) {
   std::vector<std::vector<int>> L((size_t)P), N((size_t)P);
   for (int r = 0; r < P; r++) L[(size_t)r] = {r};
   for (int s = 0; s < steps; s++) {
     for (int r = 0; r < P; r++) {
-      N[(size_t)r] = L[(size_t)r];
-      const auto &o = L[(size_t)peer(r, s)];
-      N[(size_t)r].insert(N[(size_t)r].end(), o.begin(), o.end());
+      const auto &mine = L[(size_t)r], &o = L[(size_t)peer(r, s)];
+      const bool f = own_first(r, s);
+      N[(size_t)r] = f ? mine : o;
+      N[(size_t)r].insert(N[(size_t)r].end(), f ? o.begin() : mine.begin(), f ? o.end() : mine.end());
     }
     L.swap(N);
   }
   return L[(size_t)x];
+}
+template <typename Peer>
+std::vector<int> flat_leaves(int P, int steps, int x, Peer peer) {
+  return flat_leaves(P, steps, x, peer, [](int, int) { return true; });
 }
 
 bool flat_rs_fits(const PlanArgs &a) { return a.flat_rs && a.P >= 2 && a.P <= kMaxLeaves && is_pow2(a.P); }
@@ -287,6 +294,11 @@ void ar_recursivedoubling(Builder &b, const PlanArgs &a) {
   const uint64_t n = a.count;
   const int src = a.in_place ? RB : SB;
   if (P == 1) { b.copy(src, 0, RB, 0, n); return; }
+  if (flat_rs_fits(a)) {  // one-shot, as allreduce_bine_lat: partners x ^ 2^s, acc = acc (op) received
+    std::vector<uint64_t> boff((size_t)P, 0), bcnt((size_t)P, n);
+    flat_rs(b, a, src, boff, bcnt, flat_leaves(P, log2_ceil(P), r, [](int x, int s) { return x ^ (1 << s); }), RB, 0);
+    return;
+  }
   b.tmp(T0, n);
   b.copy(src, 0, T0, 0, n);  // inplacebuf
   int tsend = T0, newrank;
@@ -627,12 +639,32 @@ void ar_bine_bbb_any_even(Builder &b, const PlanArgs &a) {
   const uint64_t n = a.count;
   if (P % 2) { b.fail(BINE_ERR_ARG); return; }  // assert(size % 2 == 0), :931
   Blocks bl(n, P);
-  b.tmp(T0, n);
-  if (!a.in_place) b.copy(SB, 0, RB, 0, n);
+  if (flat_rs_fits(a)) {
+    // power-of-two P: rank x ends the reduce-scatter with block x, reduced
+    // as acc = acc (op) received with the negabinary partners (the same trees
+    // as the block-by-block reduce-scatter's first levels; tests/test_flat_symbolic.py)
+    std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
+    for (int x = 0; x < P; x++) { boff[(size_t)x] = bl.off(x); bcnt[(size_t)x] = bl.cnt(x); }
+    flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt,
+            flat_leaves(P, log2_ceil(P), r, [P](int x, int s) { return nb_partner(x, 1 << s, P); }), RB, boff[(size_t)r]);
+    if (a.flat_ag) {
+      for (int x = 0; x < P; x++)
+        if (x != r) b.send(x, RB, boff[(size_t)r], bcnt[(size_t)r]);
+      for (int x = 0; x < P; x++)
+        if (x != r) b.recv(x, RB, boff[(size_t)x], bcnt[(size_t)x]);
+      b.end();
+      return;
+    }
+  } else {
+    b.tmp(T0, n);
+    if (!a.in_place) b.copy(SB, 0, RB, 0, n);
+  }
+  const bool flat = flat_rs_fits(a);
   int mask = 1, rstep = log2_ceil(P) - 1;
   std::vector<int> kof((size_t)P, -1);
   for (int blk = 1; blk < P; blk++) kof[(size_t)blk] = 31 - __builtin_clz(get_nu((uint32_t)blk, (uint32_t)P));
   while (mask < P) {
+    if (flat) { mask <<= 1; rstep--; continue; }
     const int partner = nb_partner(r, mask, P);
     std::vector<int> got;
     for (int blk = 1; blk < P; blk++) {
@@ -759,6 +791,14 @@ void rs_recursive_distance_doubling(Builder &b, const PlanArgs &a) {
   const uint64_t count = ds.total;
   if (!count) return;
   const int src = a.in_place ? RB : SB;
+  if (flat_rs_fits(a)) {
+    // rank x computes block inverse_rank(x) (bit reversal, an involution) with
+    // partners x ^ 2^s and sends it there: rank y evaluates the tree of
+    // inverse_rank(y)
+    flat_rs_block(b, a, src, ds.d, rc, flat_leaves(P, steps, (int)top_bits((uint32_t)r, steps),
+                                                   [](int x, int s) { return x ^ (1 << s); }));
+    return;
+  }
   b.tmp(T0, count); b.tmp(T1, count);
   b.copy(src, 0, T1, 0, count);
   int w = P >> 1, dist = 1, sidx = 0, ridx = 0, last = P;
@@ -828,6 +868,17 @@ void rs_butterfly(Builder &b, const PlanArgs &a) {
   const int src = a.in_place ? RB : SB;
   if (P < 2) { b.copy(src, 0, RB, 0, ds.total); return; }  // the reference returns without copying
   const uint64_t total = ds.total;
+  if (is_pow2(P) && flat_rs_fits(a)) {
+    // partners x ^ 2^s; every combine keeps the higher rank's accumulator as
+    // the inout side (:680-690: reduce(own, received) when rank < peer, then
+    // the buffers swap); rank x ends with block mirror(x) and swaps it with
+    // rank mirror(x), so rank y evaluates the tree of mirror(y)
+    const int L = log2_ceil(P);
+    flat_rs_block(b, a, src, ds.d, rc,
+                  flat_leaves(P, L, (int)mirror((uint32_t)r, L), [](int x, int s) { return x ^ (1 << s); },
+                              [](int x, int s) { return x > (x ^ (1 << s)); }));
+    return;
+  }
   b.tmp(T0, total); b.tmp(T1, total);
   int ps = T0, pr = T1;
   b.copy(src, 0, ps, 0, total);
@@ -1024,6 +1075,14 @@ void rs_bine_bbb_any_even(Builder &b, const PlanArgs &a) {
   const int src = a.in_place ? RB : SB;
   if (P == 1) { b.copy(src, 0, RB, 0, (uint64_t)rc[0]); return; }
   if (P % 2) { b.fail(BINE_ERR_ARG); return; }  // the reference hangs for odd P > 1
+  if (flat_rs_fits(a)) {
+    // power-of-two P: the trees of reduce_scatter_bine_block_by_block (top
+    // level swapped: the last step reduces (own, received), :1265)
+    const int L = log2_ceil(P);
+    flat_rs_block(b, a, src, ds.d, rc, flat_leaves(P, L, r, [P](int x, int s) { return nb_partner(x, 1 << s, P); }),
+                  1u << (L - 1));
+    return;
+  }
   b.tmp(T0, ds.total); b.tmp(T1, ds.total);
   b.copy(src, 0, T1, 0, ds.total);
   std::vector<int> kof((size_t)P, -1);

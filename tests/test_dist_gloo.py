@@ -52,6 +52,11 @@ FLAT_CASES = [
     ("reduce", "bine_bdw", "double", 1000),
     ("reduce", "bine_lat", "float", 1000),
     ("allreduce", "bine_lat", "double", 1000),
+    ("allreduce", "recursivedoubling", "int32", 65),
+    ("allreduce", "bine_block_by_block_any_even", "float", 1003),
+    ("reduce_scatter", "butterfly", "float", 64),
+    ("reduce_scatter", "recursive_distance_doubling", "float", 64),
+    ("reduce_scatter", "bine_block_by_block_any_even", "float", 64),
 ]
 
 

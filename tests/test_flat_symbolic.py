@@ -46,7 +46,10 @@ CASES = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
          ("allreduce", "bine_bdw_remap_segmented"), ("allreduce", "rabenseifner"), ("allreduce", "bine_lat"),
          ("reduce_scatter", "bine_permute_remap"), ("reduce_scatter", "bine_send_remap"),
          ("reduce_scatter", "bine_static"), ("reduce_scatter", "bine_block_by_block"),
-         ("reduce_scatter", "recursivehalving"), ("reduce", "bine_bdw"), ("reduce", "bine_lat")]
+         ("reduce_scatter", "recursivehalving"), ("reduce", "bine_bdw"), ("reduce", "bine_lat"),
+         ("allreduce", "recursivedoubling"), ("reduce_scatter", "recursive_distance_doubling"),
+         ("reduce_scatter", "butterfly"), ("allreduce", "bine_block_by_block_any_even"),
+         ("reduce_scatter", "bine_block_by_block_any_even")]
 
 
 @pytest.mark.parametrize("coll,algo", CASES)

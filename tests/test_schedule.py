@@ -388,7 +388,9 @@ FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("reduce_scatter", "bine_send_remap"), ("reduce_scatter", "bine_static"),
            ("reduce_scatter", "bine_block_by_block"), ("reduce", "bine_bdw"),
            ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving"), ("reduce", "bine_lat"),
-           ("allreduce", "bine_lat")]
+           ("allreduce", "bine_lat"), ("allreduce", "recursivedoubling"),
+           ("reduce_scatter", "recursive_distance_doubling"), ("reduce_scatter", "butterfly"),
+           ("allreduce", "bine_block_by_block_any_even"), ("reduce_scatter", "bine_block_by_block_any_even")]
 
 
 def _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag):
