@@ -195,8 +195,9 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
  * BINE_FLAT_AG=1 turns it on); collective. */
 int bine_comm_set_flat_ag(bine_comm_t comm, int on);
 
-/* Flat reduce-scatter phase for every reduce-family algorithm but the two
- * rings, at power-of-two P <= 16: allreduce_bine_bdw_remap / _static /
+/* Flat reduce-scatter phase for every reduce-family algorithm at
+ * power-of-two P <= 16 (the rings: the same exchange, their chain folded by
+ * P-1 pairwise reductions, since a chain is not a balanced tree): allreduce_bine_bdw_remap / _static /
  * _remap_segmented / _block_by_block_any_even / allreduce_rabenseifner,
  * reduce_scatter_bine_permute_remap / _send_remap / _static / _block_by_block /
  * _block_by_block_any_even / _recursivehalving / _recursive_distance_doubling /

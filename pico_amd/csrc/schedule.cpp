@@ -284,6 +284,32 @@ void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t>
   }
 }
 
+// The rings' reduction is a chain, not a balanced tree: block b travels the
+// ring and every rank folds its own contribution in as the inout side,
+// v = x_j (op) v.  Flat form: the same all-peers exchange as flat_rs, then the
+// chain folded over the staged leaves (`order` = leaf ranks in chain order,
+// this rank's own leaf last) with P-1 pairwise reductions, each on a staged
+// slot, the last one into (out, out_off).
+void flat_chain(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &boff,
+                const std::vector<uint64_t> &bcnt, const std::vector<int> &order, int out, uint64_t out_off) {
+  const int P = a.P, r = a.rank;
+  uint64_t cmax = 0;
+  for (int x = 0; x < P; x++) cmax = std::max(cmax, bcnt[(size_t)x]);
+  const uint64_t mine = bcnt[(size_t)r];
+  const uint64_t ch = a.flat_chunk ? a.flat_chunk : std::max<uint64_t>(cmax, 1);
+  b.tmp(T0, (uint64_t)(P - 1) * mine);
+  for (uint64_t k = 0; k * ch < cmax; k++) {
+    const uint64_t o = k * ch;
+    for (int x = 0; x < P; x++)
+      if (x != r && o < bcnt[(size_t)x]) b.send(x, src, boff[(size_t)x] + o, std::min(ch, bcnt[(size_t)x] - o));
+    const uint64_t base = (uint64_t)(P - 1) * o, cl = o < mine ? std::min(ch, mine - o) : 0;
+    for (int j = 0; j + 1 < P; j++) b.recv(order[(size_t)j], T0, base + (uint64_t)j * cl, cl);
+    b.end();
+    for (int j = 1; j + 1 < P; j++) b.reduce(T0, base + (uint64_t)(j - 1) * cl, T0, base + (uint64_t)j * cl, cl);
+    b.reduce3(T0, base + (uint64_t)(P - 2) * cl, src, boff[(size_t)r] + o, out, out_off + o, cl);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // allreduce -- libbine_allreduce.c
 // ---------------------------------------------------------------------------
@@ -346,6 +372,29 @@ void ar_ring(Builder &b, const PlanArgs &a) {
   if (P == 1) { b.copy(src, 0, RB, 0, n); return; }
   if (n < (uint64_t)P) { ar_recursivedoubling(b, a); return; }
   Blocks bl(n, P);
+  if (flat_rs_fits(a)) {
+    // block y starts at rank y and ends, folded, at rank y - 1: rank r
+    // computes block r + 1 from the chain r + 1, r + 2, ..., r + P - 1, r
+    std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
+    for (int x = 0; x < P; x++) { boff[(size_t)x] = bl.off((x + 1) % P); bcnt[(size_t)x] = bl.cnt((x + 1) % P); }
+    std::vector<int> order;
+    for (int j = 1; j <= P; j++) order.push_back((r + j) % P);
+    flat_chain(b, a, src, boff, bcnt, order, RB, boff[(size_t)r]);
+    if (a.flat_ag) {
+      for (int x = 0; x < P; x++)
+        if (x != r) b.send(x, RB, boff[(size_t)r], bcnt[(size_t)r]);
+      for (int x = 0; x < P; x++)
+        if (x != r) b.recv(x, RB, boff[(size_t)x], bcnt[(size_t)x]);
+      b.end();
+      return;
+    }
+    const int to = (r + 1) % P, from = (r + P - 1) % P;
+    for (int k = 0; k < P - 1; k++) {  // :282-304
+      const int rf = (r + P - k) % P, sf = (r + 1 + P - k) % P;
+      b.send(to, RB, bl.off(sf), bl.cnt(sf)); b.recv(from, RB, bl.off(rf), bl.cnt(rf)); b.end();
+    }
+    return;
+  }
   b.tmp(T0, bl.early); b.tmp(T1, bl.early);
   const int ib[2] = {T0, T1};
   b.copy(src, 0, RB, 0, n);
@@ -835,6 +884,19 @@ void rs_ring(Builder &b, const PlanArgs &a) {
   const int src = a.in_place ? RB : SB;
   auto cnt = [&](int i) { return (uint64_t)rc[(size_t)i]; };
   if (P == 1) { b.copy(src, 0, RB, 0, ds.total); return; }
+  if (flat_rs_fits(a)) {
+    // block r starts at rank r + 1 and ends, folded, at rank r: chain
+    // r + 1, ..., r + P - 1, r; in place through TMP1 (rbuf's blocks are still sent)
+    std::vector<uint64_t> cnt((size_t)P);
+    for (int x = 0; x < P; x++) cnt[(size_t)x] = (uint64_t)rc[(size_t)x];
+    std::vector<int> order;
+    for (int j = 1; j <= P; j++) order.push_back((r + j) % P);
+    if (!a.in_place) { flat_chain(b, a, src, ds.d, cnt, order, RB, 0); return; }
+    b.tmp(T1, cnt[(size_t)r]);
+    flat_chain(b, a, src, ds.d, cnt, order, T1, 0);
+    b.copy(T1, 0, RB, 0, cnt[(size_t)r]);
+    return;
+  }
   b.tmp(T0, ds.total); b.tmp(T1, ds.maxc); b.tmp(T2, ds.maxc);
   const int ib[2] = {T1, T2};
   b.copy(src, 0, T0, 0, ds.total);

@@ -57,6 +57,8 @@ FLAT_CASES = [
     ("reduce_scatter", "butterfly", "float", 64),
     ("reduce_scatter", "recursive_distance_doubling", "float", 64),
     ("reduce_scatter", "bine_block_by_block_any_even", "float", 64),
+    ("allreduce", "ring", "float", 1000),
+    ("reduce_scatter", "ring", "double", 64),
 ]
 
 

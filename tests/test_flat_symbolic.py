@@ -49,7 +49,7 @@ CASES = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
          ("reduce_scatter", "recursivehalving"), ("reduce", "bine_bdw"), ("reduce", "bine_lat"),
          ("allreduce", "recursivedoubling"), ("reduce_scatter", "recursive_distance_doubling"),
          ("reduce_scatter", "butterfly"), ("allreduce", "bine_block_by_block_any_even"),
-         ("reduce_scatter", "bine_block_by_block_any_even")]
+         ("reduce_scatter", "bine_block_by_block_any_even"), ("allreduce", "ring"), ("reduce_scatter", "ring")]
 
 
 @pytest.mark.parametrize("coll,algo", CASES)
@@ -68,11 +68,17 @@ def test_flat_plans_build_the_literal_expressions(coll, algo, P):
             ranks = [0] if coll == "reduce" else range(P)
             for r in ranks:
                 assert list(flat[r]) == list(literal[r]), (coll, algo, P, in_place, r)
-            # and the flat schedule really is the flat one (a REDUCE_TREE, no pairwise reductions)
+            # and the flat schedule really is the flat one: one all-peers exchange, then a
+            # REDUCE_TREE (the rings: their chain folded by pairwise reductions)
             prims, _ = plan_sim.scheduled_prims(coll, algo, P, 0, 16, flat_rs=True, flat_ag=True,
                                                 count=n, rcounts=rc, esz=8, segsize=64 * 8, in_place=in_place)
-            assert any(p["type"] == "REDUCE_TREE" for p in prims)
-            assert not any(p["type"] in ("REDUCE", "REDUCE3") for p in prims)
+            if algo == "ring":
+                assert not any(p["type"] == "REDUCE_TREE" for p in prims)
+                first = [p for p in prims if p["group"] == min(q["group"] for q in prims if q["type"] == "SEND")]
+                assert {p["peer"] for p in first if p["type"] == "SEND"} == set(range(1, P)) or P == 1
+            else:
+                assert any(p["type"] == "REDUCE_TREE" for p in prims)
+                assert not any(p["type"] in ("REDUCE", "REDUCE3") for p in prims)
 
 
 def test_symbolic_check_sees_operand_order():

@@ -409,7 +409,8 @@ FLAT_RS = [("allreduce", "bine_bdw_remap"), ("allreduce", "bine_bdw_static"),
            ("allreduce", "rabenseifner"), ("reduce_scatter", "recursivehalving"), ("reduce", "bine_lat"),
            ("allreduce", "bine_lat"), ("allreduce", "recursivedoubling"),
            ("reduce_scatter", "recursive_distance_doubling"), ("reduce_scatter", "butterfly"),
-           ("allreduce", "bine_block_by_block_any_even"), ("reduce_scatter", "bine_block_by_block_any_even")]
+           ("allreduce", "bine_block_by_block_any_even"), ("reduce_scatter", "bine_block_by_block_any_even"),
+           ("allreduce", "ring"), ("reduce_scatter", "ring")]
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])
