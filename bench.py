@@ -405,6 +405,19 @@ def _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, per_peer=3
     return out
 
 
+def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, world, bine_ms):
+    """RCCL's own ncclAllReduce (fp32 SUM) on the same communicator, buffers and
+    stream: the vendor collective the Bine path competes with on this node.
+    Its reduction order is RCCL's, not the reference's (a baseline, not a
+    libbine result)."""
+    ms, _ = _timed(torch, dist, comm, stream,
+                   lambda: pico_amd.vendor_allreduce(sbuf, rbuf, nelem, "float", "sum", comm, stream=stream), 10, 3)
+    S = nelem * 4
+    return {"ms": round(ms, 4), "algbw_per_rank_GBs": round(S / (ms * 1e-3) / 1e9, 2),
+            "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2),
+            "bine_speedup": round(ms / bine_ms, 3)}
+
+
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
 CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 
@@ -502,6 +515,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         if extras else {}
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}
+    vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
+                                                                      stream, world, ms)) if extras else {}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
@@ -545,7 +560,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "transport_trials_ms": {f"{m}/{ch >> 20}MiB": round(v, 4) for (m, ch), v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": extra,
-                       "rccl_p2p_probe": probe},
+                       "rccl_p2p_probe": probe,
+                       "rccl_allreduce_baseline": vendor},
             "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
                          "traffic": egress,

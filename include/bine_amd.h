@@ -270,6 +270,14 @@ int bine_exchange(bine_comm_t comm, int nsend, const int *send_peers, const void
                   const size_t *sbytes, int nrecv, const int *recv_peers, void *const *rbufs,
                   const size_t *rbytes, void *stream);
 
+/* RCCL's own ncclAllReduce on the communicator's RCCL communicator -- the
+ * vendor collective, NOT a libbine algorithm (its reduction order is RCCL's,
+ * so fp results are not the reference's bits).  A measurement baseline only:
+ * bench.py times it beside the Bine path on the same node, buffers and
+ * stream ordering.  RCCL communicators only (loopback: BINE_ERR_UNSUPPORTED). */
+int bine_vendor_allreduce(bine_comm_t comm, const void *sbuf, void *rbuf, size_t count, int dtype,
+                          int op, void *stream);
+
 /* ---- loopback drivers: run one collective on all virtual ranks ---------------
  * (one host thread per rank; returns the first non-success status) */
 int bine_loopback_run_allreduce(bine_comm_t *comms, int nranks, int algo,

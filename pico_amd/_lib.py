@@ -122,6 +122,7 @@ def lib():
         "bine_comm_set_profile": ([vp, i], i),
         "bine_comm_profile": ([vp, vp, ctypes.c_int64], ctypes.c_int64),
         "bine_exchange": ([vp, i, vp, vp, vp, i, vp, vp, vp, vp], i),
+        "bine_vendor_allreduce": ([vp, vp, vp, sz, i, i, vp], i),
         "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int64), vp], ctypes.c_int64),
     }

@@ -339,6 +339,13 @@ def exchange(comm: Comm, sends=(), recvs=(), stream=None) -> None:
     check(lib().bine_exchange(comm.handle, ns, sp, sb, sz, nr, rp, rb, rz, _stream(stream, comm)), "exchange")
 
 
+def vendor_allreduce(sbuf, rbuf, count: int, dtype, op: str, comm: Comm, stream=None) -> None:
+    """RCCL's own ncclAllReduce on the same communicator (bine_vendor_allreduce):
+    a measurement baseline beside the Bine path, not a libbine algorithm."""
+    check(lib().bine_vendor_allreduce(comm.handle, _ptr(sbuf), _ptr(rbuf), count, _dtype(dtype, rbuf), OPS[op],
+                                      _stream(stream, comm)), "vendor_allreduce")
+
+
 def allgather(algo, sbuf, rbuf, count: int, dtype, comm: Comm, stream=None) -> None:
     """count = elements per rank; rbuf holds comm.size * count elements."""
     check(lib().bine_allgather(comm.handle, _algo("allgather", algo), _ptr(sbuf), _ptr(rbuf), count,
@@ -401,4 +408,4 @@ globals().update(ENTRY_POINTS)
 __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "reduce_batch",
-           "exchange", "reduce_tree"] + list(ENTRY_POINTS)
+           "exchange", "vendor_allreduce", "reduce_tree"] + list(ENTRY_POINTS)

@@ -77,8 +77,23 @@ struct XRecv { int peer; void *ptr; size_t bytes; };
 struct Transport {
   virtual ~Transport() = default;
   virtual int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) = 0;
+  virtual int vendor_allreduce(const void *, void *, size_t, int, int, hipStream_t) { return BINE_ERR_UNSUPPORTED; }
   virtual void retire() {}
 };
+
+static bool nccl_type(int dtype, ncclDataType_t *t) {
+  switch (dtype) {
+    case BINE_INT8: *t = ncclInt8; return true;
+    case BINE_UINT8: *t = ncclUint8; return true;
+    case BINE_INT32: *t = ncclInt32; return true;
+    case BINE_UINT32: *t = ncclUint32; return true;
+    case BINE_INT64: *t = ncclInt64; return true;
+    case BINE_UINT64: *t = ncclUint64; return true;
+    case BINE_FLOAT: *t = ncclFloat32; return true;
+    case BINE_DOUBLE: *t = ncclFloat64; return true;
+    default: return false;  // 16-bit integers: no RCCL type
+  }
+}
 
 struct RcclTransport final : Transport {
   ncclComm_t comm = nullptr;
@@ -96,6 +111,13 @@ struct RcclTransport final : Transport {
     const ncclResult_t r1 = ncclGroupEnd();
     NCCL_TRY(r0);
     NCCL_TRY(r1);
+    return BINE_SUCCESS;
+  }
+  int vendor_allreduce(const void *s, void *r, size_t n, int dtype, int op, hipStream_t st) override {
+    static const ncclRedOp_t ops[BINE_NUM_OPS] = {ncclSum, ncclProd, ncclMax, ncclMin};
+    ncclDataType_t t;
+    if (!nccl_type(dtype, &t) || op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_ARG;
+    NCCL_TRY(ncclAllReduce(s, r, n, t, ops[op], comm, st));
     return BINE_SUCCESS;
   }
 };
@@ -807,6 +829,21 @@ int bine_exchange(bine_comm_t c, int nsend, const int *send_peers, const void *c
   int rc = stream_join(c, c->cstream, K);
   if (rc) return rc;
   if ((rc = c->tx->exchange(xs, xr, c->cstream))) return rc;
+  return stream_join(c, K, c->cstream);
+}
+
+int bine_vendor_allreduce(bine_comm_t c, const void *sbuf, void *rbuf, size_t count, int dtype, int op,
+                          void *stream) {
+  if (!c) return BINE_ERR_ARG;
+  if (c->hub) return BINE_ERR_UNSUPPORTED;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t K = (hipStream_t)stream;
+  c->last_user = K;
+  c->used_user = true;
+  int rc = stream_join(c, c->cstream, K);
+  if (rc) return rc;
+  if ((rc = c->tx->vendor_allreduce(sbuf, rbuf, count, dtype, op, c->cstream))) return rc;
   return stream_join(c, K, c->cstream);
 }
 

@@ -136,6 +136,19 @@ def worker(rank, P, port, q):
         n_ok += 1
     else:
         bad.append(("exchange", "data"))
+    # RCCL's own allreduce (the bench's vendor baseline): int64 SUM is order-free
+    vi = [O.fill("int64", nb, 1234 + r) for r in range(P)]
+    vs = torch.from_numpy(vi[rank]).to("cuda:0")
+    vr = torch.zeros(nb, dtype=torch.int64, device="cuda:0")
+    pico_amd.vendor_allreduce(vs, vr, nb, "int64", "sum", comm)
+    torch.cuda.synchronize()
+    want_v = vi[0].copy()
+    for x in vi[1:]:
+        want_v = want_v + x  # two's complement wrap, as RCCL's int64 add
+    if np.array_equal(vr.cpu().numpy(), want_v):
+        n_ok += 1
+    else:
+        bad.append(("vendor_allreduce", "int64"))
     for b in bad[:20]:
         print(f"rank {rank} MISMATCH {b}", flush=True)
     comm.destroy()
