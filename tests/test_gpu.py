@@ -808,3 +808,15 @@ def test_trees_within_pico_core_tolerance(dev, P):
     finally:
         for c in comms(P):
             c.set_trees(False)
+
+
+def test_vendor_allreduce_needs_rccl():
+    """bine_vendor_allreduce is RCCL's own collective (the bench's baseline):
+    on an in-process loopback communicator it reports BINE_ERR_UNSUPPORTED
+    (no silent fallback).  Its results over real RCCL are checked in
+    tools/rccl_matrix.py (int64 SUM, 4 processes)."""
+    c = comms(2)[0]
+    x = torch.ones(16, dtype=torch.float32, device="cuda:0")
+    with pytest.raises(pico_amd.BineError) as e:
+        pico_amd.vendor_allreduce(x, x, 16, "float", "sum", c)
+    assert e.value.status == 6  # BINE_ERR_UNSUPPORTED
