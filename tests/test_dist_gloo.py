@@ -1,4 +1,4 @@
-"""Multi-process (world_size 2 and 4, gloo, CPU) execution of the product's
+"""Multi-process (world_size 2, 4 and 8 -- the driver's node size --, gloo, CPU) execution of the product's
 per-rank plans: every process builds ITS OWN plan with libbine_amd.so's planner
 and executes it with torch.distributed point-to-point (one batch of isend /
 irecv per exchange group = ncclGroupStart/End semantics), the element
@@ -158,7 +158,7 @@ def _worker(rank, P, port, q):
     q.put((rank, bad))
 
 
-@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("P", [2, 4, 8])
 def test_plans_over_gloo(P):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
