@@ -564,7 +564,10 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "rccl_allreduce_baseline": vendor},
             "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
-                         "traffic": egress,
+                         # traffic = PMC-measured HBM bytes (the N = 1 line); at N > 1 the
+                         # bound is the link, whose bytes come from the executed schedule
+                         "traffic": None,
+                         "egress_bytes": egress,
                          "link_time_bytes": L,
                          "note": "achieved = this rank's xGMI egress bytes (executed schedule) / t; peak = "
                                  "153 GB/s per link x egress / link_time_bytes (sum over exchange ops of the "
