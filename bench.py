@@ -456,12 +456,15 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # edge-disjoint pairings; "flatrs" = the reduce-scatter phase as one
     # all-peers exchange whose owner evaluates the reference's reduction tree
     # in one fused kernel.  All but "trees" are bit-identical to the reference.
-    modes = {"off": ["direct"], "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "trees"],
+    # "+ag" = the same flatrs+flat plan with its one-to-all exchanges run as
+    # RCCL's ncclAllGather (+ device copies) instead of P-1 send/recv pairs.
+    modes = {"off": ["direct"], "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag",
+                                         "trees"],
              "relay": ["relay"], "trees": ["trees"], "flat": ["flat"], "relay+flat": ["relay+flat"],
-             "flatrs+flat": ["flatrs+flat"], "flatrs": ["flatrs"]
+             "flatrs+flat": ["flatrs+flat"], "flatrs": ["flatrs"], "flatrs+flat+ag": ["flatrs+flat+ag"]
              }.get(relay, ["direct"])
     if world <= 2:
-        modes = [m for m in modes if "relay" not in m] or ["direct"]
+        modes = [m for m in modes if "relay" not in m and "+ag" not in m] or ["direct"]
     if world not in (4, 8):
         modes = [m for m in modes if m != "trees"] or ["direct"]
     if world & (world - 1):
@@ -474,6 +477,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         comm.set_trees(m == "trees")
         comm.set_flat_ag("flat" in m)
         comm.set_flat_rs("flatrs" in m)
+        comm.set_coll_ag("+ag" in m)
         comm.set_chunk(ch)
 
     # measured, not guessed: each transport is timed briefly on this hardware

@@ -195,6 +195,20 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
  * BINE_FLAT_AG=1 turns it on); collective. */
 int bine_comm_set_flat_ag(bine_comm_t comm, int on);
 
+/* Transport option for RCCL communicators (P >= 3): an exchange in which
+ * every rank sends ONE buffer to all P-1 others and receives one message of
+ * the same size from each -- the flat allgather phase, the one-shot form of
+ * allreduce_bine_lat, the allgather family's flat form -- runs as RCCL's
+ * ncclAllGather into a staging area followed by P-1 device copies to the
+ * receive locations, instead of P-1 ncclSend/ncclRecv pairs.  The same bytes
+ * land in the same places (results unchanged); whether RCCL's collective
+ * kernels move them faster than its point-to-point path on a given node is
+ * measured by bench.py.  The decision is local to each rank but the same on
+ * every rank for the plans of this library; a caller of bine_exchange with
+ * this option on must keep that shape symmetric too.  Off by default
+ * (BINE_COLL_AG=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
+int bine_comm_set_coll_ag(bine_comm_t comm, int on);
+
 /* Flat reduce-scatter phase for every reduce-family algorithm at
  * power-of-two P <= 16 (the rings: the same exchange, their chain folded by
  * P-1 pairwise reductions, since a chain is not a balanced tree): allreduce_bine_bdw_remap / _static /

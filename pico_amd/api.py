@@ -133,6 +133,11 @@ class Comm:
         """Multi-tree mode (allreduce, P = 4 / 8); collective."""
         check(lib().bine_comm_set_trees(self.handle, int(on)), "bine_comm_set_trees")
 
+    def set_coll_ag(self, on: bool) -> None:
+        """RCCL communicators: run one-buffer-to-all-peers exchanges (the flat
+        allgather phase) as ncclAllGather + device copies; bit-identical."""
+        check(lib().bine_comm_set_coll_ag(self.handle, int(on)), "bine_comm_set_coll_ag")
+
     def set_flat_ag(self, on: bool) -> None:
         """Allreduce (remap / static, power-of-two P): one all-peers allgather
         exchange after the Bine reduce-scatter; bit-identical; collective."""

@@ -97,10 +97,55 @@ static bool nccl_type(int dtype, ncclDataType_t *t) {
 
 struct RcclTransport final : Transport {
   ncclComm_t comm = nullptr;
+  int rank = 0, size = 1;
+  // bine_comm_set_coll_ag: an exchange in which this rank sends ONE buffer to
+  // every other rank and receives one equal-sized message from each (the flat
+  // allgather phase, the one-shot latency form, the allgather family's flat
+  // form) runs as ncclAllGather into `stage`, then the P-1 received blocks are
+  // copied to their destinations.  Same bytes in the same places: result bits
+  // unchanged.  The test is local but globally consistent: with block sizes
+  // b_0..b_{P-1}, rank x matches iff b_y == b_x for every y, i.e. all ranks
+  // match or none does.
+  bool coll_ag = false;
+  void *stage = nullptr;
+  size_t stage_bytes = 0;
   ~RcclTransport() override {
+    if (stage) (void)hipFree(stage);
     if (comm) ncclCommDestroy(comm);
   }
+  bool allgather_shape(const std::vector<XSend> &s, const std::vector<XRecv> &r) const {
+    if (size < 3 || (int)s.size() != size - 1 || (int)r.size() != size - 1) return false;
+    const size_t b = s[0].bytes;
+    std::vector<char> seen_s((size_t)size, 0), seen_r((size_t)size, 0);
+    for (const auto &x : s) {
+      if (x.ptr != s[0].ptr || x.bytes != b || x.peer == rank || seen_s[(size_t)x.peer]) return false;
+      seen_s[(size_t)x.peer] = 1;
+    }
+    for (const auto &x : r) {
+      if (x.bytes != b || x.peer == rank || seen_r[(size_t)x.peer]) return false;
+      seen_r[(size_t)x.peer] = 1;
+    }
+    return true;
+  }
+  int allgather(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) {
+    const size_t b = s[0].bytes, need = b * (size_t)size;
+    if (need > stage_bytes) {
+      HIP_TRY(hipStreamSynchronize(st));  // the old area may still be read by enqueued copies
+      if (stage) HIP_TRY(hipFree(stage));
+      stage = nullptr;
+      stage_bytes = 0;
+      HIP_TRY(hipMalloc(&stage, need));
+      stage_bytes = need;
+    }
+    static const bool trace = getenv("BINE_TRACE") && atoi(getenv("BINE_TRACE")) != 0;
+    if (trace) fprintf(stderr, "[bine r%d] coll_ag ncclAllGather %zu B per rank\n", rank, b);
+    NCCL_TRY(ncclAllGather(s[0].ptr, stage, b, ncclUint8, comm, st));
+    for (const auto &x : r)
+      HIP_TRY(hipMemcpyAsync(x.ptr, (const char *)stage + (size_t)x.peer * b, b, hipMemcpyDeviceToDevice, st));
+    return BINE_SUCCESS;
+  }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
+    if (coll_ag && allgather_shape(s, r)) return allgather(s, r, st);
     NCCL_TRY(ncclGroupStart());
     // the group is always closed, also when posting an operation failed
     ncclResult_t r0 = ncclSuccess;
@@ -703,6 +748,9 @@ int bine_comm_init_rccl(bine_comm_t *out, int nranks, int rank, const void *id, 
   int rc = comm_setup(c.get());
   if (rc) return rc;
   auto tx = std::make_unique<RcclTransport>();
+  tx->rank = rank;
+  tx->size = nranks;
+  if (const char *e = getenv("BINE_COLL_AG")) tx->coll_ag = atoi(e) != 0;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   NCCL_TRY(ncclCommInitRank(&tx->comm, nranks, u, rank));
@@ -941,6 +989,15 @@ int bine_comm_set_trees(bine_comm_t c, int on) {
   if (!c) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->trees = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_coll_ag(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (!r) return BINE_ERR_UNSUPPORTED;  // loopback: no RCCL collective to use
+  std::lock_guard<std::mutex> g(c->mu);
+  r->coll_ag = on != 0;
   return BINE_SUCCESS;
 }
 
