@@ -605,7 +605,7 @@ def main():
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
     ap.add_argument("--relay", default="auto",
                     help="transport at N > 1: auto | off (direct) | flat | relay | relay+flat | flatrs | "
-                         "flatrs+flat | trees")
+                         "flatrs+flat | flatrs+flat+ag | trees")
     ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/8/16/32/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")
