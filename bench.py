@@ -457,14 +457,16 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # all-peers exchange whose owner evaluates the reference's reduction tree
     # in one fused kernel.  All but "trees" are bit-identical to the reference.
     # "+ag" = the same flatrs+flat plan with its one-to-all exchanges run as
-    # RCCL's ncclAllGather (+ device copies) instead of P-1 send/recv pairs.
+    # RCCL's ncclAllGather (+ device copies) instead of P-1 send/recv pairs;
+    # "+a2a" = its all-peers exchanges (both phases) as one ncclAllToAllv each.
     modes = {"off": ["direct"], "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag",
-                                         "trees"],
+                                         "flatrs+flat+a2a", "trees"],
              "relay": ["relay"], "trees": ["trees"], "flat": ["flat"], "relay+flat": ["relay+flat"],
-             "flatrs+flat": ["flatrs+flat"], "flatrs": ["flatrs"], "flatrs+flat+ag": ["flatrs+flat+ag"]
+             "flatrs+flat": ["flatrs+flat"], "flatrs": ["flatrs"], "flatrs+flat+ag": ["flatrs+flat+ag"],
+             "flatrs+flat+a2a": ["flatrs+flat+a2a"]
              }.get(relay, ["direct"])
     if world <= 2:
-        modes = [m for m in modes if "relay" not in m and "+ag" not in m] or ["direct"]
+        modes = [m for m in modes if "relay" not in m and "+ag" not in m and "+a2a" not in m] or ["direct"]
     if world not in (4, 8):
         modes = [m for m in modes if m != "trees"] or ["direct"]
     if world & (world - 1):
@@ -478,6 +480,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         comm.set_flat_ag("flat" in m)
         comm.set_flat_rs("flatrs" in m)
         comm.set_coll_ag("+ag" in m)
+        comm.set_coll_a2a("+a2a" in m)
         comm.set_chunk(ch)
 
     # measured, not guessed: each transport is timed briefly on this hardware
@@ -605,7 +608,7 @@ def main():
     ap.add_argument("--elems", type=int, default=C3_ELEMS)
     ap.add_argument("--relay", default="auto",
                     help="transport at N > 1: auto | off (direct) | flat | relay | relay+flat | flatrs | "
-                         "flatrs+flat | flatrs+flat+ag | trees")
+                         "flatrs+flat | flatrs+flat+ag | flatrs+flat+a2a | trees")
     ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/8/16/32/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")

@@ -209,6 +209,15 @@ int bine_comm_set_flat_ag(bine_comm_t comm, int on);
  * (BINE_COLL_AG=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_coll_ag(bine_comm_t comm, int on);
 
+/* Transport option for RCCL communicators (P >= 3), used only with relay and
+ * multi-tree mode off: an exchange with exactly one message of the same size
+ * to and from every other rank (the flat reduce-scatter and allgather phases)
+ * runs as ONE ncclAllToAllv (RCCL's all-to-all kernels) instead of P-1
+ * ncclSend/ncclRecv pairs; same bytes, same places, results unchanged.  Takes
+ * precedence over bine_comm_set_coll_ag.  Off by default (BINE_COLL_A2A=1);
+ * collective; loopback: BINE_ERR_UNSUPPORTED. */
+int bine_comm_set_coll_a2a(bine_comm_t comm, int on);
+
 /* Flat reduce-scatter phase for every reduce-family algorithm at
  * power-of-two P <= 16 (the rings: the same exchange, their chain folded by
  * P-1 pairwise reductions, since a chain is not a balanced tree): allreduce_bine_bdw_remap / _static /

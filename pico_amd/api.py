@@ -133,6 +133,11 @@ class Comm:
         """Multi-tree mode (allreduce, P = 4 / 8); collective."""
         check(lib().bine_comm_set_trees(self.handle, int(on)), "bine_comm_set_trees")
 
+    def set_coll_a2a(self, on: bool) -> None:
+        """RCCL communicators, relay / trees off: exchanges with one equal-sized
+        message to and from every peer as one ncclAllToAllv; bit-identical."""
+        check(lib().bine_comm_set_coll_a2a(self.handle, int(on)), "bine_comm_set_coll_a2a")
+
     def set_coll_ag(self, on: bool) -> None:
         """RCCL communicators: run one-buffer-to-all-peers exchanges (the flat
         allgather phase) as ncclAllGather + device copies; bit-identical."""

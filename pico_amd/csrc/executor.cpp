@@ -78,6 +78,9 @@ struct Transport {
   virtual ~Transport() = default;
   virtual int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) = 0;
   virtual int vendor_allreduce(const void *, void *, size_t, int, int, hipStream_t) { return BINE_ERR_UNSUPPORTED; }
+  virtual int alltoallv(const std::vector<XSend> &, const std::vector<XRecv> &, hipStream_t) {
+    return BINE_ERR_UNSUPPORTED;
+  }
   virtual void retire() {}
 };
 
@@ -156,6 +159,27 @@ struct RcclTransport final : Transport {
     const ncclResult_t r1 = ncclGroupEnd();
     NCCL_TRY(r0);
     NCCL_TRY(r1);
+    return BINE_SUCCESS;
+  }
+  // one message to and from every peer as ONE ncclAllToAllv: displacements
+  // from the lowest send / receive address (nothing to or from self)
+  int alltoallv(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
+    std::vector<size_t> sc((size_t)size, 0), sd((size_t)size, 0), rc((size_t)size, 0), rd((size_t)size, 0);
+    const char *sb = (const char *)s[0].ptr;
+    char *rb = (char *)r[0].ptr;
+    for (const auto &x : s) sb = std::min(sb, (const char *)x.ptr);
+    for (const auto &x : r) rb = std::min(rb, (char *)x.ptr);
+    for (const auto &x : s) {
+      sc[(size_t)x.peer] = x.bytes;
+      sd[(size_t)x.peer] = (size_t)((const char *)x.ptr - sb);
+    }
+    for (const auto &x : r) {
+      rc[(size_t)x.peer] = x.bytes;
+      rd[(size_t)x.peer] = (size_t)((char *)x.ptr - rb);
+    }
+    static const bool trace = getenv("BINE_TRACE") && atoi(getenv("BINE_TRACE")) != 0;
+    if (trace) fprintf(stderr, "[bine r%d] coll_a2a ncclAllToAllv %zu B per peer\n", rank, s[0].bytes);
+    NCCL_TRY(ncclAllToAllv(sb, sc.data(), sd.data(), rb, rc.data(), rd.data(), ncclUint8, comm, st));
     return BINE_SUCCESS;
   }
   int vendor_allreduce(const void *s, void *r, size_t n, int dtype, int op, hipStream_t st) override {
@@ -269,6 +293,7 @@ struct bine_comm {
   size_t single_stream_bytes = 1 << 20;  // collectives up to this size run on the caller's stream only
   bool flat_ag = false;        // allreduce: one-step all-peers allgather phase
   bool flat_rs = false;        // one-step all-peers reduce-scatter phase + tree kernel
+  bool coll_a2a = false;       // all-peers exchanges as ncclAllToAllv (no relay / trees)
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
   std::vector<hipEvent_t> ev;
@@ -314,6 +339,7 @@ static int comm_setup(bine_comm *c) {
   if (const char *e = getenv("BINE_TREES")) c->trees = atoi(e) != 0;
   if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) != 0;
   if (const char *e = getenv("BINE_FLAT_RS")) c->flat_rs = atoi(e) != 0;
+  if (const char *e = getenv("BINE_COLL_A2A")) c->coll_a2a = atoi(e) != 0;
   if (const char *e = getenv("BINE_SINGLE_STREAM_BYTES")) c->single_stream_bytes = (size_t)strtoull(e, nullptr, 10);
   return BINE_SUCCESS;
 }
@@ -428,6 +454,28 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
 
 // single = true: every op on the caller's stream K in issue order (small
 // collectives: no overlap to win, so no cross-stream event edges to pay for)
+// bine_comm_set_coll_a2a: an exchange with exactly one message of B bytes to
+// and from every other rank.  With relay and multi-tree mode off (settings are
+// collective) such exchanges come only from the flat phases, where rank x
+// sends peer y the part y evaluates (e_y bytes) and receives e_x from each:
+// x matches iff e_y == e_x for all y -- every rank or none.
+static bool a2a_shape(const bine_comm *c, const std::vector<XSend> &s, const std::vector<XRecv> &r) {
+  const int P = c->size;
+  if (!c->coll_a2a || c->hub || c->relay_min_bytes || c->trees || P < 3) return false;  // hub: loopback
+  if ((int)s.size() != P - 1 || (int)r.size() != P - 1) return false;
+  const size_t b = s[0].bytes;
+  std::vector<char> ss((size_t)P, 0), rs((size_t)P, 0);
+  for (const auto &x : s) {
+    if (x.bytes != b || x.peer == c->rank || ss[(size_t)x.peer]) return false;
+    ss[(size_t)x.peer] = 1;
+  }
+  for (const auto &x : r) {
+    if (x.bytes != b || x.peer == c->rank || rs[(size_t)x.peer]) return false;
+    rs[(size_t)x.peer] = 1;
+  }
+  return true;
+}
+
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
                    hipStream_t K, bool single = false) {
   char *base[6];
@@ -485,7 +533,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
         if (x.type == BINE_PRIM_SEND) sends.push_back({x.peer, ptr(x.src_buf, x.src_off), x.count * esz});
         else recvs.push_back({x.peer, ptr(x.dst_buf, x.dst_off), x.count * esz});
       }
-      rc = c->tx->exchange(sends, recvs, C);
+      rc = a2a_shape(c, sends, recvs) ? c->tx->alltoallv(sends, recvs, C) : c->tx->exchange(sends, recvs, C);
       if (rc) return rc;
     } else {
       rc = run_local(o.prims, ptr, dtype, op, esz, K);
@@ -989,6 +1037,14 @@ int bine_comm_set_trees(bine_comm_t c, int on) {
   if (!c) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   c->trees = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_coll_a2a(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  if (!dynamic_cast<RcclTransport *>(c->tx.get())) return BINE_ERR_UNSUPPORTED;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->coll_a2a = on != 0;
   return BINE_SUCCESS;
 }
 
