@@ -2,36 +2,37 @@
 """Benchmark of the MI355X Bine reduce-family path (BASELINE.json metric:
 "device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X").
 
-N = 1 (default): BASELINE config C2, the workload the metric's single-GPU
-configuration names -- the fp32 MPI_Reduce_local replacement kernel on 64 MiB
-(inout = inout + in, 16,777,216 elements), i.e. the per-step arithmetic of the
-Bine allreduce.  value = HBM GB/s = 3 * 64 MiB / t (read in, read inout, write
-inout).  Buffers rotate over 4 independent sets (768 MiB)
-so that no launch is served from the 256 MiB Infinity Cache.
+Every N measures the metric's own workload, BASELINE config C3:
+allreduce_bine_bdw_remap, fp32 SUM, 256 MiB (67,108,864 elements) per rank,
+inputs resident in HBM (pico_core's rand_r distribution, seed 1234 + rank,
+generated on the device), `value` = per-rank algorithmic bandwidth S / t.
 
-N > 1 (torch.distributed.run, one process per GPU): BASELINE config C3,
-allreduce_bine_bdw_remap fp32 256 MiB per rank over RCCL P2P / xGMI.
-value = whole-job algorithmic throughput = N * 256 MiB / t; per-rank busbw
-2 (N-1)/N * S / t and algbw S / t are reported beside it.  The transport is
-the literal Bine schedule (one peer per step), its multi-link relay (same
-schedule, parts routed over two hops through the other ranks, identical
-results), the flat phases (the allgather and/or the reduce-scatter as one
-all-peers exchange, the reference's reduction tree evaluated by one fused
-kernel; identical results) or multi-tree mode (N = 4, 8: P-1 relabelled
-instances over edge-disjoint pairings; integers identical, fp within
-rounding); --relay auto
-(default) times every transport x pipelining chunk (4 / 8 / 16 / 32 / 64 MiB) briefly
-and keeps the fastest.
+* N = 1: a size-1 RCCL communicator.  The reference's P = 1 allreduce is its
+  sbuf -> rbuf copy (libbine_allreduce.c:849-852), here one k_copy launch;
+  roofline = HBM, 2 S bytes per launch.  The C2 reduce kernel, the flat
+  reduce-scatter's tree kernel and the reduce kernel at small windows are
+  reported as side kernels, each with its own roofline and parity check.
+* N > 1 (torch.distributed.run, one process per GPU): RCCL P2P over xGMI.
+  Every transport (the literal schedule and its bit-identical multi-link
+  forms) is timed briefly and CHECKED (digest of every rank's output against
+  tests/golden/bench_digests.json, the oracle's values for these exact inputs);
+  a transport whose output is wrong is excluded.  The fastest correct
+  transport x pipelining chunk is then timed and checked again, and C1, C4, C5
+  run on it, each checked the same way.
 
-Timing: W untimed warm-up steps, then K steps between a barrier +
-device synchronize on both sides, HIP events on the stream the kernels run on,
-max over ranks.  One JSON line on rank 0.
+Statistic (the reference's: pico_core/pico_core.c:133-140,
+plot/summarize_data.py:24-48): an event pair per iteration on the stream the
+collective is issued on (K iterations back to back between a barrier +
+device synchronize on both sides), the max over ranks per iteration, the
+first 20 % dropped, the median.  One JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import statistics
 import sys
 import time
 
@@ -40,31 +41,137 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
 XGMI_LINK_GBS = 153.0          # one xGMI link (task statement); 7 links per GPU
+TARGET_BUSBW_GBS = 7 * XGMI_LINK_GBS   # BASELINE.json north_star: min(HBM, per-rank xGMI) = 1071 GB/s
+METRIC = "device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X"
+C1_ELEMS = 262_144             # 1 MiB fp32
 C2_ELEMS = 16_777_216          # 64 MiB fp32
 C3_ELEMS = 67_108_864          # 256 MiB fp32
+C4_ELEMS = 268_435_456         # 1 GiB fp32 reduce_scatter input per rank
+C5_ELEMS = 33_554_432          # 256 MiB of fp64 / int64
+TREE_LEAVES, TREE_ELEMS, TREE_SEED = 8, 4_194_304, 5000   # flat reduce-scatter at C3, P = 8, 16 MiB chunks
 MIB = 1 << 20
-
-
-def _pmc_traffic(kernel_prefix: str):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC passes (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
-    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        k = d["kernels"][kernel_prefix]
-        return float(k["hbm_bytes_per_launch"])
-    except Exception:
-        return None
-
-
+WARMUP_DROP = 0.2              # plot/summarize_data.py:24 warmup_ratio
+GOLDEN = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
 REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
+# ---- host / runtime facts ---------------------------------------------------------
+
+def host_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_usable": aff}
+
+
+def _pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
+    (profiles/latest_pmc.json, written by tools/pmc_summary.py), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "latest_pmc.json")) as f:
+            return float(json.load(f)["kernels"][kernel_prefix]["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+# ---- parity: committed oracle digests --------------------------------------------
+
+_GOLD = None
+
+
+def golden(key: str):
+    """per-rank digests for `key` (tools/make_bench_digests.py), or None"""
+    global _GOLD
+    if _GOLD is None:
+        try:
+            with open(GOLDEN) as f:
+                _GOLD = json.load(f)["digests"]
+        except OSError:
+            _GOLD = {}
+    return _GOLD.get(key)
+
+
+def gkey(cfg, coll, algo, dtype, n, P, trees=False):
+    return f"{cfg}/{coll}/{algo}/{dtype}/N{n}/P{P}" + ("/trees" if trees else "")
+
+
+def check_digest(pico_amd, buf, count, dtype, key, rank, stream=None):
+    """(ok, digest): bine_checksum of the device buffer vs the committed oracle
+    digest of this rank (ok None when no golden entry exists)"""
+    d = pico_amd.checksum(buf, count, dtype, stream=stream)
+    want = golden(key)
+    return (None if want is None else d == int(want[rank])), d
+
+
+def all_ok(torch, dist, ok):
+    """every rank's verdict (None = unchecked counts as not failed)"""
+    if dist is None:
+        return ok
+    t = torch.tensor([0 if ok is False else 1, 1 if ok is None else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if int(t[0]) == 0:
+        return False
+    return None if int(t[1]) == 1 and ok is None else True
+
+
+# ---- timing (the reference's statistic) --------------------------------------------
+
+def timed(torch, stream, call, steps, warmup, dist=None, syncs=()):
+    """K iterations of call() back to back, each bracketed by its own event
+    pair on `stream`; per iteration the max over ranks; the first 20 %
+    dropped; the median (pico_core.c:133-140, summarize_data.py:24-48).
+    Returns {median_ms, mean_ms (of the kept samples), min_ms, max_ms, samples,
+    issue_ms (host time per call spent enqueueing, max over ranks), wall_s}."""
+    def sync():
+        torch.cuda.synchronize()
+        for s in syncs:
+            s()
+    for _ in range(warmup):
+        call()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    issue = 0.0
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        ti = time.perf_counter()
+        call()
+        issue += time.perf_counter() - ti
+        b.record(stream)
+    sync()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    per = [a.elapsed_time(b) for a, b in evs]
+    t = torch.tensor(per + [issue * 1e3 / steps, wall], dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per = [float(x) for x in t[:steps]]
+    kept = per[int(steps * WARMUP_DROP):] or per
+    return {"median_ms": statistics.median(kept), "mean_ms": statistics.fmean(kept), "min_ms": min(kept),
+            "max_ms": max(kept), "samples": len(kept), "issue_ms": float(t[steps]), "wall_s": float(t[steps + 1])}
+
+
+def _r(x, n=4):
+    return None if x is None else round(x, n)
+
+
+# ---- CPU baseline (rank 0, N = 1) --------------------------------------------------
+
 def _ref_bench(np_: int, args, timeout: float):
-    """Run oracle/_ref/ref_bench (the real reference libbine + MPICH, built from
-    the reference sources by `make -C oracle ref`) under mpiexec as a child
+    """oracle/_ref/ref_bench (the real reference libbine + MPICH, built from the
+    reference sources by `make -C oracle ref`) under mpiexec as a child
     process; its JSON line, or None."""
     import subprocess
     env = dict(os.environ)
@@ -79,82 +186,84 @@ def _ref_bench(np_: int, args, timeout: float):
     return None
 
 
-def cpu_baseline_c2(budget_s: float = 10.0):
-    """CPU baseline of the C2 workload on the box's host cores.
-
-    kind "reference": the reference's own arithmetic -- MPICH 3.3.2's
-    MPI_Reduce_local, which libbine calls per step (libbine_allreduce.c:888) --
-    timed by oracle/_ref/ref_bench on one core for ~budget_s, plus CPU libbine
-    allreduce_bine_bdw_remap at the C3 shape (256 MiB/rank fp32) for P = 2, 4, 8
-    host ranks (one per core), the figure the north star asks to report beside
-    the GPU numbers.  Falls back to the oracle's restatement (kind "port") when
-    the reference build is absent (oracle/_ref is built only where
-    /root/reference is mounted)."""
-    if os.path.exists(REF_BENCH) and os.path.exists(MPIEXEC):
+def cpu_baseline(gpu_digest=None, budget_s: float = 5.0):
+    """The same workload on the box's host cores: the REAL reference libbine's
+    allreduce_bine_bdw_remap (oracle/_ref/ref_bench, compiled from the
+    reference sources against MPICH 3.3.2) on 256 MiB fp32 per rank at P = 1
+    (`value`: the single-GPU line's comparison), and at P = 2, 4, 8 host ranks
+    (one per core), same statistic; its output digest is compared with the
+    GPU's and the oracle's.  Plus C1 (the reference's own CPU configuration)
+    and MPICH's MPI_Reduce_local on C2 (libbine's arithmetic).  Falls back to
+    the oracle's restatement (kind "port") when the reference build is absent."""
+    S = C3_ELEMS * 4
+    host = host_info()
+    if not (os.path.exists(REF_BENCH) and os.path.exists(MPIEXEC)):
+        return cpu_baseline_port(budget_s, host)
+    c3 = {}
+    for p in (1, 2, 4, 8):
         try:
-            rl = _ref_bench(1, ["reduce_local", C2_ELEMS, budget_s], budget_s + 60)
+            ar = _ref_bench(p, ["allreduce", "bine_bdw_remap", C3_ELEMS, 10 if p == 1 else 5], 180)
         except Exception:
-            rl = None
-        if rl:
-            per = rl["s_per_call"]
-            out = {"value": round(3 * C2_ELEMS * 4 / per / 1e9, 3), "unit": "GB/s", "cores": 1,
-                   "kind": "reference",
-                   "sample": f"MPICH 3.3.2 MPI_Reduce_local fp32 SUM (libbine's arithmetic), 64 MiB, "
-                             f"{rl['calls']} calls in {rl['seconds']:.1f} s on one host core "
-                             f"({per * 1e3:.2f} ms/call), oracle/_ref/ref_bench"}
-            c3 = {}
-            for p in (2, 4, 8):
-                try:
-                    ar = _ref_bench(p, ["allreduce", "bine_bdw_remap", C3_ELEMS, 5], 120)
-                except Exception:
-                    ar = None
-                if ar and ar.get("rc") == 0:
-                    t = ar["median_s"]
-                    S = C3_ELEMS * 4
-                    c3[f"P{p}"] = {"ms": round(t * 1e3, 2), "algbw_per_rank_GBs": round(S / t / 1e9, 3),
-                                   "busbw_per_rank_GBs": round(2 * (p - 1) / p * S / t / 1e9, 3),
-                                   "cores": p}
-            try:  # C1: the reference's own configuration, 1 MiB/rank fp32, P = 4
-                c1 = _ref_bench(4, ["allreduce", "bine_bdw_remap", 262_144, 200], 120)
-            except Exception:
-                c1 = None
-            if c1 and c1.get("rc") == 0:
-                out["libbine_allreduce_bine_bdw_remap_c1_P4"] = {"us": round(c1["median_s"] * 1e6, 2), "cores": 4,
-                                                                  "iterations": 200}
-            if c3:
-                out["libbine_allreduce_bine_bdw_remap_c3"] = c3
-                out["libbine_sample"] = ("real libbine allreduce_bine_bdw_remap fp32 256 MiB/rank, P host ranks "
-                                         "(mpiexec, one per core), 5 iterations, max over ranks, median after "
-                                         "dropping the first 20 %")
-            return out
-    return cpu_baseline_c2_port(budget_s)
+            ar = None
+        if ar and ar.get("rc") == 0:
+            t = ar["median_s"]
+            want = golden(gkey("C3", "allreduce", "bine_bdw_remap", "float", C3_ELEMS, p))
+            c3[f"P{p}"] = {"ms": round(t * 1e3, 3), "algbw_per_rank_GBs": round(S / t / 1e9, 3),
+                           "busbw_per_rank_GBs": round(2 * (p - 1) / p * S / t / 1e9, 3), "cores": p,
+                           "iterations": ar["iters"],
+                           "output_digest_equals_oracle": (None if want is None
+                                                           else int(ar["digest"]) == int(want[0]))}
+            if p == 1 and gpu_digest is not None:
+                c3["P1"]["output_digest_equals_gpu"] = int(ar["digest"]) == int(gpu_digest)
+    if "P1" not in c3:
+        return cpu_baseline_port(budget_s, host)
+    out = {"value": c3["P1"]["algbw_per_rank_GBs"], "unit": "GB/s", "cores": 1, "kind": "reference",
+           "sample": (f"real libbine allreduce_bine_bdw_remap fp32 256 MiB, P = 1 host rank (its sbuf->rbuf "
+                      f"copy, libbine_allreduce.c:849-852), {c3['P1']['iterations']} iterations, median after "
+                      f"dropping the first 20 %: {c3['P1']['ms']} ms"),
+           "host": dict(host, mpi="MPICH 3.3.2 (/opt/conda), mpiexec Hydra, one rank per core"),
+           "libbine_allreduce_bine_bdw_remap_c3": c3}
+    try:
+        c1 = _ref_bench(4, ["allreduce", "bine_bdw_remap", C1_ELEMS, 200], 120)
+    except Exception:
+        c1 = None
+    if c1 and c1.get("rc") == 0:
+        out["libbine_allreduce_bine_bdw_remap_c1_P4"] = {"us": round(c1["median_s"] * 1e6, 2), "cores": 4,
+                                                          "iterations": 200}
+    try:
+        rl = _ref_bench(1, ["reduce_local", C2_ELEMS, budget_s], budget_s + 60)
+    except Exception:
+        rl = None
+    if rl:
+        per = rl["s_per_call"]
+        out["mpich_reduce_local_c2"] = {"GBs": round(3 * C2_ELEMS * 4 / per / 1e9, 3), "ms_per_call": round(per * 1e3, 3),
+                                        "calls": rl["calls"], "cores": 1}
+    return out
 
 
-def cpu_baseline_c2_port(budget_s: float = 10.0):
-    """The oracle's MPI_Reduce_local (MPICH semantics, one host core) on the C2
-    workload, bounded to ~budget_s of CPU time."""
+def cpu_baseline_port(budget_s: float, host):
+    """the oracle's allreduce_bine_bdw_remap at P = 1 on the C3 buffer (its copy)"""
     import numpy as np
     from oracle import oracle as O
-    a = O.fill("float", C2_ELEMS, 1234)
-    b = O.fill("float", C2_ELEMS, 1235)
-    O.reduce_local(a, b, "float")  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        O.reduce_local(a, b, "float")
+    sb = [O.fill("float", C3_ELEMS, 1234)]
+    n, t0, ts = 0, time.perf_counter(), []
+    while time.perf_counter() - t0 < budget_s and n < 50:
+        t1 = time.perf_counter()
+        O.allreduce("bine_bdw_remap", sb, "float")
+        ts.append(time.perf_counter() - t1)
         n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 2000:
-            break
-    per = el / n
-    return {"value": round(3 * C2_ELEMS * 4 / per / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"oracle orc_reduce_local fp32 SUM, 64 MiB, {n} calls in {el:.1f} s on one host core "
-                      f"({per * 1e3:.2f} ms/call)"}
+    t = float(np.median(ts[int(len(ts) * WARMUP_DROP):] or ts))
+    return {"value": round(C3_ELEMS * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle allreduce_bine_bdw_remap fp32 256 MiB P = 1, {n} calls, median {t * 1e3:.2f} ms",
+            "host": host}
 
 
-def bench_c2(steps: int, warmup: int):
-    import torch
-    import pico_amd
-    dev = torch.device("cuda:0")
+# ---- N = 1 ------------------------------------------------------------------------
+
+def _side_reduce(torch, pico_amd, dev, stream, steps, warmup):
+    """C2: the MPI_Reduce_local kernel, inout = inout + in on 64 MiB fp32, 4
+    rotating buffer sets (768 MiB, beyond the 256 MiB Infinity Cache); then
+    one call on fresh inputs (seeds 1234 / 1235) checked against the oracle."""
     sets = 4
     ins, ios = [], []
     for k in range(sets):
@@ -164,114 +273,143 @@ def bench_c2(steps: int, warmup: int):
         pico_amd.fill_pico(b, C2_ELEMS, "float", 1235 + 2 * k)
         ins.append(a)
         ios.append(b)
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
-    for i in range(warmup):
-        pico_amd.reduce_local(ins[i % sets], ios[i % sets], C2_ELEMS, "float", "sum", stream=stream)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for i in range(steps):
-        pico_amd.reduce_local(ins[i % sets], ios[i % sets], C2_ELEMS, "float", "sum", stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    ms = e0.elapsed_time(e1) / steps
-    alg_bytes = 3 * C2_ELEMS * 4
-    gbs = alg_bytes / (ms * 1e-3) / 1e9
-    traffic = _pmc_traffic("k_reduce")
+    i = [0]
+
+    def call():
+        pico_amd.reduce_local(ins[i[0] % sets], ios[i[0] % sets], C2_ELEMS, "float", "sum", stream=stream)
+        i[0] += 1
+    st = timed(torch, stream, call, steps, warmup)
+    pico_amd.fill_pico(ins[0], C2_ELEMS, "float", 1234)
+    pico_amd.fill_pico(ios[0], C2_ELEMS, "float", 1235)
+    pico_amd.reduce_local(ins[0], ios[0], C2_ELEMS, "float", "sum", stream=stream)
+    ok, _ = check_digest(pico_amd, ios[0], C2_ELEMS, "float", f"C2/reduce_local/sum/float/N{C2_ELEMS}", 0)
     del ins, ios
-    tree = _bench_tree_kernel(torch, pico_amd, dev, stream, steps, warmup)
-    return {
-        "metric": "device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X",
-        "value": round(gbs, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
-        "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f32", "data": "synthetic (pico_core rand_r distribution, generated on device)",
-        "config": {"workload": "C2: fp32 MPI_Reduce_local replacement kernel, inout=inout+in, 64 MiB "
-                               "(16,777,216 elem), 1 MI355X, 4 rotating buffer sets",
-                   "value_definition": "HBM GB/s = 3*64MiB/t (BASELINE.md 3)",
-                   "side_kernels": {"k_reduce_tree": tree}},
-        "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(gbs / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "kernel": "bine::k_reduce<float,SUM>", "algorithmic_bytes_per_launch": alg_bytes},
-        "wall_s": round(wall, 4),
-    }
+    torch.cuda.empty_cache()
+    alg = 3 * C2_ELEMS * 4
+    return {"kernel": "bine::k_reduce<float,SUM>", "workload": "C2: fp32 inout += in, 64 MiB, 1 GPU",
+            "parity_ok": ok, "us_median": round(st["median_ms"] * 1e3, 3), "samples": st["samples"],
+            "roofline": {"bound": "hbm", "achieved": round(alg / (st["mean_ms"] * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg / (st["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": _pmc_traffic("k_reduce"), "algorithmic_bytes_per_launch": alg}}
 
 
-TREE_LEAVES, TREE_ELEMS = 8, 4_194_304   # flat reduce-scatter at C3, P = 8, 16 MiB chunks
-
-
-def _bench_tree_kernel(torch, pico_amd, dev, stream, steps, warmup):
-    """The flat reduce-scatter's fused tree kernel at its C3 shape (P = 8
-    leaves x 16 MiB chunk -> 16 MiB out; algorithmic bytes 9 x 16 MiB per
-    launch), 4 rotating sets (576 MiB, beyond the Infinity Cache), HIP events
-    on the launch stream."""
+def _side_tree(torch, pico_amd, dev, stream, steps, warmup):
+    """the flat reduce-scatter's tree kernel at its C3 shape (8 leaves x 16 MiB
+    -> 16 MiB; 9 x 16 MiB per launch), 4 rotating sets; set 0 = leaf j seeded
+    5000 + j, checked against the oracle's pairwise tree"""
     sets = 4
     bufs = []
     for k in range(sets):
         leaves = [torch.empty(TREE_ELEMS, dtype=torch.float32, device=dev) for _ in range(TREE_LEAVES)]
         for j, t in enumerate(leaves):
-            pico_amd.fill_pico(t, TREE_ELEMS, "float", 5000 + 16 * k + j)
+            pico_amd.fill_pico(t, TREE_ELEMS, "float", TREE_SEED + 16 * k + j)
         bufs.append((leaves, torch.empty(TREE_ELEMS, dtype=torch.float32, device=dev)))
-    torch.cuda.synchronize()
+    i = [0]
 
-    def run(i):
-        leaves, out = bufs[i % sets]
+    def call():
+        leaves, out = bufs[i[0] % sets]
         rc = pico_amd.reduce_tree(leaves, out, TREE_ELEMS, "float", "sum", stream=stream)
         assert rc == 0, rc
-    for i in range(warmup):
-        run(i)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for i in range(steps):
-        run(i)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / steps * 1e3
-    alg = (TREE_LEAVES + 1) * TREE_ELEMS * 4
-    gbs = alg / (us * 1e-6) / 1e9
+        i[0] += 1
+    st = timed(torch, stream, call, steps, warmup)
+    ok, _ = check_digest(pico_amd, bufs[0][1], TREE_ELEMS, "float",
+                         f"tree/reduce_tree/sum/float/N{TREE_ELEMS}/L{TREE_LEAVES}", 0)
     del bufs
     torch.cuda.empty_cache()
+    alg = (TREE_LEAVES + 1) * TREE_ELEMS * 4
     return {"kernel": "bine::k_reduce_tree<float,SUM,8>", "leaves": TREE_LEAVES, "elems_per_leaf": TREE_ELEMS,
-            "us": round(us, 2), "algorithmic_bytes_per_launch": alg, "achieved_GBs": round(gbs, 1),
-            "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_reduce_tree")}
+            "parity_ok": ok, "us_median": round(st["median_ms"] * 1e3, 3), "samples": st["samples"],
+            "roofline": {"bound": "hbm", "achieved": round(alg / (st["mean_ms"] * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg / (st["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": _pmc_traffic("k_reduce_tree"), "algorithmic_bytes_per_launch": alg}}
 
 
-def _timed(torch, dist, comm, stream, call, steps, warmup):
-    """max-over-ranks ms per call() and wall seconds of `steps` timed calls;
-    _timed.issue_ms = max-over-ranks host time per call spent enqueueing (a
-    value close to the ms per call means the host, not the GPU, set the pace)"""
-    for _ in range(warmup):
-        call()
+def _side_small_windows(torch, pico_amd, dev, stream):
+    """k_reduce at the windows of C1 and of pipelines' tail chunks: 16
+    rotating windows in a 1 GiB region, launches back to back (the
+    launch-to-launch boundary is part of each window's time)"""
+    region = 1 << 28   # elements (1 GiB fp32) per operand
+    a = torch.empty(region, dtype=torch.float32, device=dev)
+    b = torch.empty(region, dtype=torch.float32, device=dev)
+    pico_amd.fill_pico(a, region, "float", 7)
+    pico_amd.fill_pico(b, region, "float", 8)
+    out = {}
+    for w in (256 << 10, 1 << 20, 4 << 20, 16 << 20):
+        n = w // 4
+        i = [0]
+
+        def call():
+            off = (i[0] % 16) * (region // 16)
+            pico_amd.reduce_local(a[off:], b[off:], n, "float", "sum", stream=stream)
+            i[0] += 1
+        st = timed(torch, stream, call, 64, 8)
+        gbs = 3 * w / (st["mean_ms"] * 1e-3) / 1e9
+        out[f"{w >> 10}KiB"] = {"us": round(st["mean_ms"] * 1e3, 3), "GBs": round(gbs, 1),
+                                "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    del a, b
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_n1(steps: int, warmup: int, want_cpu: bool, cpu_budget: float):
+    import pico_amd
+    pico_amd.lib()      # map the RCCL this library was compiled against before torch loads its own
+    import torch
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(0)
+    comm = pico_amd.Comm.rccl(0, 1, pico_amd.Comm.unique_id(), 0)
+    n = C3_ELEMS
+    S = n * 4
+    sbuf = torch.empty(n, dtype=torch.float32, device=dev)
+    rbuf = torch.zeros(n, dtype=torch.float32, device=dev)
+    pico_amd.fill_pico(sbuf, n, "float", 1234)
     torch.cuda.synchronize()
-    comm.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(steps):
-        call()
-    issue = time.perf_counter() - t0
-    e1.record(stream)
-    torch.cuda.synchronize()
-    comm.synchronize()
-    wall = time.perf_counter() - t0
-    dist.barrier()
-    t = torch.tensor([e0.elapsed_time(e1) / steps, wall, issue * 1e3 / steps], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    _timed.issue_ms = float(t[2])
-    return float(t[0]), float(t[1])
+    stream = torch.cuda.current_stream(dev)
+    st = timed(torch, stream,
+               lambda: pico_amd.allreduce("bine_bdw_remap", sbuf, rbuf, n, "float", "sum", comm, stream=stream),
+               steps, warmup, syncs=(comm.synchronize,))
+    key = gkey("C3", "allreduce", "bine_bdw_remap", "float", n, 1)
+    ok, dig = check_digest(pico_amd, rbuf, n, "float", key, 0)
+    ok_in, _ = check_digest(pico_amd, sbuf, n, "float", key, 0)   # input untouched (P = 1: output == input)
+    comm.destroy()
+    del sbuf, rbuf
+    torch.cuda.empty_cache()
+    ms = st["median_ms"]
+    algbw = S / (ms * 1e-3) / 1e9
+    hbm = 2 * S / (st["mean_ms"] * 1e-3) / 1e9
+    side = {"k_reduce_C2": _side_reduce(torch, pico_amd, dev, stream, steps, warmup),
+            "k_reduce_tree_C3_flat_rs_chunk": _side_tree(torch, pico_amd, dev, stream, steps, warmup),
+            "k_reduce_small_windows": _side_small_windows(torch, pico_amd, dev, stream)}
+    out = {
+        "metric": METRIC, "value": round(algbw, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (pico_core rand_r distribution, seed 1234 + rank, generated on device)",
+        "config": {"workload": "C3 at P = 1: allreduce_bine_bdw_remap fp32 SUM 256 MiB/rank (67,108,864 elem) "
+                               "through a size-1 RCCL communicator = the reference's sbuf->rbuf copy "
+                               "(libbine_allreduce.c:849-852), device-resident, 1 MI355X",
+                   "value_definition": "per-rank algbw = S / t, t = median after dropping the first 20 % of "
+                                       "per-iteration event times (pico_core.c:133-140, summarize_data.py:24-48)",
+                   "stats_ms": {k: _r(v, 5) for k, v in st.items()},
+                   "parity": {"ok": bool(ok) and bool(ok_in), "check": "bine_checksum(rbuf) == oracle digest "
+                              f"{key} (tests/golden/bench_digests.json), input untouched", "digest": str(dig)},
+                   "rccl": pico_amd.rccl_version(), "host": host_info(),
+                   "side_kernels": side},
+        "roofline": {"bound": "hbm", "achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(hbm / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_copy"),
+                     "kernel": "bine::k_copy (the P = 1 allreduce is one launch)",
+                     "algorithmic_bytes_per_launch": 2 * S,
+                     "note": "achieved = 2 S (read sbuf + write rbuf) / mean per-iteration event time of the "
+                             "kept samples; traffic = PMC FETCH_SIZE x 2 (gfx950) + WRITE_SIZE per launch"},
+        "wall_s": round(st["wall_s"], 4),
+    }
+    if want_cpu:
+        out["cpu_baseline"] = cpu_baseline(dig, cpu_budget)
+    return out
 
 
-def _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup):
-    return _timed(torch, dist, comm, stream,
-                  lambda: pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream),
-                  steps, warmup)
-
+# ---- N > 1 ------------------------------------------------------------------------
 
 BIT_EXACT_MARGIN = 1.03   # a bit-exact transport within 3 % of multi-tree mode is preferred
 
@@ -301,11 +439,20 @@ def _side(rank, what, fn):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def overlap_frac(exchange_busy, local_busy, span):
+    """share of the local (reduction) time hidden under exchanges: (exchange
+    busy + local busy - span) / local busy, clipped to [0, 1]"""
+    if local_busy <= 0:
+        return None
+    return max(0.0, min(1.0, (exchange_busy + local_busy - span) / local_busy))
+
+
 def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
     """One extra collective (outside the timed region) with per-op timing
     events (bine_comm_set_profile): where the time of this rank goes -- busy
     time of the comm stream (exchanges) and of the compute stream (reductions),
-    their span, and the exchange ops' egress rates."""
+    their span, how much of the reductions the exchanges hide, and the
+    exchange ops' egress rates."""
     comm.set_profile(True)
     try:
         pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
@@ -319,61 +466,84 @@ def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
     span = max(o["start_ms"] + o["ms"] for o in ops)
     xs = [o for o in ops if o["xchg"]]
     ls = [o for o in ops if not o["xchg"]]
-    out = {"ops": len(ops), "span_ms": round(span, 4),
-           "exchange_busy_ms": round(sum(o["ms"] for o in xs), 4),
-           "local_busy_ms": round(sum(o["ms"] for o in ls), 4),
-           "exchanges": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4), "peers": o["nprims"],
-                          "egress_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 2) if o["ms"] > 0 else None}
-                         for o in xs[:24]],
-           "local": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4),
-                      "hbm_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 1) if o["ms"] > 0 else None}
-                     for o in ls[:24]]}
-    return out
+    xb, lb = sum(o["ms"] for o in xs), sum(o["ms"] for o in ls)
+    ov = overlap_frac(xb, lb, span)
+    return {"ops": len(ops), "span_ms": round(span, 4), "exchange_busy_ms": round(xb, 4),
+            "local_busy_ms": round(lb, 4), "overlap_frac": None if ov is None else round(ov, 4),
+            "exchanges": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4), "peers": o["nprims"],
+                           "egress_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 2) if o["ms"] > 0 else None}
+                          for o in xs[:24]],
+            "local": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4),
+                       "hbm_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 1) if o["ms"] > 0 else None}
+                      for o in ls[:24]]}
 
 
-def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev):
-    """BASELINE configs C1, C4 and C5 with the transport chosen for C3
-    (reported beside the headline; a few steps each)"""
+def apply_transport(comm, mode, chunk):
+    comm.set_relay(RELAY_MIN_BYTES if "relay" in mode else 0)
+    comm.set_trees(mode == "trees")
+    comm.set_flat_ag("flat" in mode)
+    comm.set_flat_rs("flatrs" in mode)
+    comm.set_coll_ag("+ag" in mode)
+    comm.set_coll_a2a("+a2a" in mode)
+    comm.set_chunk(chunk)
+
+
+def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk):
+    """BASELINE configs C1, C4 and C5 on the transport chosen for C3 (C1: the
+    bit-exact flat phases instead of multi-tree mode, a large-message mode),
+    each checked against the oracle's digests of its inputs (seed 1234 + rank)"""
     out = {}
-    # C1 shape on the GPUs: fp32 allreduce 1 MiB per rank (the reference's own
-    # CPU configuration: libbine bine_bdw_remap_over 381.9 us at P = 4 through
-    # pico_core, BASELINE.md section 2) -- latency-bound, so the literal
-    # schedule and the latency-optimal Bine variant are both timed
-    n1 = 262_144
+    # C1: fp32 allreduce 1 MiB per rank (the reference's own CPU configuration:
+    # libbine bine_bdw_remap_over 381.9 us at P = 4 through pico_core,
+    # BASELINE.md section 2) -- latency-bound: the bandwidth and the
+    # latency-optimal Bine variants are both timed
+    apply_transport(comm, "flatrs+flat" if mode == "trees" else mode, chunk)
+    n1 = C1_ELEMS
     sb = torch.empty(n1, dtype=torch.float32, device=dev)
     rb = torch.empty(n1, dtype=torch.float32, device=dev)
-    pico_amd.fill_pico(sb, n1, "float", 55 + rank)
+    pico_amd.fill_pico(sb, n1, "float", 1234 + rank)
     for algo in ("bine_bdw_remap", "bine_lat"):
-        ms, _ = _timed(torch, dist, comm, stream,
-                       lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream), 50, 10)
-        out[f"C1_allreduce_{algo}_f32_1MiB"] = {"us": round(ms * 1e3, 2),
-                                                "algbw_per_rank_GBs": round(n1 * 4 / (ms * 1e-3) / 1e9, 2)}
+        st = timed(torch, stream, lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
+                   50, 10, dist, (comm.synchronize,))
+        ok, _ = check_digest(pico_amd, rb, n1, "float", gkey("C1", "allreduce", algo, "float", n1, world), rank)
+        out[f"C1_allreduce_{algo}_f32_1MiB"] = {
+            "us": round(st["median_ms"] * 1e3, 2), "algbw_per_rank_GBs": round(n1 * 4 / (st["median_ms"] * 1e-3) / 1e9, 2),
+            "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
     del sb, rb
+    apply_transport(comm, mode, chunk)
+    trees = mode == "trees"
     # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
-    n = 268_435_456
+    n = C4_ELEMS
     sb = torch.empty(n, dtype=torch.float32, device=dev)
     rb = torch.empty(n // world, dtype=torch.float32, device=dev)
-    pico_amd.fill_pico(sb, n, "float", 77 + rank)
+    pico_amd.fill_pico(sb, n, "float", 1234 + rank)
     rc = [n // world] * world
-    ms, _ = _timed(torch, dist, comm, stream,
-                   lambda: pico_amd.reduce_scatter("bine_permute_remap", sb, rb, rc, "float", "sum", comm,
-                                                   stream=stream), 5, 2)
+    st = timed(torch, stream,
+               lambda: pico_amd.reduce_scatter("bine_permute_remap", sb, rb, rc, "float", "sum", comm, stream=stream),
+               5, 2, dist, (comm.synchronize,))
+    ok, _ = check_digest(pico_amd, rb, n // world, "float",
+                         gkey("C4", "reduce_scatter", "bine_permute_remap", "float", n, world, trees), rank)
     S = n * 4
     out["C4_reduce_scatter_bine_permute_remap_f32_1GiB"] = {
-        "ms": round(ms, 4), "busbw_per_rank_GBs": round((world - 1) / world * S / (ms * 1e-3) / 1e9, 2)}
+        "ms": round(st["median_ms"], 4), "busbw_per_rank_GBs": round((world - 1) / world * S / (st["median_ms"] * 1e-3) / 1e9, 2),
+        "parity_ok": all_ok(torch, dist, ok)}
     del sb, rb
     # C5: allreduce_bine_bdw_remap fp64 / int64 SUM, 256 MiB per rank
-    n = 33_554_432
+    n = C5_ELEMS
     for dt, tdt in (("double", torch.float64), ("int64", torch.int64)):
         sb = torch.empty(n, dtype=tdt, device=dev)
         rb = torch.empty(n, dtype=tdt, device=dev)
-        pico_amd.fill_pico(sb, n, dt, 99 + rank)
-        ms, _ = _timed(torch, dist, comm, stream,
-                       lambda: pico_amd.allreduce("bine_bdw_remap", sb, rb, n, dt, "sum", comm, stream=stream), 5, 2)
+        pico_amd.fill_pico(sb, n, dt, 1234 + rank)
+        st = timed(torch, stream,
+                   lambda: pico_amd.allreduce("bine_bdw_remap", sb, rb, n, dt, "sum", comm, stream=stream),
+                   5, 2, dist, (comm.synchronize,))
+        ok, _ = check_digest(pico_amd, rb, n, dt, gkey("C5", "allreduce", "bine_bdw_remap", dt, n, world, trees), rank)
         S = n * 8
+        ms = st["median_ms"]
         out[f"C5_allreduce_bine_bdw_remap_{dt}_256MiB"] = {
             "ms": round(ms, 4), "algbw_per_rank_GBs": round(S / (ms * 1e-3) / 1e9, 2),
-            "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2)}
+            "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2),
+            "parity_ok": all_ok(torch, dist, ok)}
         del sb, rb
     torch.cuda.empty_cache()
     return out
@@ -383,7 +553,7 @@ def _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, per_peer=3
     """RCCL P2P calibration of this node through the same transport the
     collectives use (bine_exchange = one ncclGroupStart/End): (a) one peer,
     rank r <-> r^1 both ways; (b) all P-1 peers at once (what relay / trees
-    modes do per step).  GB/s per rank and direction, max-over-ranks time."""
+    modes do per step).  GB/s per rank and direction."""
     out = {"bytes_per_peer": per_peer}
     sb = torch.empty(per_peer * (world - 1), dtype=torch.uint8, device=dev)
     rb = torch.empty(per_peer * (world - 1), dtype=torch.uint8, device=dev)
@@ -391,15 +561,16 @@ def _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, per_peer=3
     torch.cuda.synchronize()
     if world % 2 == 0:
         peer = rank ^ 1
-        ms, _ = _timed(torch, dist, comm, stream,
-                       lambda: pico_amd.exchange(comm, [(peer, sb, per_peer)], [(peer, rb, per_peer)], stream=stream),
-                       10, 3)
-        out["one_peer_GBs"] = round(per_peer / (ms * 1e-3) / 1e9, 2)
+        st = timed(torch, stream,
+                   lambda: pico_amd.exchange(comm, [(peer, sb, per_peer)], [(peer, rb, per_peer)], stream=stream),
+                   10, 3, dist, (comm.synchronize,))
+        out["one_peer_GBs"] = round(per_peer / (st["median_ms"] * 1e-3) / 1e9, 2)
     peers = [p for p in range(world) if p != rank]
     sends = [(p, sb[i * per_peer:], per_peer) for i, p in enumerate(peers)]
     recvs = [(p, rb[i * per_peer:], per_peer) for i, p in enumerate(peers)]
-    ms, _ = _timed(torch, dist, comm, stream, lambda: pico_amd.exchange(comm, sends, recvs, stream=stream), 10, 3)
-    out["all_peers_egress_GBs"] = round(len(peers) * per_peer / (ms * 1e-3) / 1e9, 2)
+    st = timed(torch, stream, lambda: pico_amd.exchange(comm, sends, recvs, stream=stream), 10, 3, dist,
+               (comm.synchronize,))
+    out["all_peers_egress_GBs"] = round(len(peers) * per_peer / (st["median_ms"] * 1e-3) / 1e9, 2)
     del sb, rb
     torch.cuda.empty_cache()
     return out
@@ -410,8 +581,10 @@ def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, wo
     stream: the vendor collective the Bine path competes with on this node.
     Its reduction order is RCCL's, not the reference's (a baseline, not a
     libbine result)."""
-    ms, _ = _timed(torch, dist, comm, stream,
-                   lambda: pico_amd.vendor_allreduce(sbuf, rbuf, nelem, "float", "sum", comm, stream=stream), 10, 3)
+    st = timed(torch, stream,
+               lambda: pico_amd.vendor_allreduce(sbuf, rbuf, nelem, "float", "sum", comm, stream=stream),
+               10, 3, dist, (comm.synchronize,))
+    ms = st["median_ms"]
     S = nelem * 4
     return {"ms": round(ms, 4), "algbw_per_rank_GBs": round(S / (ms * 1e-3) / 1e9, 2),
             "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2),
@@ -420,13 +593,59 @@ def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, wo
 
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
 CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
+MODES = {"off": ["direct"],
+         "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+flat+a2a",
+                  "trees"]}
+
+
+def transport_modes(relay: str, world: int):
+    """transports: "direct" = the literal Bine schedule (one peer per step);
+    "relay" = the same schedule with permutation steps routed over all links
+    (two hops); "+flat" = the allgather phase as one all-peers exchange (one
+    hop on every link); "flatrs" = the reduce-scatter phase as one all-peers
+    exchange whose owner evaluates the reference's reduction tree in one fused
+    kernel; "+ag" / "+a2a" = the flat exchanges as ncclAllGather /
+    ncclAllToAllv; "trees" = P-1 relabelled instances over edge-disjoint
+    pairings.  All but "trees" are bit-identical to the reference."""
+    modes = MODES.get(relay, [relay])
+    if world <= 2:
+        modes = [m for m in modes if "relay" not in m and "+ag" not in m and "+a2a" not in m] or ["direct"]
+    if world not in (4, 8):
+        modes = [m for m in modes if m != "trees"] or ["direct"]
+    if world & (world - 1):
+        modes = [m for m in modes if "flat" not in m] or ["direct"]
+    return modes
+
+
+def link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen):
+    """bytes this rank puts on xGMI per allreduce (executed schedule) and the
+    schedule-aware link bound: exchange ops run one after another, the links
+    of one op in parallel, so at B GB/s per link the schedule needs at least
+    L / B, L = sum over ops of the busiest link's bytes"""
+    ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4, chunk_bytes=chunk,
+                                  relay_min_bytes=RELAY_MIN_BYTES if "relay" in chosen else 0,
+                                  trees=chosen == "trees", flat_ag="flat" in chosen, flat_rs="flatrs" in chosen)
+    egress = 4 * sum(p["count"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND")
+    peers = len({p["peer"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND"})
+    L = 0
+    op_links = []  # per exchange op: (busiest directed link's bytes, peers it talks to)
+    for o in ops:
+        if o["xchg"]:
+            lk = {}
+            for p in o["prims"]:
+                if p["type"] in ("SEND", "RECV"):
+                    lk[(p["type"], p["peer"])] = lk.get((p["type"], p["peer"]), 0) + 4 * p["count"]
+            L += max(lk.values())
+            op_links.append((max(lk.values()), len({p["peer"] for p in o["prims"]})))
+    return egress, peers, L, op_links
 
 
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
                     chunk_mib: int = 0):
+    import pico_amd
+    pico_amd.lib()      # map the RCCL this library was compiled against before torch loads its own
     import torch
     import torch.distributed as dist
-    import pico_amd
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     if os.environ.get("BINE_FAKE_HOSTS") == "1":
@@ -444,82 +663,84 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     pico_amd.fill_pico(sbuf, nelem, "float", 1234 + rank)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
-    # transport: direct (one peer per step, the literal Bine schedule), the
-    # multi-link relay of the same schedule (identical results), or multi-tree
-    # (P-1 relabelled instances over edge-disjoint pairings; integer results
-    # identical, fp within rounding).  "auto" times each briefly (max over
-    # ranks, so every rank picks the same) and keeps the fastest.
-    # transports: "direct" = the literal Bine schedule (one peer per step);
-    # "relay" = the same schedule with permutation steps routed over all links
-    # (two hops); "+flat" = the allgather phase as one all-peers exchange
-    # (one hop on every link); "trees" = P-1 relabelled instances over
-    # edge-disjoint pairings; "flatrs" = the reduce-scatter phase as one
-    # all-peers exchange whose owner evaluates the reference's reduction tree
-    # in one fused kernel.  All but "trees" are bit-identical to the reference.
-    # "+ag" = the same flatrs+flat plan with its one-to-all exchanges run as
-    # RCCL's ncclAllGather (+ device copies) instead of P-1 send/recv pairs;
-    # "+a2a" = its all-peers exchanges (both phases) as one ncclAllToAllv each.
-    modes = {"off": ["direct"], "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag",
-                                         "flatrs+flat+a2a", "trees"],
-             "relay": ["relay"], "trees": ["trees"], "flat": ["flat"], "relay+flat": ["relay+flat"],
-             "flatrs+flat": ["flatrs+flat"], "flatrs": ["flatrs"], "flatrs+flat+ag": ["flatrs+flat+ag"],
-             "flatrs+flat+a2a": ["flatrs+flat+a2a"]
-             }.get(relay, ["direct"])
-    if world <= 2:
-        modes = [m for m in modes if "relay" not in m and "+ag" not in m and "+a2a" not in m] or ["direct"]
-    if world not in (4, 8):
-        modes = [m for m in modes if m != "trees"] or ["direct"]
-    if world & (world - 1):
-        modes = [m for m in modes if "flat" not in m] or ["direct"]
+    modes = transport_modes(relay, world)
     chunks = [chunk_mib << 20] if chunk_mib else list(CHUNK_TRIALS)
+    key = gkey("C3", "allreduce", algo, "float", nelem, world)
+    key_trees = gkey("C3", "allreduce", algo, "float", nelem, world, True)
 
-    def use(cfg):
-        m, ch = cfg
-        comm.set_relay(RELAY_MIN_BYTES if "relay" in m else 0)
-        comm.set_trees(m == "trees")
-        comm.set_flat_ag("flat" in m)
-        comm.set_flat_rs("flatrs" in m)
-        comm.set_coll_ag("+ag" in m)
-        comm.set_coll_a2a("+a2a" in m)
-        comm.set_chunk(ch)
+    def run():
+        pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
+
+    def parity(mode):
+        ok, d = check_digest(pico_amd, rbuf, nelem, "float", key_trees if mode == "trees" else key, rank, stream)
+        return all_ok(torch, dist, ok), d
 
     # measured, not guessed: each transport is timed briefly on this hardware
-    # (max over ranks, so every rank picks the same), then the pipelining chunk
-    # for the fastest one; the fastest pair is kept
-    trials = {}
+    # (max over ranks, so every rank picks the same) and its output checked
+    # against the oracle's digest; then the pipelining chunk for the fastest
+    # correct one; the fastest pair is kept
+    trials, verdicts = {}, {}
 
     def trial(cfg):
         # a setting the planner rejects fails identically on every rank before
         # any transfer (plans are a pure function of the arguments): skip it
-        use(cfg)
+        apply_transport(comm, *cfg)
         try:
-            trials[cfg] = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, 3, 2)[0]
+            rbuf.fill_(float("nan"))   # a transport that writes nothing cannot pass on the last one's output
+            st = timed(torch, stream, run, 3, 2, dist, (comm.synchronize,))
+            ok, _ = parity(cfg[0])
+            verdicts[cfg] = ok
+            trials[cfg] = st["median_ms"] if ok is not False else float("inf")
+            if ok is False and rank == 0:
+                print(f"bench: transport {cfg[0]} / chunk {cfg[1] >> 20} MiB EXCLUDED: output digest differs "
+                      "from the oracle's", file=sys.stderr)
         except pico_amd.BineError as e:
             if rank == 0:
                 print(f"bench: transport {cfg[0]} / chunk {cfg[1] >> 20} MiB skipped: {e}", file=sys.stderr)
             torch.cuda.synchronize()
             comm.synchronize()
             trials[cfg] = float("inf")
+            verdicts[cfg] = "error"
 
     mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
     if len(modes) > 1 or len(chunks) > 1:
         for m in modes:
             trial((m, mid))
-        m_best = _prefer_exact({c[0]: v for c, v in trials.items() if c[1] == mid})
+        finite = {c[0]: v for c, v in trials.items() if c[1] == mid and v != float("inf")}
+        m_best = _prefer_exact(finite) if finite else "direct"
         for ch in chunks:
             if (m_best, ch) not in trials:
                 trial((m_best, ch))
-        best = min((c for c in trials if c[0] == m_best), key=trials.get)
+        cands = [c for c in trials if c[0] == m_best and trials[c] != float("inf")]
+        best = min(cands, key=trials.get) if cands else ("direct", mid)
     else:
         best = (modes[0], chunks[0])
-    use(best)
     chosen, chunk = best
-    ms, wall = _time_allreduce(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream, steps, warmup)
-    issue_ms = _timed.issue_ms
+    apply_transport(comm, chosen, chunk)
+    rbuf.fill_(float("nan"))
+    st = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
+    ok_head, dig = parity(chosen)
+    ok_trees_tol = None
+    if chosen == "trees":
+        # fp results of multi-tree mode are the reference's schedule on
+        # relabelled ranks: checked exactly against that (digest above) and
+        # against the reference's own bits with pico_core's ground-truth
+        # tolerance (pico_core_utils.c:960-992: |a - b| <= P * 1e-6 * 100)
+        tree_out = rbuf.clone()
+        apply_transport(comm, "flatrs+flat", chunk)
+        run()
+        torch.cuda.synchronize()
+        ok_exact, _ = parity("flatrs+flat")
+        tol = world * 1e-6 * 100.0
+        ok_trees_tol = all_ok(torch, dist, bool(ok_exact) and float((tree_out - rbuf).abs().max()) <= tol)
+        del tree_out
+        apply_transport(comm, chosen, chunk)
+    ms = st["median_ms"]
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
-    extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
-        if extras else {}
+    extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
+                                                           chosen, chunk)) if extras else {}
+    apply_transport(comm, chosen, chunk)
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}
     vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
@@ -527,64 +748,60 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
-    # bytes this rank puts on xGMI per allreduce (from the executed schedule)
-    ops, _, _ = pico_amd.schedule("allreduce", algo, world, rank, count=nelem, esz=4, chunk_bytes=chunk,
-                                  relay_min_bytes=RELAY_MIN_BYTES if "relay" in chosen else 0,
-                                  trees=chosen == "trees", flat_ag="flat" in chosen,
-                                  flat_rs="flatrs" in chosen)
-    egress = 4 * sum(p["count"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND")
-    peers = len({p["peer"] for o in ops if o["xchg"] for p in o["prims"] if p["type"] == "SEND"})
-    # schedule-aware link roofline: exchange ops run one after another, the
-    # links of one op in parallel, so at B GB/s per link the schedule needs at
-    # least L / B, L = sum over ops of the busiest link's bytes; peak = the
-    # egress rate that bound allows (one link: 153; all 7 links: 1071)
-    L = 0
-    op_links = []  # per exchange op: (busiest directed link's bytes, peers it talks to)
-    for o in ops:
-        if o["xchg"]:
-            lk = {}
-            for p in o["prims"]:
-                if p["type"] in ("SEND", "RECV"):
-                    lk[(p["type"], p["peer"])] = lk.get((p["type"], p["peer"]), 0) + 4 * p["count"]
-            L += max(lk.values())
-            op_links.append((max(lk.values()), len({p["peer"] for p in o["prims"]})))
+    egress, peers, L, op_links = link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen)
+    # schedule-aware link roofline: peak = the egress rate the schedule's link
+    # time allows at 153 GB/s per link (153 for the literal one-peer-per-step
+    # schedule, up to 7 x 153 when every step loads all links)
     link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
+    achieved = egress / (st["mean_ms"] * 1e-3) / 1e9
     out = None
     if rank == 0:
         out = {
-            "metric": "device-resident fp32 allreduce GB/s per rank @256 MiB, 1/2/4/8 MI355X",
-            "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps, "warmup": warmup,
-            "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic (pico_core rand_r distribution, generated on device)",
-            "config": {"workload": f"C3: allreduce_{algo} fp32 {S // MIB} MiB/rank over RCCL P2P (xGMI), "
-                                   f"{world} x MI355X", "value_definition": "N * S / t (whole job)",
+            "metric": METRIC, "value": round(algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
+            "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (pico_core rand_r distribution, seed 1234 + rank, generated on device)",
+            "config": {"workload": f"C3: allreduce_{algo} fp32 SUM {S // MIB} MiB/rank over RCCL P2P (xGMI), "
+                                   f"{world} x MI355X, device-resident",
+                       "value_definition": "per-rank algbw = S / t, t = per-iteration max over ranks, median after "
+                                           "dropping the first 20 % (pico_core.c:133-140, summarize_data.py:24-48)",
+                       "stats_ms": {k: _r(v, 5) for k, v in st.items()},
                        "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
+                       "whole_job_GBs": round(world * algbw, 2),
+                       "busbw_frac_of_target_1071": round(busbw / TARGET_BUSBW_GBS, 4),
                        "transport": chosen,
                        "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
                        "chunk_bytes": chunk,
-                       "host_issue_ms_per_step": round(issue_ms, 4),
+                       "parity": {"headline_ok": ok_head, "digest": str(dig),
+                                  "check": f"bine_checksum(rbuf) on every rank == oracle digest {key}"
+                                           + (" (trees: relabelled-schedule digest)" if chosen == "trees" else ""),
+                                  "trees_within_pico_core_eps": ok_trees_tol,
+                                  "trials": {f"{m}/{ch >> 20}MiB": v for (m, ch), v in verdicts.items()}},
+                       "host_issue_ms_per_step": round(st["issue_ms"], 4),
                        "step_profile_rank0": steps_prof,
                        "transport_trials_ms": {f"{m}/{ch >> 20}MiB": round(v, 4) for (m, ch), v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": extra,
                        "rccl_p2p_probe": probe,
-                       "rccl_allreduce_baseline": vendor},
-            "roofline": {"bound": "xgmi", "achieved": round(egress / (ms * 1e-3) / 1e9, 2), "peak": link_peak,
-                         "unit": "GB/s", "frac": round(egress / (ms * 1e-3) / 1e9 / link_peak, 4),
+                       "rccl_allreduce_baseline": vendor,
+                       "rccl": pico_amd.rccl_version(), "host": host_info()},
+            "roofline": {"bound": "xgmi", "achieved": round(achieved, 2), "peak": link_peak,
+                         "unit": "GB/s", "frac": round(achieved / link_peak, 4),
+                         "frac_of_target_1071_busbw": round(busbw / TARGET_BUSBW_GBS, 4),
                          # traffic = PMC-measured HBM bytes (the N = 1 line); at N > 1 the
                          # bound is the link, whose bytes come from the executed schedule
                          "traffic": None,
                          "egress_bytes": egress,
                          "link_time_bytes": L,
-                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / t; peak = "
-                                 "153 GB/s per link x egress / link_time_bytes (sum over exchange ops of the "
-                                 "busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
-                                 "to 7 x 153 when every step loads all links"},
-            "wall_s": round(wall, 4),
+                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / mean per-iteration "
+                                 "time; peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
+                                 "of the busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
+                                 "to 7 x 153 when every step loads all links; frac_of_target_1071_busbw = busbw / "
+                                 "(7 x 153), the BASELINE target's denominator"},
+            "wall_s": round(st["wall_s"], 4),
         }
-        # the same egress against what RCCL P2P itself moves on this node
-        # the same schedule bound with RCCL's own measured P2P rate per link
-        # per exchange op: its busiest link at what RCCL moves per link in that
+        # the same egress against what RCCL P2P itself moves on this node: per
+        # exchange op its busiest link at what RCCL moves per link in that
         # pattern -- the one-peer rate for a one-peer op, the all-peers egress
         # rate / (P - 1) when the op talks to several peers at once
         one, allp = probe.get("one_peer_GBs"), probe.get("all_peers_egress_GBs")
@@ -611,8 +828,8 @@ def main():
                          "flatrs+flat | flatrs+flat+ag | flatrs+flat+a2a | trees")
     ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/8/16/32/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C4/C5 side measurements")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C1/C4/C5 side measurements")
+    ap.add_argument("--cpu-budget", type=float, default=5.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
         res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay, not args.no_extras,
@@ -620,9 +837,7 @@ def main():
         if res is not None:
             print(json.dumps(res), flush=True)
         return
-    res = bench_c2(args.steps, args.warmup)
-    if not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline_c2(args.cpu_budget)
+    res = bench_n1(args.steps, args.warmup, not args.no_cpu_baseline, args.cpu_budget)
     print(json.dumps(res), flush=True)
 
 

@@ -131,6 +131,10 @@ int bine_reduce_batch(int n, const void *const *a, const void *const *b, void *c
 int bine_reduce_tree(int nleaves, const void *const *leaves, void *out, size_t count, int dtype, int op,
                      void *stream);
 int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
+/* copy_buffer on the device (libbine_utils.h:176-190; the sbuf -> rbuf copy of
+ * e.g. allreduce_bine_bdw_remap, libbine_allreduce.c:849-852): dst[0:bytes) =
+ * src[0:bytes), stream-ordered, the kernel every COPY primitive runs. */
+int bine_copy(void *dst, const void *src, size_t bytes, void *stream);
 /* Order-independent 64-bit digest of a buffer: sum over i of
  * mix64(bits(x[i]) + i * 0x9E3779B97F4A7C15) mod 2^64 (bits zero-extended).
  * Result written to *out (host pointer) after an internal synchronize. */
@@ -139,6 +143,11 @@ int bine_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void 
 /* ---- communicators ---------------------------------------------------------- */
 #define BINE_UNIQUE_ID_BYTES 128
 int bine_get_unique_id(void *id /* BINE_UNIQUE_ID_BYTES */);
+/* RCCL version codes (NCCL_VERSION encoding, e.g. 22606 = 2.26.6): the library
+ * the process maps (ncclGetVersion) and the headers this library was compiled
+ * against.  bine_comm_init_rccl refuses a runtime of another major version or
+ * older than 2.26.0 (BINE_ERR_RCCL, reason in bine_last_error). */
+int bine_rccl_version(int *runtime, int *compiled);
 /* One process per GPU, RCCL P2P over xGMI.  `id` from rank 0's
  * bine_get_unique_id(), broadcast by the caller (MPI, torch.distributed...). */
 int bine_comm_init_rccl(bine_comm_t *comm, int nranks, int rank, const void *id, int device);

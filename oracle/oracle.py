@@ -145,6 +145,48 @@ def allgather(algo, sbufs, dtype, in_place_rbufs=None):
     return rbufs, rets.tolist()
 
 
+def _mix64(x):
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def digest(a: np.ndarray) -> int:
+    """bine_checksum's order-independent digest on the host (sum over i of
+    mix64(bits(x[i]) + i * 0x9E3779B97F4A7C15) mod 2^64), in slabs to bound
+    memory -- the size-independent form in which full-size oracle outputs are
+    compared with the device's (tests/golden/bench_digests.json)."""
+    bits_t = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize]
+    raw = a.view(bits_t)
+    tot = np.uint64(0)
+    slab = 1 << 22
+    with np.errstate(over="ignore"):
+        for s in range(0, a.size, slab):
+            bits = raw[s:s + slab].astype(np.uint64)
+            idx = np.arange(s, s + bits.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+            tot = tot + _mix64(bits + idx).sum(dtype=np.uint64)
+    return int(tot)
+
+
+def reduce_tree(leaves, dtype: str, op: str = "sum", swap: int = 0) -> np.ndarray:
+    """The flat reduce-scatter's tree (bine_reduce_tree) as the literal
+    schedule computes it: pairwise MPI_Reduce_local calls level by level,
+    v[j] = v[j] (op) v[j + w] (libbine_allreduce.c:888's operand order:
+    inout = the left subtree; levels whose bit is set in `swap` keep the right
+    subtree as inout, libbine_reduce_scatter.c:1143)."""
+    v = [np.array(x, copy=True) for x in leaves]
+    w, lvl = 1, 0
+    while w < len(v):
+        for j in range(0, len(v), 2 * w):
+            if (swap >> lvl) & 1:
+                reduce_local(v[j], v[j + w], dtype, op)
+                v[j] = v[j + w]
+            else:
+                reduce_local(v[j + w], v[j], dtype, op)
+        w, lvl = 2 * w, lvl + 1
+    return v[0]
+
+
 def rs_rcounts(N: int, P: int, kind: str = "even"):
     """Block sizes used by the golden capture (oracle/ref_golden.c)."""
     return [N // P + ((i % 3) if kind == "ragged" else 0) for i in range(P)]

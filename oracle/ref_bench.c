@@ -18,7 +18,9 @@
  *       every rank fills N floats (seed 1234 + rank, pico_core_utils.c:902-923)
  *       and calls allreduce_<algo> <iters> times; per iteration the time is
  *       the max over ranks (pico_core.c:133-140), the statistic the median
- *       after dropping the first 20 % (plot/summarize_data.py:24-48).
+ *       after dropping the first 20 % (plot/summarize_data.py:24-48).  Also
+ *       prints the bine_checksum digest of rank 0's output, so bench.py can
+ *       compare the REAL reference's result with the GPU's in the same run.
  * Prints one JSON object on rank 0.
  */
 #include <mpi.h>
@@ -43,6 +45,19 @@ static ar_fn pick_allreduce(const char *a) {
 /* pico_core's float distribution (pico_core_utils.c:911), glibc rand_r */
 static void fill_float(float *buf, size_t n, unsigned int seed) {
   for (size_t i = 0; i < n; i++) buf[i] = (float)rand_r(&seed) / (float)RAND_MAX * 100.0f;
+}
+
+/* bine_checksum's digest (include/bine_amd.h) of n 32-bit words */
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static uint64_t digest32(const void *buf, size_t n) {
+  const uint32_t *w = (const uint32_t *)buf;
+  uint64_t acc = 0;
+  for (size_t i = 0; i < n; i++) acc += mix64((uint64_t)w[i] + (uint64_t)i * 0x9E3779B97F4A7C15ull);
+  return acc;
 }
 
 static int cmp_double(const void *a, const void *b) {
@@ -106,7 +121,8 @@ int main(int argc, char **argv) {
     double med = (m % 2) ? t[skip + m / 2] : 0.5 * (t[skip + m / 2 - 1] + t[skip + m / 2]);
     if (rank == 0)
       printf("{\"mode\": \"allreduce\", \"algo\": \"%s\", \"P\": %d, \"N\": %zu, \"iters\": %d, "
-             "\"median_s\": %.9f, \"rc\": %d}\n", argv[2], P, N, iters, med, rc);
+             "\"median_s\": %.9f, \"rc\": %d, \"digest\": \"%llu\"}\n", argv[2], P, N, iters, med, rc,
+             (unsigned long long)digest32(rb, N));
     free(sb); free(rb); free(t);
   } else {
     if (!rank) fprintf(stderr, "unknown mode %s\n", argv[1]);

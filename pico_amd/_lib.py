@@ -92,6 +92,8 @@ def lib():
         "bine_reduce_local": ([vp, vp, sz, i, i, vp], i),
         "bine_reduce3": ([vp, vp, vp, sz, i, i, vp], i),
         "bine_fill_pico": ([vp, sz, i, u32, vp], i),
+        "bine_copy": ([vp, vp, sz, vp], i),
+        "bine_rccl_version": ([ctypes.POINTER(i), ctypes.POINTER(i)], i),
         "bine_checksum": ([vp, sz, i, ctypes.POINTER(u64), vp], i),
         "bine_get_unique_id": ([vp], i),
         "bine_comm_init_rccl": ([ctypes.POINTER(vp), i, i, vp, i], i),

@@ -203,6 +203,24 @@ def fill_pico(buf, count: int, dtype=None, seed: int = 1234, stream=None) -> Non
           "bine_fill_pico")
 
 
+def copy(dst, src, nbytes: int, stream=None) -> None:
+    """copy_buffer on the device (bine_copy: the k_copy kernel every COPY
+    primitive runs)."""
+    check(lib().bine_copy(_ptr(dst), _ptr(src), nbytes, _stream(stream, None)), "bine_copy")
+
+
+def rccl_version() -> dict:
+    """{"runtime": code, "compiled": code, ...}: the RCCL this process maps vs the
+    headers libbine_amd.so was compiled against (NCCL_VERSION codes)."""
+    rt, ct = ctypes.c_int(), ctypes.c_int()
+    check(lib().bine_rccl_version(ctypes.byref(rt), ctypes.byref(ct)), "bine_rccl_version")
+
+    def fmt(v):
+        return f"{v // 10000}.{v // 100 % 100}.{v % 100}"
+    return {"runtime": fmt(rt.value), "compiled": fmt(ct.value), "runtime_code": rt.value,
+            "compiled_code": ct.value}
+
+
 def checksum(buf, count: int, dtype=None, stream=None) -> int:
     out = ctypes.c_uint64()
     check(lib().bine_checksum(_ptr(buf), count, _dtype(dtype, buf), ctypes.byref(out), _stream(stream, None)),
@@ -415,7 +433,8 @@ for _n in ALGOS["allgather"]:
     ENTRY_POINTS["allgather_" + _n] = _mk_ag(_n)
 globals().update(ENTRY_POINTS)
 
-__all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum",
+__all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum", "copy",
+           "rccl_version",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "reduce_batch",
            "exchange", "vendor_allreduce", "reduce_tree"] + list(ENTRY_POINTS)

@@ -113,6 +113,9 @@ int launch_reduce_batch(int n, const void *const *a, const void *const *b, void 
 constexpr int kMaxLeaves = 16;
 int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream,
                        unsigned swap = 0);
+// copy_buffer on the device (k_copy); hipMemcpyAsync when src / dst are not
+// co-aligned mod 16 B
+int launch_copy(void *dst, const void *src, size_t bytes, void *stream);
 int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
 int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
 

@@ -143,8 +143,10 @@ struct RcclTransport final : Transport {
     static const bool trace = getenv("BINE_TRACE") && atoi(getenv("BINE_TRACE")) != 0;
     if (trace) fprintf(stderr, "[bine r%d] coll_ag ncclAllGather %zu B per rank\n", rank, b);
     NCCL_TRY(ncclAllGather(s[0].ptr, stage, b, ncclUint8, comm, st));
-    for (const auto &x : r)
-      HIP_TRY(hipMemcpyAsync(x.ptr, (const char *)stage + (size_t)x.peer * b, b, hipMemcpyDeviceToDevice, st));
+    for (const auto &x : r) {
+      const int rc = launch_copy(x.ptr, (const char *)stage + (size_t)x.peer * b, b, st);
+      if (rc) return rc;
+    }
     return BINE_SUCCESS;
   }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
@@ -445,8 +447,7 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
       rc = launch_reduce(ptr(p.src_buf, p.src_off), ptr(p.aux_buf, p.aux_off), ptr(p.dst_buf, p.dst_off), p.count,
                          dtype, op, K);
     else
-      HIP_TRY(hipMemcpyAsync(ptr(p.dst_buf, p.dst_off), ptr(p.src_buf, p.src_off), p.count * esz,
-                             hipMemcpyDeviceToDevice, K));
+      rc = launch_copy(ptr(p.dst_buf, p.dst_off), ptr(p.src_buf, p.src_off), p.count * esz, K);
     if (rc) return rc;
   }
   return BINE_SUCCESS;
@@ -770,6 +771,11 @@ int bine_reduce_tree(int nleaves, const void *const *leaves, void *out, size_t c
   return launch_reduce_tree(nleaves, leaves, out, count, dtype, op, stream);
 }
 
+int bine_copy(void *dst, const void *src, size_t bytes, void *stream) {
+  if ((!dst || !src) && bytes) return BINE_ERR_ARG;
+  return launch_copy(dst, src, bytes, stream);
+}
+
 int bine_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream) {
   return launch_fill_pico(buf, count, dtype, seed, stream);
 }
@@ -787,8 +793,34 @@ int bine_get_unique_id(void *id) {
   return BINE_SUCCESS;
 }
 
+// RCCL the process actually maps vs the headers this library was compiled
+// against.  In a torch process the loader resolves librccl.so.1 to torch's
+// bundled RCCL (2.26.x in this image) although the headers are ROCm's (2.27.x):
+// the calls used here (group P2P, AllGather, AllToAllv, AllReduce, CommInitRank,
+// 128-byte unique ids) have one ABI across that range, so a different minor
+// version is accepted and reported (bench.py records both); a different major
+// version, or a runtime older than the oldest one the RCCL matrix was run on,
+// is refused at communicator creation.
+constexpr int kMinRcclVersion = 22600;  // 2.26.0
+
+int bine_rccl_version(int *runtime, int *compiled) {
+  int v = 0;
+  NCCL_TRY(ncclGetVersion(&v));
+  if (runtime) *runtime = v;
+  if (compiled) *compiled = NCCL_VERSION_CODE;
+  return BINE_SUCCESS;
+}
+
 int bine_comm_init_rccl(bine_comm_t *out, int nranks, int rank, const void *id, int device) {
   if (!out || nranks < 1 || rank < 0 || rank >= nranks || !id) return BINE_ERR_ARG;
+  int rv = 0;
+  int rc0 = bine_rccl_version(&rv, nullptr);
+  if (rc0) return rc0;
+  if (rv / 10000 != NCCL_VERSION_CODE / 10000 || rv < kMinRcclVersion) {
+    set_err("RCCL runtime %d is not ABI-compatible with the headers this library was built with (%d; need major "
+            "%d, >= %d)", rv, NCCL_VERSION_CODE, NCCL_VERSION_CODE / 10000, kMinRcclVersion);
+    return BINE_ERR_RCCL;
+  }
   auto c = std::make_unique<bine_comm>();
   c->rank = rank;
   c->size = nranks;

@@ -4,10 +4,18 @@
 //    32 call sites of libbine's reduce family (e.g. libbine_allreduce.c:888):
 //    out[i] = b[i] (op) a[i], out may alias b.  HBM-bound streaming kernel:
 //    16 B per lane per access (global_load_dwordx4), U independent 16-B vectors
-//    per lane in flight, grid capped near the chip's resident-wave capacity and
-//    grid-strided.  No LDS: every byte is touched once, so staging through LDS
-//    would only add instructions.  Arithmetic follows MPICH 3.3.2 exactly
-//    (inout (op) in, no FMA contraction, no denormal flushing, integer wrap).
+//    per lane in flight, one tile of 256 x U vectors per workgroup (no grid
+//    cap below 16,384 workgroups, no grid-stride loop: measured faster on
+//    MI355X, profiles/r1_explore.txt).  No LDS: every byte is touched once, so
+//    staging through LDS would only add instructions.  Arithmetic follows
+//    MPICH 3.3.2 exactly (inout (op) in, no FMA contraction, no denormal
+//    flushing, integer wrap).
+//  * k_copy: the device form of libbine's copy_buffer (libbine_utils.h:176-190,
+//    e.g. the sbuf -> rbuf copy of allreduce_bine_bdw_remap at
+//    libbine_allreduce.c:849-852 -- the whole P = 1 allreduce).  16-B vectors,
+//    8 per lane in flight, non-temporal loads AND stores: 83 us for 256 MiB
+//    (6.44 TB/s of read + write) vs 98.6 us for hipMemcpyAsync D2D
+//    (tools/copy_variants.hip, profiles/r2_copy_variants.txt).
 //  * k_fill_pico: pico_core's rand_r() input distributions
 //    (pico_core_utils.c:902-923) generated in parallel by LCG jump-ahead,
 //    bit-identical to the sequential host generator.
@@ -232,6 +240,56 @@ int launch_reduce(const void *a, const void *b, void *out, size_t count, int dty
 }
 
 // ----------------------------------------------------------------------------
+// device copy (copy_buffer): one tile of kBlock * kCopyU 16-B vectors per
+// workgroup, loads issued before stores, both non-temporal (the copied bytes
+// are not re-read by this launch).  Bytes before the first 16-B boundary of
+// `dst` and after the last full vector go byte-wise through workgroup 0.
+constexpr int kCopyU = 8;
+
+__global__ __launch_bounds__(kBlock) void k_copy(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                 size_t head, size_t nvec, size_t n) {
+  if (blockIdx.x == 0) {
+    for (size_t i = threadIdx.x; i < head; i += kBlock) dst[i] = src[i];
+    for (size_t i = head + nvec * 16 + threadIdx.x; i < n; i += kBlock) dst[i] = src[i];
+  }
+  const u32x4 *vs = reinterpret_cast<const u32x4 *>(src + head);
+  u32x4 *vd = reinterpret_cast<u32x4 *>(dst + head);
+  const size_t base = (size_t)blockIdx.x * kBlock * kCopyU + threadIdx.x;
+  if (base + (kCopyU - 1) * (size_t)kBlock < nvec) {
+    u32x4 x[kCopyU];
+#pragma unroll
+    for (int u = 0; u < kCopyU; u++) x[u] = __builtin_nontemporal_load(vs + base + (size_t)u * kBlock);
+#pragma unroll
+    for (int u = 0; u < kCopyU; u++) __builtin_nontemporal_store(x[u], vd + base + (size_t)u * kBlock);
+  } else {
+#pragma unroll
+    for (int u = 0; u < kCopyU; u++) {
+      const size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) vd[i] = vs[i];
+    }
+  }
+}
+
+int launch_copy(void *dst, const void *src, size_t bytes, void *stream) {
+  if (bytes == 0 || dst == src) return BINE_SUCCESS;
+  hipStream_t st = (hipStream_t)stream;
+  const uintptr_t so = (uintptr_t)src, dO = (uintptr_t)dst;
+  if ((so ^ dO) & 15) {
+    // not co-aligned mod 16 B (never the case for the plans' element offsets of
+    // 16-B aligned buffers): the runtime's device copy
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+  }
+  size_t head = (16 - (dO & 15)) & 15;
+  if (head > bytes) head = bytes;
+  const size_t nvec = (bytes - head) / 16;
+  const size_t tiles = (nvec + (size_t)kBlock * kCopyU - 1) / ((size_t)kBlock * kCopyU);
+  const unsigned blocks = (unsigned)(tiles ? tiles : 1);
+  hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(kBlock), 0, st, (const uint8_t *)src, (uint8_t *)dst, head, nvec,
+                     bytes);
+  return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
 // batched reduction: up to kMaxBatch independent windows in one launch (the
 // P-1 per-instance chunk reductions of a multi-tree round).  The grid is the
 // concatenation of every window's tiles; a workgroup finds its window by a
@@ -402,9 +460,13 @@ __device__ __forceinline__ void tree_tile(const u32x4 *const *lp, u32x4 *vo, siz
     for (int u = 0; u < U; u++) {
       const size_t i = base + (size_t)u * kBlock;
       if (!GUARD || i < nvec) {
-        // own leaf: plain load; received leaves: read once, non-temporal (two
-        // separate statements: a select between the two loads of one address
-        // is folded into one plain load)
+        // tree position 0: plain load; positions 1..NL-1: non-temporal.  The
+        // rank's own leaf sits at position `pos` of the primitive, which is 0
+        // only on some ranks, so this is "one plain + NL-1 non-temporal
+        // streams", not "own leaf cached": at the C3 chunk (16 MiB per leaf)
+        // no leaf is L2-resident anyway, and the mix measured fastest
+        // (tools/tree_variants.hip).  Two separate statements: a select
+        // between the two loads of one address is folded into one plain load.
         if (g == 0) v[u][0] = lp[0][i];
 #pragma unroll
         for (int j = g == 0 ? 1 : 0; j < G; j++) v[u][j] = __builtin_nontemporal_load(lp[g * G + j] + i);

@@ -15,6 +15,19 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+@pytest.mark.timeout(400)
+def test_rccl_large_messages_4_ranks():
+    """64 MiB per rank, fp32 + fp64, default 16 MiB chunks (several chunks per
+    pipelined step), every bench transport, digests vs the oracle
+    (tools/rccl_large.py)"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "4"], env=env,
+                       capture_output=True, text=True, timeout=380)
+    tail = "\n".join(r.stdout.splitlines()[-16:])
+    assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
+    assert "RESULT P=4" in r.stdout
+
+
 def test_rccl_matrix_4_ranks():
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_matrix.py"), "4"], env=env,

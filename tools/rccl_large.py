@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""The large-message RCCL path in real processes.
+
+P processes share the one GPU of the test box (distinct NCCL_HOSTIDs: RCCL's
+socket transport on `lo`, as tools/rccl_matrix.py) and run
+allreduce_bine_bdw_remap on 64 MiB per rank in fp32 and fp64 with the DEFAULT
+16 MiB pipelining chunk -- so the chunked two-stream pipeline (receive of chunk
+k+1 on the comm stream beside the reduction of chunk k on the compute stream,
+the device form of libbine_allreduce.c:1218-1253) runs over real RCCL with
+several chunks per step -- for every transport bench.py may pick (direct,
+relay, flat, flatrs+flat, +ag, +a2a, trees), plus reduce_scatter_bine_permute_remap
+on a 64 MiB input per rank (direct, flatrs).  Every rank's output digest is
+compared with the oracle's (trees: the relabelled schedule's), computed once
+in the parent.  Each worker loads libbine_amd.so before torch, as bench.py
+does, so the RCCL under test is the one the library was compiled against.
+usage: python tools/rccl_large.py [P]   (exit 0 = every rank, every case ok)
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+N32 = 16_777_216   # 64 MiB fp32
+N64 = 8_388_608    # 64 MiB fp64
+MODES = ("direct", "relay", "flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+flat+a2a", "trees")
+RS_MODES = ("direct", "flatrs")
+
+
+def expected(P):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle as O
+    import test_trees as TT
+    want = {}
+    for dt, n in (("float", N32), ("double", N64)):
+        sb = O.inputs(dt, n, P)
+        out, rets = O.allreduce("bine_bdw_remap", sb, dt)
+        assert not any(rets)
+        want[("ar", dt, False)] = [O.digest(x) for x in out]
+        if P in (4, 8):
+            out = TT.relabelled_oracle("bine_bdw_remap", sb, dt)
+            want[("ar", dt, True)] = [O.digest(x) for x in out]
+    rc = [N32 // P] * P
+    sb = O.inputs("float", N32, P)
+    out, rets = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
+    assert not any(rets)
+    want[("rs", "float", False)] = [O.digest(x) for x in out]
+    return want
+
+
+def worker(rank, P, port, want, q):
+    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
+    import pico_amd
+    pico_amd.lib()
+    import torch
+    import torch.distributed as dist
+    import bench
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    comm = pico_amd.Comm.from_torch_distributed(0)
+    bad, n_ok = [], 0
+    modes = [m for m in MODES if m in bench.transport_modes("auto", P)]
+    for dt, n, tdt in (("float", N32, torch.float32), ("double", N64, torch.float64)):
+        s = torch.empty(n, dtype=tdt, device="cuda:0")
+        r = torch.empty(n, dtype=tdt, device="cuda:0")
+        pico_amd.fill_pico(s, n, dt, 1234 + rank)
+        for m in modes:
+            bench.apply_transport(comm, m, 0)   # 0: the library default chunk (16 MiB)
+            for it in range(2):
+                r.fill_(float("nan"))
+                pico_amd.allreduce("bine_bdw_remap", s, r, n, dt, "sum", comm)
+                torch.cuda.synchronize()
+                comm.synchronize()
+                d = pico_amd.checksum(r, n, dt)
+                if d == want[("ar", dt, m == "trees")][rank]:
+                    n_ok += 1
+                else:
+                    bad.append(f"allreduce {dt} {m} iter {it}")
+            print(f"rank {rank} allreduce {dt} {m}: {'ok' if not bad else 'BAD'}", flush=True)
+        del s, r
+    s = torch.empty(N32, dtype=torch.float32, device="cuda:0")
+    r = torch.empty(N32 // P, dtype=torch.float32, device="cuda:0")
+    pico_amd.fill_pico(s, N32, "float", 1234 + rank)
+    for m in RS_MODES:
+        bench.apply_transport(comm, m, 0)
+        r.fill_(float("nan"))
+        pico_amd.reduce_scatter("bine_permute_remap", s, r, [N32 // P] * P, "float", "sum", comm)
+        torch.cuda.synchronize()
+        comm.synchronize()
+        if pico_amd.checksum(r, N32 // P, "float") == want[("rs", "float", False)][rank]:
+            n_ok += 1
+        else:
+            bad.append(f"reduce_scatter {m}")
+    for b in bad:
+        print(f"rank {rank} MISMATCH {b}", flush=True)
+    print(f"rank {rank} rccl {pico_amd.rccl_version()}", flush=True)
+    comm.destroy()
+    dist.destroy_process_group()
+    q.put((rank, n_ok, len(bad)))
+
+
+if __name__ == "__main__":
+    import multiprocessing as mp
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    want = expected(P)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=worker, args=(r, P, 29591, want, q)) for r in range(P)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(600)
+    res = [q.get() for _ in range(sum(1 for p in ps if p.exitcode == 0))]
+    print("RESULT P=%d" % P, sorted(res), "exitcodes", [p.exitcode for p in ps], flush=True)
+    sys.exit(0 if len(res) == P and all(b == 0 for _, _, b in res) else 1)

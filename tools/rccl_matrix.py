@@ -40,9 +40,10 @@ def worker(rank, P, port, q):
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
     import numpy as np
+    import pico_amd
+    pico_amd.lib()   # as bench.py: the RCCL libbine_amd.so was compiled against, loaded before torch's
     import torch
     import torch.distributed as dist
-    import pico_amd
     from oracle import oracle as O
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
