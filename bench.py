@@ -124,12 +124,17 @@ def all_ok(torch, dist, ok):
 
 # ---- timing (the reference's statistic) --------------------------------------------
 
-def timed(torch, stream, call, steps, warmup, dist=None, syncs=()):
-    """K iterations of call() back to back, each bracketed by its own event
-    pair on `stream`; per iteration the max over ranks; the first 20 %
+def timed(torch, stream, call, steps, warmup, dist=None, syncs=(), per_iter=True):
+    """K iterations of call() back to back between a barrier + device
+    synchronize on both sides.  per_iter: each iteration bracketed by its own
+    event pair on `stream`; per iteration the max over ranks; the first 20 %
     dropped; the median (pico_core.c:133-140, summarize_data.py:24-48).
+    Always: one event pair around the whole timed region, region_ms = its
+    time / K (the average launch duration a kernel-trace profile reports for
+    single-kernel calls; per-iteration events add a dispatch bubble each).
     Returns {median_ms, mean_ms (of the kept samples), min_ms, max_ms, samples,
-    issue_ms (host time per call spent enqueueing, max over ranks), wall_s}."""
+    region_ms, issue_ms (host time per call spent enqueueing, max over ranks),
+    wall_s}; without per_iter the per-iteration fields are region_ms."""
     def sync():
         torch.cuda.synchronize()
         for s in syncs:
@@ -140,27 +145,51 @@ def timed(torch, stream, call, steps, warmup, dist=None, syncs=()):
     if dist is not None:
         dist.barrier()
     sync()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    evs = [(ev(), ev()) for _ in range(steps)] if per_iter else []
+    r0, r1 = ev(), ev()
     issue = 0.0
     t0 = time.perf_counter()
-    for a, b in evs:
-        a.record(stream)
+    r0.record(stream)
+    for i in range(steps):
+        if per_iter:
+            evs[i][0].record(stream)
         ti = time.perf_counter()
         call()
         issue += time.perf_counter() - ti
-        b.record(stream)
+        if per_iter:
+            evs[i][1].record(stream)
+    r1.record(stream)
     sync()
     wall = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
     per = [a.elapsed_time(b) for a, b in evs]
-    t = torch.tensor(per + [issue * 1e3 / steps, wall], dtype=torch.float64)
+    t = torch.tensor(per + [r0.elapsed_time(r1) / steps, issue * 1e3 / steps, wall], dtype=torch.float64)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    per = [float(x) for x in t[:steps]]
-    kept = per[int(steps * WARMUP_DROP):] or per
+    region = float(t[len(per)])
+    per = [float(x) for x in t[:len(per)]] or [region]
+    kept = per[int(len(per) * WARMUP_DROP):] or per
     return {"median_ms": statistics.median(kept), "mean_ms": statistics.fmean(kept), "min_ms": min(kept),
-            "max_ms": max(kept), "samples": len(kept), "issue_ms": float(t[steps]), "wall_s": float(t[steps + 1])}
+            "max_ms": max(kept), "samples": len(kept) if per_iter else 0, "region_ms": region,
+            "issue_ms": float(t[len(t) - 2]), "wall_s": float(t[len(t) - 1])}
+
+
+class quiet_stdout:
+    """fd 1 -> fd 2 while RCCL initialises a communicator: RCCL prints its
+    version banner on stdout, and bench.py's stdout is one JSON line"""
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
 
 
 def _r(x, n=4):
@@ -278,7 +307,7 @@ def _side_reduce(torch, pico_amd, dev, stream, steps, warmup):
     def call():
         pico_amd.reduce_local(ins[i[0] % sets], ios[i[0] % sets], C2_ELEMS, "float", "sum", stream=stream)
         i[0] += 1
-    st = timed(torch, stream, call, steps, warmup)
+    st = timed(torch, stream, call, steps, warmup, per_iter=False)
     pico_amd.fill_pico(ins[0], C2_ELEMS, "float", 1234)
     pico_amd.fill_pico(ios[0], C2_ELEMS, "float", 1235)
     pico_amd.reduce_local(ins[0], ios[0], C2_ELEMS, "float", "sum", stream=stream)
@@ -287,10 +316,10 @@ def _side_reduce(torch, pico_amd, dev, stream, steps, warmup):
     torch.cuda.empty_cache()
     alg = 3 * C2_ELEMS * 4
     return {"kernel": "bine::k_reduce<float,SUM>", "workload": "C2: fp32 inout += in, 64 MiB, 1 GPU",
-            "parity_ok": ok, "us_median": round(st["median_ms"] * 1e3, 3), "samples": st["samples"],
-            "roofline": {"bound": "hbm", "achieved": round(alg / (st["mean_ms"] * 1e-3) / 1e9, 1),
+            "parity_ok": ok, "us_per_launch": round(st["region_ms"] * 1e3, 3), "launches": steps,
+            "roofline": {"bound": "hbm", "achieved": round(alg / (st["region_ms"] * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(alg / (st["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "frac": round(alg / (st["region_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic": _pmc_traffic("k_reduce"), "algorithmic_bytes_per_launch": alg}}
 
 
@@ -312,17 +341,17 @@ def _side_tree(torch, pico_amd, dev, stream, steps, warmup):
         rc = pico_amd.reduce_tree(leaves, out, TREE_ELEMS, "float", "sum", stream=stream)
         assert rc == 0, rc
         i[0] += 1
-    st = timed(torch, stream, call, steps, warmup)
+    st = timed(torch, stream, call, steps, warmup, per_iter=False)
     ok, _ = check_digest(pico_amd, bufs[0][1], TREE_ELEMS, "float",
                          f"tree/reduce_tree/sum/float/N{TREE_ELEMS}/L{TREE_LEAVES}", 0)
     del bufs
     torch.cuda.empty_cache()
     alg = (TREE_LEAVES + 1) * TREE_ELEMS * 4
     return {"kernel": "bine::k_reduce_tree<float,SUM,8>", "leaves": TREE_LEAVES, "elems_per_leaf": TREE_ELEMS,
-            "parity_ok": ok, "us_median": round(st["median_ms"] * 1e3, 3), "samples": st["samples"],
-            "roofline": {"bound": "hbm", "achieved": round(alg / (st["mean_ms"] * 1e-3) / 1e9, 1),
+            "parity_ok": ok, "us_per_launch": round(st["region_ms"] * 1e3, 3), "launches": steps,
+            "roofline": {"bound": "hbm", "achieved": round(alg / (st["region_ms"] * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(alg / (st["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "frac": round(alg / (st["region_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic": _pmc_traffic("k_reduce_tree"), "algorithmic_bytes_per_launch": alg}}
 
 
@@ -344,9 +373,9 @@ def _side_small_windows(torch, pico_amd, dev, stream):
             off = (i[0] % 16) * (region // 16)
             pico_amd.reduce_local(a[off:], b[off:], n, "float", "sum", stream=stream)
             i[0] += 1
-        st = timed(torch, stream, call, 64, 8)
-        gbs = 3 * w / (st["mean_ms"] * 1e-3) / 1e9
-        out[f"{w >> 10}KiB"] = {"us": round(st["mean_ms"] * 1e3, 3), "GBs": round(gbs, 1),
+        st = timed(torch, stream, call, 64, 8, per_iter=False)
+        gbs = 3 * w / (st["region_ms"] * 1e-3) / 1e9
+        out[f"{w >> 10}KiB"] = {"us": round(st["region_ms"] * 1e3, 3), "GBs": round(gbs, 1),
                                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     del a, b
     torch.cuda.empty_cache()
@@ -355,11 +384,11 @@ def _side_small_windows(torch, pico_amd, dev, stream):
 
 def bench_n1(steps: int, warmup: int, want_cpu: bool, cpu_budget: float):
     import pico_amd
-    pico_amd.lib()      # map the RCCL this library was compiled against before torch loads its own
     import torch
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
-    comm = pico_amd.Comm.rccl(0, 1, pico_amd.Comm.unique_id(), 0)
+    with quiet_stdout():
+        comm = pico_amd.Comm.rccl(0, 1, pico_amd.Comm.unique_id(), 0)
     n = C3_ELEMS
     S = n * 4
     sbuf = torch.empty(n, dtype=torch.float32, device=dev)
@@ -378,10 +407,11 @@ def bench_n1(steps: int, warmup: int, want_cpu: bool, cpu_budget: float):
     torch.cuda.empty_cache()
     ms = st["median_ms"]
     algbw = S / (ms * 1e-3) / 1e9
-    hbm = 2 * S / (st["mean_ms"] * 1e-3) / 1e9
+    hbm = 2 * S / (st["region_ms"] * 1e-3) / 1e9
     side = {"k_reduce_C2": _side_reduce(torch, pico_amd, dev, stream, steps, warmup),
-            "k_reduce_tree_C3_flat_rs_chunk": _side_tree(torch, pico_amd, dev, stream, steps, warmup),
-            "k_reduce_small_windows": _side_small_windows(torch, pico_amd, dev, stream)}
+            "k_reduce_tree_C3_flat_rs_chunk": _side_tree(torch, pico_amd, dev, stream, steps, warmup)}
+    if os.environ.get("BENCH_NO_SMALL_WINDOWS") != "1":   # PMC passes: one k_reduce shape only
+        side["k_reduce_small_windows"] = _side_small_windows(torch, pico_amd, dev, stream)
     out = {
         "metric": METRIC, "value": round(algbw, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
         "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -400,8 +430,9 @@ def bench_n1(steps: int, warmup: int, want_cpu: bool, cpu_budget: float):
                      "frac": round(hbm / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_copy"),
                      "kernel": "bine::k_copy (the P = 1 allreduce is one launch)",
                      "algorithmic_bytes_per_launch": 2 * S,
-                     "note": "achieved = 2 S (read sbuf + write rbuf) / mean per-iteration event time of the "
-                             "kept samples; traffic = PMC FETCH_SIZE x 2 (gfx950) + WRITE_SIZE per launch"},
+                     "note": "achieved = 2 S (read sbuf + write rbuf) / (timed-region event time / K), the "
+                             "average launch duration; traffic = PMC FETCH_SIZE x 2 (gfx950) + WRITE_SIZE per "
+                             "launch (profiles/latest_pmc.json)"},
         "wall_s": round(st["wall_s"], 4),
     }
     if want_cpu:
@@ -439,20 +470,33 @@ def _side(rank, what, fn):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
-def overlap_frac(exchange_busy, local_busy, span):
-    """share of the local (reduction) time hidden under exchanges: (exchange
-    busy + local busy - span) / local busy, clipped to [0, 1]"""
-    if local_busy <= 0:
+def overlap_frac(exchanges, locals_):
+    """share of the local (reduction) time that runs while some exchange is in
+    flight: sum over local ops of |local interval & union of exchange
+    intervals| / sum of local durations; intervals are (start, duration)"""
+    tot = sum(d for _, d in locals_)
+    if tot <= 0:
         return None
-    return max(0.0, min(1.0, (exchange_busy + local_busy - span) / local_busy))
+    iv = sorted((s, s + d) for s, d in exchanges if d > 0)
+    merged = []
+    for a, b in iv:
+        if merged and a <= merged[-1][1]:
+            merged[-1][1] = max(merged[-1][1], b)
+        else:
+            merged.append([a, b])
+    hid = 0.0
+    for s, d in locals_:
+        a, b = s, s + d
+        hid += sum(max(0.0, min(b, y) - max(a, x)) for x, y in merged)
+    return min(1.0, hid / tot)
 
 
 def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
     """One extra collective (outside the timed region) with per-op timing
     events (bine_comm_set_profile): where the time of this rank goes -- busy
     time of the comm stream (exchanges) and of the compute stream (reductions),
-    their span, how much of the reductions the exchanges hide, and the
-    exchange ops' egress rates."""
+    their span, the share of the reductions' time during which an exchange
+    is in flight (overlap_frac), and the exchange ops' egress rates."""
     comm.set_profile(True)
     try:
         pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
@@ -467,7 +511,7 @@ def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
     xs = [o for o in ops if o["xchg"]]
     ls = [o for o in ops if not o["xchg"]]
     xb, lb = sum(o["ms"] for o in xs), sum(o["ms"] for o in ls)
-    ov = overlap_frac(xb, lb, span)
+    ov = overlap_frac([(o["start_ms"], o["ms"]) for o in xs], [(o["start_ms"], o["ms"]) for o in ls])
     return {"ops": len(ops), "span_ms": round(span, 4), "exchange_busy_ms": round(xb, 4),
             "local_busy_ms": round(lb, 4), "overlap_frac": None if ov is None else round(ov, 4),
             "exchanges": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4), "peers": o["nprims"],
@@ -643,7 +687,6 @@ def link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen):
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
                     chunk_mib: int = 0):
     import pico_amd
-    pico_amd.lib()      # map the RCCL this library was compiled against before torch loads its own
     import torch
     import torch.distributed as dist
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -656,7 +699,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist.init_process_group("gloo")
-    comm = pico_amd.Comm.from_torch_distributed(local)
+    with quiet_stdout():
+        comm = pico_amd.Comm.from_torch_distributed(local)
     dev = torch.device("cuda", local)
     sbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
     rbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
@@ -753,7 +797,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # time allows at 153 GB/s per link (153 for the literal one-peer-per-step
     # schedule, up to 7 x 153 when every step loads all links)
     link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
-    achieved = egress / (st["mean_ms"] * 1e-3) / 1e9
+    achieved = egress / (st["region_ms"] * 1e-3) / 1e9
     out = None
     if rank == 0:
         out = {
@@ -793,8 +837,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                          "traffic": None,
                          "egress_bytes": egress,
                          "link_time_bytes": L,
-                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / mean per-iteration "
-                                 "time; peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
+                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / (timed-region "
+                                 "time / K); peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
                                  "of the busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
                                  "to 7 x 153 when every step loads all links; frac_of_target_1071_busbw = busbw / "
                                  "(7 x 153), the BASELINE target's denominator"},

@@ -80,6 +80,17 @@ def lib():
         return _lib
     if not os.path.exists(CORE):
         raise ImportError(f"{CORE} not built -- run __graft_entry__.build() (make -C pico_amd/csrc)")
+    # One HIP runtime per process: torch (ROCm wheel) bundles its own
+    # libamdhip64 / libhsa-runtime64 / librccl.  Loaded first, they satisfy this
+    # library's DT_NEEDED by soname and the whole process shares them; loaded
+    # after /opt/rocm's copies (this library first, torch later) the process
+    # would hold two HIP runtimes and one of them sees no device.  So torch, if
+    # installed, is imported before the library is mapped.  The RCCL version
+    # in use is reported by bine_rccl_version() (and recorded by bench.py).
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover -- plain ctypes use without torch: /opt/rocm's runtime
+        pass
     L = ctypes.CDLL(CORE)
     vp, sz, i, u32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
     sigs = {

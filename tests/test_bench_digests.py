@@ -80,10 +80,11 @@ def test_oracle_reduce_tree_is_pairwise_reduce_local():
 
 
 def test_overlap_fraction():
-    assert bench.overlap_frac(10.0, 4.0, 10.0) == 1.0      # reductions fully hidden
-    assert bench.overlap_frac(10.0, 4.0, 14.0) == 0.0      # serial
-    assert bench.overlap_frac(10.0, 4.0, 12.0) == 0.5
-    assert bench.overlap_frac(1.0, 0.0, 1.0) is None
+    assert bench.overlap_frac([(0.0, 10.0)], [(2.0, 4.0)]) == 1.0                  # reductions fully hidden
+    assert bench.overlap_frac([(0.0, 10.0)], [(10.0, 4.0)]) == 0.0                 # serial
+    assert bench.overlap_frac([(0.0, 10.0)], [(8.0, 4.0)]) == 0.5
+    assert bench.overlap_frac([(0.0, 5.0), (4.0, 3.0)], [(6.0, 2.0), (9.0, 1.0)]) == 1 / 3   # union of exchanges
+    assert bench.overlap_frac([(0.0, 1.0)], []) is None
 
 
 def test_transport_modes():

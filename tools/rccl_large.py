@@ -11,8 +11,7 @@ several chunks per step -- for every transport bench.py may pick (direct,
 relay, flat, flatrs+flat, +ag, +a2a, trees), plus reduce_scatter_bine_permute_remap
 on a 64 MiB input per rank (direct, flatrs).  Every rank's output digest is
 compared with the oracle's (trees: the relabelled schedule's), computed once
-in the parent.  Each worker loads libbine_amd.so before torch, as bench.py
-does, so the RCCL under test is the one the library was compiled against.
+in the parent.
 usage: python tools/rccl_large.py [P]   (exit 0 = every rank, every case ok)
 """
 import os
@@ -54,7 +53,6 @@ def worker(rank, P, port, want, q):
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
     import pico_amd
-    pico_amd.lib()
     import torch
     import torch.distributed as dist
     import bench

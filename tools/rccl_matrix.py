@@ -41,7 +41,6 @@ def worker(rank, P, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
     import numpy as np
     import pico_amd
-    pico_amd.lib()   # as bench.py: the RCCL libbine_amd.so was compiled against, loaded before torch's
     import torch
     import torch.distributed as dist
     from oracle import oracle as O
