@@ -356,27 +356,33 @@ def _side_tree(torch, pico_amd, dev, stream, steps, warmup):
 
 
 def _side_small_windows(torch, pico_amd, dev, stream):
-    """k_reduce at the windows of C1 and of pipelines' tail chunks: 16
-    rotating windows in a 1 GiB region, launches back to back (the
-    launch-to-launch boundary is part of each window's time)"""
+    """k_reduce at the windows of C1 and of pipelines' tail chunks: 64
+    launches over 16 rotating windows of a 1 GiB region, captured once into a
+    HIP graph and replayed, so the launches run back to back with the host out
+    of the loop (the executor issues them from C++; issued one by one from
+    Python through ctypes they would measure the interpreter).  Per window:
+    time per launch incl. the launch-to-launch boundary, HBM GB/s, fraction."""
     region = 1 << 28   # elements (1 GiB fp32) per operand
     a = torch.empty(region, dtype=torch.float32, device=dev)
     b = torch.empty(region, dtype=torch.float32, device=dev)
     pico_amd.fill_pico(a, region, "float", 7)
     pico_amd.fill_pico(b, region, "float", 8)
+    torch.cuda.synchronize()
     out = {}
+    launches = 64
     for w in (256 << 10, 1 << 20, 4 << 20, 16 << 20):
         n = w // 4
-        i = [0]
-
-        def call():
-            off = (i[0] % 16) * (region // 16)
-            pico_amd.reduce_local(a[off:], b[off:], n, "float", "sum", stream=stream)
-            i[0] += 1
-        st = timed(torch, stream, call, 64, 8, per_iter=False)
-        gbs = 3 * w / (st["region_ms"] * 1e-3) / 1e9
-        out[f"{w >> 10}KiB"] = {"us": round(st["region_ms"] * 1e3, 3), "GBs": round(gbs, 1),
-                                "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream(dev)
+        with torch.cuda.graph(g, stream=cs):
+            for i in range(launches):
+                off = (i % 16) * (region // 16)
+                pico_amd.reduce_local(a[off:], b[off:], n, "float", "sum", stream=cs)
+        st = timed(torch, stream, g.replay, 8, 2, per_iter=False)
+        us = st["region_ms"] * 1e3 / launches
+        gbs = 3 * w / (us * 1e-6) / 1e9
+        out[f"{w >> 10}KiB"] = {"us_per_launch": round(us, 3), "GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        del g
     del a, b
     torch.cuda.empty_cache()
     return out
@@ -407,7 +413,7 @@ def bench_n1(steps: int, warmup: int, want_cpu: bool, cpu_budget: float):
     torch.cuda.empty_cache()
     ms = st["median_ms"]
     algbw = S / (ms * 1e-3) / 1e9
-    hbm = 2 * S / (st["region_ms"] * 1e-3) / 1e9
+    hbm = 2 * S / (st["mean_ms"] * 1e-3) / 1e9
     side = {"k_reduce_C2": _side_reduce(torch, pico_amd, dev, stream, steps, warmup),
             "k_reduce_tree_C3_flat_rs_chunk": _side_tree(torch, pico_amd, dev, stream, steps, warmup)}
     if os.environ.get("BENCH_NO_SMALL_WINDOWS") != "1":   # PMC passes: one k_reduce shape only
@@ -430,9 +436,10 @@ def bench_n1(steps: int, warmup: int, want_cpu: bool, cpu_budget: float):
                      "frac": round(hbm / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_copy"),
                      "kernel": "bine::k_copy (the P = 1 allreduce is one launch)",
                      "algorithmic_bytes_per_launch": 2 * S,
-                     "note": "achieved = 2 S (read sbuf + write rbuf) / (timed-region event time / K), the "
-                             "average launch duration; traffic = PMC FETCH_SIZE x 2 (gfx950) + WRITE_SIZE per "
-                             "launch (profiles/latest_pmc.json)"},
+                     "note": "achieved = 2 S (read sbuf + write rbuf) / mean of the kept per-iteration event "
+                             "times (one k_copy launch each; agrees with the kernel-trace average within ~1 %, "
+                             "profiles/r2_bench_kernel_stats.csv); traffic = PMC FETCH_SIZE x 2 (gfx950) + "
+                             "WRITE_SIZE per launch (profiles/latest_pmc.json)"},
         "wall_s": round(st["wall_s"], 4),
     }
     if want_cpu:
@@ -492,6 +499,11 @@ def overlap_frac(exchanges, locals_):
 
 
 def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
+    return step_profile(torch, comm,
+                        lambda: pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream))
+
+
+def step_profile(torch, comm, call):
     """One extra collective (outside the timed region) with per-op timing
     events (bine_comm_set_profile): where the time of this rank goes -- busy
     time of the comm stream (exchanges) and of the compute stream (reductions),
@@ -499,7 +511,7 @@ def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
     is in flight (overlap_frac), and the exchange ops' egress rates."""
     comm.set_profile(True)
     try:
-        pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
+        call()
         torch.cuda.synchronize()
         comm.synchronize()
         ops = comm.profile()
@@ -638,8 +650,9 @@ def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, wo
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
 CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 MODES = {"off": ["direct"],
-         "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+flat+a2a",
-                  "trees"]}
+         # "+a2a" is not tried: RCCL runs ncclAllToAllv as the same grouped P2P kernel
+         # (rcclGenericKernel) as P-1 ncclSend/ncclRecv pairs (profiles/r2_a2a_vs_p2p_kernels.txt)
+         "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag", "trees"]}
 
 
 def transport_modes(relay: str, world: int):
@@ -797,7 +810,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # time allows at 153 GB/s per link (153 for the literal one-peer-per-step
     # schedule, up to 7 x 153 when every step loads all links)
     link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
-    achieved = egress / (st["region_ms"] * 1e-3) / 1e9
+    achieved = egress / (st["mean_ms"] * 1e-3) / 1e9
     out = None
     if rank == 0:
         out = {
@@ -837,8 +850,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                          "traffic": None,
                          "egress_bytes": egress,
                          "link_time_bytes": L,
-                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / (timed-region "
-                                 "time / K); peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
+                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / mean kept "
+                                 "per-iteration time; peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
                                  "of the busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
                                  "to 7 x 153 when every step loads all links; frac_of_target_1071_busbw = busbw / "
                                  "(7 x 153), the BASELINE target's denominator"},

@@ -221,10 +221,13 @@ int bine_comm_set_coll_ag(bine_comm_t comm, int on);
 /* Transport option for RCCL communicators (P >= 3), used only with relay and
  * multi-tree mode off: an exchange with exactly one message of the same size
  * to and from every other rank (the flat reduce-scatter and allgather phases)
- * runs as ONE ncclAllToAllv (RCCL's all-to-all kernels) instead of P-1
- * ncclSend/ncclRecv pairs; same bytes, same places, results unchanged.  Takes
- * precedence over bine_comm_set_coll_ag.  Off by default (BINE_COLL_A2A=1);
- * collective; loopback: BINE_ERR_UNSUPPORTED. */
+ * runs as ONE ncclAllToAllv call instead of P-1 ncclSend/ncclRecv pairs; same
+ * bytes, same places, results unchanged.  RCCL 2.26 implements ncclAllToAllv
+ * with the same grouped point-to-point kernel (rcclGenericKernel, one launch
+ * per exchange either way: profiles/r2_a2a_vs_p2p_kernels.txt), so this is an
+ * API variant, not a different data path; bench.py no longer trials it.
+ * Takes precedence over bine_comm_set_coll_ag.  Off by default
+ * (BINE_COLL_A2A=1); collective; loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_coll_a2a(bine_comm_t comm, int on);
 
 /* Flat reduce-scatter phase for every reduce-family algorithm at

@@ -46,17 +46,22 @@ def intersect(u, v):
     return t
 
 
-d = sys.argv[1]
-ks = rows(os.path.join(d, "**", "*kernel_trace.csv"))
-ms = rows(os.path.join(d, "**", "*memory_copy_trace.csv"))
-red = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ks if "k_reduce" in r["Kernel_Name"]]
-cpk = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ks
-       if "k_reduce" not in r["Kernel_Name"] and "fill" not in r["Kernel_Name"]]
-cps = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ms]
-R, X = union(red), union(cpk + cps)
-span = (max(b for _, b in R + X) - min(a for a, _ in R + X)) if R and X else 0
-print(f"reduction kernels: {len(red)} launches, busy {total(R) / 1e6:.3f} ms")
-print(f"exchange copies:   {len(cpk)} copy kernels + {len(cps)} SDMA copies, busy {total(X) / 1e6:.3f} ms")
-print(f"both at once:      {intersect(R, X) / 1e6:.3f} ms "
-      f"({100 * intersect(R, X) / max(1, total(R)):.1f} % of reduction time overlapped)")
-print(f"trace span:        {span / 1e6:.3f} ms")
+def main():
+    d = sys.argv[1]
+    ks = rows(os.path.join(d, "**", "*kernel_trace.csv"))
+    ms = rows(os.path.join(d, "**", "*memory_copy_trace.csv"))
+    red = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ks if "k_reduce" in r["Kernel_Name"]]
+    cpk = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ks
+           if "k_reduce" not in r["Kernel_Name"] and "fill" not in r["Kernel_Name"]]
+    cps = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ms]
+    R, X = union(red), union(cpk + cps)
+    span = (max(b for _, b in R + X) - min(a for a, _ in R + X)) if R and X else 0
+    print(f"reduction kernels: {len(red)} launches, busy {total(R) / 1e6:.3f} ms")
+    print(f"exchange copies:   {len(cpk)} copy kernels + {len(cps)} SDMA copies, busy {total(X) / 1e6:.3f} ms")
+    print(f"both at once:      {intersect(R, X) / 1e6:.3f} ms "
+          f"({100 * intersect(R, X) / max(1, total(R)):.1f} % of reduction time overlapped)")
+    print(f"trace span:        {span / 1e6:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
