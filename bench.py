@@ -534,7 +534,8 @@ def step_profile(torch, comm, call):
                       for o in ls[:24]]}
 
 
-def apply_transport(comm, mode, chunk):
+def apply_transport(comm, mode, chunk, graphs=False):
+    comm.set_graphs(graphs)
     comm.set_relay(RELAY_MIN_BYTES if "relay" in mode else 0)
     comm.set_trees(mode == "trees")
     comm.set_flat_ag("flat" in mode)
@@ -559,12 +560,18 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
     rb = torch.empty(n1, dtype=torch.float32, device=dev)
     pico_amd.fill_pico(sb, n1, "float", 1234 + rank)
     for algo in ("bine_bdw_remap", "bine_lat"):
-        st = timed(torch, stream, lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
-                   50, 10, dist, (comm.synchronize,))
-        ok, _ = check_digest(pico_amd, rb, n1, "float", gkey("C1", "allreduce", algo, "float", n1, world), rank)
-        out[f"C1_allreduce_{algo}_f32_1MiB"] = {
-            "us": round(st["median_ms"] * 1e3, 2), "algbw_per_rank_GBs": round(n1 * 4 / (st["median_ms"] * 1e-3) / 1e9, 2),
-            "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
+        for g in (False, True):   # eager issue, then the HIP-graph replay (bine_comm_set_graphs)
+            comm.set_graphs(g)
+            rb.fill_(float("nan"))
+            st = timed(torch, stream,
+                       lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
+                       50, 10, dist, (comm.synchronize,))
+            ok, _ = check_digest(pico_amd, rb, n1, "float", gkey("C1", "allreduce", algo, "float", n1, world), rank)
+            out[f"C1_allreduce_{algo}_f32_1MiB" + ("_graph" if g else "")] = {
+                "us": round(st["median_ms"] * 1e3, 2),
+                "algbw_per_rank_GBs": round(n1 * 4 / (st["median_ms"] * 1e-3) / 1e9, 2),
+                "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
+    comm.set_graphs(False)
     del sb, rb
     apply_transport(comm, mode, chunk)
     trees = mode == "trees"
@@ -697,8 +704,13 @@ def link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen):
     return egress, peers, L, op_links
 
 
+def tname(cfg):
+    """trial label: transport/chunk[+graph]"""
+    return f"{cfg[0]}/{cfg[1] >> 20}MiB" + ("+graph" if len(cfg) > 2 and cfg[2] else "")
+
+
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
-                    chunk_mib: int = 0):
+                    chunk_mib: int = 0, graph_trial: bool = True):
     import pico_amd
     import torch
     import torch.distributed as dist
@@ -715,11 +727,14 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     with quiet_stdout():
         comm = pico_amd.Comm.from_torch_distributed(local)
     dev = torch.device("cuda", local)
+    # one non-NULL stream for everything (torch ops, fills, checksums and the
+    # collectives): graph mode cannot capture the legacy NULL stream
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
     rbuf = torch.empty(nelem, dtype=torch.float32, device=dev)
     pico_amd.fill_pico(sbuf, nelem, "float", 1234 + rank)
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
     modes = transport_modes(relay, world)
     chunks = [chunk_mib << 20] if chunk_mib else list(CHUNK_TRIALS)
     key = gkey("C3", "allreduce", algo, "float", nelem, world)
@@ -741,6 +756,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     def trial(cfg):
         # a setting the planner rejects fails identically on every rank before
         # any transfer (plans are a pure function of the arguments): skip it
+        if len(cfg) == 2:
+            cfg = cfg + (False,)
         apply_transport(comm, *cfg)
         try:
             rbuf.fill_(float("nan"))   # a transport that writes nothing cannot pass on the last one's output
@@ -749,11 +766,11 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             verdicts[cfg] = ok
             trials[cfg] = st["median_ms"] if ok is not False else float("inf")
             if ok is False and rank == 0:
-                print(f"bench: transport {cfg[0]} / chunk {cfg[1] >> 20} MiB EXCLUDED: output digest differs "
-                      "from the oracle's", file=sys.stderr)
+                print(f"bench: transport {tname(cfg)} EXCLUDED: output digest differs from the oracle's",
+                      file=sys.stderr)
         except pico_amd.BineError as e:
             if rank == 0:
-                print(f"bench: transport {cfg[0]} / chunk {cfg[1] >> 20} MiB skipped: {e}", file=sys.stderr)
+                print(f"bench: transport {tname(cfg)} skipped: {e}", file=sys.stderr)
             torch.cuda.synchronize()
             comm.synchronize()
             trials[cfg] = float("inf")
@@ -762,18 +779,23 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
     if len(modes) > 1 or len(chunks) > 1:
         for m in modes:
-            trial((m, mid))
+            trial((m, mid, False))
         finite = {c[0]: v for c, v in trials.items() if c[1] == mid and v != float("inf")}
         m_best = _prefer_exact(finite) if finite else "direct"
         for ch in chunks:
-            if (m_best, ch) not in trials:
-                trial((m_best, ch))
+            if (m_best, ch, False) not in trials:
+                trial((m_best, ch, False))
         cands = [c for c in trials if c[0] == m_best and trials[c] != float("inf")]
-        best = min(cands, key=trials.get) if cands else ("direct", mid)
+        best = min(cands, key=trials.get) if cands else ("direct", mid, False)
     else:
-        best = (modes[0], chunks[0])
-    chosen, chunk = best
-    apply_transport(comm, chosen, chunk)
+        best = (modes[0], chunks[0], False)
+    if graph_trial:
+        # the same transport x chunk issued as one HIP-graph replay per call
+        trial((best[0], best[1], True))
+        if trials[(best[0], best[1], True)] < trials.get(best, float("inf")):
+            best = (best[0], best[1], True)
+    chosen, chunk, graphs = best
+    apply_transport(comm, chosen, chunk, graphs)
     rbuf.fill_(float("nan"))
     st = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
     ok_head, dig = parity(chosen)
@@ -784,20 +806,20 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         # against the reference's own bits with pico_core's ground-truth
         # tolerance (pico_core_utils.c:960-992: |a - b| <= P * 1e-6 * 100)
         tree_out = rbuf.clone()
-        apply_transport(comm, "flatrs+flat", chunk)
+        apply_transport(comm, "flatrs+flat", chunk, graphs)
         run()
         torch.cuda.synchronize()
         ok_exact, _ = parity("flatrs+flat")
         tol = world * 1e-6 * 100.0
         ok_trees_tol = all_ok(torch, dist, bool(ok_exact) and float((tree_out - rbuf).abs().max()) <= tol)
         del tree_out
-        apply_transport(comm, chosen, chunk)
+        apply_transport(comm, chosen, chunk, graphs)
     ms = st["median_ms"]
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
                                                            chosen, chunk)) if extras else {}
-    apply_transport(comm, chosen, chunk)
+    apply_transport(comm, chosen, chunk, graphs)
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}
     vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
@@ -826,17 +848,17 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
                        "whole_job_GBs": round(world * algbw, 2),
                        "busbw_frac_of_target_1071": round(busbw / TARGET_BUSBW_GBS, 4),
-                       "transport": chosen,
+                       "transport": chosen, "graph_replay": graphs,
                        "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
                        "chunk_bytes": chunk,
                        "parity": {"headline_ok": ok_head, "digest": str(dig),
                                   "check": f"bine_checksum(rbuf) on every rank == oracle digest {key}"
                                            + (" (trees: relabelled-schedule digest)" if chosen == "trees" else ""),
                                   "trees_within_pico_core_eps": ok_trees_tol,
-                                  "trials": {f"{m}/{ch >> 20}MiB": v for (m, ch), v in verdicts.items()}},
+                                  "trials": {tname(c): v for c, v in verdicts.items()}},
                        "host_issue_ms_per_step": round(st["issue_ms"], 4),
                        "step_profile_rank0": steps_prof,
-                       "transport_trials_ms": {f"{m}/{ch >> 20}MiB": round(v, 4) for (m, ch), v in trials.items()},
+                       "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": extra,
                        "rccl_p2p_probe": probe,
@@ -886,11 +908,12 @@ def main():
     ap.add_argument("--chunk-mib", type=int, default=0, help="N > 1: pipelining chunk (0: try 4/8/16/32/64 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C1/C4/C5 side measurements")
+    ap.add_argument("--no-graph-trial", action="store_true", help="N > 1: do not trial HIP-graph replay")
     ap.add_argument("--cpu-budget", type=float, default=5.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
         res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay, not args.no_extras,
-                              args.chunk_mib)
+                              args.chunk_mib, not args.no_graph_trial)
         if res is not None:
             print(json.dumps(res), flush=True)
         return

@@ -251,6 +251,19 @@ int bine_comm_set_coll_a2a(bine_comm_t comm, int on);
  * (BINE_FLAT_RS=1 turns it on); collective. */
 int bine_comm_set_flat_rs(bine_comm_t comm, int on);
 
+/* Graph mode (RCCL communicators): the first collective call for a given
+ * (algorithm, arguments, buffers, dtype, op, stream) captures the whole issue
+ * sequence -- RCCL's grouped P2P launches on the comm stream, the reduction
+ * kernels on the caller's stream and the event hand-offs between them -- into
+ * one HIP graph; every later call with the same key replays it with one
+ * hipGraphLaunch, so the host issue cost of a collective is one launch.
+ * Same work, same order: results bit-identical.  The caller's stream must not
+ * be the NULL stream (not capturable; such calls run eagerly), and buffers
+ * must stay allocated while their graph is cached (up to 64 graphs; the cache
+ * is dropped when the workspace grows and when graph mode is switched off).
+ * Off by default (BINE_GRAPHS=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
+int bine_comm_set_graphs(bine_comm_t comm, int on);
+
 /* Per-op device timing ("hipEvents per step"): with profiling on, every op
  * of a collective's issue schedule -- an exchange group on the comm stream or
  * a local primitive on the caller's stream -- is bracketed by two timing

@@ -153,6 +153,12 @@ class Comm:
         reduction tree in one kernel; bit-identical); collective."""
         check(lib().bine_comm_set_flat_rs(self.handle, int(on)), "bine_comm_set_flat_rs")
 
+    def set_graphs(self, on: bool) -> None:
+        """Graph mode (RCCL communicators): capture each (collective, buffers,
+        stream) once into a HIP graph and replay it; bit-identical; the
+        stream must not be the NULL stream."""
+        check(lib().bine_comm_set_graphs(self.handle, int(on)), "bine_comm_set_graphs")
+
     def set_profile(self, on: bool) -> None:
         """Per-op device timing of the following collectives (bine_comm_set_profile)."""
         check(lib().bine_comm_set_profile(self.handle, int(on)), "bine_comm_set_profile")

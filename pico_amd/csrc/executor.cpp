@@ -298,6 +298,12 @@ struct bine_comm {
   bool coll_a2a = false;       // all-peers exchanges as ncclAllToAllv (no relay / trees)
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
+  // bine_comm_set_graphs: each (plan, buffers, stream) is captured once into a
+  // HIP graph -- both streams' work and the event hand-offs between them -- and
+  // replayed with one hipGraphLaunch per call (RCCL communicators only)
+  bool graphs = false;
+  struct GraphEntry { hipGraph_t g = nullptr; hipGraphExec_t x = nullptr; };
+  std::map<std::string, GraphEntry> graph_cache;
   std::vector<hipEvent_t> ev;
   size_t ev_next = 0;
   std::map<std::string, std::pair<bine::Plan, bine::Schedule>> plans;
@@ -312,8 +318,16 @@ struct bine_comm {
   std::mutex mu;
   // releases whatever was set up (also after a failed init); the caller has
   // drained the streams (bine_comm_destroy) or never used them (init errors)
+  void drop_graphs() {  // caller: no cached graph is still executing
+    for (auto &kv : graph_cache) {
+      if (kv.second.x) (void)hipGraphExecDestroy(kv.second.x);
+      if (kv.second.g) (void)hipGraphDestroy(kv.second.g);
+    }
+    graph_cache.clear();
+  }
   ~bine_comm() {
     (void)hipSetDevice(device);
+    drop_graphs();
     tx.reset();
     for (int t = 0; t < 4; t++)
       if (tmp[t]) (void)hipFree(tmp[t]);
@@ -342,6 +356,7 @@ static int comm_setup(bine_comm *c) {
   if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) != 0;
   if (const char *e = getenv("BINE_FLAT_RS")) c->flat_rs = atoi(e) != 0;
   if (const char *e = getenv("BINE_COLL_A2A")) c->coll_a2a = atoi(e) != 0;
+  if (const char *e = getenv("BINE_GRAPHS")) c->graphs = atoi(e) != 0;
   if (const char *e = getenv("BINE_SINGLE_STREAM_BYTES")) c->single_stream_bytes = (size_t)strtoull(e, nullptr, 10);
   return BINE_SUCCESS;
 }
@@ -380,6 +395,7 @@ static int ensure_workspace(bine_comm *c, const uint64_t *elems, size_t esz, hip
   // old buffers may still be read by enqueued work
   HIP_TRY(hipStreamSynchronize(user));
   HIP_TRY(hipStreamSynchronize(c->cstream));
+  c->drop_graphs();  // captured graphs hold the old workspace addresses
 
   for (int t = 0; t < 4; t++) {
     const size_t need = elems[t] * esz;
@@ -478,7 +494,7 @@ static bool a2a_shape(const bine_comm *c, const std::vector<XSend> &s, const std
 }
 
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
-                   hipStream_t K, bool single = false) {
+                   hipStream_t K, bool single = false, bool joined = false) {
   char *base[6];
   base[BINE_BUF_SBUF] = (char *)sbuf;
   base[BINE_BUF_RBUF] = (char *)rbuf;
@@ -486,7 +502,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   base[BINE_BUF_STAGE] = (char *)c->tmp[3];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
   hipStream_t C = single ? K : c->cstream;
-  if (sc.c_join && !single) {
+  if (sc.c_join && !single && !joined) {  // joined: the comm stream already follows K (graph capture)
     int rc = stream_join(c, C, K);
     if (rc) return rc;
   }
@@ -596,6 +612,61 @@ static void build(const PlanArgs &args, size_t ch, size_t relay_min_bytes, bool 
   }
 }
 
+// Graph mode: the first call for a (plan, buffers, dtype, op, stream,
+// transport options) key runs eagerly -- RCCL connects to new peers lazily and
+// the allgather option sizes its staging area, neither of which may happen
+// inside a capture -- and then captures the same execute() on K without
+// running it: the comm stream joins the capture through the schedule's event
+// hand-offs (c_join forks it from K, final_wait joins it back), and RCCL's
+// grouped P2P launches are captured as RCCL supports.  Every later call with
+// that key replays the graph with one hipGraphLaunch.  Work and ordering are
+// the eager schedule's, so results are bit-identical (GPU tests).
+static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule &sc, const void *sbuf, void *rbuf,
+                     size_t esz, int dtype, int op, hipStream_t K, bool single) {
+  const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
+  char buf[192];
+  snprintf(buf, sizeof buf, "|%p|%p|%d|%d|%p|%d|%d|%d", sbuf, rbuf, dtype, op, (void *)K, (int)single,
+           (int)c->coll_a2a, rt && rt->coll_ag ? 1 : 0);
+  const std::string key = plan_key_s + buf;
+  auto it = c->graph_cache.find(key);
+  if (it != c->graph_cache.end()) {
+    HIP_TRY(hipGraphLaunch(it->second.x, K));
+    return BINE_SUCCESS;
+  }
+  int rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single);  // this call, eagerly
+  if (rc) return rc;
+  if (c->graph_cache.size() >= 64) {  // bound the cache: drain, then drop every graph
+    HIP_TRY(hipStreamSynchronize(K));
+    HIP_TRY(hipStreamSynchronize(c->cstream));
+    c->drop_graphs();
+  }
+  // Capture origin: K for single-stream schedules; the COMM stream otherwise,
+  // with K forked from it and joined back at the end.  RCCL's captured P2P
+  // launches must sit on the capture's origin stream: with K as origin and the
+  // comm stream forked in, hipStreamEndCapture segfaulted (RCCL 2.26.6 / HIP
+  // 7.0, both capture modes; tools/graph_probe.py, profiles/r2_graph_capture.txt).
+  bine_comm::GraphEntry e;
+  const hipStream_t O = single ? K : c->cstream;
+  HIP_TRY(hipStreamBeginCapture(O, hipStreamCaptureModeThreadLocal));
+  if (!single) rc = stream_join(c, K, O);
+  if (!rc) rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, true);
+  if (!rc && !single) rc = stream_join(c, O, K);
+  const hipError_t ee = hipStreamEndCapture(O, &e.g);
+  if (rc || ee != hipSuccess) {
+    if (e.g) (void)hipGraphDestroy(e.g);
+    if (!rc) set_err("graph capture of the collective failed: %s", hipGetErrorString(ee));
+    return rc ? rc : BINE_ERR_HIP;
+  }
+  const hipError_t ie = hipGraphInstantiate(&e.x, e.g, nullptr, nullptr, 0);
+  if (ie != hipSuccess) {
+    (void)hipGraphDestroy(e.g);
+    set_err("hipGraphInstantiate: %s", hipGetErrorString(ie));
+    return BINE_ERR_HIP;
+  }
+  c->graph_cache.emplace(key, e);
+  return BINE_SUCCESS;
+}
+
 // chunk_bytes == kCommChunk: the communicator's setting (bine_comm_set_chunk)
 constexpr size_t kCommChunk = ~(size_t)0;
 
@@ -639,7 +710,11 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     snprintf(lbl, sizeof lbl, "bine %s P=%d count=%zu", bine_algo_name(a.algo), a.P, a.count);
     roctxRangePushA(lbl);
   }
-  rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, bytes <= c->single_stream_bytes);
+  const bool single = bytes <= c->single_stream_bytes;
+  if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on())
+    rc = run_graph(c, key, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
+  else
+    rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
   if (roctx_on()) roctxRangePop();
   return rc;
 }
@@ -1086,6 +1161,20 @@ int bine_comm_set_coll_ag(bine_comm_t c, int on) {
   if (!r) return BINE_ERR_UNSUPPORTED;  // loopback: no RCCL collective to use
   std::lock_guard<std::mutex> g(c->mu);
   r->coll_ag = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_graphs(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  if (c->hub) return BINE_ERR_UNSUPPORTED;  // loopback exchanges wait on the host: not capturable
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!on && c->graphs) {
+    (void)hipSetDevice(c->device);
+    if (c->used_user) HIP_TRY(hipStreamSynchronize(c->last_user));
+    HIP_TRY(hipStreamSynchronize(c->cstream));
+    c->drop_graphs();
+  }
+  c->graphs = on != 0;
   return BINE_SUCCESS;
 }
 

@@ -109,3 +109,30 @@ def test_copy_kernel_c3_size(dev):
     pico_amd.copy(d, s, 4 * n)
     torch.cuda.synchronize()
     assert pico_amd.checksum(d, n, "float") == GOLD[f"C3/allreduce/bine_bdw_remap/float/N{C3_N}/P1"][0]
+
+
+def test_graph_mode_size1_comm(dev):
+    """bine_comm_set_graphs on an RCCL communicator: first call eager +
+    captured, later calls replayed; the NULL stream runs eagerly"""
+    comm = pico_amd.Comm.rccl(0, 1, pico_amd.Comm.unique_id(), 0)
+    try:
+        comm.set_graphs(True)
+        n = 1 << 20
+        s = torch.empty(n, dtype=torch.float32, device=dev)
+        pico_amd.fill_pico(s, n, "float", 99)
+        r = torch.zeros(n, dtype=torch.float32, device=dev)
+        side = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        for i in range(3):
+            with torch.cuda.stream(side):
+                r.fill_(float("nan"))
+                pico_amd.allreduce("bine_bdw_remap", s, r, n, "float", "sum", comm)
+            torch.cuda.synchronize()
+            assert torch.equal(r, s), i
+        r.zero_()
+        pico_amd.allreduce("bine_bdw_remap", s, r, n, "float", "sum", comm, stream=0)   # NULL stream: eager
+        torch.cuda.synchronize()
+        assert torch.equal(r, s)
+        comm.set_graphs(False)
+    finally:
+        comm.destroy()

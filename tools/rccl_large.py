@@ -8,7 +8,9 @@ allreduce_bine_bdw_remap on 64 MiB per rank in fp32 and fp64 with the DEFAULT
 k+1 on the comm stream beside the reduction of chunk k on the compute stream,
 the device form of libbine_allreduce.c:1218-1253) runs over real RCCL with
 several chunks per step -- for every transport bench.py may pick (direct,
-relay, flat, flatrs+flat, +ag, +a2a, trees), plus reduce_scatter_bine_permute_remap
+relay, flat, flatrs+flat, +ag, +a2a, trees), each eagerly and in graph mode
+(bine_comm_set_graphs: one eager call + capture, then replays), plus
+reduce_scatter_bine_permute_remap
 on a 64 MiB input per rank (direct, flatrs).  Every rank's output digest is
 compared with the oracle's (trees: the relabelled schedule's), computed once
 in the parent.
@@ -60,24 +62,31 @@ def worker(rank, P, port, want, q):
     dist.init_process_group("gloo")
     comm = pico_amd.Comm.from_torch_distributed(0)
     bad, n_ok = [], 0
-    modes = [m for m in MODES if m in bench.transport_modes("auto", P)]
+    side = torch.cuda.Stream()   # graph mode needs a non-NULL caller stream
+    modes = [m for m in MODES if m in bench.transport_modes("auto", P) or m == "flatrs+flat+a2a"]
     for dt, n, tdt in (("float", N32, torch.float32), ("double", N64, torch.float64)):
         s = torch.empty(n, dtype=tdt, device="cuda:0")
         r = torch.empty(n, dtype=tdt, device="cuda:0")
         pico_amd.fill_pico(s, n, dt, 1234 + rank)
         for m in modes:
-            bench.apply_transport(comm, m, 0)   # 0: the library default chunk (16 MiB)
-            for it in range(2):
-                r.fill_(float("nan"))
-                pico_amd.allreduce("bine_bdw_remap", s, r, n, dt, "sum", comm)
-                torch.cuda.synchronize()
-                comm.synchronize()
-                d = pico_amd.checksum(r, n, dt)
-                if d == want[("ar", dt, m == "trees")][rank]:
-                    n_ok += 1
-                else:
-                    bad.append(f"allreduce {dt} {m} iter {it}")
-            print(f"rank {rank} allreduce {dt} {m}: {'ok' if not bad else 'BAD'}", flush=True)
+            for g in (False, True):
+                # 0: the library default chunk (16 MiB); graph mode: the first call
+                # runs eagerly and is captured (two-stream schedule, the comm stream
+                # as the capture's origin), the next ones are replays
+                bench.apply_transport(comm, m, 0, g)
+                for it in range(3 if g else 2):
+                    with torch.cuda.stream(side):
+                        r.fill_(float("nan"))
+                        pico_amd.allreduce("bine_bdw_remap", s, r, n, dt, "sum", comm)
+                    torch.cuda.synchronize()
+                    comm.synchronize()
+                    d = pico_amd.checksum(r, n, dt)
+                    if d == want[("ar", dt, m == "trees")][rank]:
+                        n_ok += 1
+                    else:
+                        bad.append(f"allreduce {dt} {m} graphs={g} iter {it}")
+            comm.set_graphs(False)
+            print(f"rank {rank} allreduce {dt} {m} (eager + graph): {'ok' if not bad else 'BAD'}", flush=True)
         del s, r
     s = torch.empty(N32, dtype=torch.float32, device="cuda:0")
     r = torch.empty(N32 // P, dtype=torch.float32, device="cuda:0")
