@@ -164,16 +164,25 @@ def timed(torch, stream, call, steps, warmup, dist=None, syncs=(), per_iter=True
     wall = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-    per = [a.elapsed_time(b) for a, b in evs]
-    t = torch.tensor(per + [r0.elapsed_time(r1) / steps, issue * 1e3 / steps, wall], dtype=torch.float64)
+    return reduce_stats(torch, dist, [a.elapsed_time(b) for a, b in evs], r0.elapsed_time(r1) / steps,
+                        issue * 1e3 / steps, wall)
+
+
+def reduce_stats(torch, dist, per, region, issue_ms, wall):
+    """the statistic over ranks: per iteration the max over ranks (as every
+    other figure), the first 20 % of iterations dropped, the median of the
+    rest (pico_core.c:133-140, summarize_data.py:24-48); `per` empty = no
+    per-iteration events (the region average stands for every field)"""
+    t = torch.tensor(list(per) + [region, issue_ms, wall], dtype=torch.float64)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    region = float(t[len(per)])
-    per = [float(x) for x in t[:len(per)]] or [region]
-    kept = per[int(len(per) * WARMUP_DROP):] or per
+    n = len(per)
+    region = float(t[n])
+    vals = [float(x) for x in t[:n]] or [region]
+    kept = vals[int(len(vals) * WARMUP_DROP):] or vals
     return {"median_ms": statistics.median(kept), "mean_ms": statistics.fmean(kept), "min_ms": min(kept),
-            "max_ms": max(kept), "samples": len(kept) if per_iter else 0, "region_ms": region,
-            "issue_ms": float(t[len(t) - 2]), "wall_s": float(t[len(t) - 1])}
+            "max_ms": max(kept), "samples": len(kept) if n else 0, "region_ms": region,
+            "issue_ms": float(t[n + 1]), "wall_s": float(t[n + 2])}
 
 
 class quiet_stdout:
@@ -545,10 +554,11 @@ def apply_transport(comm, mode, chunk, graphs=False):
     comm.set_chunk(chunk)
 
 
-def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk):
+def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk, graphs=False):
     """BASELINE configs C1, C4 and C5 on the transport chosen for C3 (C1: the
-    bit-exact flat phases instead of multi-tree mode, a large-message mode),
-    each checked against the oracle's digests of its inputs (seed 1234 + rank)"""
+    bit-exact flat phases instead of multi-tree mode, a large-message mode;
+    eager and graph-replayed), each checked against the oracle's digests of
+    its inputs (seed 1234 + rank)"""
     out = {}
     # C1: fp32 allreduce 1 MiB per rank (the reference's own CPU configuration:
     # libbine bine_bdw_remap_over 381.9 us at P = 4 through pico_core,
@@ -573,7 +583,7 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
                 "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
     comm.set_graphs(False)
     del sb, rb
-    apply_transport(comm, mode, chunk)
+    apply_transport(comm, mode, chunk, graphs)
     trees = mode == "trees"
     # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
     n = C4_ELEMS
@@ -818,7 +828,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
-                                                           chosen, chunk)) if extras else {}
+                                                           chosen, chunk, graphs)) if extras else {}
     apply_transport(comm, chosen, chunk, graphs)
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}

@@ -173,3 +173,39 @@ def test_plans_over_gloo(P):
     assert all(p.exitcode == 0 for p in ps)
     bad = [x for _, b in res for x in b]
     assert not bad, bad
+
+
+def _stats_worker(rank, P, port, q):
+    import sys
+    sys.path[:0] = [ROOT]
+    import torch
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=P, init_method=f"tcp://127.0.0.1:{port}")
+    per = [[1.0, 5.0, 3.0, 3.0, 3.0], [2.0, 1.0, 4.0, 4.0, 4.0]][rank]
+    st = bench.reduce_stats(torch, dist, per, 3.0 + rank, 0.1 * (rank + 1), 1.0)
+    verdicts = [bench.all_ok(torch, dist, v) for v in ([True, False][rank], [None, True][rank], None, True)]
+    dist.destroy_process_group()
+    q.put((rank, st, verdicts))
+
+
+def test_bench_statistic_and_verdicts_over_gloo():
+    """bench.py's cross-rank reduction: per-iteration max over ranks, first
+    20 % dropped, median; parity verdicts: any False fails every rank, None
+    (unchecked) only if no rank checked"""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_stats_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (st, v)) for r, st, v in (q.get(timeout=120) for _ in range(2)))
+    for p in ps:
+        p.join(60)
+    for r in (0, 1):
+        st, v = res[r]
+        # max over ranks per iteration [2, 5, 4, 4, 4] -> drop 1 -> [5, 4, 4, 4]
+        assert st["median_ms"] == 4.0 and st["max_ms"] == 5.0 and st["samples"] == 4
+        assert st["region_ms"] == 4.0 and abs(st["issue_ms"] - 0.2) < 1e-12
+        assert v == [False, True, None, True]
