@@ -543,8 +543,9 @@ def step_profile(torch, comm, call):
                       for o in ls[:24]]}
 
 
-def apply_transport(comm, mode, chunk, graphs=False):
+def apply_transport(comm, mode, chunk, graphs=False, stripes=1):
     comm.set_graphs(graphs)
+    comm.set_stripes(stripes)
     comm.set_relay(RELAY_MIN_BYTES if "relay" in mode else 0)
     comm.set_trees(mode == "trees")
     comm.set_flat_ag("flat" in mode)
@@ -554,7 +555,7 @@ def apply_transport(comm, mode, chunk, graphs=False):
     comm.set_chunk(chunk)
 
 
-def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk, graphs=False):
+def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk, graphs=False, stripes=1):
     """BASELINE configs C1, C4 and C5 on the transport chosen for C3 (C1: the
     bit-exact flat phases instead of multi-tree mode, a large-message mode;
     eager and graph-replayed), each checked against the oracle's digests of
@@ -564,7 +565,7 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
     # libbine bine_bdw_remap_over 381.9 us at P = 4 through pico_core,
     # BASELINE.md section 2) -- latency-bound: the bandwidth and the
     # latency-optimal Bine variants are both timed
-    apply_transport(comm, "flatrs+flat" if mode == "trees" else mode, chunk)
+    apply_transport(comm, "flatrs+flat" if mode == "trees" else mode, chunk, False, stripes)
     n1 = C1_ELEMS
     sb = torch.empty(n1, dtype=torch.float32, device=dev)
     rb = torch.empty(n1, dtype=torch.float32, device=dev)
@@ -583,7 +584,7 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
                 "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
     comm.set_graphs(False)
     del sb, rb
-    apply_transport(comm, mode, chunk, graphs)
+    apply_transport(comm, mode, chunk, graphs, stripes)
     trees = mode == "trees"
     # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
     n = C4_ELEMS
@@ -715,12 +716,13 @@ def link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen):
 
 
 def tname(cfg):
-    """trial label: transport/chunk[+graph]"""
-    return f"{cfg[0]}/{cfg[1] >> 20}MiB" + ("+graph" if len(cfg) > 2 and cfg[2] else "")
+    """trial label: transport/chunk[+sK][+graph]"""
+    return (f"{cfg[0]}/{cfg[1] >> 20}MiB" + (f"+s{cfg[3]}" if len(cfg) > 3 and cfg[3] > 1 else "")
+            + ("+graph" if len(cfg) > 2 and cfg[2] else ""))
 
 
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
-                    chunk_mib: int = 0, graph_trial: bool = True):
+                    chunk_mib: int = 0, graph_trial: bool = True, stripe_trials=(2, 4)):
     import pico_amd
     import torch
     import torch.distributed as dist
@@ -766,8 +768,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     def trial(cfg):
         # a setting the planner rejects fails identically on every rank before
         # any transfer (plans are a pure function of the arguments): skip it
-        if len(cfg) == 2:
-            cfg = cfg + (False,)
+        cfg = tuple(cfg) + (False, 1)[len(cfg) - 2:]
         apply_transport(comm, *cfg)
         try:
             rbuf.fill_(float("nan"))   # a transport that writes nothing cannot pass on the last one's output
@@ -789,23 +790,23 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
     if len(modes) > 1 or len(chunks) > 1:
         for m in modes:
-            trial((m, mid, False))
+            trial((m, mid, False, 1))
         finite = {c[0]: v for c, v in trials.items() if c[1] == mid and v != float("inf")}
         m_best = _prefer_exact(finite) if finite else "direct"
         for ch in chunks:
-            if (m_best, ch, False) not in trials:
-                trial((m_best, ch, False))
+            if (m_best, ch, False, 1) not in trials:
+                trial((m_best, ch, False, 1))
         cands = [c for c in trials if c[0] == m_best and trials[c] != float("inf")]
-        best = min(cands, key=trials.get) if cands else ("direct", mid, False)
+        best = min(cands, key=trials.get) if cands else ("direct", mid, False, 1)
     else:
-        best = (modes[0], chunks[0], False)
+        best = (modes[0], chunks[0], False, 1)
     if graph_trial:
         # the same transport x chunk issued as one HIP-graph replay per call
-        trial((best[0], best[1], True))
-        if trials[(best[0], best[1], True)] < trials.get(best, float("inf")):
-            best = (best[0], best[1], True)
-    chosen, chunk, graphs = best
-    apply_transport(comm, chosen, chunk, graphs)
+        trial((best[0], best[1], True, 1))
+        if trials[(best[0], best[1], True, 1)] < trials.get(best, float("inf")):
+            best = (best[0], best[1], True, 1)
+    chosen, chunk, graphs, stripes = best
+    apply_transport(comm, chosen, chunk, graphs, stripes)
     rbuf.fill_(float("nan"))
     st = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
     ok_head, dig = parity(chosen)
@@ -816,24 +817,34 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         # against the reference's own bits with pico_core's ground-truth
         # tolerance (pico_core_utils.c:960-992: |a - b| <= P * 1e-6 * 100)
         tree_out = rbuf.clone()
-        apply_transport(comm, "flatrs+flat", chunk, graphs)
+        apply_transport(comm, "flatrs+flat", chunk, graphs, stripes)
         run()
         torch.cuda.synchronize()
         ok_exact, _ = parity("flatrs+flat")
         tol = world * 1e-6 * 100.0
         ok_trees_tol = all_ok(torch, dist, bool(ok_exact) and float((tree_out - rbuf).abs().max()) <= tol)
         del tree_out
-        apply_transport(comm, chosen, chunk, graphs)
+        apply_transport(comm, chosen, chunk, graphs, stripes)
     ms = st["median_ms"]
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
-                                                           chosen, chunk, graphs)) if extras else {}
-    apply_transport(comm, chosen, chunk, graphs)
+                                                           chosen, chunk, graphs, stripes)) if extras else {}
+    apply_transport(comm, chosen, chunk, graphs, stripes)
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}
     vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
                                                                       stream, world, ms)) if extras else {}
+    # striped exchanges (bine_comm_set_stripes) are trialled LAST and only
+    # reported: creating ncclCommSplit children slows the parent communicator
+    # for the rest of the process even after they are destroyed (measured on
+    # RCCL's socket transport, 103 -> 220-240 ms, profiles/r2_stripes_probe.txt),
+    # so they must not run before the headline
+    stripe_ms = {}
+    for k in stripe_trials if world > 1 else ():
+        cfg = (chosen, chunk, False, k)
+        trial(cfg)
+        stripe_ms[tname(cfg)] = {"ms": round(trials[cfg], 4), "parity_ok": verdicts.get(cfg)}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
@@ -858,7 +869,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
                        "whole_job_GBs": round(world * algbw, 2),
                        "busbw_frac_of_target_1071": round(busbw / TARGET_BUSBW_GBS, 4),
-                       "transport": chosen, "graph_replay": graphs,
+                       "transport": chosen, "graph_replay": graphs, "stripes": stripes,
                        "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
                        "chunk_bytes": chunk,
                        "parity": {"headline_ok": ok_head, "digest": str(dig),
@@ -873,6 +884,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "other_baseline_configs": extra,
                        "rccl_p2p_probe": probe,
                        "rccl_allreduce_baseline": vendor,
+                       "striped_exchanges_after_headline": stripe_ms,
                        "rccl": pico_amd.rccl_version(), "host": host_info()},
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(achieved / link_peak, 4),
@@ -919,11 +931,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C1/C4/C5 side measurements")
     ap.add_argument("--no-graph-trial", action="store_true", help="N > 1: do not trial HIP-graph replay")
+    ap.add_argument("--stripes", default="2,4", help="N > 1: stripe counts to trial (comma list; empty: none)")
     ap.add_argument("--cpu-budget", type=float, default=5.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
         res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay, not args.no_extras,
-                              args.chunk_mib, not args.no_graph_trial)
+                              args.chunk_mib, not args.no_graph_trial,
+                              tuple(int(x) for x in args.stripes.split(",") if x))
         if res is not None:
             print(json.dumps(res), flush=True)
         return

@@ -159,6 +159,11 @@ class Comm:
         stream must not be the NULL stream."""
         check(lib().bine_comm_set_graphs(self.handle, int(on)), "bine_comm_set_graphs")
 
+    def set_stripes(self, k: int) -> None:
+        """RCCL communicators: split every exchange over k communicators
+        (ncclCommSplit children) on k streams; bit-identical; collective."""
+        check(lib().bine_comm_set_stripes(self.handle, k), "bine_comm_set_stripes")
+
     def set_profile(self, on: bool) -> None:
         """Per-op device timing of the following collectives (bine_comm_set_profile)."""
         check(lib().bine_comm_set_profile(self.handle, int(on)), "bine_comm_set_profile")

@@ -82,6 +82,7 @@ struct Transport {
     return BINE_ERR_UNSUPPORTED;
   }
   virtual void retire() {}
+  virtual int stripes() const { return 1; }
 };
 
 static bool nccl_type(int dtype, ncclDataType_t *t) {
@@ -112,9 +113,84 @@ struct RcclTransport final : Transport {
   bool coll_ag = false;
   void *stage = nullptr;
   size_t stage_bytes = 0;
+  uint64_t stage_gen = 0;  // bumped when `stage` moves (graph mode drops graphs holding the old one)
+  // bine_comm_set_stripes: every exchange split over `nstripe` communicators
+  // (this one + ncclCommSplit children), each on its own stream
+  int nstripe = 1;
+  std::vector<ncclComm_t> extra;      // stripe j >= 1 uses extra[j - 1]
+  std::vector<hipStream_t> xstream;   // ... and xstream[j - 1]
+  std::vector<hipEvent_t> xev;        // [0]: fork, [j]: join of stripe j
   ~RcclTransport() override {
     if (stage) (void)hipFree(stage);
+    for (auto x : extra) ncclCommDestroy(x);
+    for (auto x : xstream) (void)hipStreamDestroy(x);
+    for (auto x : xev) (void)hipEventDestroy(x);
     if (comm) ncclCommDestroy(comm);
+  }
+  int stripes() const override { return nstripe; }
+  // collective: every rank calls it with the same k, in the same order
+  int set_stripes(int k) {
+    if (k < 1 || k > 8) return BINE_ERR_ARG;
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    while ((int)extra.size() < k - 1) {
+      ncclComm_t x = nullptr;
+      NCCL_TRY(ncclCommSplit(comm, 0, rank, &x, nullptr));  // same ranks, same order; parent's config
+      extra.push_back(x);
+      hipStream_t st = nullptr;
+      HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi));
+      xstream.push_back(st);
+    }
+    // children beyond k - 1 are released: idle communicators keep RCCL proxy
+    // threads and connections alive (measured: a 4-rank socket run slowed
+    // 2.6x after a stripes-4 trial until they were destroyed)
+    while ((int)extra.size() > k - 1) {
+      NCCL_TRY(ncclCommDestroy(extra.back()));
+      extra.pop_back();
+      HIP_TRY(hipStreamDestroy(xstream.back()));
+      xstream.pop_back();
+    }
+    while ((int)xev.size() < k) {
+      hipEvent_t e = nullptr;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      xev.push_back(e);
+    }
+    nstripe = k;
+    return BINE_SUCCESS;
+  }
+  // part j of a message of b bytes: [b * j / k, b * (j + 1) / k) rounded to
+  // 16 B -- a function of (b, j, k) only, so both ends cut identically
+  static void part(size_t b, int j, int k, size_t *off, size_t *len) {
+    const size_t a = (b * (size_t)j / (size_t)k) & ~(size_t)15;
+    const size_t z = j + 1 == k ? b : (b * (size_t)(j + 1) / (size_t)k) & ~(size_t)15;
+    *off = a;
+    *len = z > a ? z - a : 0;
+  }
+  int striped(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) {
+    const int k = nstripe;
+    HIP_TRY(hipEventRecord(xev[0], st));
+    for (int j = 0; j < k; j++) {
+      hipStream_t sj = j ? xstream[(size_t)j - 1] : st;
+      ncclComm_t cj = j ? extra[(size_t)j - 1] : comm;
+      if (j) HIP_TRY(hipStreamWaitEvent(sj, xev[0], 0));
+      NCCL_TRY(ncclGroupStart());
+      ncclResult_t r0 = ncclSuccess;
+      size_t off, len;
+      for (const auto &x : s) {
+        part(x.bytes, j, k, &off, &len);
+        if (len && r0 == ncclSuccess) r0 = ncclSend((const char *)x.ptr + off, len, ncclUint8, x.peer, cj, sj);
+      }
+      for (const auto &x : r) {
+        part(x.bytes, j, k, &off, &len);
+        if (len && r0 == ncclSuccess) r0 = ncclRecv((char *)x.ptr + off, len, ncclUint8, x.peer, cj, sj);
+      }
+      const ncclResult_t r1 = ncclGroupEnd();
+      NCCL_TRY(r0);
+      NCCL_TRY(r1);
+      if (j) HIP_TRY(hipEventRecord(xev[(size_t)j], sj));
+    }
+    for (int j = 1; j < k; j++) HIP_TRY(hipStreamWaitEvent(st, xev[(size_t)j], 0));
+    return BINE_SUCCESS;
   }
   bool allgather_shape(const std::vector<XSend> &s, const std::vector<XRecv> &r) const {
     if (size < 3 || (int)s.size() != size - 1 || (int)r.size() != size - 1) return false;
@@ -139,6 +215,7 @@ struct RcclTransport final : Transport {
       stage_bytes = 0;
       HIP_TRY(hipMalloc(&stage, need));
       stage_bytes = need;
+      stage_gen++;
     }
     static const bool trace = getenv("BINE_TRACE") && atoi(getenv("BINE_TRACE")) != 0;
     if (trace) fprintf(stderr, "[bine r%d] coll_ag ncclAllGather %zu B per rank\n", rank, b);
@@ -151,6 +228,7 @@ struct RcclTransport final : Transport {
   }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
     if (coll_ag && allgather_shape(s, r)) return allgather(s, r, st);
+    if (nstripe > 1) return striped(s, r, st);
     NCCL_TRY(ncclGroupStart());
     // the group is always closed, also when posting an operation failed
     ncclResult_t r0 = ncclSuccess;
@@ -304,6 +382,7 @@ struct bine_comm {
   bool graphs = false;
   struct GraphEntry { hipGraph_t g = nullptr; hipGraphExec_t x = nullptr; };
   std::map<std::string, GraphEntry> graph_cache;
+  uint64_t graph_stage_gen = 0;  // the transport's staging-area generation the cached graphs hold
   std::vector<hipEvent_t> ev;
   size_t ev_next = 0;
   std::map<std::string, std::pair<bine::Plan, bine::Schedule>> plans;
@@ -479,6 +558,7 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
 static bool a2a_shape(const bine_comm *c, const std::vector<XSend> &s, const std::vector<XRecv> &r) {
   const int P = c->size;
   if (!c->coll_a2a || c->hub || c->relay_min_bytes || c->trees || P < 3) return false;  // hub: loopback
+  if (c->tx->stripes() > 1) return false;  // striped exchanges are grouped P2P
   if ((int)s.size() != P - 1 || (int)r.size() != P - 1) return false;
   const size_t b = s[0].bytes;
   std::vector<char> ss((size_t)P, 0), rs((size_t)P, 0);
@@ -635,6 +715,15 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
   }
   int rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single);  // this call, eagerly
   if (rc) return rc;
+  if (rt && rt->stage_gen != c->graph_stage_gen) {
+    // the allgather option's staging area moved (freed after a synchronize of
+    // the comm stream, which follows every earlier graph launch on K): drop
+    // the graphs that still point into the old one
+    HIP_TRY(hipStreamSynchronize(K));
+    HIP_TRY(hipStreamSynchronize(c->cstream));
+    c->drop_graphs();
+    c->graph_stage_gen = rt->stage_gen;
+  }
   if (c->graph_cache.size() >= 64) {  // bound the cache: drain, then drop every graph
     HIP_TRY(hipStreamSynchronize(K));
     HIP_TRY(hipStreamSynchronize(c->cstream));
@@ -711,7 +800,9 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     roctxRangePushA(lbl);
   }
   const bool single = bytes <= c->single_stream_bytes;
-  if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on())
+  // graph mode captures RCCL on the capture's origin stream only: striped
+  // exchanges (RCCL on forked streams) run eagerly
+  if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && c->tx->stripes() == 1)
     rc = run_graph(c, key, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
   else
     rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
@@ -1169,13 +1260,22 @@ int bine_comm_set_graphs(bine_comm_t c, int on) {
   if (c->hub) return BINE_ERR_UNSUPPORTED;  // loopback exchanges wait on the host: not capturable
   std::lock_guard<std::mutex> g(c->mu);
   if (!on && c->graphs) {
-    (void)hipSetDevice(c->device);
-    if (c->used_user) HIP_TRY(hipStreamSynchronize(c->last_user));
-    HIP_TRY(hipStreamSynchronize(c->cstream));
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());  // no cached graph may still run; the caller's streams may be gone
     c->drop_graphs();
   }
   c->graphs = on != 0;
   return BINE_SUCCESS;
+}
+
+int bine_comm_set_stripes(bine_comm_t c, int k) {
+  if (!c) return BINE_ERR_ARG;
+  auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (!r) return BINE_ERR_UNSUPPORTED;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // RCCL: one process per device; the caller's streams may be gone
+  return r->set_stripes(k);
 }
 
 int bine_comm_set_flat_ag(bine_comm_t c, int on) {
