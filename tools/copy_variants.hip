@@ -2,6 +2,8 @@
 // allreduce (libbine_allreduce.c:849-852 copy_buffer, 256 MiB fp32: the N = 1
 // headline workload), and (2) the element-wise reduce at the small windows of
 // C1 / the tail chunks (256 KiB .. 16 MiB), where launch and ramp cost dominate.
+// (3) the C2 reduce with operands staged through LDS by LDS-DMA vs the
+// library's register-only kernel.
 // Standalone program, not part of the library: variants interleaved
 // round-robin, median of rounds, HIP events on the launch stream.
 //   hipcc -O3 --offload-arch=gfx950 -I include -o copy_variants tools/copy_variants.hip \
@@ -100,6 +102,44 @@ __global__ __launch_bounds__(BS) void k_red(const f4 *__restrict__ a, const f4 *
       const size_t i = base + (size_t)u * BS;
       if (i < nvec) o[i] = b[i] + a[i];
     }
+  }
+}
+
+// LDS-staged element-wise reduce (north star: "LDS-staged partials"): operand
+// `a` (and optionally `b`) arrives through LDS by LDS-DMA
+// (global_load_lds_dwordx4, AUX = cache policy: 2 = nt), the other straight
+// into registers; each wave reads back only its own lanes' bytes, so
+// s_waitcnt vmcnt(0) orders it (no cross-wave barrier needed)
+template <int U, int AUX, bool BOTH>
+__global__ __launch_bounds__(256) void k_red_lds(const f4 *__restrict__ a, const f4 *b, f4 *o, size_t nvec) {
+  __shared__ f4 sa[256 * U];
+  __shared__ f4 sb[BOTH ? 256 * U : 1];
+  const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+  const int w = threadIdx.x >> 6;
+  if (base + (U - 1) * 256 >= nvec) {
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * 256;
+      if (i < nvec) o[i] = b[i] + a[i];
+    }
+    return;
+  }
+  typedef __attribute__((address_space(3))) void lds_t;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    __builtin_amdgcn_global_load_lds((const void *)(a + base + u * 256), (lds_t *)(sa + u * 256 + w * 64), 16, 0, AUX);
+    if constexpr (BOTH)
+      __builtin_amdgcn_global_load_lds((const void *)(b + base + u * 256), (lds_t *)(sb + u * 256 + w * 64), 16, 0, 0);
+  }
+  f4 y[U];
+  if constexpr (!BOTH) {
+#pragma unroll
+    for (int u = 0; u < U; u++) y[u] = b[base + u * 256];
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const f4 yy = BOTH ? sb[u * 256 + threadIdx.x] : y[u];
+    o[base + u * 256] = yy + sa[u * 256 + threadIdx.x];
   }
 }
 
@@ -254,6 +294,61 @@ int main(int argc, char **argv) {
     }
     CK(hipFree(Ra));
     CK(hipFree(Rb));
+  }
+  // ---- (3) C2 (64 MiB fp32 inout += in, 4 rotating sets): the library's
+  // register-only kernel vs LDS-staged variants
+  {
+    const size_t N = 16777216, nvec = N / 4;
+    const int sets = 4;
+    std::vector<f4 *> A(sets), B(sets);
+    for (int k = 0; k < sets; k++) {
+      CK(hipMalloc(&A[k], N * 4));
+      CK(hipMalloc(&B[k], N * 4));
+      bine_fill_pico(A[k], N, BINE_FLOAT, 1234 + 2 * k, nullptr);
+      bine_fill_pico(B[k], N, BINE_FLOAT, 1235 + 2 * k, nullptr);
+    }
+    CK(hipDeviceSynchronize());
+    std::vector<Var> vars;
+    vars.push_back({"library bine_reduce_local (registers)", [&](int k, hipStream_t st) {
+                      bine_reduce_local(A[k], B[k], N, BINE_FLOAT, BINE_SUM, st);
+                    }});
+#define LDSV(U, AUX, BOTH)                                                                                     \
+  vars.push_back({std::string("lds-dma u" #U " aux" #AUX) + (BOTH ? " +b" : ""), [&](int k, hipStream_t st) { \
+                    hipLaunchKernelGGL((k_red_lds<U, AUX, BOTH>), dim3((unsigned)((nvec + 256 * U - 1) / (256 * U))), \
+                                       dim3(256), 0, st, A[k], B[k], B[k], nvec);                              \
+                  }})
+    LDSV(4, 0, false);
+    LDSV(4, 2, false);
+    LDSV(8, 2, false);
+    LDSV(4, 2, true);
+    LDSV(2, 2, true);
+    std::vector<std::vector<float>> ms(vars.size());
+    for (int r = 0; r < rounds; r++)
+      for (size_t v = 0; v < vars.size(); v++) {
+        for (int i = 0; i < 4; i++) vars[v].run(i % sets, s);
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < 40; i++) vars[v].run(i % sets, s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float t;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms[v].push_back(t / 40);
+      }
+    printf("== C2 reduce 64 MiB fp32 (3*S = %zu B per launch): registers vs LDS-staged\n", 3 * N * 4);
+    for (size_t v = 0; v < vars.size(); v++) {
+      const double med = median(ms[v]);
+      printf("%-40s us=%8.2f  GB/s=%8.1f\n", vars[v].name.c_str(), med * 1e3, 3.0 * N * 4 / (med * 1e-3) / 1e9);
+    }
+    // parity of the LDS variants vs the library on fresh inputs
+    std::vector<float> ref(N), got(N);
+    for (size_t v = 0; v < vars.size(); v++) {
+      bine_fill_pico(A[0], N, BINE_FLOAT, 1234, nullptr);
+      bine_fill_pico(B[0], N, BINE_FLOAT, 1235, nullptr);
+      vars[v].run(0, s);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(v ? got.data() : ref.data(), B[0], N * 4, hipMemcpyDeviceToHost));
+      if (v && got != ref) printf("MISMATCH %s\n", vars[v].name.c_str());
+    }
   }
   (void)argc;
   (void)argv;
