@@ -264,6 +264,22 @@ int bine_comm_set_flat_rs(bine_comm_t comm, int on);
  * mode runs such collectives eagerly.  Loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_stripes(bine_comm_t comm, int k);
 
+/* Direct peer-memory transport (RCCL communicators, one node): exchanges
+ * move through device memory every rank maps from every peer (VMM
+ * allocations exported as POSIX file descriptors and handed over Unix
+ * sockets; on one node peer memory is reachable over xGMI by plain loads and
+ * stores) instead of RCCL's send/receive: per exchange round one kernel
+ * pushes every outgoing message into the receiver's double-buffered slot and
+ * one pulls every incoming message out of its own, with release/acquire
+ * flags at system scope.  Same bytes in the same places: results
+ * bit-identical.  Every wait has a time limit (BINE_DIRECT_TIMEOUT_S, default
+ * 10 s); a timeout disables the transport (BINE_ERR_INTERNAL from then on)
+ * instead of hanging.  The first call with on = 1 is collective (every rank
+ * of the communicator, at the same point).  Graph mode runs such
+ * collectives eagerly.  Knobs: BINE_DIRECT_SLOT_BYTES (32 MiB),
+ * BINE_DIRECT_WGS (workgroups per message, 32).  Loopback: UNSUPPORTED. */
+int bine_comm_set_direct(bine_comm_t comm, int on);
+
 /* Graph mode (RCCL communicators): the first collective call for a given
  * (algorithm, arguments, buffers, dtype, op, stream) captures the whole issue
  * sequence -- RCCL's grouped P2P launches on the comm stream, the reduction

@@ -164,6 +164,11 @@ class Comm:
         (ncclCommSplit children) on k streams; bit-identical; collective."""
         check(lib().bine_comm_set_stripes(self.handle, k), "bine_comm_set_stripes")
 
+    def set_direct(self, on: bool) -> None:
+        """RCCL communicators on one node: exchanges through mapped peer memory
+        (bine_comm_set_direct); bit-identical; the first enable is collective."""
+        check(lib().bine_comm_set_direct(self.handle, int(on)), "bine_comm_set_direct")
+
     def set_profile(self, on: bool) -> None:
         """Per-op device timing of the following collectives (bine_comm_set_profile)."""
         check(lib().bine_comm_set_profile(self.handle, int(on)), "bine_comm_set_profile")

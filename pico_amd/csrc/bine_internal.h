@@ -98,6 +98,10 @@ struct SchedCfg {
 void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, const SchedCfg &cfg, Schedule &out);
 void make_schedule(const Plan &plan, size_t chunk, bool in_place, Schedule &out);
 
+// ---- transports (executor.cpp, direct.cpp) -------------------------------------
+struct XSend { int peer; const void *ptr; size_t bytes; };
+struct XRecv { int peer; void *ptr; size_t bytes; };
+
 // ---- kernels (kernels.hip) ----------------------------------------------------
 int launch_reduce(const void *a, const void *b, void *out, size_t count, int dtype, int op,
                   void *stream);   // out = b (op) a
@@ -117,6 +121,30 @@ int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count,
 // co-aligned mod 16 B
 int launch_copy(void *dst, const void *src, size_t bytes, void *stream);
 int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
+
+// direct peer-memory transport (direct.cpp): one launch moves one round of an
+// exchange -- up to kMaxDm messages, `wgs` workgroups each (k_dm_move)
+constexpr int kMaxDm = 16;
+struct DmMsg {
+  const uint8_t *src;
+  uint8_t *dst;
+  uint64_t bytes;
+  const uint64_t *wait_ptr;  // poll until *wait_ptr >= wait_val (nullptr: no wait)
+  uint64_t wait_val;
+  uint64_t *sig_ptr;         // the last workgroup stores sig_val here (release, system scope)
+  uint64_t sig_val;
+  uint32_t *cnt_ptr;         // arrival counter; the workgroup whose increment reaches cnt_target is last
+  uint32_t cnt_target;
+};
+struct DmArgs {
+  int nmsg = 0;
+  int wgs = 1;
+  uint32_t *poison = nullptr;       // nonzero: a wait timed out -- every launch exits at once
+  uint32_t *poison_host = nullptr;  // mapped host word set together with *poison (read by the host)
+  uint64_t timeout_ticks = 0;       // wall_clock64 ticks
+  DmMsg m[kMaxDm];
+};
+int launch_dm_move(const DmArgs &a, void *stream);
 int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
 
 }  // namespace bine

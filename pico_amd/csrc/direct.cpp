@@ -1,0 +1,352 @@
+// direct.cpp -- the direct peer-memory transport of libbine_amd.so
+// (bine_comm_set_direct): exchanges move through device memory every rank
+// maps from every peer, without RCCL's FIFOs and channels.
+//
+// Each rank allocates one "inbox" with the VMM API (hipMemCreate, exportable
+// as a POSIX file descriptor), hands the descriptor to every peer over a Unix
+// socket (SCM_RIGHTS), and maps every peer's inbox (hipMemImportFromShareable
+// Handle + hipMemMap + hipMemSetAccess for its own device): on one node the
+// peers' memory is reachable over xGMI by plain loads and stores.
+//
+// Inbox layout (rank y):
+//   flags   ready[x]   sub-message sequence number x has published into y
+//           ack[x]     sequence number of y's sub-message to x that x has copied out
+//           cnt_push[x], cnt_pull[x]  arrival counters of k_dm_move (local)
+//           poison     nonzero once a wait timed out (the transport is then dead)
+//   data    region[x] = 2 slots of `slot` bytes, written only by rank x
+//
+// An exchange (sends / receives of one RCCL-style group) is cut into rounds:
+// round r carries sub-message r (at most `slot` bytes) of every message.  Per
+// round one k_dm_move launch PUSHES every send -- wait until the receiver has
+// acknowledged the slot's previous use (sequence s - 2), copy into the
+// receiver's slot s % 2, publish ready = s in the receiver's inbox -- and one
+// launch PULLS every receive -- wait for ready >= s, copy the slot into the
+// destination, publish ack = s in the sender's inbox.  Sequence numbers are
+// per ordered pair and monotonic, so flags never need resetting.  Deadlock
+// freedom: a push of round r waits only for pulls of rounds <= r - 2, which
+// every rank has issued before it (rounds of one exchange, and exchanges,
+// are issued in the same order everywhere -- the RCCL matching rule the
+// planner already obeys).  Both ends cut messages identically (sizes match
+// exactly, as RCCL requires).  Every wait has a time limit; a timeout poisons
+// the transport and every later launch exits immediately (no hang), and the
+// collective reports BINE_ERR_INTERNAL from then on.
+//
+// The received bytes are copied out of the slot (one extra local pass over
+// HBM per received byte -- HBM is ~8x the xGMI rate, so it is not the bound);
+// sends read the caller's buffer directly.  Graph capture is not possible
+// (host-side sequence numbers advance per call): graph mode runs such
+// collectives eagerly.
+#include <hip/hip_runtime.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "bine_internal.h"
+#include "direct.h"
+
+namespace bine {
+
+namespace {
+
+// BINE_TRACE=1: one stderr line per setup step
+void step(int rank, const char *what) {
+  static const bool on = getenv("BINE_TRACE") && atoi(getenv("BINE_TRACE")) != 0;
+  if (on) fprintf(stderr, "[bine dm r%d] %s\n", rank, what);
+}
+
+constexpr size_t kFlagStride = 128;  // one flag per 128-B line
+constexpr size_t kReadyOff = 0, kAckOff = 64 << 10, kCntPushOff = 128 << 10, kCntPullOff = 192 << 10,
+                 kPoisonOff = 256 << 10, kFlagsBytes = 320 << 10;
+
+int send_fd(int sock, int fd, int rank) {
+  iovec io{&rank, sizeof rank};
+  char ctl[CMSG_SPACE(sizeof(int))] = {};
+  msghdr m{};
+  m.msg_iov = &io;
+  m.msg_iovlen = 1;
+  m.msg_control = ctl;
+  m.msg_controllen = sizeof ctl;
+  cmsghdr *c = CMSG_FIRSTHDR(&m);
+  c->cmsg_level = SOL_SOCKET;
+  c->cmsg_type = SCM_RIGHTS;
+  c->cmsg_len = CMSG_LEN(sizeof(int));
+  memcpy(CMSG_DATA(c), &fd, sizeof fd);
+  return sendmsg(sock, &m, 0) == (ssize_t)sizeof rank ? 0 : -1;
+}
+
+int recv_fd(int sock, int *rank) {
+  iovec io{rank, sizeof *rank};
+  char ctl[CMSG_SPACE(sizeof(int))] = {};
+  msghdr m{};
+  m.msg_iov = &io;
+  m.msg_iovlen = 1;
+  m.msg_control = ctl;
+  m.msg_controllen = sizeof ctl;
+  if (recvmsg(sock, &m, MSG_WAITALL) != (ssize_t)sizeof *rank) return -1;
+  cmsghdr *c = CMSG_FIRSTHDR(&m);
+  if (!c || c->cmsg_type != SCM_RIGHTS) return -1;
+  int fd;
+  memcpy(&fd, CMSG_DATA(c), sizeof fd);
+  return fd;
+}
+
+// abstract Unix socket name of rank r for this communicator
+sockaddr_un addr_of(uint64_t key, int r, socklen_t *len) {
+  sockaddr_un a{};
+  a.sun_family = AF_UNIX;
+  char name[96];
+  const int n = snprintf(name, sizeof name, "bine-dm-%016llx-%d", (unsigned long long)key, r);
+  a.sun_path[0] = '\0';  // abstract namespace: no file, gone with the process
+  memcpy(a.sun_path + 1, name, (size_t)n);
+  *len = (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + n);
+  return a;
+}
+
+}  // namespace
+
+DirectState::~DirectState() {
+  (void)hipDeviceSynchronize();
+  for (size_t x = 0; x < peer.size(); x++) {
+    if ((int)x == rank || !peer[x]) continue;
+    (void)hipMemUnmap(peer[x], total);
+    (void)hipMemAddressFree(peer[x], total);
+    (void)hipMemRelease(peer_h[x]);
+  }
+  if (own) {
+    (void)hipMemUnmap(own, total);
+    (void)hipMemAddressFree(own, total);
+    (void)hipMemRelease(own_h);
+  }
+  if (own_fd >= 0) close(own_fd);
+  if (hpoison) (void)hipHostFree(hpoison);
+}
+
+static int map_handle(hipMemGenericAllocationHandle_t h, size_t size, int device, void **va, std::string &err) {
+  void *p = nullptr;
+  hipError_t e = hipMemAddressReserve(&p, size, 0, nullptr, 0);
+  if (e == hipSuccess) e = hipMemMap(p, size, 0, h, 0);
+  hipMemAccessDesc d{};
+  d.location.type = hipMemLocationTypeDevice;
+  d.location.id = device;
+  d.flags = hipMemAccessFlagsProtReadWrite;
+  if (e == hipSuccess) e = hipMemSetAccess(p, size, &d, 1);
+  if (e != hipSuccess) {
+    err = std::string("map: ") + hipGetErrorString(e);
+    return BINE_ERR_HIP;
+  }
+  *va = p;
+  return BINE_SUCCESS;
+}
+
+// Phase 1 (local): allocate, zero the flags, export the descriptor.
+int DirectState::init(int P_, int rank_, int device_, std::string &err) {
+  P = P_;
+  rank = rank_;
+  device = device_;
+  if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
+  if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
+  if (slot < (1 << 20)) slot = 1 << 20;
+  slot = slot / 4096 * 4096;
+  if (wgs < 1) wgs = 1;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+  double secs = 10.0;
+  if (const char *e = getenv("BINE_DIRECT_TIMEOUT_S")) secs = atof(e);
+  timeout_ticks = (uint64_t)(secs * khz * 1000.0);
+  step(rank, "host word");
+  if (hipHostMalloc((void **)&hpoison, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&hpoison_dev, hpoison, 0) != hipSuccess) {
+    err = "direct transport: no mapped host word";
+    return BINE_ERR_NO_MEM;
+  }
+  *(volatile uint32_t *)hpoison = 0;
+  hipMemAllocationProp p{};
+  p.type = hipMemAllocationTypePinned;
+  p.location.type = hipMemLocationTypeDevice;
+  p.location.id = device;
+  p.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+  size_t gran = 0;
+  if (hipMemGetAllocationGranularity(&gran, &p, hipMemAllocationGranularityRecommended) != hipSuccess || !gran)
+    gran = 2 << 20;
+  data_off = kFlagsBytes;
+  total = data_off + (size_t)P * 2 * slot;
+  total = (total + gran - 1) / gran * gran;
+  step(rank, "hipMemCreate");
+  hipError_t e = hipMemCreate(&own_h, total, &p, 0);
+  if (e != hipSuccess) { err = std::string("hipMemCreate: ") + hipGetErrorString(e); return BINE_ERR_NO_MEM; }
+  step(rank, "map own");
+  int rc = map_handle(own_h, total, device, &own, err);
+  if (rc) return rc;
+  step(rank, "zero flags, export");
+  e = hipMemset(own, 0, kFlagsBytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemExportToShareableHandle(&own_fd, own_h, hipMemHandleTypePosixFileDescriptor, 0);
+  if (e != hipSuccess) { err = std::string("export: ") + hipGetErrorString(e); return BINE_ERR_HIP; }
+  peer.assign((size_t)P, nullptr);
+  peer_h.assign((size_t)P, hipMemGenericAllocationHandle_t{});
+  peer[(size_t)rank] = own;
+  send_seq.assign((size_t)P, 0);
+  recv_seq.assign((size_t)P, 0);
+  cnt_push.assign((size_t)P, 0);
+  cnt_pull.assign((size_t)P, 0);
+  return BINE_SUCCESS;
+}
+
+// Phase 2 (after every rank's phase 1 succeeded -- the caller agrees on that
+// over RCCL first, so no rank waits here for a peer that gave up): hand our
+// descriptor to every peer, take theirs, map their inboxes.  Every blocking
+// step has a time limit.
+int DirectState::connect_peers(uint64_t key, std::string &err) {
+  if (P == 1) return BINE_SUCCESS;
+  int rc = BINE_SUCCESS;
+  hipError_t e;
+
+  // descriptor exchange: listen, connect to every peer and send ours, accept
+  // every peer's (sends are buffered by the kernel: no ordering deadlock)
+  int ls = socket(AF_UNIX, SOCK_STREAM, 0);
+  socklen_t len;
+  sockaddr_un me = addr_of(key, rank, &len);
+  if (ls < 0 || bind(ls, (sockaddr *)&me, len) || listen(ls, P)) {
+    err = "direct transport: cannot listen on its Unix socket";
+    if (ls >= 0) close(ls);
+    return BINE_ERR_INTERNAL;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  auto expired = [&] { return std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60); };
+  std::vector<int> conns;
+  for (int x = 0; x < P && !rc; x++) {
+    if (x == rank) continue;
+    sockaddr_un pa = addr_of(key, x, &len);
+    int s = -1;
+    while (true) {
+      s = socket(AF_UNIX, SOCK_STREAM, 0);
+      if (s >= 0 && connect(s, (sockaddr *)&pa, len) == 0) break;
+      if (s >= 0) close(s);
+      s = -1;
+      if (expired()) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+    if (s < 0 || send_fd(s, own_fd, rank)) {
+      err = "direct transport: descriptor exchange with a peer failed";
+      rc = BINE_ERR_INTERNAL;
+    }
+    if (s >= 0) conns.push_back(s);
+  }
+  step(rank, "descriptors sent");
+  std::vector<int> fds((size_t)P, -1);
+  for (int k = 0; k < P - 1 && !rc; k++) {
+    pollfd pf{ls, POLLIN, 0};
+    int s = -1;
+    while (s < 0 && !expired()) {
+      if (poll(&pf, 1, 100) > 0) s = accept(ls, nullptr, nullptr);
+    }
+    int from = -1;
+    const int fd = s >= 0 ? recv_fd(s, &from) : -1;
+    if (s >= 0) close(s);
+    if (fd < 0 || from < 0 || from >= P || from == rank || fds[(size_t)from] >= 0) {
+      err = "direct transport: bad descriptor from a peer";
+      rc = BINE_ERR_INTERNAL;
+    } else {
+      fds[(size_t)from] = fd;
+    }
+  }
+  close(ls);
+  for (int s : conns) close(s);
+  step(rank, "descriptors received; importing");
+  for (int x = 0; x < P && !rc; x++) {
+    if (x == rank) continue;
+    e = hipMemImportFromShareableHandle(&peer_h[(size_t)x], (void *)(intptr_t)fds[(size_t)x],
+                                        hipMemHandleTypePosixFileDescriptor);
+    if (e != hipSuccess) {
+      err = std::string("import: ") + hipGetErrorString(e);
+      rc = BINE_ERR_HIP;
+      break;
+    }
+    rc = map_handle(peer_h[(size_t)x], total, device, &peer[(size_t)x], err);
+  }
+  for (int fd : fds)
+    if (fd >= 0) close(fd);
+  return rc;
+}
+
+uint64_t *DirectState::ready(int owner, int from) const {
+  return (uint64_t *)((char *)peer[(size_t)owner] + kReadyOff + (size_t)from * kFlagStride);
+}
+uint64_t *DirectState::ack(int owner, int from) const {
+  return (uint64_t *)((char *)peer[(size_t)owner] + kAckOff + (size_t)from * kFlagStride);
+}
+uint32_t *DirectState::cnt(bool push, int pr) const {
+  return (uint32_t *)((char *)own + (push ? kCntPushOff : kCntPullOff) + (size_t)pr * kFlagStride);
+}
+uint32_t *DirectState::poison_ptr() const { return (uint32_t *)((char *)own + kPoisonOff); }
+uint8_t *DirectState::slot_ptr(int owner, int from, uint64_t seq) const {
+  return (uint8_t *)peer[(size_t)owner] + data_off + ((size_t)from * 2 + (size_t)(seq & 1)) * slot;
+}
+
+int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) {
+  size_t maxb = 0;
+  for (const auto &x : s) maxb = std::max(maxb, x.bytes);
+  for (const auto &x : r) maxb = std::max(maxb, x.bytes);
+  const size_t rounds = (maxb + slot - 1) / slot;
+  for (size_t k = 0; k < rounds; k++) {
+    // pushes of this round, kMaxDm messages per launch
+    DmArgs a;
+    a.wgs = wgs;
+    a.poison = poison_ptr();
+    a.poison_host = hpoison_dev;
+    a.timeout_ticks = timeout_ticks;
+    auto flush = [&]() -> int {
+      const int rc = launch_dm_move(a, st);
+      a.nmsg = 0;
+      return rc;
+    };
+    for (const auto &x : s) {
+      if (x.bytes <= k * slot) continue;
+      const size_t off = k * slot, len = std::min(slot, x.bytes - off);
+      const uint64_t seq = ++send_seq[(size_t)x.peer];
+      DmMsg &m = a.m[a.nmsg++];
+      m.src = (const uint8_t *)x.ptr + off;
+      m.dst = slot_ptr(x.peer, rank, seq);
+      m.bytes = len;
+      m.wait_ptr = seq > 2 ? ack(rank, x.peer) : nullptr;  // the receiver's copy-out of seq - 2
+      m.wait_val = seq > 2 ? seq - 2 : 0;
+      m.sig_ptr = ready(x.peer, rank);
+      m.sig_val = seq;
+      m.cnt_ptr = cnt(true, x.peer);
+      cnt_push[(size_t)x.peer] += (uint32_t)wgs;
+      m.cnt_target = cnt_push[(size_t)x.peer];
+      if (a.nmsg == kMaxDm)
+        if (int rc = flush()) return rc;
+    }
+    if (int rc = flush()) return rc;
+    for (const auto &x : r) {
+      if (x.bytes <= k * slot) continue;
+      const size_t off = k * slot, len = std::min(slot, x.bytes - off);
+      const uint64_t seq = ++recv_seq[(size_t)x.peer];
+      DmMsg &m = a.m[a.nmsg++];
+      m.src = slot_ptr(rank, x.peer, seq);
+      m.dst = (uint8_t *)x.ptr + off;
+      m.bytes = len;
+      m.wait_ptr = ready(rank, x.peer);
+      m.wait_val = seq;
+      m.sig_ptr = ack(x.peer, rank);
+      m.sig_val = seq;
+      m.cnt_ptr = cnt(false, x.peer);
+      cnt_pull[(size_t)x.peer] += (uint32_t)wgs;
+      m.cnt_target = cnt_pull[(size_t)x.peer];
+      if (a.nmsg == kMaxDm)
+        if (int rc = flush()) return rc;
+    }
+    if (int rc = flush()) return rc;
+  }
+  return BINE_SUCCESS;
+}
+
+}  // namespace bine

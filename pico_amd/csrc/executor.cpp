@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "bine_internal.h"
+#include "direct.h"
 
 namespace bine {
 
@@ -71,9 +72,6 @@ static void set_err(const char *fmt, ...) {
 // transports
 // ---------------------------------------------------------------------------
 
-struct XSend { int peer; const void *ptr; size_t bytes; };
-struct XRecv { int peer; void *ptr; size_t bytes; };
-
 struct Transport {
   virtual ~Transport() = default;
   virtual int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) = 0;
@@ -83,6 +81,7 @@ struct Transport {
   }
   virtual void retire() {}
   virtual int stripes() const { return 1; }
+  virtual bool capturable() const { return stripes() == 1; }
 };
 
 static bool nccl_type(int dtype, ncclDataType_t *t) {
@@ -128,6 +127,27 @@ struct RcclTransport final : Transport {
     if (comm) ncclCommDestroy(comm);
   }
   int stripes() const override { return nstripe; }
+  // *all = 1 iff every rank passes ok = true (an RCCL MIN reduction of one int)
+  int agree(bool ok, int *all) {
+    int *d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(int)));
+    int v = ok ? 1 : 0;
+    hipError_t e = hipMemcpy(d, &v, sizeof v, hipMemcpyHostToDevice);
+    ncclResult_t nr = ncclSuccess;
+    if (e == hipSuccess) nr = ncclAllReduce(d, d, 1, ncclInt32, ncclMin, comm, nullptr);
+    if (e == hipSuccess && nr == ncclSuccess) e = hipStreamSynchronize(nullptr);
+    if (e == hipSuccess && nr == ncclSuccess) e = hipMemcpy(&v, d, sizeof v, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    NCCL_TRY(nr);
+    HIP_TRY(e);
+    *all = v;
+    return BINE_SUCCESS;
+  }
+  // bine_comm_set_direct: exchanges through mapped peer memory (direct.cpp)
+  std::unique_ptr<DirectState> dm;
+  bool dm_on = false;
+  uint64_t key = 0;  // hash of the unique id: names the direct transport's sockets
+  bool capturable() const override { return nstripe == 1 && !dm_on; }
   // collective: every rank calls it with the same k, in the same order
   int set_stripes(int k) {
     if (k < 1 || k > 8) return BINE_ERR_ARG;
@@ -227,6 +247,13 @@ struct RcclTransport final : Transport {
     return BINE_SUCCESS;
   }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
+    if (dm_on) {
+      if (dm->poisoned()) {
+        set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
+        return BINE_ERR_INTERNAL;
+      }
+      return dm->exchange(s, r, st);
+    }
     if (coll_ag && allgather_shape(s, r)) return allgather(s, r, st);
     if (nstripe > 1) return striped(s, r, st);
     NCCL_TRY(ncclGroupStart());
@@ -558,7 +585,7 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
 static bool a2a_shape(const bine_comm *c, const std::vector<XSend> &s, const std::vector<XRecv> &r) {
   const int P = c->size;
   if (!c->coll_a2a || c->hub || c->relay_min_bytes || c->trees || P < 3) return false;  // hub: loopback
-  if (c->tx->stripes() > 1) return false;  // striped exchanges are grouped P2P
+  if (!c->tx->capturable()) return false;  // striped / direct exchanges have their own path
   if ((int)s.size() != P - 1 || (int)r.size() != P - 1) return false;
   const size_t b = s[0].bytes;
   std::vector<char> ss((size_t)P, 0), rs((size_t)P, 0);
@@ -802,7 +829,7 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   const bool single = bytes <= c->single_stream_bytes;
   // graph mode captures RCCL on the capture's origin stream only: striped
   // exchanges (RCCL on forked streams) run eagerly
-  if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && c->tx->stripes() == 1)
+  if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && c->tx->capturable())
     rc = run_graph(c, key, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
   else
     rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
@@ -999,6 +1026,9 @@ int bine_comm_init_rccl(bine_comm_t *out, int nranks, int rank, const void *id, 
   if (const char *e = getenv("BINE_COLL_AG")) tx->coll_ag = atoi(e) != 0;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
+  uint64_t h = 1469598103934665603ull;  // FNV-1a of the unique id: names the direct transport's sockets
+  for (size_t i = 0; i < sizeof u; i++) h = (h ^ ((const unsigned char *)id)[i]) * 1099511628211ull;
+  tx->key = h;
   NCCL_TRY(ncclCommInitRank(&tx->comm, nranks, u, rank));
   c->tx = std::move(tx);
   *out = c.release();
@@ -1265,6 +1295,41 @@ int bine_comm_set_graphs(bine_comm_t c, int on) {
     c->drop_graphs();
   }
   c->graphs = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_direct(bine_comm_t c, int on) {
+  if (!c) return BINE_ERR_ARG;
+  auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (!r) return BINE_ERR_UNSUPPORTED;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (on && !r->dm) {  // collective: every rank maps every peer's inbox
+    auto d = std::make_unique<DirectState>();
+    std::string err;
+    int rc = d->init(c->size, c->rank, c->device, err);
+    // every step only if every rank got through the previous one (agreed over
+    // RCCL), so no rank waits for a peer that has given up
+    int all = 0;
+    if (trace_on()) fprintf(stderr, "[bine dm r%d] phase 1 rc %d, agreeing\n", c->rank, rc);
+    int rc2 = r->agree(rc == BINE_SUCCESS, &all);
+    if (!rc2 && all) {
+      rc = d->connect_peers(r->key, err);
+      rc2 = r->agree(rc == BINE_SUCCESS, &all);
+    }
+    if (rc2) return rc2;
+    if (!all) {
+      set_err("direct transport unavailable on some rank: %s", err.empty() ? "(a peer failed)" : err.c_str());
+      return BINE_ERR_UNSUPPORTED;
+    }
+    r->dm = std::move(d);
+  }
+  if (on && r->dm->poisoned()) {
+    set_err("direct transport: poisoned by an earlier timeout");
+    return BINE_ERR_INTERNAL;
+  }
+  r->dm_on = on != 0;
   return BINE_SUCCESS;
 }
 

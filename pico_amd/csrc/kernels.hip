@@ -24,6 +24,7 @@
 //    then through LDS, then one 64-bit atomic per workgroup.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -599,6 +600,99 @@ int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count,
     default: return BINE_ERR_UNSUPPORTED;
   }
   return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
+// direct peer-memory transport (bine_comm_set_direct, direct.cpp): one launch
+// moves every message of one round of an exchange.  Message m is served by
+// `wgs` workgroups: thread 0 of each polls m.wait_ptr (system-scope acquire)
+// until it reaches m.wait_val -- the peer's acknowledgement that the slot is
+// free (push) or the peer's ready mark (pull) -- with a time limit; the
+// workgroup then copies its grid-strided share of the message; every
+// workgroup releases its stores and counts itself in at m.cnt_ptr; the last
+// one to arrive publishes m.sig_val at m.sig_ptr (system-scope release), in
+// the peer's memory.  A wait that times out (a peer gone or a protocol
+// fault) marks the transport poisoned; every later launch then exits at
+// once, so no wait outlives the time limit.
+
+__device__ __forceinline__ uint64_t ld_acq_sys(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
+  const int mi = (int)(blockIdx.x / (unsigned)a.wgs), wi = (int)(blockIdx.x % (unsigned)a.wgs);
+  if (mi >= a.nmsg) return;
+  const DmMsg &m = a.m[mi];
+  __shared__ int go;
+  if (threadIdx.x == 0) {
+    int ok = __hip_atomic_load(a.poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
+    if (ok && m.wait_ptr) {
+      const long long t0 = wall_clock64();
+      while (ld_acq_sys(m.wait_ptr) < m.wait_val) {
+        if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
+          __hip_atomic_store(a.poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ok = 0;
+          break;
+        }
+        if (__hip_atomic_load(a.poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    go = ok;
+  }
+  __syncthreads();
+  if (!go) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the peer released before its mark
+  // grid-strided 16-B vectors (src / dst co-aligned mod 16: slots and plan
+  // offsets are), bytes before the first boundary and after the last vector
+  // by workgroup 0
+  const uint8_t *src = m.src;
+  uint8_t *dst = m.dst;
+  const size_t head = std::min<uint64_t>((16 - ((uintptr_t)dst & 15)) & 15, m.bytes);
+  const size_t nvec = (m.bytes - head) / 16;
+  if (wi == 0) {
+    for (size_t i = threadIdx.x; i < head; i += kBlock) dst[i] = src[i];
+    for (size_t i = head + nvec * 16 + threadIdx.x; i < m.bytes; i += kBlock) dst[i] = src[i];
+  }
+  const u32x4 *vs = reinterpret_cast<const u32x4 *>(src + head);
+  u32x4 *vd = reinterpret_cast<u32x4 *>(dst + head);
+  constexpr int U = 4;
+  const size_t stride = (size_t)a.wgs * kBlock * U;
+  for (size_t base = (size_t)wi * kBlock * U + threadIdx.x; base < nvec; base += stride) {
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) __builtin_nontemporal_store(x[u], vd + i);
+    }
+  }
+  // release this workgroup's stores, count it in; the last one publishes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(m.cnt_ptr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == m.cnt_target) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(m.sig_ptr, m.sig_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+int launch_dm_move(const DmArgs &a, void *stream) {
+  if (a.nmsg <= 0) return BINE_SUCCESS;
+  if (a.nmsg > kMaxDm || a.wgs < 1) return BINE_ERR_ARG;
+  hipLaunchKernelGGL(k_dm_move, dim3((unsigned)(a.nmsg * a.wgs)), dim3(kBlock), 0, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
 // ----------------------------------------------------------------------------
