@@ -546,8 +546,9 @@ def step_profile(torch, comm, call):
 def apply_transport(comm, mode, chunk, graphs=False, stripes=1):
     comm.set_graphs(graphs)
     comm.set_stripes(stripes)
+    comm.set_direct("+dm" in mode)
     comm.set_relay(RELAY_MIN_BYTES if "relay" in mode else 0)
-    comm.set_trees(mode == "trees")
+    comm.set_trees(mode.startswith("trees"))
     comm.set_flat_ag("flat" in mode)
     comm.set_flat_rs("flatrs" in mode)
     comm.set_coll_ag("+ag" in mode)
@@ -629,6 +630,7 @@ def _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, per_peer=3
     rank r <-> r^1 both ways; (b) all P-1 peers at once (what relay / trees
     modes do per step).  GB/s per rank and direction."""
     out = {"bytes_per_peer": per_peer}
+    comm.set_direct(False)   # the probe measures RCCL's own point-to-point path
     sb = torch.empty(per_peer * (world - 1), dtype=torch.uint8, device=dev)
     rb = torch.empty(per_peer * (world - 1), dtype=torch.uint8, device=dev)
     sb.fill_(rank & 0xFF)
@@ -670,7 +672,9 @@ CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining c
 MODES = {"off": ["direct"],
          # "+a2a" is not tried: RCCL runs ncclAllToAllv as the same grouped P2P kernel
          # (rcclGenericKernel) as P-1 ncclSend/ncclRecv pairs (profiles/r2_a2a_vs_p2p_kernels.txt)
-         "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag", "trees"]}
+         # "+dm": the direct peer-memory transport (bine_comm_set_direct) instead of RCCL
+         "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag", "trees",
+                  "direct+dm", "flatrs+flat+dm", "relay+flat+dm"]}
 
 
 def transport_modes(relay: str, world: int):
@@ -686,7 +690,7 @@ def transport_modes(relay: str, world: int):
     if world <= 2:
         modes = [m for m in modes if "relay" not in m and "+ag" not in m and "+a2a" not in m] or ["direct"]
     if world not in (4, 8):
-        modes = [m for m in modes if m != "trees"] or ["direct"]
+        modes = [m for m in modes if not m.startswith("trees")] or ["direct"]
     if world & (world - 1):
         modes = [m for m in modes if "flat" not in m] or ["direct"]
     return modes
@@ -756,7 +760,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream)
 
     def parity(mode):
-        ok, d = check_digest(pico_amd, rbuf, nelem, "float", key_trees if mode == "trees" else key, rank, stream)
+        ok, d = check_digest(pico_amd, rbuf, nelem, "float", key_trees if mode.startswith("trees") else key, rank,
+                             stream)
         return all_ok(torch, dist, ok), d
 
     # measured, not guessed: each transport is timed briefly on this hardware

@@ -276,7 +276,8 @@ int bine_comm_set_stripes(bine_comm_t comm, int k);
  * 10 s); a timeout disables the transport (BINE_ERR_INTERNAL from then on)
  * instead of hanging.  The first call with on = 1 is collective (every rank
  * of the communicator, at the same point).  Graph mode runs such
- * collectives eagerly.  Knobs: BINE_DIRECT_SLOT_BYTES (32 MiB),
+ * collectives eagerly.  At most 4 messages to one peer per exchange group
+ * (BINE_ERR_UNSUPPORTED beyond).  Knobs: BINE_DIRECT_SLOT_BYTES (16 MiB),
  * BINE_DIRECT_WGS (workgroups per message, 32).  Loopback: UNSUPPORTED. */
 int bine_comm_set_direct(bine_comm_t comm, int on);
 

@@ -9,26 +9,28 @@
 // peers' memory is reachable over xGMI by plain loads and stores.
 //
 // Inbox layout (rank y):
-//   flags   ready[x]   sub-message sequence number x has published into y
-//           ack[x]     sequence number of y's sub-message to x that x has copied out
+//   flags   ready[x][k] latest sequence number x has published into y's slot k
+//           ack[x][k]   latest sequence number of y's slot-k sub-message to x
+//                       that x has copied out
 //           cnt_push[x], cnt_pull[x]  arrival counters of k_dm_move (local)
 //           poison     nonzero once a wait timed out (the transport is then dead)
-//   data    region[x] = 2 slots of `slot` bytes, written only by rank x
+//   data    region[x] = kSlots slots of `slot` bytes, written only by rank x
 //
 // An exchange (sends / receives of one RCCL-style group) is cut into rounds:
 // round r carries sub-message r (at most `slot` bytes) of every message.  Per
 // round one k_dm_move launch PUSHES every send -- wait until the receiver has
-// acknowledged the slot's previous use (sequence s - 2), copy into the
-// receiver's slot s % 2, publish ready = s in the receiver's inbox -- and one
-// launch PULLS every receive -- wait for ready >= s, copy the slot into the
-// destination, publish ack = s in the sender's inbox.  Sequence numbers are
-// per ordered pair and monotonic, so flags never need resetting.  Deadlock
-// freedom: a push of round r waits only for pulls of rounds <= r - 2, which
-// every rank has issued before it (rounds of one exchange, and exchanges,
-// are issued in the same order everywhere -- the RCCL matching rule the
-// planner already obeys).  Both ends cut messages identically (sizes match
-// exactly, as RCCL requires).  Every wait has a time limit; a timeout poisons
-// the transport and every later launch exits immediately (no hang), and the
+// acknowledged the slot's previous use (sequence s - kSlots), copy into the
+// receiver's slot s % kSlots, publish ready = s in the receiver's inbox -- and
+// one launch PULLS every receive -- wait for ready >= s, copy the slot into
+// the destination, publish ack = s in the sender's inbox.  Sequence numbers
+// are per ordered pair and monotonic, so flags never need resetting.
+// Deadlock freedom: at most kSlots messages per peer per exchange (more are
+// refused), so a push waits only for pulls of earlier rounds, which every
+// rank has issued before it (rounds of one exchange, and exchanges, are
+// issued in the same order everywhere -- the RCCL matching rule the planner
+// already obeys).  Both ends cut messages identically (sizes match exactly,
+// as RCCL requires).  Every wait has a time limit; a timeout poisons the
+// transport and every later launch exits immediately (no hang), and the
 // collective reports BINE_ERR_INTERNAL from then on.
 //
 // The received bytes are copied out of the slot (one extra local pass over
@@ -131,7 +133,9 @@ DirectState::~DirectState() {
 static int map_handle(hipMemGenericAllocationHandle_t h, size_t size, int device, void **va, std::string &err) {
   void *p = nullptr;
   hipError_t e = hipMemAddressReserve(&p, size, 0, nullptr, 0);
+  step(-1, e == hipSuccess ? "reserved" : "reserve failed");
   if (e == hipSuccess) e = hipMemMap(p, size, 0, h, 0);
+  step(-1, e == hipSuccess ? "mapped" : "map failed");
   hipMemAccessDesc d{};
   d.location.type = hipMemLocationTypeDevice;
   d.location.id = device;
@@ -176,7 +180,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (hipMemGetAllocationGranularity(&gran, &p, hipMemAllocationGranularityRecommended) != hipSuccess || !gran)
     gran = 2 << 20;
   data_off = kFlagsBytes;
-  total = data_off + (size_t)P * 2 * slot;
+  total = data_off + (size_t)P * kSlots * slot;
   total = (total + gran - 1) / gran * gran;
   step(rank, "hipMemCreate");
   hipError_t e = hipMemCreate(&own_h, total, &p, 0);
@@ -194,8 +198,8 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   peer[(size_t)rank] = own;
   send_seq.assign((size_t)P, 0);
   recv_seq.assign((size_t)P, 0);
-  cnt_push.assign((size_t)P, 0);
-  cnt_pull.assign((size_t)P, 0);
+  cnt_push.assign((size_t)P * kSlots, 0);
+  cnt_pull.assign((size_t)P * kSlots, 0);
   return BINE_SUCCESS;
 }
 
@@ -262,8 +266,25 @@ int DirectState::connect_peers(uint64_t key, std::string &err) {
   step(rank, "descriptors received; importing");
   for (int x = 0; x < P && !rc; x++) {
     if (x == rank) continue;
-    e = hipMemImportFromShareableHandle(&peer_h[(size_t)x], (void *)(intptr_t)fds[(size_t)x],
-                                        hipMemHandleTypePosixFileDescriptor);
+    {
+      char b[96];
+      snprintf(b, sizeof b, "import from %d (fd %d, %zu B)", x, fds[(size_t)x], total);
+      step(rank, b);
+    }
+    // HIP runtimes disagree on what osHandle is for a POSIX descriptor: the
+    // 7.0 runtime torch bundles reads it as a POINTER to the descriptor (the
+    // value form segfaults inside it), the 7.2 runtime takes the descriptor
+    // VALUE (the pointer form returns hipErrorInvalidValue, harmlessly) --
+    // measured, profiles/r2_direct_transport.txt.  So: pointer first, value
+    // on failure.
+    int fdv = fds[(size_t)x];
+    e = hipMemImportFromShareableHandle(&peer_h[(size_t)x], (void *)&fdv, hipMemHandleTypePosixFileDescriptor);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      e = hipMemImportFromShareableHandle(&peer_h[(size_t)x], (void *)(intptr_t)fdv,
+                                          hipMemHandleTypePosixFileDescriptor);
+    }
+    step(rank, e == hipSuccess ? "imported; mapping" : "import failed");
     if (e != hipSuccess) {
       err = std::string("import: ") + hipGetErrorString(e);
       rc = BINE_ERR_HIP;
@@ -276,21 +297,55 @@ int DirectState::connect_peers(uint64_t key, std::string &err) {
   return rc;
 }
 
-uint64_t *DirectState::ready(int owner, int from) const {
-  return (uint64_t *)((char *)peer[(size_t)owner] + kReadyOff + (size_t)from * kFlagStride);
+// one ready and one ack flag per (pair, slot): every flag has one writer at a
+// time, and its values only grow (a slot's next use waits for the ack of its
+// previous one).  A flag per pair would not do: two messages of one launch to
+// the same peer publish in either order, and a plain store of the smaller
+// sequence number after the larger would move the flag backwards.
+uint64_t *DirectState::ready(int owner, int from, uint64_t seq) const {
+  return (uint64_t *)((char *)peer[(size_t)owner] + kReadyOff +
+                      ((size_t)from * kSlots + (size_t)(seq % kSlots)) * kFlagStride);
 }
-uint64_t *DirectState::ack(int owner, int from) const {
-  return (uint64_t *)((char *)peer[(size_t)owner] + kAckOff + (size_t)from * kFlagStride);
+uint64_t *DirectState::ack(int owner, int from, uint64_t seq) const {
+  return (uint64_t *)((char *)peer[(size_t)owner] + kAckOff +
+                      ((size_t)from * kSlots + (size_t)(seq % kSlots)) * kFlagStride);
 }
-uint32_t *DirectState::cnt(bool push, int pr) const {
-  return (uint32_t *)((char *)own + (push ? kCntPushOff : kCntPullOff) + (size_t)pr * kFlagStride);
+// one counter per (peer, slot): two messages of one launch never share one
+// (the k-th message to a peer in a round uses slot (seq + k) % kSlots)
+uint32_t *DirectState::cnt(bool push, int pr, uint64_t seq) const {
+  return (uint32_t *)((char *)own + (push ? kCntPushOff : kCntPullOff) +
+                      ((size_t)pr * kSlots + (size_t)(seq % kSlots)) * kFlagStride);
 }
 uint32_t *DirectState::poison_ptr() const { return (uint32_t *)((char *)own + kPoisonOff); }
 uint8_t *DirectState::slot_ptr(int owner, int from, uint64_t seq) const {
-  return (uint8_t *)peer[(size_t)owner] + data_off + ((size_t)from * 2 + (size_t)(seq & 1)) * slot;
+  return (uint8_t *)peer[(size_t)owner] + data_off + ((size_t)from * kSlots + (size_t)(seq % kSlots)) * slot;
+}
+
+void DirectState::dump() const {
+  std::vector<uint64_t> rd((size_t)P, 0), ak((size_t)P, 0);
+  for (int x = 0; x < P; x++)
+    for (int k = 0; k < kSlots; k++) {
+      uint64_t a = 0, b = 0;
+      (void)hipMemcpy(&a, ready(rank, x, (uint64_t)k), 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(&b, ack(rank, x, (uint64_t)k), 8, hipMemcpyDeviceToHost);
+      rd[(size_t)x] = std::max(rd[(size_t)x], a);
+      ak[(size_t)x] = std::max(ak[(size_t)x], b);
+    }
+  for (int x = 0; x < P; x++)
+    if (x != rank)
+      fprintf(stderr, "[bine dm r%d] peer %d: ready (from it) %llu / recv_seq %llu, ack (from it) %llu / send_seq %llu\n",
+              rank, x, (unsigned long long)rd[(size_t)x], (unsigned long long)recv_seq[(size_t)x],
+              (unsigned long long)ak[(size_t)x], (unsigned long long)send_seq[(size_t)x]);
 }
 
 int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) {
+  // more messages to (or from) one peer in one exchange than slots per pair
+  // would make a push wait for a pull of the same exchange: refuse
+  std::vector<int> ns((size_t)P, 0), nr((size_t)P, 0);
+  for (const auto &x : s)
+    if (++ns[(size_t)x.peer] > kSlots) return BINE_ERR_UNSUPPORTED;
+  for (const auto &x : r)
+    if (++nr[(size_t)x.peer] > kSlots) return BINE_ERR_UNSUPPORTED;
   size_t maxb = 0;
   for (const auto &x : s) maxb = std::max(maxb, x.bytes);
   for (const auto &x : r) maxb = std::max(maxb, x.bytes);
@@ -315,13 +370,15 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.src = (const uint8_t *)x.ptr + off;
       m.dst = slot_ptr(x.peer, rank, seq);
       m.bytes = len;
-      m.wait_ptr = seq > 2 ? ack(rank, x.peer) : nullptr;  // the receiver's copy-out of seq - 2
-      m.wait_val = seq > 2 ? seq - 2 : 0;
-      m.sig_ptr = ready(x.peer, rank);
+      // the slot's previous use: sequence seq - kSlots, copied out by the receiver
+      m.wait_ptr = seq > (uint64_t)kSlots ? ack(rank, x.peer, seq) : nullptr;
+      m.wait_val = seq > (uint64_t)kSlots ? seq - kSlots : 0;
+      m.sig_ptr = ready(x.peer, rank, seq);
       m.sig_val = seq;
-      m.cnt_ptr = cnt(true, x.peer);
-      cnt_push[(size_t)x.peer] += (uint32_t)wgs;
-      m.cnt_target = cnt_push[(size_t)x.peer];
+      m.cnt_ptr = cnt(true, x.peer, seq);
+      uint32_t &cp = cnt_push[(size_t)x.peer * kSlots + (size_t)(seq % kSlots)];
+      cp += (uint32_t)wgs;
+      m.cnt_target = cp;
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }
@@ -334,13 +391,14 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.src = slot_ptr(rank, x.peer, seq);
       m.dst = (uint8_t *)x.ptr + off;
       m.bytes = len;
-      m.wait_ptr = ready(rank, x.peer);
+      m.wait_ptr = ready(rank, x.peer, seq);
       m.wait_val = seq;
-      m.sig_ptr = ack(x.peer, rank);
+      m.sig_ptr = ack(x.peer, rank, seq);
       m.sig_val = seq;
-      m.cnt_ptr = cnt(false, x.peer);
-      cnt_pull[(size_t)x.peer] += (uint32_t)wgs;
-      m.cnt_target = cnt_pull[(size_t)x.peer];
+      m.cnt_ptr = cnt(false, x.peer, seq);
+      uint32_t &cq = cnt_pull[(size_t)x.peer * kSlots + (size_t)(seq % kSlots)];
+      cq += (uint32_t)wgs;
+      m.cnt_target = cq;
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }

@@ -249,6 +249,11 @@ struct RcclTransport final : Transport {
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
     if (dm_on) {
       if (dm->poisoned()) {
+        static bool dumped = false;
+        if (!dumped && getenv("BINE_TRACE")) {
+          dumped = true;
+          dm->dump();
+        }
         set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
         return BINE_ERR_INTERNAL;
       }

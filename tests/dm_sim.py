@@ -1,0 +1,158 @@
+"""Host-only model of the direct peer-memory transport's protocol
+(pico_amd/csrc/direct.cpp) driven by the executor's real issue schedules
+(bine_plan_schedule): every rank's comm and compute streams, the cross-stream
+waits of the schedule, and per exchange the push / pull launches of each round
+with their flag waits (push: ack >= seq - SLOTS; pull: ready >= seq) and
+publications.  Messages of a started launch progress independently; a launch
+completes when all its messages have.  Runs a few consecutive collectives and
+reports a deadlock (no message or op can make progress) with the state.
+
+Used by tests/test_direct_protocol.py (CPU).  Mirrors DirectState::exchange:
+per peer, sequence numbers in the order the executor lists sends / receives;
+messages cut into sub-messages of SLOT bytes, round k = k-th sub-message.
+"""
+from __future__ import annotations
+
+import pico_amd
+
+SLOTS = 4
+
+
+def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P):
+    """DirectState::exchange for one exchange: list of launches, each a list
+    of messages {kind, peer, seq}"""
+    maxb = max([b for _, b in sends] + [b for _, b in recvs] + [0])
+    rounds = (maxb + slot - 1) // slot
+    out = []
+    ns, nr = [0] * P, [0] * P
+    for p, _ in sends:
+        ns[p] += 1
+        assert ns[p] <= SLOTS, "more messages to one peer than slots: refused by the library"
+    for p, _ in recvs:
+        nr[p] += 1
+        assert nr[p] <= SLOTS
+    for k in range(rounds):
+        push = []
+        for p, b in sends:
+            if b <= k * slot:
+                continue
+            seq_s[p] += 1
+            push.append({"kind": "push", "peer": p, "seq": seq_s[p]})
+        pull = []
+        for p, b in recvs:
+            if b <= k * slot:
+                continue
+            seq_r[p] += 1
+            pull.append({"kind": "pull", "peer": p, "seq": seq_r[p]})
+        if push:
+            out.append(push)
+        if pull:
+            out.append(pull)
+    return out
+
+
+def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay_min_bytes=0, trees=False,
+        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20):
+    """simulate `calls` consecutive collectives on all ranks; returns None if
+    every one completes, else a description of the deadlock"""
+    seq_s = [[0] * P for _ in range(P)]
+    seq_r = [[0] * P for _ in range(P)]
+    # ready[owner][from][slot], ack[owner][from][slot]: plain stores, as the
+    # kernel does (a flag per pair would move backwards -- the bug this models)
+    ready = [[[0] * SLOTS for _ in range(P)] for _ in range(P)]
+    ack = [[[0] * SLOTS for _ in range(P)] for _ in range(P)]
+    # per rank: list of ops (stream, deps, launches) over all calls
+    ranks = []
+    for r in range(P):
+        ops, c_join, final_wait = pico_amd.schedule(coll, algo, P, r, count=count, rcounts=rcounts, esz=esz,
+                                                    chunk_bytes=chunk_bytes, relay_min_bytes=relay_min_bytes,
+                                                    trees=trees, flat_ag=flat_ag, flat_rs=flat_rs)
+        seq = []
+        base = 0
+        for _call in range(calls):
+            first_c = None
+            for i, o in enumerate(ops):
+                stream = "C" if o["xchg"] else "K"
+                deps = []
+                if o["wait"] >= 0:
+                    deps.append(base + o["wait"])
+                launches = []
+                if o["xchg"]:
+                    sends = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "SEND" and p["count"]]
+                    recvs = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "RECV" and p["count"]]
+                    launches = exchange_launches(r, sends, recvs, seq_s[r], seq_r[r], slot, P)
+                    if first_c is None and c_join:
+                        first_c = base + i
+                        # c_join: the comm stream waits for the caller's stream's prior work
+                        deps.append(("K-before", base + i))
+                seq.append({"stream": stream, "deps": deps, "launches": launches, "done": False, "li": 0,
+                            "started": False})
+            if final_wait >= 0:
+                # the caller's stream waits for the comm stream's op final_wait before the next call
+                seq.append({"stream": "K", "deps": [base + final_wait], "launches": [], "done": False, "li": 0,
+                            "started": False})
+            base = len(seq)
+        ranks.append(seq)
+
+    def dep_done(r, d):
+        seq = ranks[r]
+        if isinstance(d, tuple):  # all K ops before index d
+            return all(seq[j]["done"] for j in range(d[1]) if seq[j]["stream"] == "K")
+        return seq[d]["done"]
+
+    def head(r, stream):
+        for j, op in enumerate(ranks[r]):
+            if op["stream"] == stream and not op["done"]:
+                return j
+        return None
+
+    progress = True
+    while progress:
+        progress = False
+        for r in range(P):
+            for stream in ("C", "K"):
+                j = head(r, stream)
+                if j is None:
+                    continue
+                op = ranks[r][j]
+                if not all(dep_done(r, d) for d in op["deps"]):
+                    continue
+                if op["li"] >= len(op["launches"]):
+                    op["done"] = True
+                    progress = True
+                    continue
+                # the current launch: its messages progress independently
+                launch = op["launches"][op["li"]]
+                for m in launch:
+                    if m.get("done"):
+                        continue
+                    p = m["peer"]
+                    k = m["seq"] % SLOTS
+                    if m["kind"] == "push":
+                        if m["seq"] > SLOTS and ack[r][p][k] < m["seq"] - SLOTS:
+                            continue
+                        assert ready[p][r][k] < m["seq"], "a ready flag would move backwards"
+                        ready[p][r][k] = m["seq"]
+                    else:
+                        if ready[r][p][k] < m["seq"]:
+                            continue
+                        assert ack[p][r][k] < m["seq"], "an ack flag would move backwards"
+                        ack[p][r][k] = m["seq"]
+                    m["done"] = True
+                    progress = True
+                if all(m.get("done") for m in launch):
+                    op["li"] += 1
+                    progress = True
+    stuck = []
+    for r in range(P):
+        for stream in ("C", "K"):
+            j = head(r, stream)
+            if j is not None:
+                op = ranks[r][j]
+                pend = []
+                if op["li"] < len(op["launches"]):
+                    pend = [(m["kind"], m["peer"], m["seq"]) for m in op["launches"][op["li"]] if not m.get("done")]
+                stuck.append((r, stream, j, op["deps"], pend))
+    if not stuck:
+        return None
+    return {"stuck": stuck, "ready": ready, "ack": ack}

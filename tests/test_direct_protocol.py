@@ -1,0 +1,42 @@
+"""The direct peer-memory transport's flag protocol (pico_amd/csrc/direct.cpp)
+over the executor's real issue schedules, on the host (tests/dm_sim.py):
+no deadlock and no flag that moves backwards, for every transport mode the
+bench trials, P = 2..8, consecutive collectives, including exchanges cut
+into several slot-sized rounds and launches that carry several messages to
+one peer (relay mode)."""
+import pytest
+
+import dm_sim
+
+MODES = {
+    "direct": {},
+    "flat": dict(flat_ag=True),
+    "flatrs+flat": dict(flat_ag=True, flat_rs=True),
+    "relay": dict(relay_min_bytes=256 << 10),
+    "relay+flat": dict(relay_min_bytes=256 << 10, flat_ag=True),
+    "trees": dict(trees=True),
+}
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_allreduce_protocol_completes(P, mode):
+    kw = dict(MODES[mode])
+    if mode == "trees" and P not in (4, 8):
+        pytest.skip("multi-tree mode: P = 4 or 8")
+    res = dm_sim.run("allreduce", "bine_bdw_remap", P, count=1 << 20, chunk_bytes=1 << 20, **kw)
+    assert res is None, res["stuck"][:8]
+
+
+@pytest.mark.parametrize("mode", ["direct", "relay", "flatrs+flat"])
+def test_multi_round_exchanges(mode):
+    # slot much smaller than the messages: every exchange runs several rounds
+    # and every slot is reused many times per collective
+    res = dm_sim.run("allreduce", "bine_bdw_remap", 4, count=1 << 20, chunk_bytes=4 << 20, slot=64 << 10,
+                     **MODES[mode])
+    assert res is None, res["stuck"][:8]
+
+
+def test_reduce_scatter_protocol_completes():
+    res = dm_sim.run("reduce_scatter", "bine_send_remap", 8, rcounts=[1 << 16] * 8, flat_rs=True)
+    assert res is None, res["stuck"][:8]

@@ -1,6 +1,7 @@
 #!/bin/bash
 cd "$(dirname "$0")/.."
-export PYTHONFAULTHANDLER=1 BINE_DIRECT_TIMEOUT_S=5 BINE_TRACE=1
+export PYTHONFAULTHANDLER=1 BINE_DIRECT_TIMEOUT_S=5
 bash tools/gpu_steps.sh \
-  "dm2:200:python3 -u tools/direct_probe.py 2 67108864 direct"
-grep "bine dm" gpurun_out/dm2.log | head -30
+  "dm4r:200:python3 -u tools/direct_probe.py 4 4194304 relay" \
+  "dm8r:200:python3 -u tools/direct_probe.py 8 4194304 relay" \
+  "t_large:500:python3 -u -m pytest -x -v --timeout 450 --timeout-method thread tests/test_gpu_rccl.py -k large"

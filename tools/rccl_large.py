@@ -8,7 +8,8 @@ allreduce_bine_bdw_remap on 64 MiB per rank in fp32 and fp64 with the DEFAULT
 k+1 on the comm stream beside the reduction of chunk k on the compute stream,
 the device form of libbine_allreduce.c:1218-1253) runs over real RCCL with
 several chunks per step -- for every transport bench.py may pick (direct,
-relay, flat, flatrs+flat, +ag, +a2a, trees), each eagerly and in graph mode
+relay, flat, flatrs+flat, +ag, +a2a, trees; and over the direct peer-memory
+transport "+dm"), each eagerly and in graph mode
 (bine_comm_set_graphs: one eager call + capture, then replays), plus
 reduce_scatter_bine_permute_remap
 on a 64 MiB input per rank (direct, flatrs, flatrs striped over 2
@@ -25,7 +26,8 @@ sys.path.insert(0, ROOT)
 
 N32 = 16_777_216   # 64 MiB fp32
 N64 = 8_388_608    # 64 MiB fp64
-MODES = ("direct", "relay", "flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+flat+a2a", "trees")
+MODES = ("direct", "relay", "flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+flat+a2a", "trees",
+         "direct+dm", "flatrs+flat+dm", "relay+flat+dm", "trees+dm")
 RS_MODES = (("direct", 1), ("flatrs", 1), ("flatrs", 2))
 
 
@@ -64,7 +66,8 @@ def worker(rank, P, port, want, q):
     comm = pico_amd.Comm.from_torch_distributed(0)
     bad, n_ok = [], 0
     side = torch.cuda.Stream()   # graph mode needs a non-NULL caller stream
-    modes = [m for m in MODES if m in bench.transport_modes("auto", P) or m == "flatrs+flat+a2a"]
+    modes = [m for m in MODES if m in bench.transport_modes("auto", P) or m in ("flatrs+flat+a2a", "relay+flat+dm",
+                                                                              "trees+dm")]
     for dt, n, tdt in (("float", N32, torch.float32), ("double", N64, torch.float64)):
         s = torch.empty(n, dtype=tdt, device="cuda:0")
         r = torch.empty(n, dtype=tdt, device="cuda:0")
@@ -82,7 +85,7 @@ def worker(rank, P, port, want, q):
                     torch.cuda.synchronize()
                     comm.synchronize()
                     d = pico_amd.checksum(r, n, dt)
-                    if d == want[("ar", dt, m == "trees")][rank]:
+                    if d == want[("ar", dt, m.startswith("trees"))][rank]:
                         n_ok += 1
                     else:
                         bad.append(f"allreduce {dt} {m} graphs={g} iter {it}")
