@@ -774,8 +774,10 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         # a setting the planner rejects fails identically on every rank before
         # any transfer (plans are a pure function of the arguments): skip it
         cfg = tuple(cfg) + (False, 1)[len(cfg) - 2:]
-        apply_transport(comm, *cfg)
         try:
+            # inside: enabling the direct transport fails on every rank alike
+            # when peer memory cannot be mapped (BINE_ERR_UNSUPPORTED)
+            apply_transport(comm, *cfg)
             rbuf.fill_(float("nan"))   # a transport that writes nothing cannot pass on the last one's output
             st = timed(torch, stream, run, 3, 2, dist, (comm.synchronize,))
             ok, _ = parity(cfg[0])
@@ -866,7 +868,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (pico_core rand_r distribution, seed 1234 + rank, generated on device)",
-            "config": {"workload": f"C3: allreduce_{algo} fp32 SUM {S // MIB} MiB/rank over RCCL P2P (xGMI), "
+            "config": {"workload": f"C3: allreduce_{algo} fp32 SUM {S // MIB} MiB/rank over "
+                                   f"{'mapped peer memory' if '+dm' in chosen else 'RCCL P2P'} (xGMI), "
                                    f"{world} x MI355X, device-resident",
                        "value_definition": "per-rank algbw = S / t, t = per-iteration max over ranks, median after "
                                            "dropping the first 20 % (pico_core.c:133-140, summarize_data.py:24-48)",
