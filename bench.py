@@ -684,8 +684,9 @@ def transport_modes(relay: str, world: int):
     hop on every link); "flatrs" = the reduce-scatter phase as one all-peers
     exchange whose owner evaluates the reference's reduction tree in one fused
     kernel; "+ag" / "+a2a" = the flat exchanges as ncclAllGather /
-    ncclAllToAllv; "trees" = P-1 relabelled instances over edge-disjoint
-    pairings.  All but "trees" are bit-identical to the reference."""
+    ncclAllToAllv; "+dm" = exchanges through mapped peer memory instead of
+    RCCL; "trees" = P-1 relabelled instances over edge-disjoint pairings.
+    All but "trees" are bit-identical to the reference."""
     modes = MODES.get(relay, [relay])
     if world <= 2:
         modes = [m for m in modes if "relay" not in m and "+ag" not in m and "+a2a" not in m] or ["direct"]

@@ -88,10 +88,11 @@ def test_overlap_fraction():
 
 
 def test_transport_modes():
-    assert bench.transport_modes("auto", 2) == ["direct", "flat", "flatrs+flat"]
+    assert bench.transport_modes("auto", 2) == ["direct", "flat", "flatrs+flat", "direct+dm", "flatrs+flat+dm"]
     assert "trees" in bench.transport_modes("auto", 8) and "flatrs+flat+ag" in bench.transport_modes("auto", 8)
     assert bench.transport_modes("flatrs+flat+a2a", 8) == ["flatrs+flat+a2a"]
-    assert bench.transport_modes("auto", 6) == ["direct", "relay"]
+    assert bench.transport_modes("auto", 6) == ["direct", "relay", "direct+dm"]
+    assert "relay+flat+dm" in bench.transport_modes("auto", 8)
     assert bench.transport_modes("off", 8) == ["direct"]
     assert bench.transport_modes("trees", 2) == ["direct"]
 
