@@ -34,6 +34,7 @@ import os
 import platform
 import statistics
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -727,7 +728,7 @@ def tname(cfg):
 
 
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
-                    chunk_mib: int = 0, graph_trial: bool = True, stripe_trials=(2, 4)):
+                    chunk_mib: int = 0, graph_trial: bool = True, stripe_trials=()):
     import pico_amd
     import torch
     import torch.distributed as dist
@@ -834,25 +835,6 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         del tree_out
         apply_transport(comm, chosen, chunk, graphs, stripes)
     ms = st["median_ms"]
-    steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
-                                                                      stream))
-    extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
-                                                           chosen, chunk, graphs, stripes)) if extras else {}
-    apply_transport(comm, chosen, chunk, graphs, stripes)
-    probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
-        if extras else {}
-    vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
-                                                                      stream, world, ms)) if extras else {}
-    # striped exchanges (bine_comm_set_stripes) are trialled LAST and only
-    # reported: creating ncclCommSplit children slows the parent communicator
-    # for the rest of the process even after they are destroyed (measured on
-    # RCCL's socket transport, 103 -> 220-240 ms, profiles/r2_stripes_probe.txt),
-    # so they must not run before the headline
-    stripe_ms = {}
-    for k in stripe_trials if world > 1 else ():
-        cfg = (chosen, chunk, False, k)
-        trial(cfg)
-        stripe_ms[tname(cfg)] = {"ms": round(trials[cfg], 4), "parity_ok": verdicts.get(cfg)}
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
     busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
@@ -887,13 +869,13 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                                   "trees_within_pico_core_eps": ok_trees_tol,
                                   "trials": {tname(c): v for c, v in verdicts.items()}},
                        "host_issue_ms_per_step": round(st["issue_ms"], 4),
-                       "step_profile_rank0": steps_prof,
+                       "step_profile_rank0": None,
                        "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
-                       "other_baseline_configs": extra,
-                       "rccl_p2p_probe": probe,
-                       "rccl_allreduce_baseline": vendor,
-                       "striped_exchanges_after_headline": stripe_ms,
+                       "other_baseline_configs": None,
+                       "rccl_p2p_probe": None,
+                       "rccl_allreduce_baseline": None,
+                       "striped_exchanges_after_headline": None,
                        "rccl": pico_amd.rccl_version(), "host": host_info()},
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 2), "peak": link_peak,
                          "unit": "GB/s", "frac": round(achieved / link_peak, 4),
@@ -910,6 +892,48 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                                  "(7 x 153), the BASELINE target's denominator"},
             "wall_s": round(st["wall_s"], 4),
         }
+    # the side measurements below run under a deadline: if one of them hangs
+    # (an RCCL or transport fault in a secondary configuration), every rank
+    # stops at the same budget and rank 0 still prints the headline line with
+    # what was measured so far -- a hang after the headline must not lose it
+    budget = float(os.environ.get("BENCH_SIDE_BUDGET_S", "300"))
+
+    def _cut():
+        if out is not None:
+            out["config"]["side_measurements_cut_after_s"] = budget
+            print(json.dumps(out), flush=True)
+        sys.stderr.write(f"bench: side measurements exceeded {budget:.0f} s; exiting\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    watchdog = threading.Timer(budget, _cut)
+    watchdog.daemon = True
+    watchdog.start()
+    steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
+                                                                      stream))
+    extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
+                                                           chosen, chunk, graphs, stripes)) if extras else {}
+    apply_transport(comm, chosen, chunk, graphs, stripes)
+    probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
+        if extras else {}
+    vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
+                                                                      stream, world, ms)) if extras else {}
+    # striped exchanges (bine_comm_set_stripes) are trialled LAST and only
+    # reported: creating ncclCommSplit children slows the parent communicator
+    # for the rest of the process even after they are destroyed (measured on
+    # RCCL's socket transport, 103 -> 220-240 ms, profiles/r2_stripes_probe.txt),
+    # so they must not run before the headline
+    stripe_ms = {}
+    for k in stripe_trials if world > 1 else ():
+        cfg = (chosen, chunk, False, k)
+        trial(cfg)
+        stripe_ms[tname(cfg)] = {"ms": round(trials[cfg], 4), "parity_ok": verdicts.get(cfg)}
+    watchdog.cancel()
+    if out is not None:
+        out["config"].update({"step_profile_rank0": steps_prof, "other_baseline_configs": extra,
+                              "rccl_p2p_probe": probe, "rccl_allreduce_baseline": vendor,
+                              "striped_exchanges_after_headline": stripe_ms})
+    if rank == 0:
         # the same egress against what RCCL P2P itself moves on this node: per
         # exchange op its busiest link at what RCCL moves per link in that
         # pattern -- the one-peer rate for a one-peer op, the all-peers egress
@@ -940,7 +964,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C1/C4/C5 side measurements")
     ap.add_argument("--no-graph-trial", action="store_true", help="N > 1: do not trial HIP-graph replay")
-    ap.add_argument("--stripes", default="2,4", help="N > 1: stripe counts to trial (comma list; empty: none)")
+    # off by default: a striped flatrs+flat trial over 3 communicators hung in
+    # 2 of 4 one-GPU socket-transport runs inside RCCL's communicator split
+    # (profiles/r2_direct_transport.txt), and a hang there would lose the line
+    ap.add_argument("--stripes", default="", help="N > 1: stripe counts to trial after the headline (comma list, "
+                                                  "e.g. 2,4; default none)")
     ap.add_argument("--cpu-budget", type=float, default=5.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:

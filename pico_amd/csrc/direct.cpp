@@ -17,12 +17,13 @@
 //   data    region[x] = kSlots slots of `slot` bytes, written only by rank x
 //
 // An exchange (sends / receives of one RCCL-style group) is cut into rounds:
-// round r carries sub-message r (at most `slot` bytes) of every message.  Per
-// round one k_dm_move launch PUSHES every send -- wait until the receiver has
-// acknowledged the slot's previous use (sequence s - kSlots), copy into the
-// receiver's slot s % kSlots, publish ready = s in the receiver's inbox -- and
-// one launch PULLS every receive -- wait for ready >= s, copy the slot into
-// the destination, publish ack = s in the sender's inbox.  Sequence numbers
+// round r carries sub-message r (at most `slot` bytes) of every message.  Each
+// round PUSHES every send -- wait until the receiver has acknowledged the
+// slot's previous use (sequence s - kSlots), copy into the receiver's slot
+// s % kSlots, publish ready = s in the receiver's inbox -- and PULLS every
+// receive -- wait for ready >= s, copy the slot into the destination, publish
+// ack = s in the sender's inbox.  One k_dm_move launch carries round r-1's
+// pulls together with round r's pushes.  Sequence numbers
 // are per ordered pair and monotonic, so flags never need resetting.
 // Deadlock freedom: at most kSlots messages per peer per exchange (more are
 // refused), so a push waits only for pulls of earlier rounds, which every
@@ -156,6 +157,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   device = device_;
   if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
+  if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = atoi(e) != 0;
   if (slot < (1 << 20)) slot = 1 << 20;
   slot = slot / 4096 * 4096;
   if (wgs < 1) wgs = 1;
@@ -350,18 +352,19 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   for (const auto &x : s) maxb = std::max(maxb, x.bytes);
   for (const auto &x : r) maxb = std::max(maxb, x.bytes);
   const size_t rounds = (maxb + slot - 1) / slot;
-  for (size_t k = 0; k < rounds; k++) {
-    // pushes of this round, kMaxDm messages per launch
-    DmArgs a;
-    a.wgs = wgs;
-    a.poison = poison_ptr();
-    a.poison_host = hpoison_dev;
-    a.timeout_ticks = timeout_ticks;
-    auto flush = [&]() -> int {
-      const int rc = launch_dm_move(a, st);
-      a.nmsg = 0;
-      return rc;
-    };
+  DmArgs a;
+  a.wgs = wgs;
+  a.poison = poison_ptr();
+  a.poison_host = hpoison_dev;
+  a.timeout_ticks = timeout_ticks;
+  auto flush = [&]() -> int {
+    const int rc = launch_dm_move(a, st);
+    a.nmsg = 0;
+    return rc;
+  };
+  // round k's pushes: into the receiver's slot, after its ack of the slot's
+  // previous use (sequence seq - kSlots)
+  auto pushes = [&](size_t k) -> int {
     for (const auto &x : s) {
       if (x.bytes <= k * slot) continue;
       const size_t off = k * slot, len = std::min(slot, x.bytes - off);
@@ -370,7 +373,6 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.src = (const uint8_t *)x.ptr + off;
       m.dst = slot_ptr(x.peer, rank, seq);
       m.bytes = len;
-      // the slot's previous use: sequence seq - kSlots, copied out by the receiver
       m.wait_ptr = seq > (uint64_t)kSlots ? ack(rank, x.peer, seq) : nullptr;
       m.wait_val = seq > (uint64_t)kSlots ? seq - kSlots : 0;
       m.sig_ptr = ready(x.peer, rank, seq);
@@ -382,7 +384,10 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }
-    if (int rc = flush()) return rc;
+    return BINE_SUCCESS;
+  };
+  // round k's pulls: out of our own slot once the sender marked it ready
+  auto pulls = [&](size_t k) -> int {
     for (const auto &x : r) {
       if (x.bytes <= k * slot) continue;
       const size_t off = k * slot, len = std::min(slot, x.bytes - off);
@@ -402,6 +407,21 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }
+    return BINE_SUCCESS;
+  };
+  // launch k carries round k-1's pulls and round k's pushes, so the links
+  // keep moving round k while round k-1 is copied out locally.  Deadlock-free
+  // as before: a push of round k waits only for pulls of rounds <= k-1, which
+  // every rank has issued in this or an earlier launch, and a pull of round
+  // k-1 only for pushes of round k-1 (messages of one launch progress
+  // independently).  merge = false: separate push and pull launches per round
+  for (size_t k = 0; k <= rounds; k++) {
+    if (k > 0)
+      if (int rc = pulls(k - 1)) return rc;
+    if (!merge)
+      if (int rc = flush()) return rc;
+    if (k < rounds)
+      if (int rc = pushes(k)) return rc;
     if (int rc = flush()) return rc;
   }
   return BINE_SUCCESS;

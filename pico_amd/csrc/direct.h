@@ -15,6 +15,7 @@ struct DirectState {
   static constexpr int kSlots = 4;  // slots per ordered pair: up to kSlots messages per peer per exchange round
   size_t slot = (size_t)16 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES)
   int wgs = 32;                    // workgroups per message (BINE_DIRECT_WGS)
+  bool merge = true;               // round k-1's pulls share a launch with round k's pushes (BINE_DIRECT_MERGE)
   uint64_t timeout_ticks = 0;      // wall_clock64 ticks of one wait (BINE_DIRECT_TIMEOUT_S, default 10 s)
   size_t data_off = 0, total = 0;
   hipMemGenericAllocationHandle_t own_h{};

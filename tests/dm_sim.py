@@ -18,7 +18,7 @@ import pico_amd
 SLOTS = 4
 
 
-def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P):
+def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=True):
     """DirectState::exchange for one exchange: list of launches, each a list
     of messages {kind, peer, seq}"""
     maxb = max([b for _, b in sends] + [b for _, b in recvs] + [0])
@@ -31,28 +31,38 @@ def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P):
     for p, _ in recvs:
         nr[p] += 1
         assert nr[p] <= SLOTS
-    for k in range(rounds):
-        push = []
+    def pushes(k):
+        out = []
         for p, b in sends:
-            if b <= k * slot:
-                continue
-            seq_s[p] += 1
-            push.append({"kind": "push", "peer": p, "seq": seq_s[p]})
-        pull = []
+            if b > k * slot:
+                seq_s[p] += 1
+                out.append({"kind": "push", "peer": p, "seq": seq_s[p]})
+        return out
+
+    def pulls(k):
+        out = []
         for p, b in recvs:
-            if b <= k * slot:
-                continue
-            seq_r[p] += 1
-            pull.append({"kind": "pull", "peer": p, "seq": seq_r[p]})
-        if push:
-            out.append(push)
-        if pull:
-            out.append(pull)
+            if b > k * slot:
+                seq_r[p] += 1
+                out.append({"kind": "pull", "peer": p, "seq": seq_r[p]})
+        return out
+
+    # launch k = round k-1's pulls + round k's pushes (merge), or the two as
+    # separate launches
+    for k in range(rounds + 1):
+        launch = pulls(k - 1) if k > 0 else []
+        if not merge and launch:
+            out.append(launch)
+            launch = []
+        if k < rounds:
+            launch = launch + pushes(k)
+        if launch:
+            out.append(launch)
     return out
 
 
 def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay_min_bytes=0, trees=False,
-        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20):
+        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20, merge=True):
     """simulate `calls` consecutive collectives on all ranks; returns None if
     every one completes, else a description of the deadlock"""
     seq_s = [[0] * P for _ in range(P)]
@@ -80,7 +90,7 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                 if o["xchg"]:
                     sends = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "SEND" and p["count"]]
                     recvs = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "RECV" and p["count"]]
-                    launches = exchange_launches(r, sends, recvs, seq_s[r], seq_r[r], slot, P)
+                    launches = exchange_launches(r, sends, recvs, seq_s[r], seq_r[r], slot, P, merge)
                     if first_c is None and c_join:
                         first_c = base + i
                         # c_join: the comm stream waits for the caller's stream's prior work

@@ -4,6 +4,7 @@ P processes on the one GPU of the test box (cross-process VMM mappings of one
 device; timings say nothing about xGMI), C3 allreduce (256 MiB/rank fp32) per
 transport, RCCL vs direct, per-iteration max over ranks, median; parity vs the
 committed oracle digests.  usage: python tools/direct_probe.py [P] [n] [modes]
+(PROBE_DM_ONLY=1: the direct transport only)
 """
 import json
 import os
@@ -35,7 +36,7 @@ def worker(rank, P, n, modes, port, q):
     key = bench.gkey("C3" if n == bench.C3_ELEMS else "C1", "allreduce", "bine_bdw_remap", "float", n, P)
     out = {}
     for mode in modes:
-        for direct in (False, True):
+        for direct in ((True,) if os.environ.get("PROBE_DM_ONLY") == "1" else (False, True)):
             bench.apply_transport(comm, mode, 16 << 20)
             comm.set_direct(direct)
             rb.fill_(float("nan"))
@@ -57,6 +58,7 @@ def worker(rank, P, n, modes, port, q):
 
 if __name__ == "__main__":
     import multiprocessing as mp
+    from tools._procs import join_ranks
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 67_108_864
     modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["direct", "flatrs+flat"]
@@ -65,8 +67,7 @@ if __name__ == "__main__":
     ps = [ctx.Process(target=worker, args=(r, P, n, modes, 29641, q)) for r in range(P)]
     for p in ps:
         p.start()
-    for p in ps:
-        p.join(300)
+    join_ranks(ps, 300)
     for p in ps:
         if p.is_alive():
             p.kill()

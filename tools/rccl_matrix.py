@@ -176,14 +176,14 @@ def worker(rank, P, port, q):
 
 if __name__ == "__main__":
     import multiprocessing as mp
+    from tools._procs import join_ranks
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=worker, args=(r, P, 29577, q)) for r in range(P)]
     for p in ps:
         p.start()
-    for p in ps:
-        p.join(600)
+    join_ranks(ps, 600)
     res = [q.get() for _ in range(sum(1 for p in ps if p.exitcode == 0))]
     print("RESULT P=%d" % P, sorted(res), "exitcodes", [p.exitcode for p in ps], flush=True)
     sys.exit(0 if len(res) == P and all(b == 0 for _, _, b in res) else 1)
