@@ -727,6 +727,26 @@ def tname(cfg):
             + ("+graph" if len(cfg) > 2 and cfg[2] else ""))
 
 
+def arm_deadline(budget_s, payload, what):
+    """A daemon timer: unless cancelled within budget_s seconds, print
+    payload() as the JSON line (when it is not None -- rank 0), say so on
+    stderr and end the process with status 0.  Every rank arms the same
+    budget, so all ranks stop together instead of waiting in a collective a
+    hung peer never joins."""
+    def fire():
+        line = payload()
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        sys.stderr.write(f"bench: {what} exceeded {budget_s:.0f} s; exiting\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    t = threading.Timer(budget_s, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
                     chunk_mib: int = 0, graph_trial: bool = True, stripe_trials=()):
     import pico_amd
@@ -898,17 +918,12 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # what was measured so far -- a hang after the headline must not lose it
     budget = float(os.environ.get("BENCH_SIDE_BUDGET_S", "300"))
 
-    def _cut():
+    def _partial():
         if out is not None:
             out["config"]["side_measurements_cut_after_s"] = budget
-            print(json.dumps(out), flush=True)
-        sys.stderr.write(f"bench: side measurements exceeded {budget:.0f} s; exiting\n")
-        sys.stderr.flush()
-        os._exit(0)
+        return out
 
-    watchdog = threading.Timer(budget, _cut)
-    watchdog.daemon = True
-    watchdog.start()
+    watchdog = arm_deadline(budget, _partial, "side measurements")
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,

@@ -101,3 +101,32 @@ def test_all_ok_without_dist():
     assert bench.all_ok(None, None, True) is True
     assert bench.all_ok(None, None, False) is False
     assert bench.all_ok(None, None, None) is None
+
+
+def test_arm_deadline_prints_partial_line_and_exits(tmp_path):
+    """a side measurement that hangs past the budget: the line measured so far
+    is printed and the process ends with status 0 (bench.arm_deadline)"""
+    import subprocess
+    import sys
+    script = (
+        "import sys, time; sys.path.insert(0, %r)\n"
+        "import bench\n"
+        "out = {'metric': 'm', 'value': 1.0, 'config': {}}\n"
+        "def partial():\n"
+        "    out['config']['side_measurements_cut_after_s'] = 0.3\n"
+        "    return out\n"
+        "bench.arm_deadline(0.3, partial, 'side measurements')\n"
+        "time.sleep(30)\n"
+        "print('not reached')\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert lines == [{"metric": "m", "value": 1.0, "config": {"side_measurements_cut_after_s": 0.3}}]
+    assert "not reached" not in r.stdout and "exceeded" in r.stderr
+
+
+def test_arm_deadline_cancelled_is_silent():
+    import time
+    t = bench.arm_deadline(0.2, lambda: {"x": 1}, "test")
+    t.cancel()
+    time.sleep(0.4)   # still alive: the timer did not fire
