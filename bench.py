@@ -727,6 +727,16 @@ def tname(cfg):
             + ("+graph" if len(cfg) > 2 and cfg[2] else ""))
 
 
+def _best_of(trials, verdicts, nbytes, keep):
+    """the fastest trial config passing `keep` whose output matched the
+    oracle: {transport, ms, algbw_per_rank_GBs} (None if there is none)"""
+    ok = [(v, c) for c, v in trials.items() if keep(c) and verdicts.get(c) is True and v != float("inf")]
+    if not ok:
+        return None
+    v, c = min(ok)
+    return {"transport": tname(c), "ms": round(v, 4), "algbw_per_rank_GBs": round(nbytes / (v * 1e-3) / 1e9, 2)}
+
+
 def arm_deadline(budget_s, payload, what):
     """A daemon timer: unless cancelled within budget_s seconds, print
     payload() as the JSON line (when it is not None -- rank 0), say so on
@@ -891,6 +901,9 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                        "host_issue_ms_per_step": round(st["issue_ms"], 4),
                        "step_profile_rank0": None,
                        "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
+                       # north_star names RCCL point-to-point: the fastest correct
+                       # RCCL transport's figure beside the headline, whichever won
+                       "best_rccl_p2p": _best_of(trials, verdicts, S, lambda c: "+dm" not in c[0]),
                        "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
                        "other_baseline_configs": None,
                        "rccl_p2p_probe": None,

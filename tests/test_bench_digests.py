@@ -130,3 +130,16 @@ def test_arm_deadline_cancelled_is_silent():
     t = bench.arm_deadline(0.2, lambda: {"x": 1}, "test")
     t.cancel()
     time.sleep(0.4)   # still alive: the timer did not fire
+
+
+def test_best_of_picks_fastest_verified_rccl_trial():
+    inf = float("inf")
+    trials = {("direct", 16 << 20, False, 1): 3.0, ("flat", 16 << 20, False, 1): 2.0,
+              ("flatrs+flat", 16 << 20, False, 1): 1.0, ("direct+dm", 16 << 20, False, 1): 0.5,
+              ("relay", 16 << 20, False, 1): inf}
+    verdicts = {("direct", 16 << 20, False, 1): True, ("flat", 16 << 20, False, 1): True,
+                ("flatrs+flat", 16 << 20, False, 1): False, ("direct+dm", 16 << 20, False, 1): True,
+                ("relay", 16 << 20, False, 1): "error"}
+    b = bench._best_of(trials, verdicts, 1 << 28, lambda c: "+dm" not in c[0])
+    assert b == {"transport": "flat/16MiB", "ms": 2.0, "algbw_per_rank_GBs": round((1 << 28) / 2e-3 / 1e9, 2)}
+    assert bench._best_of(trials, verdicts, 1 << 28, lambda c: False) is None
