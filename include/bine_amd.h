@@ -268,17 +268,21 @@ int bine_comm_set_stripes(bine_comm_t comm, int k);
  * move through device memory every rank maps from every peer (VMM
  * allocations exported as POSIX file descriptors and handed over Unix
  * sockets; on one node peer memory is reachable over xGMI by plain loads and
- * stores) instead of RCCL's send/receive: per exchange round one kernel
- * pushes every outgoing message into the receiver's double-buffered slot and
- * one pulls every incoming message out of its own, with release/acquire
- * flags at system scope.  Same bytes in the same places: results
- * bit-identical.  Every wait has a time limit (BINE_DIRECT_TIMEOUT_S, default
- * 10 s); a timeout disables the transport (BINE_ERR_INTERNAL from then on)
- * instead of hanging.  The first call with on = 1 is collective (every rank
- * of the communicator, at the same point).  Graph mode runs such
- * collectives eagerly.  At most 4 messages to one peer per exchange group
+ * stores) instead of RCCL's send/receive: each exchange round pushes every
+ * outgoing message into one of the receiver's 4 slots for this sender and
+ * pulls every incoming message out of its own (one kernel launch carries a
+ * round's pulls with the next round's pushes), with release/acquire flags at
+ * system scope.  Same bytes in the same places: results bit-identical.  Every
+ * wait has a time limit (BINE_DIRECT_TIMEOUT_S, default 10 s); a timeout
+ * disables the transport (BINE_ERR_INTERNAL from then on) instead of
+ * hanging.  The first call with on = 1 is collective (every rank of the
+ * communicator, at the same point).  Sequence numbers live in device memory,
+ * so graph mode captures and replays these collectives too.  At most 4
+ * messages to one peer per exchange group
  * (BINE_ERR_UNSUPPORTED beyond).  Knobs: BINE_DIRECT_SLOT_BYTES (16 MiB),
- * BINE_DIRECT_WGS (workgroups per message, 32).  Loopback: UNSUPPORTED. */
+ * BINE_DIRECT_WGS (workgroups per message, 32), BINE_DIRECT_MERGE (1; 0:
+ * separate push and pull launches).  At most 64 ranks.  Loopback:
+ * UNSUPPORTED. */
 int bine_comm_set_direct(bine_comm_t comm, int on);
 
 /* Graph mode (RCCL communicators): the first collective call for a given

@@ -122,26 +122,37 @@ int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count,
 int launch_copy(void *dst, const void *src, size_t bytes, void *stream);
 int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *stream);
 
-// direct peer-memory transport (direct.cpp): one launch moves one round of an
-// exchange -- up to kMaxDm messages, `wgs` workgroups each (k_dm_move)
+// direct peer-memory transport (direct.cpp): one launch moves up to kMaxDm
+// messages, `wgs` workgroups each (k_dm_move).  Sequence numbers live in the
+// device (per peer and direction, in the rank's own inbox) and every address
+// and flag is derived from them in the kernel, so launches carry no host-side
+// state and can be captured into a graph and replayed.
 constexpr int kMaxDm = 16;
+// the inbox layout (bytes from its base): flags region, then the data slots
+namespace dm {
+constexpr size_t kFlagStride = 128;  // one flag / counter per 128-B line
+constexpr size_t kReadyOff = 0, kAckOff = 64 << 10, kCntPushOff = 128 << 10, kCntPullOff = 192 << 10,
+                 kPoisonOff = 256 << 10, kBaseSendOff = 260 << 10, kBaseRecvOff = 264 << 10,
+                 kLaunchCntOff = 268 << 10, kPeerTabOff = 272 << 10, kFlagsBytes = 320 << 10;
+constexpr int kSlots = 4;      // slots per ordered pair
+constexpr int kMaxPeers = 64;  // P limit of the layout (flag regions: P * kSlots * 128 B <= 64 KiB)
+}  // namespace dm
 struct DmMsg {
-  const uint8_t *src;
-  uint8_t *dst;
+  const uint8_t *src;  // push: the data to send (pull: unused -- the slot)
+  uint8_t *dst;        // pull: where the data goes (push: unused -- the peer's slot)
   uint64_t bytes;
-  const uint64_t *wait_ptr;  // poll until *wait_ptr >= wait_val (nullptr: no wait)
-  uint64_t wait_val;
-  uint64_t *sig_ptr;         // the last workgroup stores sig_val here (release, system scope)
-  uint64_t sig_val;
-  uint32_t *cnt_ptr;         // arrival counter; the workgroup whose increment reaches cnt_target is last
-  uint32_t cnt_target;
+  int push;            // 1: into the peer's inbox, 0: out of our own
+  int peer;
+  int j;               // this launch's j-th message of this kind to / from `peer`: seq = base[peer] + j + 1
 };
 struct DmArgs {
   int nmsg = 0;
   int wgs = 1;
-  uint32_t *poison = nullptr;       // nonzero: a wait timed out -- every launch exits at once
-  uint32_t *poison_host = nullptr;  // mapped host word set together with *poison (read by the host)
-  uint64_t timeout_ticks = 0;       // wall_clock64 ticks
+  int rank = 0;
+  uint64_t slot = 0;               // bytes per slot
+  uint8_t *own = nullptr;          // this rank's inbox (flags, counters, sequence bases, peer table)
+  uint32_t *poison_host = nullptr; // mapped host word set together with the inbox's poison word
+  uint64_t timeout_ticks = 0;      // wall_clock64 ticks
   DmMsg m[kMaxDm];
 };
 int launch_dm_move(const DmArgs &a, void *stream);

@@ -8,12 +8,15 @@
 // Handle + hipMemMap + hipMemSetAccess for its own device): on one node the
 // peers' memory is reachable over xGMI by plain loads and stores.
 //
-// Inbox layout (rank y):
+// Inbox layout (rank y; offsets in bine_internal.h, namespace dm):
 //   flags   ready[x][k] latest sequence number x has published into y's slot k
 //           ack[x][k]   latest sequence number of y's slot-k sub-message to x
 //                       that x has copied out
-//           cnt_push[x], cnt_pull[x]  arrival counters of k_dm_move (local)
+//           cnt_push[x][k], cnt_pull[x][k]  arrival counters of k_dm_move (local)
 //           poison     nonzero once a wait timed out (the transport is then dead)
+//           base_send[x], base_recv[x]  sub-messages to / from x so far (local;
+//                       the sequence numbers live here, not on the host)
+//           launch counter, peer table (x -> x's inbox as mapped here)
 //   data    region[x] = kSlots slots of `slot` bytes, written only by rank x
 //
 // An exchange (sends / receives of one RCCL-style group) is cut into rounds:
@@ -36,9 +39,10 @@
 //
 // The received bytes are copied out of the slot (one extra local pass over
 // HBM per received byte -- HBM is ~8x the xGMI rate, so it is not the bound);
-// sends read the caller's buffer directly.  Graph capture is not possible
-// (host-side sequence numbers advance per call): graph mode runs such
-// collectives eagerly.
+// sends read the caller's buffer directly.  Launch arguments hold no
+// sequence numbers (the kernel derives every slot and flag from the device-side
+// bases), so collectives over this transport can be captured into a graph and
+// replayed (bine_comm_set_graphs).
 #include <hip/hip_runtime.h>
 #include <poll.h>
 #include <sys/socket.h>
@@ -64,9 +68,7 @@ void step(int rank, const char *what) {
   if (on) fprintf(stderr, "[bine dm r%d] %s\n", rank, what);
 }
 
-constexpr size_t kFlagStride = 128;  // one flag per 128-B line
-constexpr size_t kReadyOff = 0, kAckOff = 64 << 10, kCntPushOff = 128 << 10, kCntPullOff = 192 << 10,
-                 kPoisonOff = 256 << 10, kFlagsBytes = 320 << 10;
+using namespace dm;
 
 int send_fd(int sock, int fd, int rank) {
   iovec io{&rank, sizeof rank};
@@ -155,6 +157,10 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   P = P_;
   rank = rank_;
   device = device_;
+  if (P > kMaxPeers) {
+    err = "direct transport: more ranks than the inbox layout holds";
+    return BINE_ERR_UNSUPPORTED;
+  }
   if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = atoi(e) != 0;
@@ -198,10 +204,6 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   peer.assign((size_t)P, nullptr);
   peer_h.assign((size_t)P, hipMemGenericAllocationHandle_t{});
   peer[(size_t)rank] = own;
-  send_seq.assign((size_t)P, 0);
-  recv_seq.assign((size_t)P, 0);
-  cnt_push.assign((size_t)P * kSlots, 0);
-  cnt_pull.assign((size_t)P * kSlots, 0);
   return BINE_SUCCESS;
 }
 
@@ -210,7 +212,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
 // descriptor to every peer, take theirs, map their inboxes.  Every blocking
 // step has a time limit.
 int DirectState::connect_peers(uint64_t key, std::string &err) {
-  if (P == 1) return BINE_SUCCESS;
+  if (P == 1) return BINE_SUCCESS;  // no exchanges at P = 1
   int rc = BINE_SUCCESS;
   hipError_t e;
 
@@ -296,48 +298,42 @@ int DirectState::connect_peers(uint64_t key, std::string &err) {
   }
   for (int fd : fds)
     if (fd >= 0) close(fd);
-  return rc;
+  if (rc) return rc;
+  // the peer table the kernel reads: x -> x's inbox as mapped in this process
+  std::vector<uint64_t> tab((size_t)P);
+  for (int x = 0; x < P; x++) tab[(size_t)x] = (uint64_t)(uintptr_t)peer[(size_t)x];
+  e = hipMemcpy((char *)own + kPeerTabOff, tab.data(), tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    err = std::string("peer table: ") + hipGetErrorString(e);
+    return BINE_ERR_HIP;
+  }
+  return BINE_SUCCESS;
 }
 
-// one ready and one ack flag per (pair, slot): every flag has one writer at a
-// time, and its values only grow (a slot's next use waits for the ack of its
-// previous one).  A flag per pair would not do: two messages of one launch to
-// the same peer publish in either order, and a plain store of the smaller
-// sequence number after the larger would move the flag backwards.
-uint64_t *DirectState::ready(int owner, int from, uint64_t seq) const {
-  return (uint64_t *)((char *)peer[(size_t)owner] + kReadyOff +
-                      ((size_t)from * kSlots + (size_t)(seq % kSlots)) * kFlagStride);
-}
-uint64_t *DirectState::ack(int owner, int from, uint64_t seq) const {
-  return (uint64_t *)((char *)peer[(size_t)owner] + kAckOff +
-                      ((size_t)from * kSlots + (size_t)(seq % kSlots)) * kFlagStride);
-}
-// one counter per (peer, slot): two messages of one launch never share one
-// (the k-th message to a peer in a round uses slot (seq + k) % kSlots)
-uint32_t *DirectState::cnt(bool push, int pr, uint64_t seq) const {
-  return (uint32_t *)((char *)own + (push ? kCntPushOff : kCntPullOff) +
-                      ((size_t)pr * kSlots + (size_t)(seq % kSlots)) * kFlagStride);
-}
-uint32_t *DirectState::poison_ptr() const { return (uint32_t *)((char *)own + kPoisonOff); }
-uint8_t *DirectState::slot_ptr(int owner, int from, uint64_t seq) const {
-  return (uint8_t *)peer[(size_t)owner] + data_off + ((size_t)from * kSlots + (size_t)(seq % kSlots)) * slot;
+// One ready and one ack flag per (pair, slot), and one arrival counter per
+// (peer, slot, direction): every flag has one writer at a time and its values
+// only grow (a slot's next use waits for the ack of its previous one).  A flag
+// per pair would not do: two messages of one launch to the same peer publish
+// in either order, and a plain store of the smaller sequence number after the
+// larger would move the flag backwards.
+static uint64_t rd64(const void *p) {
+  uint64_t v = 0;
+  (void)hipMemcpy(&v, p, 8, hipMemcpyDeviceToHost);
+  return v;
 }
 
 void DirectState::dump() const {
-  std::vector<uint64_t> rd((size_t)P, 0), ak((size_t)P, 0);
-  for (int x = 0; x < P; x++)
+  for (int x = 0; x < P; x++) {
+    if (x == rank) continue;
+    uint64_t rd = 0, ak = 0;
     for (int k = 0; k < kSlots; k++) {
-      uint64_t a = 0, b = 0;
-      (void)hipMemcpy(&a, ready(rank, x, (uint64_t)k), 8, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(&b, ack(rank, x, (uint64_t)k), 8, hipMemcpyDeviceToHost);
-      rd[(size_t)x] = std::max(rd[(size_t)x], a);
-      ak[(size_t)x] = std::max(ak[(size_t)x], b);
+      rd = std::max(rd, rd64((char *)own + kReadyOff + ((size_t)x * kSlots + k) * kFlagStride));
+      ak = std::max(ak, rd64((char *)own + kAckOff + ((size_t)x * kSlots + k) * kFlagStride));
     }
-  for (int x = 0; x < P; x++)
-    if (x != rank)
-      fprintf(stderr, "[bine dm r%d] peer %d: ready (from it) %llu / recv_seq %llu, ack (from it) %llu / send_seq %llu\n",
-              rank, x, (unsigned long long)rd[(size_t)x], (unsigned long long)recv_seq[(size_t)x],
-              (unsigned long long)ak[(size_t)x], (unsigned long long)send_seq[(size_t)x]);
+    fprintf(stderr, "[bine dm r%d] peer %d: ready (from it) %llu / received %llu, ack (from it) %llu / sent %llu\n",
+            rank, x, (unsigned long long)rd, (unsigned long long)rd64((char *)own + kBaseRecvOff + 8 * (size_t)x),
+            (unsigned long long)ak, (unsigned long long)rd64((char *)own + kBaseSendOff + 8 * (size_t)x));
+  }
 }
 
 int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) {
@@ -345,42 +341,43 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   // would make a push wait for a pull of the same exchange: refuse
   std::vector<int> ns((size_t)P, 0), nr((size_t)P, 0);
   for (const auto &x : s)
-    if (++ns[(size_t)x.peer] > kSlots) return BINE_ERR_UNSUPPORTED;
+    if (x.peer < 0 || x.peer >= P || ++ns[(size_t)x.peer] > kSlots) return BINE_ERR_UNSUPPORTED;
   for (const auto &x : r)
-    if (++nr[(size_t)x.peer] > kSlots) return BINE_ERR_UNSUPPORTED;
+    if (x.peer < 0 || x.peer >= P || ++nr[(size_t)x.peer] > kSlots) return BINE_ERR_UNSUPPORTED;
   size_t maxb = 0;
   for (const auto &x : s) maxb = std::max(maxb, x.bytes);
   for (const auto &x : r) maxb = std::max(maxb, x.bytes);
   const size_t rounds = (maxb + slot - 1) / slot;
   DmArgs a;
   a.wgs = wgs;
-  a.poison = poison_ptr();
+  a.rank = rank;
+  a.slot = slot;
+  a.own = (uint8_t *)own;
   a.poison_host = hpoison_dev;
   a.timeout_ticks = timeout_ticks;
+  // j = index of a message among this launch's messages of its kind to / from
+  // its peer (the kernel adds it to the device-side base)
+  std::vector<int> js((size_t)P, 0), jr((size_t)P, 0);
   auto flush = [&]() -> int {
     const int rc = launch_dm_move(a, st);
     a.nmsg = 0;
+    std::fill(js.begin(), js.end(), 0);
+    std::fill(jr.begin(), jr.end(), 0);
     return rc;
   };
   // round k's pushes: into the receiver's slot, after its ack of the slot's
-  // previous use (sequence seq - kSlots)
+  // previous use
   auto pushes = [&](size_t k) -> int {
     for (const auto &x : s) {
       if (x.bytes <= k * slot) continue;
       const size_t off = k * slot, len = std::min(slot, x.bytes - off);
-      const uint64_t seq = ++send_seq[(size_t)x.peer];
       DmMsg &m = a.m[a.nmsg++];
       m.src = (const uint8_t *)x.ptr + off;
-      m.dst = slot_ptr(x.peer, rank, seq);
+      m.dst = nullptr;
       m.bytes = len;
-      m.wait_ptr = seq > (uint64_t)kSlots ? ack(rank, x.peer, seq) : nullptr;
-      m.wait_val = seq > (uint64_t)kSlots ? seq - kSlots : 0;
-      m.sig_ptr = ready(x.peer, rank, seq);
-      m.sig_val = seq;
-      m.cnt_ptr = cnt(true, x.peer, seq);
-      uint32_t &cp = cnt_push[(size_t)x.peer * kSlots + (size_t)(seq % kSlots)];
-      cp += (uint32_t)wgs;
-      m.cnt_target = cp;
+      m.push = 1;
+      m.peer = x.peer;
+      m.j = js[(size_t)x.peer]++;
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }
@@ -391,30 +388,24 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
     for (const auto &x : r) {
       if (x.bytes <= k * slot) continue;
       const size_t off = k * slot, len = std::min(slot, x.bytes - off);
-      const uint64_t seq = ++recv_seq[(size_t)x.peer];
       DmMsg &m = a.m[a.nmsg++];
-      m.src = slot_ptr(rank, x.peer, seq);
+      m.src = nullptr;
       m.dst = (uint8_t *)x.ptr + off;
       m.bytes = len;
-      m.wait_ptr = ready(rank, x.peer, seq);
-      m.wait_val = seq;
-      m.sig_ptr = ack(x.peer, rank, seq);
-      m.sig_val = seq;
-      m.cnt_ptr = cnt(false, x.peer, seq);
-      uint32_t &cq = cnt_pull[(size_t)x.peer * kSlots + (size_t)(seq % kSlots)];
-      cq += (uint32_t)wgs;
-      m.cnt_target = cq;
+      m.push = 0;
+      m.peer = x.peer;
+      m.j = jr[(size_t)x.peer]++;
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }
     return BINE_SUCCESS;
   };
   // launch k carries round k-1's pulls and round k's pushes, so the links
-  // keep moving round k while round k-1 is copied out locally.  Deadlock-free
-  // as before: a push of round k waits only for pulls of rounds <= k-1, which
-  // every rank has issued in this or an earlier launch, and a pull of round
-  // k-1 only for pushes of round k-1 (messages of one launch progress
-  // independently).  merge = false: separate push and pull launches per round
+  // keep moving round k while round k-1 is copied out locally.  Deadlock-free:
+  // a push of round k waits only for pulls of rounds <= k-1, which every rank
+  // has issued in this or an earlier launch, and a pull of round k-1 only for
+  // pushes of round k-1 (messages of one launch progress independently).
+  // merge = false: separate push and pull launches per round
   for (size_t k = 0; k <= rounds; k++) {
     if (k > 0)
       if (int rc = pulls(k - 1)) return rc;

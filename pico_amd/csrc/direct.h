@@ -12,7 +12,6 @@ namespace bine {
 
 struct DirectState {
   int P = 1, rank = 0, device = 0;
-  static constexpr int kSlots = 4;  // slots per ordered pair: up to kSlots messages per peer per exchange round
   size_t slot = (size_t)16 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES)
   int wgs = 32;                    // workgroups per message (BINE_DIRECT_WGS)
   bool merge = true;               // round k-1's pulls share a launch with round k's pushes (BINE_DIRECT_MERGE)
@@ -25,8 +24,6 @@ struct DirectState {
   uint32_t *hpoison_dev = nullptr;  // its device-side address
   std::vector<void *> peer;  // peer[x] = x's inbox mapped here (peer[rank] = own)
   std::vector<hipMemGenericAllocationHandle_t> peer_h;
-  std::vector<uint64_t> send_seq, recv_seq;  // per peer: last sub-message sequence number
-  std::vector<uint32_t> cnt_push, cnt_pull;  // per (peer, slot): arrival-counter targets issued so far
 
   ~DirectState();
   // phase 1, local: allocate the inbox, zero its flags, export its descriptor
@@ -36,14 +33,8 @@ struct DirectState {
   int connect_peers(uint64_t key, std::string &err);
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st);
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }
-  // stderr: this rank's flags and host-side sequence numbers (after a timeout)
+  // stderr: this rank's flags and device-side sequence bases (after a timeout)
   void dump() const;
-
-  uint64_t *ready(int owner, int from, uint64_t seq) const;
-  uint64_t *ack(int owner, int from, uint64_t seq) const;
-  uint32_t *cnt(bool push, int peer, uint64_t seq) const;
-  uint32_t *poison_ptr() const;
-  uint8_t *slot_ptr(int owner, int from, uint64_t seq) const;
 };
 
 }  // namespace bine

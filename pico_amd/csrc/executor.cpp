@@ -82,6 +82,11 @@ struct Transport {
   virtual void retire() {}
   virtual int stripes() const { return 1; }
   virtual bool capturable() const { return stripes() == 1; }
+  // device-side transport state that must see every collective's exchanges
+  // in one stream order (the direct transport's sequence bases)
+  virtual bool stream_ordered() const { return false; }
+  // non-success: the transport is unusable (checked before a graph replay)
+  virtual int health() const { return BINE_SUCCESS; }
 };
 
 static bool nccl_type(int dtype, ncclDataType_t *t) {
@@ -147,7 +152,16 @@ struct RcclTransport final : Transport {
   std::unique_ptr<DirectState> dm;
   bool dm_on = false;
   uint64_t key = 0;  // hash of the unique id: names the direct transport's sockets
-  bool capturable() const override { return nstripe == 1 && !dm_on; }
+  // direct exchanges derive their sequence numbers on the device: capturable
+  bool capturable() const override { return nstripe == 1; }
+  bool stream_ordered() const override { return dm_on; }
+  int health() const override {
+    if (dm_on && dm->poisoned()) {
+      set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
+      return BINE_ERR_INTERNAL;
+    }
+    return BINE_SUCCESS;
+  }
   // collective: every rank calls it with the same k, in the same order
   int set_stripes(int k) {
     if (k < 1 || k > 8) return BINE_ERR_ARG;
@@ -614,7 +628,12 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   base[BINE_BUF_STAGE] = (char *)c->tmp[3];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
   hipStream_t C = single ? K : c->cstream;
-  if (sc.c_join && !single && !joined) {  // joined: the comm stream already follows K (graph capture)
+  // stream-ordered transports (direct: sequence bases in device memory) need
+  // every exchange of this call after every exchange of the previous one,
+  // whichever stream that one used: the comm stream follows K at the start
+  // and K follows the comm stream at the end
+  const bool ordered = c->tx->stream_ordered() && !single;
+  if ((sc.c_join || ordered) && !single && !joined) {  // joined: the comm stream already follows K (graph capture)
     int rc = stream_join(c, C, K);
     if (rc) return rc;
   }
@@ -679,6 +698,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     }
   }
   if (sc.final_wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
+  if (ordered) return stream_join(c, K, C);
   return BINE_SUCCESS;
 }
 
@@ -737,9 +757,10 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
                      size_t esz, int dtype, int op, hipStream_t K, bool single) {
   const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
   char buf[192];
-  snprintf(buf, sizeof buf, "|%p|%p|%d|%d|%p|%d|%d|%d", sbuf, rbuf, dtype, op, (void *)K, (int)single,
-           (int)c->coll_a2a, rt && rt->coll_ag ? 1 : 0);
+  snprintf(buf, sizeof buf, "|%p|%p|%d|%d|%p|%d|%d|%d|%d", sbuf, rbuf, dtype, op, (void *)K, (int)single,
+           (int)c->coll_a2a, rt && rt->coll_ag ? 1 : 0, rt && rt->dm_on ? 1 : 0);
   const std::string key = plan_key_s + buf;
+  if (int rc = c->tx->health()) return rc;  // a replay would not pass through exchange()'s check
   auto it = c->graph_cache.find(key);
   if (it != c->graph_cache.end()) {
     HIP_TRY(hipGraphLaunch(it->second.x, K));

@@ -604,38 +604,71 @@ int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count,
 
 // ----------------------------------------------------------------------------
 // direct peer-memory transport (bine_comm_set_direct, direct.cpp): one launch
-// moves every message of one round of an exchange.  Message m is served by
-// `wgs` workgroups: thread 0 of each polls m.wait_ptr (system-scope acquire)
-// until it reaches m.wait_val -- the peer's acknowledgement that the slot is
-// free (push) or the peer's ready mark (pull) -- with a time limit; the
-// workgroup then copies its grid-strided share of the message; every
-// workgroup releases its stores and counts itself in at m.cnt_ptr; the last
-// one to arrive publishes m.sig_val at m.sig_ptr (system-scope release), in
-// the peer's memory.  A wait that times out (a peer gone or a protocol
-// fault) marks the transport poisoned; every later launch then exits at
-// once, so no wait outlives the time limit.
+// moves up to kMaxDm messages, `wgs` workgroups each.  A message's sequence
+// number is seq = base[peer] + j + 1, base = this rank's count of earlier
+// sub-messages to (push) or from (pull) that peer, kept in its own inbox and
+// advanced by the launch's last workgroup; slot = seq mod kSlots.  Everything
+// else follows from (seq, peer): the slot in the receiver's inbox, the flag to
+// wait on -- push: the receiver's ack of the slot's previous use (seq -
+// kSlots); pull: the sender's ready mark for seq -- and the flag to publish.
+// Thread 0 of each workgroup polls the wait flag (system-scope acquire) with a
+// time limit; the workgroup copies its grid-strided share; every workgroup
+// releases its stores and counts itself in; the last one of the message
+// resets the counter for the slot's next use and publishes seq in the peer's
+// inbox (system-scope release).  A wait that times out marks the transport
+// poisoned; every later launch then exits at once, so no wait outlives the
+// time limit.  No host-side state: launches can be captured and replayed.
 
 __device__ __forceinline__ uint64_t ld_acq_sys(const uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
+  using namespace dm;
   const int mi = (int)(blockIdx.x / (unsigned)a.wgs), wi = (int)(blockIdx.x % (unsigned)a.wgs);
-  if (mi >= a.nmsg) return;
   const DmMsg &m = a.m[mi];
+  uint8_t *own = a.own;
+  uint32_t *poison = reinterpret_cast<uint32_t *>(own + kPoisonOff);
+  uint64_t *base = reinterpret_cast<uint64_t *>(own + (m.push ? kBaseSendOff : kBaseRecvOff)) + m.peer;
+  const uint64_t seq = __hip_atomic_load(base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
+  const size_t k = (size_t)(seq % kSlots);
+  uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
+  const size_t data_off = kFlagsBytes;
+  const uint8_t *src;
+  uint8_t *dst;
+  const uint64_t *wait_ptr;
+  uint64_t wait_val;
+  uint64_t *sig_ptr;
+  uint32_t *cnt_ptr;
+  if (m.push) {
+    src = m.src;
+    dst = remote + data_off + ((size_t)a.rank * kSlots + k) * a.slot;
+    wait_ptr = seq > (uint64_t)kSlots ? reinterpret_cast<const uint64_t *>(own + kAckOff + ((size_t)m.peer * kSlots + k) * kFlagStride)
+                                      : nullptr;
+    wait_val = seq - kSlots;
+    sig_ptr = reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
+    cnt_ptr = reinterpret_cast<uint32_t *>(own + kCntPushOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+  } else {
+    src = own + data_off + ((size_t)m.peer * kSlots + k) * a.slot;
+    dst = m.dst;
+    wait_ptr = reinterpret_cast<const uint64_t *>(own + kReadyOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+    wait_val = seq;
+    sig_ptr = reinterpret_cast<uint64_t *>(remote + kAckOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
+    cnt_ptr = reinterpret_cast<uint32_t *>(own + kCntPullOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+  }
   __shared__ int go;
   if (threadIdx.x == 0) {
-    int ok = __hip_atomic_load(a.poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
-    if (ok && m.wait_ptr) {
+    int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
+    if (ok && wait_ptr) {
       const long long t0 = wall_clock64();
-      while (ld_acq_sys(m.wait_ptr) < m.wait_val) {
+      while (ld_acq_sys(wait_ptr) < wait_val) {
         if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
-          __hip_atomic_store(a.poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           ok = 0;
           break;
         }
-        if (__hip_atomic_load(a.poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+        if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
           ok = 0;
           break;
         }
@@ -645,13 +678,11 @@ __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
     go = ok;
   }
   __syncthreads();
-  if (!go) return;
+  if (!go) return;  // poisoned: the transport is dead, counters and bases no longer matter
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the peer released before its mark
   // grid-strided 16-B vectors (src / dst co-aligned mod 16: slots and plan
   // offsets are), bytes before the first boundary and after the last vector
   // by workgroup 0
-  const uint8_t *src = m.src;
-  uint8_t *dst = m.dst;
   const size_t head = std::min<uint64_t>((16 - ((uintptr_t)dst & 15)) & 15, m.bytes);
   const size_t nvec = (m.bytes - head) / 16;
   if (wi == 0) {
@@ -662,35 +693,53 @@ __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
   u32x4 *vd = reinterpret_cast<u32x4 *>(dst + head);
   constexpr int U = 4;
   const size_t stride = (size_t)a.wgs * kBlock * U;
-  for (size_t base = (size_t)wi * kBlock * U + threadIdx.x; base < nvec; base += stride) {
+  for (size_t b0 = (size_t)wi * kBlock * U + threadIdx.x; b0 < nvec; b0 += stride) {
     u32x4 x[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const size_t i = base + (size_t)u * kBlock;
+      const size_t i = b0 + (size_t)u * kBlock;
       if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const size_t i = base + (size_t)u * kBlock;
+      const size_t i = b0 + (size_t)u * kBlock;
       if (i < nvec) __builtin_nontemporal_store(x[u], vd + i);
     }
   }
-  // release this workgroup's stores, count it in; the last one publishes
+  // release this workgroup's stores, count it in; the last one of the message
+  // publishes, the last one of the launch advances the sequence bases
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(m.cnt_ptr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1 == m.cnt_target) {
+    const uint32_t old = __hip_atomic_fetch_add(cnt_ptr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == (uint32_t)a.wgs) {
+      __hip_atomic_store(cnt_ptr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use: a later launch
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(m.sig_ptr, m.sig_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(sig_ptr, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    uint32_t *lc = reinterpret_cast<uint32_t *>(own + kLaunchCntOff);
+    const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (ol + 1 == gridDim.x) {
+      // every workgroup has read its base: advance them for the next launch
+      // (stream-ordered after this one)
+      __hip_atomic_store(lc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = 0; i < a.nmsg; i++) {
+        uint64_t *bp = reinterpret_cast<uint64_t *>(own + (a.m[i].push ? kBaseSendOff : kBaseRecvOff)) + a.m[i].peer;
+        __hip_atomic_store(bp, __hip_atomic_load(bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
 
 int launch_dm_move(const DmArgs &a, void *stream) {
   if (a.nmsg <= 0) return BINE_SUCCESS;
-  if (a.nmsg > kMaxDm || a.wgs < 1) return BINE_ERR_ARG;
+  if (a.nmsg > kMaxDm || a.wgs < 1 || !a.own || !a.slot) return BINE_ERR_ARG;
+  for (int i = 0; i < a.nmsg; i++)
+    if (a.m[i].peer < 0 || a.m[i].peer >= dm::kMaxPeers || a.m[i].j < 0 || a.m[i].j >= dm::kSlots ||
+        a.m[i].bytes > a.slot)
+      return BINE_ERR_ARG;
   hipLaunchKernelGGL(k_dm_move, dim3((unsigned)(a.nmsg * a.wgs)), dim3(kBlock), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
