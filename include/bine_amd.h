@@ -270,8 +270,9 @@ int bine_comm_set_stripes(bine_comm_t comm, int k);
  * sockets; on one node peer memory is reachable over xGMI by plain loads and
  * stores) instead of RCCL's send/receive: each exchange round pushes every
  * outgoing message into one of the receiver's 4 slots for this sender and
- * pulls every incoming message out of its own (one kernel launch carries a
- * round's pulls with the next round's pushes), with release/acquire flags at
+ * pulls every incoming message out of its own (a one-round exchange is one
+ * kernel launch; longer ones pipeline a round's pulls with the next round's
+ * pushes), with release/acquire flags at
  * system scope.  Same bytes in the same places: results bit-identical.  Every
  * wait has a time limit (BINE_DIRECT_TIMEOUT_S, default 10 s); a timeout
  * disables the transport (BINE_ERR_INTERNAL from then on) instead of
@@ -280,7 +281,8 @@ int bine_comm_set_stripes(bine_comm_t comm, int k);
  * so graph mode captures and replays these collectives too.  At most 4
  * messages to one peer per exchange group
  * (BINE_ERR_UNSUPPORTED beyond).  Knobs: BINE_DIRECT_SLOT_BYTES (16 MiB),
- * BINE_DIRECT_WGS (workgroups per message, 32), BINE_DIRECT_MERGE (1; 0:
+ * BINE_DIRECT_WGS (workgroups per message, 32), BINE_DIRECT_MERGE (launch
+ * structure: 3 = the mix above, 2 = one launch per round, 1 = pipelined, 0 =
  * separate push and pull launches).  At most 64 ranks.  Loopback:
  * UNSUPPORTED. */
 int bine_comm_set_direct(bine_comm_t comm, int on);

@@ -163,7 +163,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   }
   if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
-  if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = atoi(e) != 0;
+  if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
   if (slot < (1 << 20)) slot = 1 << 20;
   slot = slot / 4096 * 4096;
   if (wgs < 1) wgs = 1;
@@ -400,12 +400,24 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
     }
     return BINE_SUCCESS;
   };
-  // launch k carries round k-1's pulls and round k's pushes, so the links
-  // keep moving round k while round k-1 is copied out locally.  Deadlock-free:
-  // a push of round k waits only for pulls of rounds <= k-1, which every rank
-  // has issued in this or an earlier launch, and a pull of round k-1 only for
-  // pushes of round k-1 (messages of one launch progress independently).
-  // merge = false: separate push and pull launches per round
+  // merge = 2: launch k carries round k's pushes and then round k's pulls --
+  // one launch per round, a pull's workgroups waiting for the peer's push of
+  // the same round.  The pushes come first in workgroup order, so they
+  // are dispatched before any pull can occupy the chip waiting, and a push
+  // waits only for pulls of rounds <= k-1 (issued in earlier launches
+  // everywhere): no cycle.  merge = 1: launch k carries round k-1's pulls and
+  // round k's pushes.  merge = 0: separate push and pull launches per round.
+  // merge = 3 (default): 2 for a one-round exchange (one launch: the latency
+  // case, and a pull overlaps the pushes still in flight), 1 for several
+  // rounds (the links stay busy while the previous round is copied out)
+  if (merge == 2 || (merge == 3 && rounds == 1)) {
+    for (size_t k = 0; k < rounds; k++) {
+      if (int rc = pushes(k)) return rc;
+      if (int rc = pulls(k)) return rc;
+      if (int rc = flush()) return rc;
+    }
+    return BINE_SUCCESS;
+  }
   for (size_t k = 0; k <= rounds; k++) {
     if (k > 0)
       if (int rc = pulls(k - 1)) return rc;

@@ -14,7 +14,9 @@ struct DirectState {
   int P = 1, rank = 0, device = 0;
   size_t slot = (size_t)16 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES)
   int wgs = 32;                    // workgroups per message (BINE_DIRECT_WGS)
-  bool merge = true;               // round k-1's pulls share a launch with round k's pushes (BINE_DIRECT_MERGE)
+  int merge = 3;                   // launch structure (BINE_DIRECT_MERGE): 2 = pushes + pulls of a round in one
+                                   // launch, 1 = round k-1's pulls with round k's pushes, 0 = separate launches,
+                                   // 3 = 2 for one-round exchanges, else 1
   uint64_t timeout_ticks = 0;      // wall_clock64 ticks of one wait (BINE_DIRECT_TIMEOUT_S, default 10 s)
   size_t data_off = 0, total = 0;
   hipMemGenericAllocationHandle_t own_h{};

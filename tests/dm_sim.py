@@ -18,7 +18,7 @@ import pico_amd
 SLOTS = 4
 
 
-def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=True):
+def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3):
     """DirectState::exchange for one exchange: list of launches, each a list
     of messages {kind, peer, seq}"""
     maxb = max([b for _, b in sends] + [b for _, b in recvs] + [0])
@@ -47,8 +47,15 @@ def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=True):
                 out.append({"kind": "pull", "peer": p, "seq": seq_r[p]})
         return out
 
-    # launch k = round k-1's pulls + round k's pushes (merge), or the two as
-    # separate launches
+    # merge 2: launch k = round k's pushes + round k's pulls; merge 1: round
+    # k-1's pulls + round k's pushes; merge 0: separate launches; merge 3
+    # (the library's default): 2 for one round, else 1
+    if merge == 2 or (merge == 3 and rounds == 1):
+        for k in range(rounds):
+            launch = pushes(k) + pulls(k)
+            if launch:
+                out.append(launch)
+        return out
     for k in range(rounds + 1):
         launch = pulls(k - 1) if k > 0 else []
         if not merge and launch:
@@ -62,7 +69,7 @@ def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=True):
 
 
 def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay_min_bytes=0, trees=False,
-        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20, merge=True):
+        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20, merge=3):
     """simulate `calls` consecutive collectives on all ranks; returns None if
     every one completes, else a description of the deadlock"""
     seq_s = [[0] * P for _ in range(P)]

@@ -28,12 +28,13 @@ def test_allreduce_protocol_completes(P, mode):
     assert res is None, res["stuck"][:8]
 
 
-@pytest.mark.parametrize("merge", [True, False])
+@pytest.mark.parametrize("merge", [3, 2, 1, 0])
 @pytest.mark.parametrize("mode", ["direct", "relay", "flatrs+flat"])
 def test_multi_round_exchanges(mode, merge):
     # slot much smaller than the messages: every exchange runs several rounds
-    # and every slot is reused many times per collective; merged launches
-    # (round k-1's pulls with round k's pushes) and separate ones
+    # and every slot is reused many times per collective; every launch
+    # structure: one launch per round (2), round k-1's pulls with round k's
+    # pushes (1), separate launches (0), the default mix (3)
     res = dm_sim.run("allreduce", "bine_bdw_remap", 4, count=1 << 20, chunk_bytes=4 << 20, slot=64 << 10,
                      merge=merge, **MODES[mode])
     assert res is None, res["stuck"][:8]
