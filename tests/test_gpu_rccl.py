@@ -28,6 +28,18 @@ def test_rccl_large_messages_4_ranks():
     assert "RESULT P=4" in r.stdout
 
 
+@pytest.mark.timeout(400)
+def test_rccl_large_messages_8_ranks():
+    """the same at P = 8 (8 processes on the box's one GPU): every transport
+    incl. multi-tree and the direct peer-memory transport, eager and graph"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "8"], env=env,
+                       capture_output=True, text=True, timeout=380)
+    tail = "\n".join(r.stdout.splitlines()[-16:])
+    assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
+    assert "RESULT P=8" in r.stdout
+
+
 def test_rccl_matrix_4_ranks():
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_matrix.py"), "4"], env=env,
