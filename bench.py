@@ -827,6 +827,37 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             verdicts[cfg] = "error"
 
     mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
+    S = nelem * 4
+
+    def headline(cfg, st, ok_head, dig, ok_trees_tol=None):
+        """rank 0's JSON line for a timed, checked configuration (None elsewhere)"""
+        if rank != 0:
+            return None
+        return _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, st, ok_head, dig,
+                              ok_trees_tol, trials, verdicts)
+
+    # A provisional line first: the literal Bine schedule over RCCL P2P (the
+    # path every test exercises) timed in full and checked.  The trials below
+    # then run under a deadline: should one of them hang inside RCCL or the
+    # direct transport on the driver's node (configurations no one-GPU box can
+    # rehearse over xGMI), every rank stops at the same budget and rank 0
+    # prints this line instead of losing the run.
+    base_cfg = ("direct", mid, False, 1)
+    apply_transport(comm, *base_cfg)
+    rbuf.fill_(float("nan"))
+    st0 = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
+    ok0, dig0 = parity("direct")
+    provisional = headline(base_cfg, st0, ok0, dig0)
+    trial_budget = float(os.environ.get("BENCH_TRIAL_BUDGET_S", "300"))
+
+    def _provisional():
+        if provisional is not None:
+            provisional["config"]["transport_trials_cut_after_s"] = trial_budget
+            provisional["config"]["transport_trials_ms"] = {tname(c): round(v, 4) for c, v in trials.items()}
+            provisional["config"]["parity"]["trials"] = {tname(c): v for c, v in verdicts.items()}
+        return provisional
+
+    watchdog = arm_deadline(trial_budget, _provisional, "transport trials")
     if len(modes) > 1 or len(chunks) > 1:
         for m in modes:
             trial((m, mid, False, 1))
@@ -836,7 +867,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             if (m_best, ch, False, 1) not in trials:
                 trial((m_best, ch, False, 1))
         cands = [c for c in trials if c[0] == m_best and trials[c] != float("inf")]
-        best = min(cands, key=trials.get) if cands else ("direct", mid, False, 1)
+        best = min(cands, key=trials.get) if cands else base_cfg
     else:
         best = (modes[0], chunks[0], False, 1)
     if graph_trial:
@@ -844,17 +875,27 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         trial((best[0], best[1], True, 1))
         if trials[(best[0], best[1], True, 1)] < trials.get(best, float("inf")):
             best = (best[0], best[1], True, 1)
+    if best == base_cfg and ok0 is not False:
+        st, ok_head, dig = st0, ok0, dig0
+    else:
+        apply_transport(comm, *best)
+        rbuf.fill_(float("nan"))
+        st = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
+        ok_head, dig = parity(best[0])
+        # the faster of the two full, checked runs is the headline (the trials'
+        # 3-step estimates can mislead; the provisional run is a measurement too)
+        if ok_head is False or (ok0 is not False and st0["median_ms"] < st["median_ms"]):
+            best, st, ok_head, dig = base_cfg, st0, ok0, dig0
     chosen, chunk, graphs, stripes = best
     apply_transport(comm, chosen, chunk, graphs, stripes)
-    rbuf.fill_(float("nan"))
-    st = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
-    ok_head, dig = parity(chosen)
     ok_trees_tol = None
     if chosen == "trees":
         # fp results of multi-tree mode are the reference's schedule on
         # relabelled ranks: checked exactly against that (digest above) and
         # against the reference's own bits with pico_core's ground-truth
         # tolerance (pico_core_utils.c:960-992: |a - b| <= P * 1e-6 * 100)
+        run()
+        torch.cuda.synchronize()
         tree_out = rbuf.clone()
         apply_transport(comm, "flatrs+flat", chunk, graphs, stripes)
         run()
@@ -864,67 +905,9 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         ok_trees_tol = all_ok(torch, dist, bool(ok_exact) and float((tree_out - rbuf).abs().max()) <= tol)
         del tree_out
         apply_transport(comm, chosen, chunk, graphs, stripes)
+    watchdog.cancel()
     ms = st["median_ms"]
-    S = nelem * 4
-    algbw = S / (ms * 1e-3) / 1e9
-    busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
-    egress, peers, L, op_links = link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen)
-    # schedule-aware link roofline: peak = the egress rate the schedule's link
-    # time allows at 153 GB/s per link (153 for the literal one-peer-per-step
-    # schedule, up to 7 x 153 when every step loads all links)
-    link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
-    achieved = egress / (st["mean_ms"] * 1e-3) / 1e9
-    out = None
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
-            "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (pico_core rand_r distribution, seed 1234 + rank, generated on device)",
-            "config": {"workload": f"C3: allreduce_{algo} fp32 SUM {S // MIB} MiB/rank over "
-                                   f"{'mapped peer memory' if '+dm' in chosen else 'RCCL P2P'} (xGMI), "
-                                   f"{world} x MI355X, device-resident",
-                       "value_definition": "per-rank algbw = S / t, t = per-iteration max over ranks, median after "
-                                           "dropping the first 20 % (pico_core.c:133-140, summarize_data.py:24-48)",
-                       "stats_ms": {k: _r(v, 5) for k, v in st.items()},
-                       "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
-                       "whole_job_GBs": round(world * algbw, 2),
-                       "busbw_frac_of_target_1071": round(busbw / TARGET_BUSBW_GBS, 4),
-                       "transport": chosen, "graph_replay": graphs, "stripes": stripes,
-                       "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
-                       "chunk_bytes": chunk,
-                       "parity": {"headline_ok": ok_head, "digest": str(dig),
-                                  "check": f"bine_checksum(rbuf) on every rank == oracle digest {key}"
-                                           + (" (trees: relabelled-schedule digest)" if chosen == "trees" else ""),
-                                  "trees_within_pico_core_eps": ok_trees_tol,
-                                  "trials": {tname(c): v for c, v in verdicts.items()}},
-                       "host_issue_ms_per_step": round(st["issue_ms"], 4),
-                       "step_profile_rank0": None,
-                       "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
-                       # north_star names RCCL point-to-point: the fastest correct
-                       # RCCL transport's figure beside the headline, whichever won
-                       "best_rccl_p2p": _best_of(trials, verdicts, S, lambda c: "+dm" not in c[0]),
-                       "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
-                       "other_baseline_configs": None,
-                       "rccl_p2p_probe": None,
-                       "rccl_allreduce_baseline": None,
-                       "striped_exchanges_after_headline": None,
-                       "rccl": pico_amd.rccl_version(), "host": host_info()},
-            "roofline": {"bound": "xgmi", "achieved": round(achieved, 2), "peak": link_peak,
-                         "unit": "GB/s", "frac": round(achieved / link_peak, 4),
-                         "frac_of_target_1071_busbw": round(busbw / TARGET_BUSBW_GBS, 4),
-                         # traffic = PMC-measured HBM bytes (the N = 1 line); at N > 1 the
-                         # bound is the link, whose bytes come from the executed schedule
-                         "traffic": None,
-                         "egress_bytes": egress,
-                         "link_time_bytes": L,
-                         "note": "achieved = this rank's xGMI egress bytes (executed schedule) / mean kept "
-                                 "per-iteration time; peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
-                                 "of the busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
-                                 "to 7 x 153 when every step loads all links; frac_of_target_1071_busbw = busbw / "
-                                 "(7 x 153), the BASELINE target's denominator"},
-            "wall_s": round(st["wall_s"], 4),
-        }
+    out = headline(best, st, ok_head, dig, ok_trees_tol)
     # the side measurements below run under a deadline: if one of them hangs
     # (an RCCL or transport fault in a secondary configuration), every rank
     # stops at the same budget and rank 0 still prints the headline line with
@@ -960,14 +943,21 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     if out is not None:
         out["config"].update({"step_profile_rank0": steps_prof, "other_baseline_configs": extra,
                               "rccl_p2p_probe": probe, "rccl_allreduce_baseline": vendor,
-                              "striped_exchanges_after_headline": stripe_ms})
+                              "striped_exchanges_after_headline": stripe_ms,
+                              "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
+                              "provisional_literal_rccl": {"ms": round(st0["median_ms"], 4),
+                                                           "algbw_per_rank_GBs": round(S / (st0["median_ms"] * 1e-3) / 1e9, 2),
+                                                           "parity_ok": ok0}})
+        out["config"]["parity"]["trials"] = {tname(c): v for c, v in verdicts.items()}
     if rank == 0:
         # the same egress against what RCCL P2P itself moves on this node: per
         # exchange op its busiest link at what RCCL moves per link in that
         # pattern -- the one-peer rate for a one-peer op, the all-peers egress
         # rate / (P - 1) when the op talks to several peers at once
         one, allp = probe.get("one_peer_GBs"), probe.get("all_peers_egress_GBs")
+        L = out["roofline"]["link_time_bytes"]
         if one and L:
+            op_links = link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen)[3]
             per_link_all = min(one, allp / (world - 1)) if allp else one
             t_rccl = sum(b / ((one if npeers <= 1 else per_link_all) * 1e9) for b, npeers in op_links)
             out["roofline"]["rccl_p2p_one_link_GBs"] = one
@@ -977,6 +967,72 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     dist.destroy_process_group()
     return out
 
+
+def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, st, ok_head, dig, ok_trees_tol,
+                   trials, verdicts):
+    """the N > 1 JSON line for one timed configuration cfg = (transport, chunk,
+    graphs, stripes): per-rank algbw, busbw, schedule-aware link roofline"""
+    chosen, chunk, graphs, stripes = cfg
+    ms = st["median_ms"]
+    S = nelem * 4
+    algbw = S / (ms * 1e-3) / 1e9
+    busbw = 2 * (world - 1) / world * S / (ms * 1e-3) / 1e9
+    egress, peers, L, _ = link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen)
+    # schedule-aware link roofline: peak = the egress rate the schedule's link
+    # time allows at 153 GB/s per link (153 for the literal one-peer-per-step
+    # schedule, up to 7 x 153 when every step loads all links)
+    link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
+    achieved = egress / (st["mean_ms"] * 1e-3) / 1e9
+    out = {
+        "metric": METRIC, "value": round(algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (pico_core rand_r distribution, seed 1234 + rank, generated on device)",
+        "config": {"workload": f"C3: allreduce_{algo} fp32 SUM {S // MIB} MiB/rank over "
+                               f"{'mapped peer memory' if '+dm' in chosen else 'RCCL P2P'} (xGMI), "
+                               f"{world} x MI355X, device-resident",
+                   "value_definition": "per-rank algbw = S / t, t = per-iteration max over ranks, median after "
+                                       "dropping the first 20 % (pico_core.c:133-140, summarize_data.py:24-48)",
+                   "stats_ms": {k: _r(v, 5) for k, v in st.items()},
+                   "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
+                   "whole_job_GBs": round(world * algbw, 2),
+                   "busbw_frac_of_target_1071": round(busbw / TARGET_BUSBW_GBS, 4),
+                   "transport": chosen, "graph_replay": graphs, "stripes": stripes,
+                   "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
+                   "chunk_bytes": chunk,
+                   "parity": {"headline_ok": ok_head, "digest": str(dig),
+                              "check": f"bine_checksum(rbuf) on every rank == oracle digest {key}"
+                                       + (" (trees: relabelled-schedule digest)" if chosen == "trees" else ""),
+                              "trees_within_pico_core_eps": ok_trees_tol,
+                              "trials": {tname(c): v for c, v in verdicts.items()}},
+                   "host_issue_ms_per_step": round(st["issue_ms"], 4),
+                   "step_profile_rank0": None,
+                   "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
+                   # north_star names RCCL point-to-point: the fastest correct
+                   # RCCL transport's figure beside the headline, whichever won
+                   "best_rccl_p2p": _best_of(trials, verdicts, S, lambda c: "+dm" not in c[0]),
+                   "xgmi_egress_bytes_per_rank": egress, "peers_per_rank": peers,
+                   "other_baseline_configs": None,
+                   "rccl_p2p_probe": None,
+                   "rccl_allreduce_baseline": None,
+                   "striped_exchanges_after_headline": None,
+                   "rccl": pico_amd.rccl_version(), "host": host_info()},
+        "roofline": {"bound": "xgmi", "achieved": round(achieved, 2), "peak": link_peak,
+                     "unit": "GB/s", "frac": round(achieved / link_peak, 4),
+                     "frac_of_target_1071_busbw": round(busbw / TARGET_BUSBW_GBS, 4),
+                     # traffic = PMC-measured HBM bytes (the N = 1 line); at N > 1 the
+                     # bound is the link, whose bytes come from the executed schedule
+                     "traffic": None,
+                     "egress_bytes": egress,
+                     "link_time_bytes": L,
+                     "note": "achieved = this rank's xGMI egress bytes (executed schedule) / mean kept "
+                             "per-iteration time; peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
+                             "of the busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
+                             "to 7 x 153 when every step loads all links; frac_of_target_1071_busbw = busbw / "
+                             "(7 x 153), the BASELINE target's denominator"},
+        "wall_s": round(st["wall_s"], 4),
+    }
+    return out
 
 def main():
     ap = argparse.ArgumentParser()
