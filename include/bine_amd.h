@@ -35,8 +35,17 @@ typedef enum {
 
 /* reduction operators, MPI_Reduce_local semantics of MPICH 3.3.2:
  * inout[i] = inout[i] (op) in[i]; MAX/MIN select inout when inout > in
- * (resp. <), else in (NaN behaviour follows from that). */
-typedef enum { BINE_SUM = 0, BINE_PROD = 1, BINE_MAX = 2, BINE_MIN = 3, BINE_NUM_OPS = 4 } bine_op_t;
+ * (resp. <), else in (NaN behaviour follows from that).  The logical ops
+ * (MPICH's MPIR_LLAND/LLOR/LLXOR: C truthiness, result 0 or 1 of the element
+ * type; defined on every type, floats included -- -0.0 is false, NaN true)
+ * and the bitwise ops (integer types only; BINE_ERR_ARG on float / double,
+ * where MPICH reports MPI_ERR_OP) complete the predefined MPI_Op set
+ * libbine's callers can pass (MAXLOC / MINLOC need pair types, not provided). */
+typedef enum {
+  BINE_SUM = 0, BINE_PROD = 1, BINE_MAX = 2, BINE_MIN = 3,
+  BINE_LAND = 4, BINE_BAND = 5, BINE_LOR = 6, BINE_BOR = 7, BINE_LXOR = 8, BINE_BXOR = 9,
+  BINE_NUM_OPS = 10
+} bine_op_t;
 
 typedef enum {
   BINE_SUCCESS = 0,

@@ -34,7 +34,18 @@ size_t orc_dtype_size(int dt) {
 
 /* MPICH 3.3.2 MPIR_OP_TYPE_REDUCE_CASE: a = inout, b = in, a[i] = OP(a[i], b[i])
  * with MPIR_MAX(a,b) = a > b ? a : b and MPIR_MIN(a,b) = a < b ? a : b.
- * Signed integer SUM/PROD wrap (computed unsigned: same bits, no UB). */
+ * Signed integer SUM/PROD wrap (computed unsigned: same bits, no UB).
+ * Logical ops (opland.c / oplor.c / oplxor.c): MPIR_LLAND(a,b) = a && b,
+ * MPIR_LLOR = a || b, MPIR_LLXOR = (a && !b) || (!a && b) -- C truthiness, the
+ * 0/1 result stored in the element type; MPICH accepts them on floating types
+ * too.  Bitwise ops (opband.c / opbor.c / opbxor.c): integer types only
+ * (floating types: MPI_ERR_OP, here -1).  Checked against MPICH's own
+ * MPI_Reduce_local by tests/golden (the reference's vectors, sparse inputs). */
+#define RL_LOGIC                                                              \
+      case ORC_LAND: for (size_t i = 0; i < n; i++) a[i] = (a[i] && b[i]); break; \
+      case ORC_LOR:  for (size_t i = 0; i < n; i++) a[i] = (a[i] || b[i]); break; \
+      case ORC_LXOR: for (size_t i = 0; i < n; i++) a[i] = ((a[i] && !b[i]) || (!a[i] && b[i])); break
+
 #define RL_INT(T, UT)                                                         \
   do {                                                                        \
     T *a = (T *)inout; const T *b = (const T *)in;                            \
@@ -43,6 +54,10 @@ size_t orc_dtype_size(int dt) {
       case ORC_PROD: for (size_t i = 0; i < n; i++) a[i] = (T)((UT)a[i] * (UT)b[i]); break; \
       case ORC_MAX:  for (size_t i = 0; i < n; i++) a[i] = a[i] > b[i] ? a[i] : b[i]; break; \
       case ORC_MIN:  for (size_t i = 0; i < n; i++) a[i] = a[i] < b[i] ? a[i] : b[i]; break; \
+      case ORC_BAND: for (size_t i = 0; i < n; i++) a[i] = (T)(a[i] & b[i]); break; \
+      case ORC_BOR:  for (size_t i = 0; i < n; i++) a[i] = (T)(a[i] | b[i]); break; \
+      case ORC_BXOR: for (size_t i = 0; i < n; i++) a[i] = (T)(a[i] ^ b[i]); break; \
+      RL_LOGIC;                                                               \
       default: return -1;                                                     \
     }                                                                         \
   } while (0)
@@ -55,6 +70,7 @@ size_t orc_dtype_size(int dt) {
       case ORC_PROD: for (size_t i = 0; i < n; i++) a[i] = a[i] * b[i]; break; \
       case ORC_MAX:  for (size_t i = 0; i < n; i++) a[i] = a[i] > b[i] ? a[i] : b[i]; break; \
       case ORC_MIN:  for (size_t i = 0; i < n; i++) a[i] = a[i] < b[i] ? a[i] : b[i]; break; \
+      RL_LOGIC;                                                               \
       default: return -1;                                                     \
     }                                                                         \
   } while (0)

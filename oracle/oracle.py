@@ -20,7 +20,7 @@ DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 
 NP_DTYPES = {"int8": np.int8, "uint8": np.uint8, "int16": np.int16, "uint16": np.uint16,
              "int32": np.int32, "uint32": np.uint32, "int64": np.int64, "uint64": np.uint64,
              "float": np.float32, "double": np.float64}
-OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9}
 OK, ERR_ARG, ERR_SIZE, ASSERT, DEADLOCK = 0, 12, 51, -2, -3
 
 _lib = None
@@ -70,7 +70,22 @@ def fill(dtype: str, n: int, seed: int) -> np.ndarray:
     return a
 
 
-def inputs(dtype: str, n: int, P: int, seed_base: int = 1234):
+def sparsify(x: np.ndarray, dtype: str, rank: int) -> np.ndarray:
+    """oracle/ref_golden.c sparsify(): with j = i + rank, zero where j % 3 == 0;
+    float / double also -0.0 where j % 5 == 1 and NaN where j % 11 == 2 (later
+    rules win) -- inputs on which the logical ops and MAX / MIN show their
+    operand semantics"""
+    j = np.arange(x.size) + rank
+    x[j % 3 == 0] = 0
+    if dtype in ("float", "double"):
+        x[j % 5 == 1] = -0.0
+        x[j % 11 == 2] = np.nan
+    return x
+
+
+def inputs(dtype: str, n: int, P: int, seed_base: int = 1234, sparse: bool = False):
+    if sparse:
+        return [sparsify(fill(dtype, n, seed_base + r), dtype, r) for r in range(P)]
     return [fill(dtype, n, seed_base + r) for r in range(P)]
 
 

@@ -20,7 +20,11 @@
  *                pico_core_utils.c:511-514), rbuf = P * N zeroed elements
  *   rcounts_kind even   -> rcounts[i] = N / P  (pico_core_utils.c:535-536)
  *                ragged -> rcounts[i] = N / P + (i % 3)   (exercises displs)
+ *                a "_sparse" suffix (e.g. even_sparse) post-processes the
+ *                inputs so that the logical ops and MAX / MIN see zeros, -0.0
+ *                and NaN (sparsify() below; tests/golden_util.py repeats it)
  */
+#include <math.h>
 #include <mpi.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -97,6 +101,12 @@ static int op_of(const char *s, MPI_Op *op) {
   if (!strcmp(s, "prod")) { *op = MPI_PROD; return 0; }
   if (!strcmp(s, "max"))  { *op = MPI_MAX;  return 0; }
   if (!strcmp(s, "min"))  { *op = MPI_MIN;  return 0; }
+  if (!strcmp(s, "land")) { *op = MPI_LAND; return 0; }
+  if (!strcmp(s, "band")) { *op = MPI_BAND; return 0; }
+  if (!strcmp(s, "lor"))  { *op = MPI_LOR;  return 0; }
+  if (!strcmp(s, "bor"))  { *op = MPI_BOR;  return 0; }
+  if (!strcmp(s, "lxor")) { *op = MPI_LXOR; return 0; }
+  if (!strcmp(s, "bxor")) { *op = MPI_BXOR; return 0; }
   return -1;
 }
 
@@ -110,6 +120,31 @@ static void fill(void *buf, const char *dt, size_t n, unsigned int seed) {
     else if (!strcmp(dt, "float"))  ((float *)buf)[i] = (float)rand_r(&seed) / (float)RAND_MAX * 100.0f;
     else if (!strcmp(dt, "double")) ((double *)buf)[i] = (double)rand_r(&seed) / (double)RAND_MAX * 100.0;
     else if (!strcmp(dt, "uint8"))  ((unsigned char *)buf)[i] = (unsigned char)(rand_r(&seed) % 256);
+  }
+}
+
+/* j = i + rank: zero where j % 3 == 0; floating types also -0.0 where
+ * j % 5 == 1 and NaN where j % 11 == 2 (later rules win) */
+static void sparsify(void *buf, const char *dt, size_t n, int rank) {
+  for (size_t i = 0; i < n; i++) {
+    const size_t j = i + (size_t)rank;
+    const int z = j % 3 == 0;
+    if (!strcmp(dt, "int8"))        { if (z) ((int8_t *)buf)[i] = 0; }
+    else if (!strcmp(dt, "int16"))  { if (z) ((int16_t *)buf)[i] = 0; }
+    else if (!strcmp(dt, "int32"))  { if (z) ((int32_t *)buf)[i] = 0; }
+    else if (!strcmp(dt, "int64"))  { if (z) ((int64_t *)buf)[i] = 0; }
+    else if (!strcmp(dt, "uint8"))  { if (z) ((unsigned char *)buf)[i] = 0; }
+    else if (!strcmp(dt, "float")) {
+      float *f = (float *)buf;
+      if (z) f[i] = 0.0f;
+      if (j % 5 == 1) f[i] = -0.0f;
+      if (j % 11 == 2) f[i] = NAN;
+    } else if (!strcmp(dt, "double")) {
+      double *f = (double *)buf;
+      if (z) f[i] = 0.0;
+      if (j % 5 == 1) f[i] = -0.0;
+      if (j % 11 == 2) f[i] = NAN;
+    }
   }
 }
 
@@ -158,6 +193,7 @@ int main(int argc, char **argv) {
       void *sbuf = malloc(total * esz + 16);
       void *rbuf = calloc(outn * esz + total * esz + 16, 1);
       fill(sbuf, dts[d], total, seed_base + (unsigned)rank);
+      if (strstr(rk, "_sparse")) sparsify(sbuf, dts[d], total, rank);
       int ret = -12345;
       if (!strcmp(coll, "fill")) {           /* pins the input generator itself */
         memcpy(rbuf, sbuf, total * esz);

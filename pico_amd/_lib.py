@@ -18,7 +18,7 @@ DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 
           "int64": 6, "uint64": 7, "float": 8, "double": 9}
 DTYPE_SIZE = {"int8": 1, "uint8": 1, "int16": 2, "uint16": 2, "int32": 4, "uint32": 4,
               "int64": 8, "uint64": 8, "float": 4, "double": 8}
-OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9}
 STATUS = {0: "SUCCESS", 1: "ERR_ARG", 2: "ERR_SIZE", 3: "ERR_NO_MEM", 4: "ERR_HIP", 5: "ERR_RCCL",
           6: "ERR_UNSUPPORTED", 7: "ERR_INTERNAL"}
 ALGOS = {

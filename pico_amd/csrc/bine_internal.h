@@ -117,6 +117,13 @@ int launch_reduce_batch(int n, const void *const *a, const void *const *b, void 
 constexpr int kMaxLeaves = 16;
 int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream,
                        unsigned swap = 0);
+// the logical / bitwise ops' instantiations (kernels.hip compiled with
+// BINE_OPSET=1); the entry points above forward those ops here
+int launch_reduce_logic(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream);
+int launch_reduce_batch_logic(int n, const void *const *a, const void *const *b, void *const *out,
+                              const size_t *count, int dtype, int op, void *stream);
+int launch_reduce_tree_logic(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op,
+                             void *stream, unsigned swap);
 // copy_buffer on the device (k_copy); hipMemcpyAsync when src / dst are not
 // co-aligned mod 16 B
 int launch_copy(void *dst, const void *src, size_t bytes, void *stream);

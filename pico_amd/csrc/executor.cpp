@@ -309,9 +309,10 @@ struct RcclTransport final : Transport {
     return BINE_SUCCESS;
   }
   int vendor_allreduce(const void *s, void *r, size_t n, int dtype, int op, hipStream_t st) override {
-    static const ncclRedOp_t ops[BINE_NUM_OPS] = {ncclSum, ncclProd, ncclMax, ncclMin};
+    // RCCL has no logical / bitwise reductions: the vendor baseline covers the arithmetic four
+    static const ncclRedOp_t ops[4] = {ncclSum, ncclProd, ncclMax, ncclMin};
     ncclDataType_t t;
-    if (!nccl_type(dtype, &t) || op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_ARG;
+    if (!nccl_type(dtype, &t) || op < 0 || op > BINE_MIN) return BINE_ERR_ARG;
     NCCL_TRY(ncclAllReduce(s, r, n, t, ops[op], comm, st));
     return BINE_SUCCESS;
   }
@@ -817,6 +818,10 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   if (!c) return BINE_ERR_ARG;
   if (dtype < 0 || dtype >= BINE_NUM_DTYPES) return BINE_ERR_UNSUPPORTED;
   if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+  // bitwise ops are undefined on floating types (MPICH: MPI_ERR_OP); refused
+  // before any exchange, identically on every rank
+  if ((op == BINE_BAND || op == BINE_BOR || op == BINE_BXOR) && (dtype == BINE_FLOAT || dtype == BINE_DOUBLE))
+    return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   if (chunk_bytes == kCommChunk) chunk_bytes = c->chunk_bytes ? c->chunk_bytes : default_chunk_bytes();
   HIP_TRY(hipSetDevice(c->device));

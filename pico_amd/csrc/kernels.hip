@@ -31,6 +31,20 @@
 
 #include "bine_internal.h"
 
+// This file is compiled twice (Makefile): BINE_OPSET 0 -> kernels.o, the
+// arithmetic ops SUM / PROD / MAX / MIN and every other kernel; BINE_OPSET 1
+// -> kernels_logic.o, the reduction kernels' instantiations for the logical
+// and bitwise ops only (launch_*_logic, reached from the opset-0 entry
+// points).  Two translation units compile in parallel.
+#ifndef BINE_OPSET
+#define BINE_OPSET 0
+#endif
+#if BINE_OPSET == 0
+#define BINE_FN(name) name
+#else
+#define BINE_FN(name) name##_logic
+#endif
+
 namespace bine {
 
 // ----------------------------------------------------------------------------
@@ -53,9 +67,83 @@ __device__ __forceinline__ T apply(T io, T in) {
     else return io * in;
   } else if constexpr (OP == BINE_MAX) {
     return io > in ? io : in;
-  } else {
+  } else if constexpr (OP == BINE_MIN) {
     return io < in ? io : in;
+  } else if constexpr (OP == BINE_LAND) {  // MPIR_LLAND: C truthiness (-0.0 false, NaN true), 0 / 1
+    return (T)(io != (T)0 && in != (T)0);
+  } else if constexpr (OP == BINE_LOR) {
+    return (T)(io != (T)0 || in != (T)0);
+  } else if constexpr (OP == BINE_LXOR) {
+    return (T)((io != (T)0) != (in != (T)0));
+  } else if constexpr (OP == BINE_BAND) {
+    return (T)(io & in);
+  } else if constexpr (OP == BINE_BOR) {
+    return (T)(io | in);
+  } else {
+    static_assert(OP == BINE_BXOR, "unknown op");
+    return (T)(io ^ in);
   }
+}
+
+// Which element types each op is instantiated for.  The bitwise ops act on
+// bits alone, so every integer type runs them as bytes (canon_dtype below);
+// the logical ops depend only on whether an element is zero, so signed
+// integers run them as the unsigned type of their width.  The four
+// arithmetic ops exist for every type.
+template <typename T>
+constexpr bool kLogicT = std::is_unsigned_v<T> || std::is_floating_point_v<T>;
+template <typename T>
+constexpr bool kBitsT = std::is_same_v<T, uint8_t>;
+
+// BINE_OP_SWITCH(T, CALL): `return CALL(OP)` for the op in variable `op`,
+// only for the (T, OP) pairs instantiated; hipErrorInvalidValue otherwise
+#if BINE_OPSET == 0
+#define BINE_OP_SWITCH(T, CALL)                                      \
+  switch (op) {                                                      \
+    case BINE_SUM: return CALL(BINE_SUM);                            \
+    case BINE_PROD: return CALL(BINE_PROD);                          \
+    case BINE_MAX: return CALL(BINE_MAX);                            \
+    case BINE_MIN: return CALL(BINE_MIN);                            \
+    default: break;                                                  \
+  }                                                                  \
+  return hipErrorInvalidValue;
+#else
+#define BINE_OP_SWITCH(T, CALL)                                      \
+  switch (op) {                                                      \
+    case BINE_LAND: if constexpr (kLogicT<T>) return CALL(BINE_LAND); break; \
+    case BINE_LOR: if constexpr (kLogicT<T>) return CALL(BINE_LOR); break;   \
+    case BINE_LXOR: if constexpr (kLogicT<T>) return CALL(BINE_LXOR); break; \
+    case BINE_BAND: if constexpr (kBitsT<T>) return CALL(BINE_BAND); break;  \
+    case BINE_BOR: if constexpr (kBitsT<T>) return CALL(BINE_BOR); break;    \
+    case BINE_BXOR: if constexpr (kBitsT<T>) return CALL(BINE_BXOR); break;  \
+    default: break;                                                  \
+  }                                                                  \
+  return hipErrorInvalidValue;
+#endif
+
+[[maybe_unused]] static bool logic_op(int op) { return op >= BINE_LAND && op < BINE_NUM_OPS; }
+
+// the element type an op runs on (see kLogicT / kBitsT); *scale = elements
+// of the run type per element of `dtype`; -1: the op is not defined on the
+// type (bitwise ops on float / double: MPICH's MPI_ERR_OP)
+static int canon_dtype(int dtype, int op, size_t *scale) {
+  *scale = 1;
+  if (dtype < 0 || dtype >= BINE_NUM_DTYPES || op < 0 || op >= BINE_NUM_OPS) return -1;
+  if (op == BINE_BAND || op == BINE_BOR || op == BINE_BXOR) {
+    if (dtype == BINE_FLOAT || dtype == BINE_DOUBLE) return -1;
+    *scale = bine_dtype_size(dtype);
+    return BINE_UINT8;
+  }
+  if (op == BINE_LAND || op == BINE_LOR || op == BINE_LXOR) {
+    switch (dtype) {
+      case BINE_INT8: return BINE_UINT8;
+      case BINE_INT16: return BINE_UINT16;
+      case BINE_INT32: return BINE_UINT32;
+      case BINE_INT64: return BINE_UINT64;
+      default: return dtype;
+    }
+  }
+  return dtype;
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -130,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const T *__restrict__ a, cons
 constexpr int kDefaultUnroll = 4, kDefaultMaxBlocks = 16384, kDefaultNT = 1;
 static int g_unroll = 0, g_maxblocks = 0, g_nt = kDefaultNT;
 
-static void read_tuning() {
+[[maybe_unused]] static void read_tuning() {
   if (g_unroll) return;
   const char *u = getenv("BINE_REDUCE_UNROLL");
   const char *m = getenv("BINE_REDUCE_MAXBLOCKS");
@@ -209,18 +297,20 @@ static hipError_t reduce_t(const void *a, const void *b, void *out, size_t n, hi
 
 template <typename T>
 static hipError_t reduce_op(const void *a, const void *b, void *out, size_t n, int op, hipStream_t st) {
-  switch (op) {
-    case BINE_SUM: return reduce_t<T, BINE_SUM>(a, b, out, n, st);
-    case BINE_PROD: return reduce_t<T, BINE_PROD>(a, b, out, n, st);
-    case BINE_MAX: return reduce_t<T, BINE_MAX>(a, b, out, n, st);
-    case BINE_MIN: return reduce_t<T, BINE_MIN>(a, b, out, n, st);
-    default: return hipErrorInvalidValue;
-  }
+#define CALL(OP) reduce_t<T, OP>(a, b, out, n, st)
+  BINE_OP_SWITCH(T, CALL)
+#undef CALL
 }
 
-int launch_reduce(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream) {
+int BINE_FN(launch_reduce)(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream) {
   if (count == 0) return BINE_SUCCESS;
-  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+#if BINE_OPSET == 0
+  if (logic_op(op)) return launch_reduce_logic(a, b, out, count, dtype, op, stream);
+#endif
+  size_t scale;
+  dtype = canon_dtype(dtype, op, &scale);
+  if (dtype < 0) return BINE_ERR_ARG;
+  count *= scale;
   read_tuning();
   hipStream_t st = (hipStream_t)stream;
   hipError_t e;
@@ -240,6 +330,7 @@ int launch_reduce(const void *a, const void *b, void *out, size_t count, int dty
   return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
+#if BINE_OPSET == 0
 // ----------------------------------------------------------------------------
 // device copy (copy_buffer): one tile of kBlock * kCopyU 16-B vectors per
 // workgroup, loads issued before stores, both non-temporal (the copied bytes
@@ -289,6 +380,8 @@ int launch_copy(void *dst, const void *src, size_t bytes, void *stream) {
                      bytes);
   return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
+
+#endif  // BINE_OPSET == 0
 
 // ----------------------------------------------------------------------------
 // batched reduction: up to kMaxBatch independent windows in one launch (the
@@ -370,19 +463,22 @@ static hipError_t batch_t(int n, const void *const *a, const void *const *b, voi
 template <typename T>
 static hipError_t batch_op(int n, const void *const *a, const void *const *b, void *const *out, const size_t *c,
                            int op, hipStream_t st) {
-  switch (op) {
-    case BINE_SUM: return batch_t<T, BINE_SUM>(n, a, b, out, c, st);
-    case BINE_PROD: return batch_t<T, BINE_PROD>(n, a, b, out, c, st);
-    case BINE_MAX: return batch_t<T, BINE_MAX>(n, a, b, out, c, st);
-    case BINE_MIN: return batch_t<T, BINE_MIN>(n, a, b, out, c, st);
-    default: return hipErrorInvalidValue;
-  }
+#define CALL(OP) batch_t<T, OP>(n, a, b, out, c, st)
+  BINE_OP_SWITCH(T, CALL)
+#undef CALL
 }
 
-int launch_reduce_batch(int n, const void *const *a, const void *const *b, void *const *out, const size_t *count,
-                        int dtype, int op, void *stream) {
+int BINE_FN(launch_reduce_batch)(int n, const void *const *a, const void *const *b, void *const *out,
+                                 const size_t *count_in, int dtype, int op, void *stream) {
   if (n < 1 || n > kMaxBatch) return BINE_ERR_ARG;
-  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+#if BINE_OPSET == 0
+  if (logic_op(op)) return launch_reduce_batch_logic(n, a, b, out, count_in, dtype, op, stream);
+#endif
+  size_t scale;
+  dtype = canon_dtype(dtype, op, &scale);
+  if (dtype < 0) return BINE_ERR_ARG;
+  size_t count[kMaxBatch];
+  for (int k = 0; k < n; k++) count[k] = count_in[k] * scale;
   hipStream_t st = (hipStream_t)stream;
   hipError_t e;
   switch (dtype) {
@@ -565,24 +661,25 @@ static hipError_t tree_op(int nl, TreeArgs &t, int op, hipStream_t st) {
   t.vec = co ? 1 : 0;
   t.head = co ? std::min<uint64_t>(((16 - (oo & 15)) & 15) / sizeof(T), t.n) : t.n;
   t.nvec = co ? (t.n - t.head) / V : 0;
-  switch (op) {
-    case BINE_SUM: return tree_t<T, BINE_SUM>(nl, t, st);
-    case BINE_PROD: return tree_t<T, BINE_PROD>(nl, t, st);
-    case BINE_MAX: return tree_t<T, BINE_MAX>(nl, t, st);
-    case BINE_MIN: return tree_t<T, BINE_MIN>(nl, t, st);
-    default: return hipErrorInvalidValue;
-  }
+#define CALL(OP) tree_t<T, OP>(nl, t, st)
+  BINE_OP_SWITCH(T, CALL)
+#undef CALL
 }
 
-int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op, void *stream,
-                       unsigned swap) {
+int BINE_FN(launch_reduce_tree)(int nl, const void *const *leaf, void *out, size_t count, int dtype, int op,
+                                void *stream, unsigned swap) {
   if (count == 0) return BINE_SUCCESS;
+#if BINE_OPSET == 0
+  if (logic_op(op)) return launch_reduce_tree_logic(nl, leaf, out, count, dtype, op, stream, swap);
+#endif
   if (nl < 2 || nl > kMaxLeaves || (nl & (nl - 1))) return BINE_ERR_ARG;
-  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+  size_t scale;
+  dtype = canon_dtype(dtype, op, &scale);
+  if (dtype < 0) return BINE_ERR_ARG;
   TreeArgs t{};
   for (int j = 0; j < nl; j++) t.leaf[j] = leaf[j];
   t.out = out;
-  t.n = count;
+  t.n = count * scale;
   t.swap = swap;
   hipStream_t st = (hipStream_t)stream;
   hipError_t e;
@@ -602,6 +699,7 @@ int launch_reduce_tree(int nl, const void *const *leaf, void *out, size_t count,
   return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
+#if BINE_OPSET == 0
 // ----------------------------------------------------------------------------
 // direct peer-memory transport (bine_comm_set_direct, direct.cpp): one launch
 // moves up to kMaxDm messages, `wgs` workgroups each.  A message's sequence
@@ -889,3 +987,8 @@ extern "C" int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal
   bine::g_nt = nontemporal;
   return BINE_SUCCESS;
 }
+
+#endif  // BINE_OPSET == 0
+#if BINE_OPSET != 0
+}  // namespace bine
+#endif

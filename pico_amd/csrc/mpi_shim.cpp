@@ -88,12 +88,27 @@ int map_dtype(MPI_Datatype d) {
   return -1;
 }
 
-int map_op(MPI_Op o) {
-  if (o == MPI_SUM) return BINE_SUM;
-  if (o == MPI_PROD) return BINE_PROD;
-  if (o == MPI_MAX) return BINE_MAX;
-  if (o == MPI_MIN) return BINE_MIN;
-  return -1;
+// The predefined MPI_Ops MPICH's MPI_Reduce_local applies, and the (op, type)
+// pairs it accepts (MPICH 3.3.2, probed with its own MPI_Reduce_local):
+// MPI_BYTE only under the bitwise ops, floating types under every op but the
+// bitwise ones.  -1 = MPI_ERR_OP (the reference's MPI_Reduce_local would fail).
+int map_op(MPI_Op o, MPI_Datatype d) {
+  int r = -1;
+  if (o == MPI_SUM) r = BINE_SUM;
+  else if (o == MPI_PROD) r = BINE_PROD;
+  else if (o == MPI_MAX) r = BINE_MAX;
+  else if (o == MPI_MIN) r = BINE_MIN;
+  else if (o == MPI_LAND) r = BINE_LAND;
+  else if (o == MPI_BAND) r = BINE_BAND;
+  else if (o == MPI_LOR) r = BINE_LOR;
+  else if (o == MPI_BOR) r = BINE_BOR;
+  else if (o == MPI_LXOR) r = BINE_LXOR;
+  else if (o == MPI_BXOR) r = BINE_BXOR;
+  if (r < 0) return -1;
+  const bool bits = r == BINE_BAND || r == BINE_BOR || r == BINE_BXOR;
+  if (d == MPI_BYTE && !bits) return -1;
+  if (bits && (d == MPI_FLOAT || d == MPI_DOUBLE)) return -1;
+  return r;
 }
 
 int get_entry(MPI_Comm comm, Entry **out) {
@@ -191,7 +206,7 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
 
 int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype dtype, MPI_Op op,
                  MPI_Comm comm) {
-  const int dt = map_dtype(dtype), o = map_op(op);
+  const int dt = map_dtype(dtype), o = map_op(op, dtype);
   if (dt < 0) return MPI_ERR_TYPE;
   if (o < 0) return MPI_ERR_OP;
   if (count == 0) return MPI_SUCCESS;
@@ -207,7 +222,7 @@ int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datat
 
 int do_reduce_scatter(int algo, const void *sbuf, void *rbuf, const int rcounts[], MPI_Datatype dtype, MPI_Op op,
                       MPI_Comm comm) {
-  const int dt = map_dtype(dtype), o = map_op(op);
+  const int dt = map_dtype(dtype), o = map_op(op, dtype);
   if (dt < 0) return MPI_ERR_TYPE;
   if (o < 0) return MPI_ERR_OP;
   Entry *e;
@@ -226,7 +241,7 @@ int do_reduce_scatter(int algo, const void *sbuf, void *rbuf, const int rcounts[
 
 int do_reduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype dtype, MPI_Op op, int root,
               MPI_Comm comm) {
-  const int dt = map_dtype(dtype), o = map_op(op);
+  const int dt = map_dtype(dtype), o = map_op(op, dtype);
   if (dt < 0) return MPI_ERR_TYPE;
   if (o < 0) return MPI_ERR_OP;
   if (count == 0) return MPI_SUCCESS;

@@ -39,7 +39,15 @@ def select(**kw):
 
 def rcounts(c):
     P, N = c["P"], c["N"]
-    return [N // P + ((i % 3) if c["rcounts"] == "ragged" else 0) for i in range(P)]
+    return [N // P + ((i % 3) if c["rcounts"].startswith("ragged") else 0) for i in range(P)]
+
+
+def inputs(c, total=None):
+    """every rank's send buffer of case c (pico_core's generator, seed_base +
+    rank; sparsified for the "*_sparse" input kinds, oracle/ref_golden.c)"""
+    from oracle import oracle as O
+    n = c["N"] if total is None else total
+    return O.inputs(c["dtype"], n, c["P"], c["seed_base"], sparse=c["rcounts"].endswith("_sparse"))
 
 
 def sha(a: np.ndarray) -> str:

@@ -192,7 +192,7 @@ def test_collectives_match_reference_goldens(dev, key, cs, relay):
         if relay and P < 3:
             continue
         rk = G.rcounts(c) if coll == "reduce_scatter" else None
-        sb = O.inputs(dt, sum(rk) if rk else N, P, c["seed_base"])
+        sb = G.inputs(c, sum(rk) if rk else N)
         outs, st = run_loopback(coll, algo, sb, dt, c["op"], rk, c["segsize"], relay=relay)
         if coll == "allgather" and c["status"] == "ok" and not any(c["rets"]) and any(st) and (
                 (algo == "recursivedoubling" and P & (P - 1))):
@@ -699,7 +699,7 @@ def test_multi_tree_allreduce_on_device(dev, P):
         for c in G.select(coll="allreduce", algo="bine_bdw_remap", P=P, op="sum"):
             if c["dtype"] not in ("int32", "int64", "int8", "int16", "uint8") or c["status"] != "ok":
                 continue
-            sb = O.inputs(c["dtype"], c["N"], P, c["seed_base"])
+            sb = G.inputs(c)
             outs, st = run_loopback("allreduce", "bine_bdw_remap", sb, c["dtype"])
             if any(st) or G.check_rank_outputs(c, outs):
                 bad.append((c["id"], st))

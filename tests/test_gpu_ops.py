@@ -1,0 +1,162 @@
+"""GPU parity of the logical and bitwise MPI_Ops (MPI_LAND / LOR / LXOR /
+BAND / BOR / BXOR) -- the predefined operators beyond pico_core's MPI_SUM that
+libbine's callers may pass (every reduce-family entry point forwards its
+MPI_Op to MPI_Reduce_local, e.g. libbine_allreduce.c:888).
+
+Semantics are MPICH 3.3.2's (logical ops: C truthiness on every type, floats
+included, result 0 / 1; bitwise ops: integer types only), pinned by golden
+vectors of the real reference on sparsified inputs (tools/make_golden.py
+ops_jobs; those cases also run through tests/test_gpu.py's golden test).
+Here: the kernels directly (reduce_local, reduce_tree, reduce_batch) on every
+dtype with zeros / -0.0 / NaN / denormals, and whole collectives in every
+transport setting, bit-exact vs the oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from test_gpu import ALL_DT, _host_tree, comms, from_dev, run_loopback, sha, to_dev
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import pico_amd  # noqa: E402
+
+LOGIC = ["land", "lor", "lxor"]
+BITS = ["band", "bor", "bxor"]
+
+
+def sparse(dtype, n, seed, rank=0):
+    """pico_core's generator, sparsified (zeros, -0.0, NaN) as in the goldens;
+    floats also get denormals and infinities"""
+    x = O.sparsify(O.fill(dtype, n, seed), dtype, rank)
+    if dtype in ("float", "double"):
+        j = np.arange(n)
+        x[j % 13 == 4] = np.finfo(x.dtype).tiny / 4
+        x[j % 17 == 6] = -np.inf
+    return x
+
+
+def _valid(dtype, op):
+    return not (op in BITS and dtype in ("float", "double"))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("dtype", ALL_DT)
+@pytest.mark.parametrize("op", LOGIC + BITS)
+def test_reduce_local_logic_bits(dev, dtype, op):
+    """vector body, head / tail elements and operands not co-aligned mod 16 B"""
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    if not _valid(dtype, op):
+        a = to_dev(O.fill(dtype, 64, 1))
+        with pytest.raises(pico_amd.BineError):
+            pico_amd.reduce_local(a, a.data_ptr(), 64, dtype, op)
+        return
+    for n in (1, 3, 17, 1000, 100003):
+        for shift_a, shift_b in ((0, 0), (1, 1), (1, 0)):
+            a = sparse(dtype, n, 11 + n)
+            b = sparse(dtype, n, 97 + n, rank=1)
+            ta = to_dev(np.concatenate([np.zeros(shift_a, a.dtype), a]))
+            tb = to_dev(np.concatenate([np.zeros(shift_b, b.dtype), b]))
+            pico_amd.reduce_local(ta.data_ptr() + shift_a * esz, tb.data_ptr() + shift_b * esz, n, dtype, op)
+            torch.cuda.synchronize()
+            exp = b.copy()
+            O.reduce_local(a, exp, dtype, op)
+            assert from_dev(tb, dtype, n, shift_b * esz).tobytes() == exp.tobytes(), (n, shift_a, shift_b)
+
+
+@pytest.mark.parametrize("dtype", ["int8", "uint16", "int32", "int64", "float", "double"])
+def test_reduce_tree_and_batch_logic_bits(dev, dtype):
+    """the flat reduce-scatter's fused tree kernel and the multi-tree batch
+    kernel under the new ops (bitwise ops run byte-wise on integer types)"""
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for op in LOGIC + BITS:
+        if not _valid(dtype, op):
+            out = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+            assert pico_amd.reduce_tree([out, out], out, 4, dtype, op) != 0
+            continue
+        for nl in (2, 8, 16):
+            for n in (4099, 3):
+                host = [sparse(dtype, n, 300 + j, rank=j) for j in range(nl)]
+                want = _host_tree(host, dtype, op)
+                leaves = [to_dev(h, pad=16) for h in host]
+                out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
+                assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
+                torch.cuda.synchronize()
+                assert sha(from_dev(out, dtype, n)) == sha(want), (op, nl, n)
+        counts = [5003, 16, 1]
+        ins = [sparse(dtype, c, 40 + k) for k, c in enumerate(counts)]
+        ios = [sparse(dtype, c, 50 + k, rank=2) for k, c in enumerate(counts)]
+        tin, tio = [to_dev(x, pad=16) for x in ins], [to_dev(x, pad=16) for x in ios]
+        assert pico_amd.reduce_batch(tin, tio, counts, dtype, op) == 0
+        torch.cuda.synchronize()
+        for k, c in enumerate(counts):
+            exp = ios[k].copy()
+            O.reduce_local(ins[k], exp, dtype, op)
+            assert from_dev(tio[k], dtype, c).tobytes() == exp.tobytes(), (op, k)
+
+
+AR_ALGOS = ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented", "bine_lat",
+            "bine_block_by_block_any_even", "ring", "rabenseifner", "recursivedoubling"]
+RS_ALGOS = ["bine_permute_remap", "bine_send_remap", "bine_static", "bine_block_by_block",
+            "bine_block_by_block_any_even", "recursivehalving", "recursive_distance_doubling", "ring", "butterfly"]
+
+
+@pytest.mark.parametrize("mode", ["literal", "flat"])
+@pytest.mark.parametrize("P", [4, 8])
+def test_collectives_logic_bits_every_algorithm(dev, P, mode):
+    """every reduce-family algorithm under LAND / LXOR (int8, float, sparse
+    inputs) and BOR / BXOR (int16, int64), literal schedule and with the flat
+    phases (fused tree kernel) -- bit-exact vs the oracle"""
+    flat = mode == "flat"
+    for c in comms(P):
+        c.set_flat_ag(flat)
+        c.set_flat_rs(flat)
+    bad = []
+    try:
+        for op, dts in (("land", ("int8", "float")), ("lxor", ("double", "uint8")), ("bor", ("int16",)),
+                        ("bxor", ("int64", "int8"))):
+            for dt in dts:
+                n = 1003
+                sb = [sparse(dt, n, 1234 + r, rank=r) for r in range(P)]
+                for algo in AR_ALGOS:
+                    want, rets = O.allreduce(algo, sb, dt, op)
+                    outs, st = run_loopback("allreduce", algo, sb, dt, op)
+                    if any(rets) or any(st):
+                        if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
+                            bad.append(("ar", algo, op, dt, st, rets))
+                        continue
+                    if any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                        bad.append(("ar", algo, op, dt))
+                rc = [n // P + (1 if i == 0 else 0) for i in range(P)]
+                sbr = [sparse(dt, sum(rc), 77 + r, rank=r) for r in range(P)]
+                for algo in RS_ALGOS:
+                    r_ = rc if algo != "bine_permute_remap" else [n // P] * P
+                    s_ = sbr if algo != "bine_permute_remap" else [x[: sum(r_)] for x in sbr]
+                    want, rets = O.reduce_scatter(algo, s_, r_, dt, op)
+                    outs, st = run_loopback("reduce_scatter", algo, s_, dt, op, rcounts=r_)
+                    if any(rets) or any(st):
+                        if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
+                            bad.append(("rs", algo, op, dt, st, rets))
+                        continue
+                    if any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                        bad.append(("rs", algo, op, dt))
+    finally:
+        for c in comms(P):
+            c.set_flat_ag(False)
+            c.set_flat_rs(False)
+    assert not bad, bad[:8]
+
+
+def test_collective_bitwise_on_float_is_refused(dev):
+    """MPICH has no bitwise op on floating types (MPI_ERR_OP): the collective
+    returns BINE_ERR_ARG on every rank before any exchange"""
+    P = 4
+    sb = [O.fill("float", 64, r) for r in range(P)]
+    _, st = run_loopback("allreduce", "bine_bdw_remap", sb, "float", "band")
+    assert st == [1] * P

@@ -25,16 +25,16 @@ TABLES = os.path.join(G.GOLDEN, "tables.json")
 def _run(c, ref_bugs=True):
     P, N, dt = c["P"], c["N"], c["dtype"]
     if c["coll"] == "allreduce":
-        sb = O.inputs(dt, N, P, c["seed_base"])
+        sb = G.inputs(c)
         return O.allreduce(c["algo"], sb, dt, c["op"], c["segsize"], ref_bugs=ref_bugs)
     if c["coll"] == "reduce_scatter":
         rc = G.rcounts(c)
-        sb = O.inputs(dt, sum(rc), P, c["seed_base"])
+        sb = G.inputs(c, sum(rc))
         return O.reduce_scatter(c["algo"], sb, rc, dt, c["op"])
     if c["coll"] == "allgather":
-        sb = O.inputs(dt, N, P, c["seed_base"])
+        sb = G.inputs(c)
         return O.allgather(c["algo"], sb, dt)
-    sb = O.inputs(dt, N, P, c["seed_base"])
+    sb = G.inputs(c)
     o, rets = O.reduce(c["algo"], sb, dt, c["op"])
     return [o] + [np.zeros(0)] * (P - 1), rets
 
@@ -70,12 +70,12 @@ def test_oracle_matches_reference_goldens(key, cs):
 
 def test_fill_matches_pico_core_generator():
     cs = G.select(coll="fill")
-    assert len(cs) == 7
+    assert len(cs) == 14   # 7 dtypes x {plain, sparsified} inputs
     for c in cs:
         exp = G.outputs(c)
+        got = G.inputs(c)
         for r in range(c["P"]):
-            got = O.fill(c["dtype"], c["N"], c["seed_base"] + r)
-            assert got.tobytes() == exp[r].tobytes(), (c["dtype"], r)
+            assert got[r].tobytes() == exp[r].tobytes(), (c["dtype"], c["rcounts"], r)
 
 
 def test_segmented_tail_bug_is_opt_in():
@@ -138,6 +138,24 @@ def test_reduce_local_semantics():
     x = np.array([127, -128], np.int8); y = np.array([1, -1], np.int8)
     O.reduce_local(x, y, "int8", "sum")
     assert y.tolist() == [-128, 127]          # wrap-around, no UB
+
+
+def test_reduce_local_logical_and_bitwise_semantics():
+    """MPICH's MPIR_LLAND / LLOR / LLXOR (C truthiness, 0 / 1 in the element
+    type, floats included: -0.0 is false, NaN true) and the bitwise ops; the
+    collectives' cases are pinned by the reference's vectors (ops_jobs in
+    tools/make_golden.py)"""
+    a = np.array([0.0, -0.0, np.nan, 2.5, 0.0, 1.0], np.float32)
+    b = np.array([1.0, 1.0, 1.0, 0.0, 0.0, -3.0], np.float32)
+    for op, want in (("land", [0, 0, 1, 0, 0, 1]), ("lor", [1, 1, 1, 1, 0, 1]), ("lxor", [1, 1, 0, 1, 0, 0])):
+        io = b.copy()
+        O.reduce_local(a, io, "float", op)
+        assert io.tolist() == want, op
+    x = np.array([0x0F, -1, 0x55], np.int8)
+    for op, want in (("band", [0x0C, 0x3C, 0x14]), ("bor", [0x3F, -1, 0x7D]), ("bxor", [0x33, -0x3D, 0x69])):
+        io = np.array([0x3C, 0x3C, 0x3C], np.int8)
+        O.reduce_local(x, io, "int8", op)
+        assert io.tolist() == want, op
 
 
 def test_permute_remap_unequal_blocks_is_err_arg():

@@ -106,6 +106,47 @@ def allgather_jobs():
     return jobs
 
 
+LOGIC_OPS = ["land", "lor", "lxor"]
+BIT_OPS = ["band", "bor", "bxor"]
+LOGIC_DT = ["float", "double", "int32", "int8", "uint8"]
+BIT_DT = ["int64", "int32", "int16", "int8", "uint8"]
+
+
+def ops_jobs():
+    """MPICH's logical and bitwise MPI_Ops through the reference's collectives
+    (logical ops on sparsified inputs -- zeros, -0.0, NaN -- so that both truth
+    values occur), and MAX / MIN on sparsified floats (NaN / signed-zero
+    operand order through every schedule), plus the sparsified inputs
+    themselves ("fill")"""
+    jobs = [(8, "fill", "-", "sum", 0, "even_sparse", ALL_DT, [64], True)]
+    for P in (1, 2, 4, 8):
+        for op in LOGIC_OPS + BIT_OPS:
+            rk, dts = ("even_sparse", LOGIC_DT) if op in LOGIC_OPS else ("even", BIT_DT)
+            for a in ("bine_bdw_remap", "bine_bdw_static", "bine_lat", "ring"):
+                jobs.append((P, "allreduce", a, op, 0, rk, dts, [13, 4096], True))
+            for a in ("bine_permute_remap", "bine_static", "bine_block_by_block"):
+                jobs.append((P, "reduce_scatter", a, op, 0, rk, dts, [P * 3, P * 1024], True))
+            for a in ("bine_bdw", "bine_lat"):
+                jobs.append((P, "reduce", a, op, 0, rk, dts, [13, 4096], True))
+        for op in ("max", "min"):
+            for a in ("bine_bdw_remap", "bine_lat", "rabenseifner"):
+                jobs.append((P, "allreduce", a, op, 0, "even_sparse", ["float", "double"], [13, 4096], True))
+            for a in ("bine_block_by_block", "bine_send_remap", "butterfly"):
+                jobs.append((P, "reduce_scatter", a, op, 0, "even_sparse", ["float", "double"], [P * 3, P * 1024],
+                             True))
+            jobs.append((P, "reduce", "bine_lat", op, 0, "even_sparse", ["float"], [13, 4096], True))
+    for P in (3, 6):
+        for op in ("land", "bxor", "max"):
+            rk, dts = ("even", ["int32"]) if op == "bxor" else ("even_sparse", ["float", "int8"])
+            for a in ("ring", "bine_lat", "recursivedoubling"):
+                jobs.append((P, "allreduce", a, op, 0, rk, dts, [13, 4096], True))
+    return jobs
+
+
+def _is_ops_case(c):
+    return c["op"] in LOGIC_OPS + BIT_OPS or c["rcounts"].endswith("_sparse")
+
+
 def main():
     if not os.path.exists(BIN):
         sys.exit("build the reference first: make -C oracle ref")
@@ -115,6 +156,11 @@ def main():
         # regenerate one collective's cases, keep everything else as it is
         old = json.load(open(os.path.join(OUT, "index.json")))["cases"]
         prev = dict(np.load(os.path.join(OUT, "outputs.npz")))
+        if only == "ops":
+            index = [c for c in old if not _is_ops_case(c)]
+            keep = {c["id"] for c in index}
+            arrays = {k: v for k, v in prev.items() if k in keep}
+            return capture(ops_jobs(), index, arrays)
         index = [c for c in old if c["coll"] != only]
         arrays = {k: v for k, v in prev.items() if not k.startswith(only + ".")}
         jobs = {"allgather": allgather_jobs}[only]()
@@ -156,6 +202,7 @@ def main():
     jobs.append((8, "reduce_scatter", "bine_permute_remap", "sum", 0, "even", ["float"], [8 * 131072 + 8 * 3], False))
     jobs.append((8, "allreduce", "bine_bdw_remap", "sum", 0, "even", ["double", "int64"], [262147], False))
     jobs += allgather_jobs()
+    jobs += ops_jobs()
     capture(jobs, [], {})
 
 
