@@ -875,17 +875,13 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         trial((best[0], best[1], True, 1))
         if trials[(best[0], best[1], True, 1)] < trials.get(best, float("inf")):
             best = (best[0], best[1], True, 1)
-    if best == base_cfg and ok0 is not False:
-        st, ok_head, dig = st0, ok0, dig0
-    else:
+    run1 = None
+    if best != base_cfg:
         apply_transport(comm, *best)
         rbuf.fill_(float("nan"))
-        st = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
-        ok_head, dig = parity(best[0])
-        # the faster of the two full, checked runs is the headline (the trials'
-        # 3-step estimates can mislead; the provisional run is a measurement too)
-        if ok_head is False or (ok0 is not False and st0["median_ms"] < st["median_ms"]):
-            best, st, ok_head, dig = base_cfg, st0, ok0, dig0
+        st1 = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
+        run1 = (st1,) + parity(best[0])
+    best, (st, ok_head, dig) = pick_headline(base_cfg, (st0, ok0, dig0), best, run1)
     chosen, chunk, graphs, stripes = best
     apply_transport(comm, chosen, chunk, graphs, stripes)
     ok_trees_tol = None
@@ -966,6 +962,20 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     comm.destroy()
     dist.destroy_process_group()
     return out
+
+
+def pick_headline(base, run0, best, run1):
+    """the headline among two full, checked runs (st, ok, digest): the
+    provisional literal schedule `base` and the trials' pick `best` (run1 None
+    when that is the same configuration).  A run whose check failed never wins
+    over one that did not; otherwise the faster median wins (the trials'
+    3-step estimates can mislead, the provisional run is a measurement too)."""
+    if run1 is None:
+        return base, run0
+    ok0, ok1 = run0[1], run1[1]
+    if (ok1 is False) != (ok0 is False):
+        return (base, run0) if ok1 is False else (best, run1)
+    return (base, run0) if run0[0]["median_ms"] < run1[0]["median_ms"] else (best, run1)
 
 
 def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, st, ok_head, dig, ok_trees_tol,
