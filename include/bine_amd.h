@@ -30,7 +30,13 @@ extern "C" {
 typedef enum {
   BINE_INT8 = 0, BINE_UINT8 = 1, BINE_INT16 = 2, BINE_UINT16 = 3,
   BINE_INT32 = 4, BINE_UINT32 = 5, BINE_INT64 = 6, BINE_UINT64 = 7,
-  BINE_FLOAT = 8, BINE_DOUBLE = 9, BINE_NUM_DTYPES = 10
+  BINE_FLOAT = 8, BINE_DOUBLE = 9,
+  /* MPI's (value, index) pair types, for BINE_MAXLOC / BINE_MINLOC only; C
+   * layouts as MPI defines them: FLOAT_INT {float; int} 8 B, DOUBLE_INT
+   * {double; int} 16 B, LONG_INT {long; int} 16 B, 2INT {int; int} 8 B,
+   * SHORT_INT {short; int} 8 B (padding bytes are never written) */
+  BINE_FLOAT_INT = 10, BINE_DOUBLE_INT = 11, BINE_LONG_INT = 12, BINE_2INT = 13, BINE_SHORT_INT = 14,
+  BINE_NUM_DTYPES = 15
 } bine_dtype_t;
 
 /* reduction operators, MPI_Reduce_local semantics of MPICH 3.3.2:
@@ -40,11 +46,15 @@ typedef enum {
  * type; defined on every type, floats included -- -0.0 is false, NaN true)
  * and the bitwise ops (integer types only; BINE_ERR_ARG on float / double,
  * where MPICH reports MPI_ERR_OP) complete the predefined MPI_Op set
- * libbine's callers can pass (MAXLOC / MINLOC need pair types, not provided). */
+ * libbine's callers can pass.  MAXLOC / MINLOC (MPICH's opmaxloc.c /
+ * opminloc.c: equal values keep the smaller index, otherwise the larger /
+ * smaller value's pair; a NaN never replaces nor is replaced) apply to the
+ * pair types only, and the pair types to them only. */
 typedef enum {
   BINE_SUM = 0, BINE_PROD = 1, BINE_MAX = 2, BINE_MIN = 3,
   BINE_LAND = 4, BINE_BAND = 5, BINE_LOR = 6, BINE_BOR = 7, BINE_LXOR = 8, BINE_BXOR = 9,
-  BINE_NUM_OPS = 10
+  BINE_MAXLOC = 10, BINE_MINLOC = 11,
+  BINE_NUM_OPS = 12
 } bine_op_t;
 
 typedef enum {
@@ -113,6 +123,10 @@ const char *bine_last_error(void);
  * (1, 2, 4, 8), grid cap (0 = 2048), non-temporal loads of `in` (fp32 SUM only) */
 int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);
 size_t bine_dtype_size(int dtype);
+/* 1 if MPICH's MPI_Reduce_local accepts (dtype, op): no bitwise op on float /
+ * double, MAXLOC / MINLOC exactly on the pair types; 0 otherwise (the
+ * collectives then return BINE_ERR_ARG, the libbine.h shim MPI_ERR_OP) */
+int bine_op_valid(int dtype, int op);
 /* -1 if unknown; `collective` = "allreduce" | "reduce_scatter" | "reduce" */
 int bine_algo_from_name(const char *collective, const char *name);
 const char *bine_algo_name(int algo);

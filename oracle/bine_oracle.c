@@ -28,6 +28,8 @@ size_t orc_dtype_size(int dt) {
     case ORC_INT16: case ORC_UINT16: return 2;
     case ORC_INT32: case ORC_UINT32: case ORC_FLOAT: return 4;
     case ORC_INT64: case ORC_UINT64: case ORC_DOUBLE: return 8;
+    case ORC_FLOAT_INT: case ORC_2INT: case ORC_SHORT_INT: return 8;
+    case ORC_DOUBLE_INT: case ORC_LONG_INT: return 16;
     default: return 0;
   }
 }
@@ -75,8 +77,41 @@ size_t orc_dtype_size(int dt) {
     }                                                                         \
   } while (0)
 
+/* MPI's pair types, C layout, with the padding spelled out as members: C
+ * leaves implicit padding unspecified, and gcc -O2 does store garbage there
+ * when it merges the field updates (measured); as members, the inout
+ * operand's padding bytes survive, as on the device */
+typedef struct { float v; int i; } orc_float_int;
+typedef struct { double v; int i, pad_; } orc_double_int;
+typedef struct { long v; int i, pad_; } orc_long_int;
+typedef struct { int v; int i; } orc_2int;
+typedef struct { short v, pad_; int i; } orc_short_int;
+
+/* MPICH 3.3.2 opmaxloc.c / opminloc.c, a = inout, b = in: equal values keep
+ * MPL_MIN of the indices, a strictly larger (MAXLOC) / smaller (MINLOC) `in`
+ * value replaces the pair.  Field by field (MPICH assigns the struct; its
+ * padding bytes are not part of the type map and never travel). */
+#define RL_PAIR(T)                                                            \
+  do {                                                                        \
+    T *a = (T *)inout; const T *b = (const T *)in;                            \
+    if (op != ORC_MAXLOC && op != ORC_MINLOC) return -1;                      \
+    for (size_t i = 0; i < n; i++) {                                          \
+      if (a[i].v == b[i].v) a[i].i = a[i].i < b[i].i ? a[i].i : b[i].i;       \
+      else if (op == ORC_MAXLOC ? a[i].v < b[i].v : a[i].v > b[i].v) {        \
+        a[i].v = b[i].v;                                                      \
+        a[i].i = b[i].i;                                                      \
+      }                                                                       \
+    }                                                                         \
+  } while (0)
+
 int orc_reduce_local(const void *in, void *inout, size_t n, int dtype, int op) {
+  if (dtype < ORC_FLOAT_INT && (op == ORC_MAXLOC || op == ORC_MINLOC)) return -1;
   switch (dtype) {
+    case ORC_FLOAT_INT:  RL_PAIR(orc_float_int); break;
+    case ORC_DOUBLE_INT: RL_PAIR(orc_double_int); break;
+    case ORC_LONG_INT:   RL_PAIR(orc_long_int); break;
+    case ORC_2INT:       RL_PAIR(orc_2int); break;
+    case ORC_SHORT_INT:  RL_PAIR(orc_short_int); break;
     case ORC_INT8:   RL_INT(int8_t, uint8_t); break;
     case ORC_UINT8:  RL_INT(uint8_t, uint8_t); break;
     case ORC_INT16:  RL_INT(int16_t, uint16_t); break;
@@ -94,7 +129,31 @@ int orc_reduce_local(const void *in, void *inout, size_t n, int dtype, int op) {
 
 /* pico_core_utils.c:902-923 (rand_r distributions).  The int64 pair is drawn
  * high word first. */
+/* pico_core has no generator for MPI's pair types; the golden harness
+ * (oracle/ref_golden.c fill) and this one draw value = rand_r() % 16 (halved
+ * for the floating values: ties and fractions) and index = rand_r() % 1000,
+ * padding 0 */
+#define FILL_PAIR(T, VT, HALF)                                                \
+  do {                                                                        \
+    T *p = (T *)buf;                                                          \
+    memset(p, 0, n * sizeof(T));                                              \
+    for (size_t i = 0; i < n; i++) {                                          \
+      const int r = rand_r(&seed) % 16;                                       \
+      p[i].v = HALF ? (VT)r / (VT)2 : (VT)r;                                  \
+      p[i].i = rand_r(&seed) % 1000;                                          \
+    }                                                                         \
+    return 0;                                                                 \
+  } while (0)
+
 int orc_fill(void *buf, int dtype, size_t n, unsigned int seed) {
+  switch (dtype) {
+    case ORC_FLOAT_INT:  FILL_PAIR(orc_float_int, float, 1);
+    case ORC_DOUBLE_INT: FILL_PAIR(orc_double_int, double, 1);
+    case ORC_LONG_INT:   FILL_PAIR(orc_long_int, long, 0);
+    case ORC_2INT:       FILL_PAIR(orc_2int, int, 0);
+    case ORC_SHORT_INT:  FILL_PAIR(orc_short_int, short, 0);
+    default: break;
+  }
   for (size_t i = 0; i < n; i++) {
     switch (dtype) {
       case ORC_INT8:   ((int8_t *)buf)[i] = (int8_t)((rand_r(&seed) % 256) - 128); break;

@@ -16,11 +16,39 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
 
 DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 5,
-          "int64": 6, "uint64": 7, "float": 8, "double": 9}
+          "int64": 6, "uint64": 7, "float": 8, "double": 9,
+          "float_int": 10, "double_int": 11, "long_int": 12, "2int": 13, "short_int": 14}
+
+
+def _pair(v: str, size: int) -> np.dtype:
+    """C layout of MPI's {value; int index} pair types (index after the value,
+    aligned to 4 B; the struct padded to the value's alignment)"""
+    off = 4 if v == "<i2" else np.dtype(v).itemsize
+    return np.dtype({"names": ["v", "i"], "formats": [v, "<i4"], "offsets": [0, off], "itemsize": size})
+
+
 NP_DTYPES = {"int8": np.int8, "uint8": np.uint8, "int16": np.int16, "uint16": np.uint16,
              "int32": np.int32, "uint32": np.uint32, "int64": np.int64, "uint64": np.uint64,
-             "float": np.float32, "double": np.float64}
-OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9}
+             "float": np.float32, "double": np.float64,
+             "float_int": _pair("<f4", 8), "double_int": _pair("<f8", 16), "long_int": _pair("<i8", 16),
+             "2int": _pair("<i4", 8), "short_int": _pair("<i2", 8)}
+PAIRS = ("float_int", "double_int", "long_int", "2int", "short_int")
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9,
+       "maxloc": 10, "minloc": 11}
+
+
+def canonical(a: np.ndarray) -> bytes:
+    """the bytes of `a` with the padding of MPI's pair types zeroed: padding is
+    not part of the type map (MPICH moves only the fields between ranks, the
+    golden harness zeroes it in the reference's outputs), and numpy itself
+    does not carry it through copies of padded structured arrays"""
+    a = np.ascontiguousarray(a)
+    if a.dtype.names:
+        z = np.zeros(a.shape, a.dtype)
+        for f in a.dtype.names:
+            z[f] = a[f]
+        return z.tobytes()
+    return a.tobytes()
 OK, ERR_ARG, ERR_SIZE, ASSERT, DEADLOCK = 0, 12, 51, -2, -3
 
 _lib = None
@@ -65,7 +93,7 @@ def _ptrs(arrs):
 
 def fill(dtype: str, n: int, seed: int) -> np.ndarray:
     """pico_core's generator (pico_core_utils.c:883-928) with seed `seed`."""
-    a = np.empty(n, dtype=NP_DTYPES[dtype])
+    a = np.zeros(n, dtype=NP_DTYPES[dtype])   # pair types: padding bytes stay 0
     lib().orc_fill(a.ctypes.data, DTYPES[dtype], n, seed)
     return a
 
@@ -76,10 +104,11 @@ def sparsify(x: np.ndarray, dtype: str, rank: int) -> np.ndarray:
     rules win) -- inputs on which the logical ops and MAX / MIN show their
     operand semantics"""
     j = np.arange(x.size) + rank
-    x[j % 3 == 0] = 0
-    if dtype in ("float", "double"):
-        x[j % 5 == 1] = -0.0
-        x[j % 11 == 2] = np.nan
+    v = x["v"] if x.dtype.names else x
+    v[j % 3 == 0] = 0
+    if dtype in ("float", "double", "float_int", "double_int"):
+        v[j % 5 == 1] = -0.0
+        v[j % 11 == 2] = np.nan
     return x
 
 

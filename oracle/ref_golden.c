@@ -85,6 +85,13 @@ static ag_fn pick_allgather(const char *a) {
   return NULL;
 }
 
+/* MPI's {value; int index} pair types, C layout */
+typedef struct { float v; int i; } p_float_int;
+typedef struct { double v; int i; } p_double_int;
+typedef struct { long v; int i; } p_long_int;
+typedef struct { int v; int i; } p_2int;
+typedef struct { short v; int i; } p_short_int;
+
 static int dtype_of(const char *s, MPI_Datatype *dt, size_t *sz) {
   if (!strcmp(s, "float"))  { *dt = MPI_FLOAT;         *sz = 4; return 0; }
   if (!strcmp(s, "double")) { *dt = MPI_DOUBLE;        *sz = 8; return 0; }
@@ -93,6 +100,11 @@ static int dtype_of(const char *s, MPI_Datatype *dt, size_t *sz) {
   if (!strcmp(s, "int32"))  { *dt = MPI_INT32_T;       *sz = 4; return 0; }
   if (!strcmp(s, "int64"))  { *dt = MPI_INT64_T;       *sz = 8; return 0; }
   if (!strcmp(s, "uint8"))  { *dt = MPI_UNSIGNED_CHAR; *sz = 1; return 0; }
+  if (!strcmp(s, "float_int"))  { *dt = MPI_FLOAT_INT;  *sz = sizeof(p_float_int); return 0; }
+  if (!strcmp(s, "double_int")) { *dt = MPI_DOUBLE_INT; *sz = sizeof(p_double_int); return 0; }
+  if (!strcmp(s, "long_int"))   { *dt = MPI_LONG_INT;   *sz = sizeof(p_long_int); return 0; }
+  if (!strcmp(s, "2int"))       { *dt = MPI_2INT;       *sz = sizeof(p_2int); return 0; }
+  if (!strcmp(s, "short_int"))  { *dt = MPI_SHORT_INT;  *sz = sizeof(p_short_int); return 0; }
   return -1;
 }
 
@@ -107,11 +119,33 @@ static int op_of(const char *s, MPI_Op *op) {
   if (!strcmp(s, "bor"))  { *op = MPI_BOR;  return 0; }
   if (!strcmp(s, "lxor")) { *op = MPI_LXOR; return 0; }
   if (!strcmp(s, "bxor")) { *op = MPI_BXOR; return 0; }
+  if (!strcmp(s, "maxloc")) { *op = MPI_MAXLOC; return 0; }
+  if (!strcmp(s, "minloc")) { *op = MPI_MINLOC; return 0; }
   return -1;
 }
 
+/* pico_core has no generator for the pair types: value = rand_r() % 16
+ * (halved for floating values: ties and fractions), index = rand_r() % 1000,
+ * padding 0 (the oracle's orc_fill draws the same) */
+#define FILL_PAIR(T, VT, HALF)                                 \
+  do {                                                         \
+    T *p = (T *)buf;                                           \
+    memset(p, 0, n * sizeof(T));                               \
+    for (size_t i = 0; i < n; i++) {                           \
+      const int r = rand_r(&seed) % 16;                        \
+      p[i].v = HALF ? (VT)r / (VT)2 : (VT)r;                   \
+      p[i].i = rand_r(&seed) % 1000;                           \
+    }                                                          \
+    return;                                                    \
+  } while (0)
+
 /* pico_core's generator (pico_core_utils.c:902-923), glibc rand_r. */
 static void fill(void *buf, const char *dt, size_t n, unsigned int seed) {
+  if (!strcmp(dt, "float_int"))  FILL_PAIR(p_float_int, float, 1);
+  if (!strcmp(dt, "double_int")) FILL_PAIR(p_double_int, double, 1);
+  if (!strcmp(dt, "long_int"))   FILL_PAIR(p_long_int, long, 0);
+  if (!strcmp(dt, "2int"))       FILL_PAIR(p_2int, int, 0);
+  if (!strcmp(dt, "short_int"))  FILL_PAIR(p_short_int, short, 0);
   for (size_t i = 0; i < n; i++) {
     if (!strcmp(dt, "int8"))        ((int8_t *)buf)[i] = (int8_t)((rand_r(&seed) % 256) - 128);
     else if (!strcmp(dt, "int16"))  ((int16_t *)buf)[i] = (int16_t)((rand_r(&seed) % 65536) - 32768);
@@ -144,7 +178,19 @@ static void sparsify(void *buf, const char *dt, size_t n, int rank) {
       if (z) f[i] = 0.0;
       if (j % 5 == 1) f[i] = -0.0;
       if (j % 11 == 2) f[i] = NAN;
-    }
+    } else if (!strcmp(dt, "float_int")) {
+      p_float_int *f = (p_float_int *)buf;
+      if (z) f[i].v = 0.0f;
+      if (j % 5 == 1) f[i].v = -0.0f;
+      if (j % 11 == 2) f[i].v = NAN;
+    } else if (!strcmp(dt, "double_int")) {
+      p_double_int *f = (p_double_int *)buf;
+      if (z) f[i].v = 0.0;
+      if (j % 5 == 1) f[i].v = -0.0;
+      if (j % 11 == 2) f[i].v = NAN;
+    } else if (!strcmp(dt, "long_int"))  { if (z) ((p_long_int *)buf)[i].v = 0; }
+    else if (!strcmp(dt, "2int"))        { if (z) ((p_2int *)buf)[i].v = 0; }
+    else if (!strcmp(dt, "short_int"))   { if (z) ((p_short_int *)buf)[i].v = 0; }
   }
 }
 
@@ -219,6 +265,13 @@ int main(int argc, char **argv) {
       } else {
         MPI_Abort(MPI_COMM_WORLD, 6);
       }
+      /* pair types: MPICH moves only the type map's bytes, so the padding of
+       * the output holds whatever the buffers held -- zero it (the tests compare
+       * the defined bytes) */
+      if (outn && (!strcmp(dts[d], "double_int") || !strcmp(dts[d], "long_int")))
+        for (size_t k = 0; k < outn; k++) memset((char *)rbuf + k * esz + 12, 0, 4);
+      if (outn && !strcmp(dts[d], "short_int"))
+        for (size_t k = 0; k < outn; k++) memset((char *)rbuf + k * esz + 2, 0, 2);
       char path[1024];
       snprintf(path, sizeof path, "%s/%s.N%zu.r%d.bin", outdir, dts[d], N, rank);
       FILE *fp = fopen(path, "wb");

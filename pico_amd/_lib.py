@@ -15,10 +15,14 @@ SHIM = os.path.join(LIBDIR, "libbine.so")
 
 # include/bine_amd.h enums
 DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 5,
-          "int64": 6, "uint64": 7, "float": 8, "double": 9}
+          "int64": 6, "uint64": 7, "float": 8, "double": 9,
+          # MPI's (value, index) pair types, MAXLOC / MINLOC only
+          "float_int": 10, "double_int": 11, "long_int": 12, "2int": 13, "short_int": 14}
 DTYPE_SIZE = {"int8": 1, "uint8": 1, "int16": 2, "uint16": 2, "int32": 4, "uint32": 4,
-              "int64": 8, "uint64": 8, "float": 4, "double": 8}
-OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9}
+              "int64": 8, "uint64": 8, "float": 4, "double": 8,
+              "float_int": 8, "double_int": 16, "long_int": 16, "2int": 8, "short_int": 8}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9,
+       "maxloc": 10, "minloc": 11}
 STATUS = {0: "SUCCESS", 1: "ERR_ARG", 2: "ERR_SIZE", 3: "ERR_NO_MEM", 4: "ERR_HIP", 5: "ERR_RCCL",
           6: "ERR_UNSUPPORTED", 7: "ERR_INTERNAL"}
 ALGOS = {
@@ -97,6 +101,7 @@ def lib():
         "bine_status_string": ([i], ctypes.c_char_p),
         "bine_last_error": ([], ctypes.c_char_p),
         "bine_dtype_size": ([i], sz),
+        "bine_op_valid": ([i, i], i),
         "bine_algo_from_name": ([ctypes.c_char_p, ctypes.c_char_p], i),
         "bine_algo_name": ([i], ctypes.c_char_p),
         "bine_set_reduce_tuning": ([i, i, i], i),

@@ -5,8 +5,10 @@ Every function named after a libbine entry point (reference include/libbine.h:
 ``allreduce_bine_bdw_remap(sbuf, rbuf, count, dtype, op, comm)`` -- where the
 buffers are device tensors (torch, ROCm) or raw device addresses, ``dtype`` is a
 libbine element-type name ("float", "double", "int32", ...) or a torch dtype,
-``op`` is "sum" | "prod" | "max" | "min" | "land" | "lor" | "lxor" | "band" | "bor" | "bxor"
-(MPICH semantics; bitwise ops on integer types only), and ``comm`` is a :class:`Comm`.
+``op`` is "sum" | "prod" | "max" | "min" | "land" | "lor" | "lxor" | "band" | "bor" | "bxor" |
+"maxloc" | "minloc" (MPICH semantics; bitwise ops on integer types only, the loc ops on
+the pair types "float_int" | "double_int" | "long_int" | "2int" | "short_int" only), and
+``comm`` is a :class:`Comm`.
 Errors raise :class:`BineError` carrying the status the reference would return
 as an MPI error class.  The work runs in libbine_amd.so (HIP kernels + RCCL);
 there is no fallback.

@@ -818,10 +818,9 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   if (!c) return BINE_ERR_ARG;
   if (dtype < 0 || dtype >= BINE_NUM_DTYPES) return BINE_ERR_UNSUPPORTED;
   if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
-  // bitwise ops are undefined on floating types (MPICH: MPI_ERR_OP); refused
+  // (op, type) pairs MPICH's MPI_Reduce_local rejects (MPI_ERR_OP): refused
   // before any exchange, identically on every rank
-  if ((op == BINE_BAND || op == BINE_BOR || op == BINE_BXOR) && (dtype == BINE_FLOAT || dtype == BINE_DOUBLE))
-    return BINE_ERR_ARG;
+  if (!bine_op_valid(dtype, op)) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   if (chunk_bytes == kCommChunk) chunk_bytes = c->chunk_bytes ? c->chunk_bytes : default_chunk_bytes();
   HIP_TRY(hipSetDevice(c->device));
@@ -914,12 +913,23 @@ const char *bine_status_string(int s) {
 
 const char *bine_last_error(void) { return g_err.c_str(); }
 
+int bine_op_valid(int dtype, int op) {
+  if (dtype < 0 || dtype >= BINE_NUM_DTYPES || op < 0 || op >= BINE_NUM_OPS) return 0;
+  const bool pair = dtype >= BINE_FLOAT_INT, loc = op == BINE_MAXLOC || op == BINE_MINLOC;
+  if (pair != loc) return 0;  // pair types under MAXLOC / MINLOC only, and those ops on pairs only
+  if ((op == BINE_BAND || op == BINE_BOR || op == BINE_BXOR) && (dtype == BINE_FLOAT || dtype == BINE_DOUBLE))
+    return 0;  // no bitwise ops on floating types
+  return 1;
+}
+
 size_t bine_dtype_size(int dt) {
   switch (dt) {
     case BINE_INT8: case BINE_UINT8: return 1;
     case BINE_INT16: case BINE_UINT16: return 2;
     case BINE_INT32: case BINE_UINT32: case BINE_FLOAT: return 4;
     case BINE_INT64: case BINE_UINT64: case BINE_DOUBLE: return 8;
+    case BINE_FLOAT_INT: case BINE_2INT: case BINE_SHORT_INT: return 8;
+    case BINE_DOUBLE_INT: case BINE_LONG_INT: return 16;
     default: return 0;
   }
 }

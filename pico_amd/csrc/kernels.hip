@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -56,6 +57,38 @@ using uint_of = std::conditional_t<sizeof(T) == 1, uint8_t,
                 std::conditional_t<sizeof(T) == 2, uint16_t,
                 std::conditional_t<sizeof(T) == 4, uint32_t, uint64_t>>>;
 
+// MPI's (value, index) pair types, C layout.  The padding of the C structs is
+// spelled out as members, so that a pair passed and returned by value keeps
+// the inout operand's padding bytes (implicit padding is unspecified after a
+// copy -- measured: garbage in the padding of returned {double; int} pairs).
+template <typename V>
+struct Pair {
+  V v;
+  int i;
+};
+template <>
+struct Pair<double> {
+  double v;
+  int i, pad_;
+};
+template <>
+struct Pair<long> {
+  long v;
+  int i, pad_;
+};
+template <>
+struct Pair<short> {
+  short v, pad_;
+  int i;
+};
+static_assert(sizeof(Pair<double>) == 16 && sizeof(Pair<long>) == 16 && sizeof(Pair<short>) == 8 &&
+                  sizeof(Pair<float>) == 8 && sizeof(Pair<int>) == 8 && offsetof(Pair<short>, i) == 4,
+              "MPI pair layouts");
+template <typename T>
+struct is_pair : std::false_type {};
+template <typename V>
+struct is_pair<Pair<V>> : std::true_type {};
+
 // MPICH's MPIR_OP_TYPE_REDUCE_CASE: a = inout, b = in, a = OP(a, b)
 template <typename T, int OP>
 __device__ __forceinline__ T apply(T io, T in) {
@@ -79,6 +112,16 @@ __device__ __forceinline__ T apply(T io, T in) {
     return (T)(io & in);
   } else if constexpr (OP == BINE_BOR) {
     return (T)(io | in);
+  } else if constexpr (OP == BINE_MAXLOC || OP == BINE_MINLOC) {
+    // MPICH opmaxloc.c / opminloc.c (a = inout, b = in): equal values keep
+    // the smaller index; otherwise a strictly larger (smaller) value of `in`
+    // replaces the pair -- field by field, so io's padding bytes stay
+    if (io.v == in.v) io.i = io.i < in.i ? io.i : in.i;
+    else if (OP == BINE_MAXLOC ? io.v < in.v : io.v > in.v) {
+      io.v = in.v;
+      io.i = in.i;
+    }
+    return io;
   } else {
     static_assert(OP == BINE_BXOR, "unknown op");
     return (T)(io ^ in);
@@ -94,6 +137,8 @@ template <typename T>
 constexpr bool kLogicT = std::is_unsigned_v<T> || std::is_floating_point_v<T>;
 template <typename T>
 constexpr bool kBitsT = std::is_same_v<T, uint8_t>;
+template <typename T>
+constexpr bool kPairT = is_pair<T>::value;
 
 // BINE_OP_SWITCH(T, CALL): `return CALL(OP)` for the op in variable `op`,
 // only for the (T, OP) pairs instantiated; hipErrorInvalidValue otherwise
@@ -116,6 +161,8 @@ constexpr bool kBitsT = std::is_same_v<T, uint8_t>;
     case BINE_BAND: if constexpr (kBitsT<T>) return CALL(BINE_BAND); break;  \
     case BINE_BOR: if constexpr (kBitsT<T>) return CALL(BINE_BOR); break;    \
     case BINE_BXOR: if constexpr (kBitsT<T>) return CALL(BINE_BXOR); break;  \
+    case BINE_MAXLOC: if constexpr (kPairT<T>) return CALL(BINE_MAXLOC); break; \
+    case BINE_MINLOC: if constexpr (kPairT<T>) return CALL(BINE_MINLOC); break; \
     default: break;                                                  \
   }                                                                  \
   return hipErrorInvalidValue;
@@ -128,9 +175,8 @@ constexpr bool kBitsT = std::is_same_v<T, uint8_t>;
 // type (bitwise ops on float / double: MPICH's MPI_ERR_OP)
 static int canon_dtype(int dtype, int op, size_t *scale) {
   *scale = 1;
-  if (dtype < 0 || dtype >= BINE_NUM_DTYPES || op < 0 || op >= BINE_NUM_OPS) return -1;
+  if (!bine_op_valid(dtype, op)) return -1;
   if (op == BINE_BAND || op == BINE_BOR || op == BINE_BXOR) {
-    if (dtype == BINE_FLOAT || dtype == BINE_DOUBLE) return -1;
     *scale = bine_dtype_size(dtype);
     return BINE_UINT8;
   }
@@ -325,6 +371,13 @@ int BINE_FN(launch_reduce)(const void *a, const void *b, void *out, size_t count
     case BINE_UINT64: e = reduce_op<uint64_t>(a, b, out, count, op, st); break;
     case BINE_FLOAT: e = reduce_op<float>(a, b, out, count, op, st); break;
     case BINE_DOUBLE: e = reduce_op<double>(a, b, out, count, op, st); break;
+#if BINE_OPSET == 1
+    case BINE_FLOAT_INT: e = reduce_op<Pair<float>>(a, b, out, count, op, st); break;
+    case BINE_DOUBLE_INT: e = reduce_op<Pair<double>>(a, b, out, count, op, st); break;
+    case BINE_LONG_INT: e = reduce_op<Pair<long>>(a, b, out, count, op, st); break;
+    case BINE_2INT: e = reduce_op<Pair<int>>(a, b, out, count, op, st); break;
+    case BINE_SHORT_INT: e = reduce_op<Pair<short>>(a, b, out, count, op, st); break;
+#endif
     default: return BINE_ERR_UNSUPPORTED;
   }
   return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
@@ -492,6 +545,13 @@ int BINE_FN(launch_reduce_batch)(int n, const void *const *a, const void *const 
     case BINE_UINT64: e = batch_op<uint64_t>(n, a, b, out, count, op, st); break;
     case BINE_FLOAT: e = batch_op<float>(n, a, b, out, count, op, st); break;
     case BINE_DOUBLE: e = batch_op<double>(n, a, b, out, count, op, st); break;
+#if BINE_OPSET == 1
+    case BINE_FLOAT_INT: e = batch_op<Pair<float>>(n, a, b, out, count, op, st); break;
+    case BINE_DOUBLE_INT: e = batch_op<Pair<double>>(n, a, b, out, count, op, st); break;
+    case BINE_LONG_INT: e = batch_op<Pair<long>>(n, a, b, out, count, op, st); break;
+    case BINE_2INT: e = batch_op<Pair<int>>(n, a, b, out, count, op, st); break;
+    case BINE_SHORT_INT: e = batch_op<Pair<short>>(n, a, b, out, count, op, st); break;
+#endif
     default: return BINE_ERR_UNSUPPORTED;
   }
   if (e == hipErrorInvalidValue) return BINE_ERR_ARG;  // not co-aligned: caller falls back
@@ -694,6 +754,13 @@ int BINE_FN(launch_reduce_tree)(int nl, const void *const *leaf, void *out, size
     case BINE_UINT64: e = tree_op<uint64_t>(nl, t, op, st); break;
     case BINE_FLOAT: e = tree_op<float>(nl, t, op, st); break;
     case BINE_DOUBLE: e = tree_op<double>(nl, t, op, st); break;
+#if BINE_OPSET == 1
+    case BINE_FLOAT_INT: e = tree_op<Pair<float>>(nl, t, op, st); break;
+    case BINE_DOUBLE_INT: e = tree_op<Pair<double>>(nl, t, op, st); break;
+    case BINE_LONG_INT: e = tree_op<Pair<long>>(nl, t, op, st); break;
+    case BINE_2INT: e = tree_op<Pair<int>>(nl, t, op, st); break;
+    case BINE_SHORT_INT: e = tree_op<Pair<short>>(nl, t, op, st); break;
+#endif
     default: return BINE_ERR_UNSUPPORTED;
   }
   return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;

@@ -85,13 +85,19 @@ int map_dtype(MPI_Datatype d) {
   if (d == MPI_UINT32_T || d == MPI_UNSIGNED) return BINE_UINT32;
   if (d == MPI_INT64_T || d == MPI_LONG || d == MPI_LONG_LONG) return BINE_INT64;
   if (d == MPI_UINT64_T || d == MPI_UNSIGNED_LONG || d == MPI_UNSIGNED_LONG_LONG) return BINE_UINT64;
+  if (d == MPI_FLOAT_INT) return BINE_FLOAT_INT;
+  if (d == MPI_DOUBLE_INT) return BINE_DOUBLE_INT;
+  if (d == MPI_LONG_INT) return BINE_LONG_INT;
+  if (d == MPI_2INT) return BINE_2INT;
+  if (d == MPI_SHORT_INT) return BINE_SHORT_INT;
   return -1;
 }
 
 // The predefined MPI_Ops MPICH's MPI_Reduce_local applies, and the (op, type)
 // pairs it accepts (MPICH 3.3.2, probed with its own MPI_Reduce_local):
 // MPI_BYTE only under the bitwise ops, floating types under every op but the
-// bitwise ones.  -1 = MPI_ERR_OP (the reference's MPI_Reduce_local would fail).
+// bitwise ones, the (value, index) pair types under MAXLOC / MINLOC only.
+// -1 = MPI_ERR_OP (the reference's MPI_Reduce_local would fail).
 int map_op(MPI_Op o, MPI_Datatype d) {
   int r = -1;
   if (o == MPI_SUM) r = BINE_SUM;
@@ -104,11 +110,13 @@ int map_op(MPI_Op o, MPI_Datatype d) {
   else if (o == MPI_BOR) r = BINE_BOR;
   else if (o == MPI_LXOR) r = BINE_LXOR;
   else if (o == MPI_BXOR) r = BINE_BXOR;
+  else if (o == MPI_MAXLOC) r = BINE_MAXLOC;
+  else if (o == MPI_MINLOC) r = BINE_MINLOC;
   if (r < 0) return -1;
   const bool bits = r == BINE_BAND || r == BINE_BOR || r == BINE_BXOR;
-  if (d == MPI_BYTE && !bits) return -1;
-  if (bits && (d == MPI_FLOAT || d == MPI_DOUBLE)) return -1;
-  return r;
+  if (d == MPI_BYTE) return bits ? r : -1;
+  const int dt = map_dtype(d);
+  return dt < 0 || bine_op_valid(dt, r) ? r : -1;  // unknown types are reported as MPI_ERR_TYPE
 }
 
 int get_entry(MPI_Comm comm, Entry **out) {

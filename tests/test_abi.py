@@ -54,3 +54,18 @@ def test_dtype_sizes():
     L = pico_amd.lib()
     for name, code in pico_amd.DTYPES.items():
         assert L.bine_dtype_size(code) == _lib.DTYPE_SIZE[name]
+
+
+def test_op_valid_matches_mpich_table():
+    """bine_op_valid (host-only) against the (op, type) pairs MPICH 3.3.2's
+    MPI_Reduce_local accepts (probed with it): no bitwise op on float /
+    double, MAXLOC / MINLOC exactly on the pair types"""
+    import pico_amd
+    from pico_amd._lib import DTYPES, OPS
+    lib = pico_amd.lib()
+    for d, dv in DTYPES.items():
+        for o, ov in OPS.items():
+            pair, loc = d in ("float_int", "double_int", "long_int", "2int", "short_int"), o in ("maxloc", "minloc")
+            want = pair == loc and not (o in ("band", "bor", "bxor") and d in ("float", "double"))
+            assert bool(lib.bine_op_valid(dv, ov)) == want, (d, o)
+    assert not lib.bine_op_valid(15, 0) and not lib.bine_op_valid(0, 12)

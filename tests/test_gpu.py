@@ -48,7 +48,7 @@ def from_dev(t, dtype: str, n: int, off_bytes: int = 0) -> np.ndarray:
 
 
 def sha(a):
-    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    return hashlib.sha256(O.canonical(np.asarray(a))).hexdigest()   # pair types: padding zeroed
 
 
 # ---- the arithmetic boundary -------------------------------------------------------

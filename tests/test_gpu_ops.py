@@ -1,5 +1,5 @@
-"""GPU parity of the logical and bitwise MPI_Ops (MPI_LAND / LOR / LXOR /
-BAND / BOR / BXOR) -- the predefined operators beyond pico_core's MPI_SUM that
+"""GPU parity of the logical, bitwise and location MPI_Ops (MPI_LAND / LOR / LXOR /
+BAND / BOR / BXOR, MAXLOC / MINLOC on the pair types) -- the predefined operators beyond pico_core's MPI_SUM that
 libbine's callers may pass (every reduce-family entry point forwards its
 MPI_Op to MPI_Reduce_local, e.g. libbine_allreduce.c:888).
 
@@ -160,3 +160,112 @@ def test_collective_bitwise_on_float_is_refused(dev):
     sb = [O.fill("float", 64, r) for r in range(P)]
     _, st = run_loopback("allreduce", "bine_bdw_remap", sb, "float", "band")
     assert st == [1] * P
+
+
+# ---- MAXLOC / MINLOC on MPI's (value, index) pair types ----------------------------
+
+PAIRS = ["float_int", "double_int", "long_int", "2int", "short_int"]
+
+
+@pytest.mark.parametrize("dtype", PAIRS)
+@pytest.mark.parametrize("op", ["maxloc", "minloc"])
+def test_reduce_local_loc_pairs(dev, dtype, op):
+    """MPICH's opmaxloc.c / opminloc.c field by field (ties keep the smaller
+    index; NaN values never replace nor get replaced); compared on the defined
+    bytes (padding is not part of MPI's type map)"""
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for n in (1, 3, 17, 1000, 100003):
+        for shift in (0, 1):
+            a = O.sparsify(O.fill(dtype, n, 11 + n), dtype, 0)
+            b = O.sparsify(O.fill(dtype, n, 97 + n), dtype, 1)
+            # (np.concatenate would promote the padded struct dtypes to packed ones)
+            ha, hb = np.zeros(n + shift, a.dtype), np.zeros(n + shift, b.dtype)
+            ha[shift:], hb[shift:] = a, b
+            ta, tb = to_dev(ha), to_dev(hb)
+            pico_amd.reduce_local(ta.data_ptr() + shift * esz, tb.data_ptr() + shift * esz, n, dtype, op)
+            torch.cuda.synchronize()
+            exp = b.copy()
+            O.reduce_local(a, exp, dtype, op)
+            assert sha(from_dev(tb, dtype, n, shift * esz)) == sha(exp), (n, shift)
+
+
+def test_loc_ops_refuse_other_types(dev):
+    """MAXLOC / MINLOC only on pair types, pair types only under them (MPICH:
+    MPI_ERR_OP)"""
+    t = to_dev(O.fill("float", 64, 1))
+    with pytest.raises(pico_amd.BineError):
+        pico_amd.reduce_local(t, t.data_ptr(), 16, "float", "maxloc")
+    p = to_dev(O.fill("float_int", 64, 1))
+    for op in ("sum", "max", "land", "band"):
+        with pytest.raises(pico_amd.BineError):
+            pico_amd.reduce_local(p, p.data_ptr(), 16, "float_int", op)
+
+
+@pytest.mark.parametrize("dtype", PAIRS)
+def test_reduce_tree_and_batch_loc_pairs(dev, dtype):
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for op in ("maxloc", "minloc"):
+        for nl in (2, 8, 16):
+            for n in (4099, 3):
+                host = [O.sparsify(O.fill(dtype, n, 300 + j), dtype, j) for j in range(nl)]
+                want = _host_tree(host, dtype, op)
+                leaves = [to_dev(h, pad=16) for h in host]
+                out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
+                assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
+                torch.cuda.synchronize()
+                assert sha(from_dev(out, dtype, n)) == sha(want), (op, nl, n)
+        counts = [5003, 16, 1]
+        ins = [O.fill(dtype, c, 40 + k) for k, c in enumerate(counts)]
+        ios = [O.fill(dtype, c, 50 + k) for k, c in enumerate(counts)]
+        tin, tio = [to_dev(x, pad=16) for x in ins], [to_dev(x, pad=16) for x in ios]
+        assert pico_amd.reduce_batch(tin, tio, counts, dtype, op) == 0
+        torch.cuda.synchronize()
+        for k, c in enumerate(counts):
+            exp = ios[k].copy()
+            O.reduce_local(ins[k], exp, dtype, op)
+            assert sha(from_dev(tio[k], dtype, c)) == sha(exp), (op, k)
+
+
+@pytest.mark.parametrize("mode", ["literal", "flat"])
+@pytest.mark.parametrize("P", [4, 8])
+def test_collectives_loc_pairs_every_algorithm(dev, P, mode):
+    """every reduce-family algorithm under MAXLOC / MINLOC on 8- and 16-byte
+    pair types, literal schedule and flat phases, bit-exact vs the oracle (the
+    oracle is pinned by the reference's vectors for the unpadded pair types;
+    for the padded ones the reference's copy_buffer copies MPI_Type_size x
+    count bytes, libbine_utils.h:176-190, and its outputs are wrong)"""
+    flat = mode == "flat"
+    for c in comms(P):
+        c.set_flat_ag(flat)
+        c.set_flat_rs(flat)
+    bad = []
+    try:
+        for op, dt in (("maxloc", "float_int"), ("minloc", "double_int"), ("maxloc", "short_int"),
+                       ("minloc", "2int"), ("maxloc", "long_int")):
+            n = 1003
+            sb = [O.sparsify(O.fill(dt, n, 1234 + r), dt, r) for r in range(P)]
+            for algo in AR_ALGOS:
+                want, rets = O.allreduce(algo, sb, dt, op)
+                outs, st = run_loopback("allreduce", algo, sb, dt, op)
+                if any(rets) or any(st):
+                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
+                        bad.append(("ar", algo, op, dt, st, rets))
+                    continue
+                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                    bad.append(("ar", algo, op, dt))
+            rc = [n // P] * P
+            sbr = [x[: sum(rc)] for x in sb]
+            for algo in RS_ALGOS:
+                want, rets = O.reduce_scatter(algo, sbr, rc, dt, op)
+                outs, st = run_loopback("reduce_scatter", algo, sbr, dt, op, rcounts=rc)
+                if any(rets) or any(st):
+                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
+                        bad.append(("rs", algo, op, dt, st, rets))
+                    continue
+                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                    bad.append(("rs", algo, op, dt))
+    finally:
+        for c in comms(P):
+            c.set_flat_ag(False)
+            c.set_flat_rs(False)
+    assert not bad, bad[:8]

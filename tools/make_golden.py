@@ -34,7 +34,13 @@ BIN = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
 OUT = os.path.join(ROOT, "tests", "golden")
 MPI = "/opt/conda/bin"
 SEED = 1234
-ESZ = {"float": 4, "double": 8, "int8": 1, "int16": 2, "int32": 4, "int64": 8, "uint8": 1}
+ESZ = {"float": 4, "double": 8, "int8": 1, "int16": 2, "int32": 4, "int64": 8, "uint8": 1,
+       "float_int": 8, "double_int": 16, "long_int": 16, "2int": 8, "short_int": 8}
+# MPI's pair types whose size equals their extent: the reference's copy_buffer
+# copies MPI_Type_size x count bytes (libbine_utils.h:176-190), so for the
+# padded ones (double_int, long_int, short_int: size 12 / 12 / 6 < extent 16 /
+# 16 / 8) its outputs are wrong or it crashes -- no vector to pin against
+PAIR_DT = ["float_int", "2int"]
 
 SMALL_N = [1, 2, 7, 8, 13, 64, 333]
 MID_N = [4096, 65537]
@@ -75,10 +81,10 @@ def run_case(P, coll, algo, op, segsize, rk, dtypes, ns, timeout=120):
             rets, outs = [], []
             for r in range(P):
                 path = os.path.join(tmp, f"{dt}.N{n}.r{r}.bin")
-                if not os.path.exists(path):
+                raw = open(path, "rb").read() if os.path.exists(path) else b""
+                if len(raw) < 16:   # missing, or cut short by a crash of the reference
                     rets = None
                     break
-                raw = open(path, "rb").read()
                 ret, outn = np.frombuffer(raw[:16], dtype=np.int64)
                 rets.append(int(ret))
                 outs.append(raw[16:16 + int(outn) * ESZ[dt]])
@@ -135,6 +141,15 @@ def ops_jobs():
                 jobs.append((P, "reduce_scatter", a, op, 0, "even_sparse", ["float", "double"], [P * 3, P * 1024],
                              True))
             jobs.append((P, "reduce", "bine_lat", op, 0, "even_sparse", ["float"], [13, 4096], True))
+        for op in ("maxloc", "minloc"):
+            # MPI's pair types; the floating values sparsified (zeros, -0.0, NaN)
+            for a in ("bine_bdw_remap", "bine_lat", "ring", "rabenseifner"):
+                jobs.append((P, "allreduce", a, op, 0, "even_sparse", PAIR_DT, [13, 1000], True))
+            for a in ("bine_permute_remap", "bine_block_by_block", "butterfly"):
+                jobs.append((P, "reduce_scatter", a, op, 0, "even_sparse", PAIR_DT, [P * 3, P * 250], True))
+            jobs.append((P, "reduce", "bine_bdw", op, 0, "even_sparse", PAIR_DT, [13, 1000], True))
+    jobs.append((8, "fill", "-", "sum", 0, "even", PAIR_DT, [64], True))
+    jobs.append((8, "fill", "-", "sum", 0, "even_sparse", PAIR_DT, [64], True))
     for P in (3, 6):
         for op in ("land", "bxor", "max"):
             rk, dts = ("even", ["int32"]) if op == "bxor" else ("even_sparse", ["float", "int8"])
@@ -144,7 +159,8 @@ def ops_jobs():
 
 
 def _is_ops_case(c):
-    return c["op"] in LOGIC_OPS + BIT_OPS or c["rcounts"].endswith("_sparse")
+    return c["op"] in LOGIC_OPS + BIT_OPS + ["maxloc", "minloc"] or c["rcounts"].endswith("_sparse") or \
+        c["dtype"] in ("float_int", "double_int", "long_int", "2int", "short_int")
 
 
 def main():
