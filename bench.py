@@ -544,10 +544,23 @@ def step_profile(torch, comm, call):
                       for o in ls[:24]]}
 
 
+def dm_wgs(mode):
+    """the direct transport's workgroups per message a mode names: "+dm" ->
+    0 (the default, 32), "+dm64" -> 64; None when the mode does not use it"""
+    i = mode.find("+dm")
+    if i < 0:
+        return None
+    digits = mode[i + 3:].split("+")[0]
+    return int(digits) if digits.isdigit() else 0
+
+
 def apply_transport(comm, mode, chunk, graphs=False, stripes=1):
     comm.set_graphs(graphs)
     comm.set_stripes(stripes)
-    comm.set_direct("+dm" in mode)
+    w = dm_wgs(mode)
+    comm.set_direct(w is not None)
+    if w is not None:
+        comm.set_direct_wgs(w)
     comm.set_relay(RELAY_MIN_BYTES if "relay" in mode else 0)
     comm.set_trees(mode.startswith("trees"))
     comm.set_flat_ag("flat" in mode)
@@ -669,6 +682,7 @@ def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, wo
 
 
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
+DM_WGS_TRIALS = (16, 64)       # direct transport: workgroups per message tried beside the default 32
 CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 MODES = {"off": ["direct"],
          # "+a2a" is not tried: RCCL runs ncclAllToAllv as the same grouped P2P kernel
@@ -868,6 +882,14 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                 trial((m_best, ch, False, 1))
         cands = [c for c in trials if c[0] == m_best and trials[c] != float("inf")]
         best = min(cands, key=trials.get) if cands else base_cfg
+        if dm_wgs(best[0]) == 0:
+            # the direct transport's workgroups per message at the chosen chunk
+            # (default 32): how many it takes to fill a link is the node's to say
+            for w in DM_WGS_TRIALS:
+                trial((best[0] + str(w), best[1], False, 1))
+            cands = [c for c in trials if c[1] == best[1] and not c[2] and trials[c] != float("inf")
+                     and (c[0] == best[0] or c[0] in [best[0] + str(w) for w in DM_WGS_TRIALS])]
+            best = min(cands, key=trials.get)
     else:
         best = (modes[0], chunks[0], False, 1)
     if graph_trial:

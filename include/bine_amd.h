@@ -36,7 +36,10 @@ typedef enum {
    * {double; int} 16 B, LONG_INT {long; int} 16 B, 2INT {int; int} 8 B,
    * SHORT_INT {short; int} 8 B (padding bytes are never written) */
   BINE_FLOAT_INT = 10, BINE_DOUBLE_INT = 11, BINE_LONG_INT = 12, BINE_2INT = 13, BINE_SHORT_INT = 14,
-  BINE_NUM_DTYPES = 15
+  /* C99 complex types {re; im} (MPI_C_FLOAT_COMPLEX, MPI_C_DOUBLE_COMPLEX),
+   * SUM / PROD only, as MPICH */
+  BINE_C_FLOAT_COMPLEX = 15, BINE_C_DOUBLE_COMPLEX = 16,
+  BINE_NUM_DTYPES = 17
 } bine_dtype_t;
 
 /* reduction operators, MPI_Reduce_local semantics of MPICH 3.3.2:
@@ -124,8 +127,9 @@ const char *bine_last_error(void);
 int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);
 size_t bine_dtype_size(int dtype);
 /* 1 if MPICH's MPI_Reduce_local accepts (dtype, op): no bitwise op on float /
- * double, MAXLOC / MINLOC exactly on the pair types; 0 otherwise (the
- * collectives then return BINE_ERR_ARG, the libbine.h shim MPI_ERR_OP) */
+ * double, MAXLOC / MINLOC exactly on the pair types, SUM / PROD only on the
+ * complex types; 0 otherwise (the collectives then return BINE_ERR_ARG, the
+ * libbine.h shim MPI_ERR_OP) */
 int bine_op_valid(int dtype, int op);
 /* -1 if unknown; `collective` = "allreduce" | "reduce_scatter" | "reduce" */
 int bine_algo_from_name(const char *collective, const char *name);
@@ -309,6 +313,10 @@ int bine_comm_set_stripes(bine_comm_t comm, int k);
  * separate push and pull launches).  At most 64 ranks.  Loopback:
  * UNSUPPORTED. */
 int bine_comm_set_direct(bine_comm_t comm, int on);
+/* Workgroups per message of the direct transport's copy launches (0: the
+ * default, BINE_DIRECT_WGS or 32).  Local, not collective; drops cached graphs
+ * (their launches carry the old grid).  bench.py trials it on the node. */
+int bine_comm_set_direct_wgs(bine_comm_t comm, int wgs);
 
 /* Graph mode (RCCL communicators): the first collective call for a given
  * (algorithm, arguments, buffers, dtype, op, stream) captures the whole issue

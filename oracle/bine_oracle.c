@@ -30,6 +30,8 @@ size_t orc_dtype_size(int dt) {
     case ORC_INT64: case ORC_UINT64: case ORC_DOUBLE: return 8;
     case ORC_FLOAT_INT: case ORC_2INT: case ORC_SHORT_INT: return 8;
     case ORC_DOUBLE_INT: case ORC_LONG_INT: return 16;
+    case ORC_C_FLOAT_COMPLEX: return 8;
+    case ORC_C_DOUBLE_COMPLEX: return 16;
     default: return 0;
   }
 }
@@ -104,9 +106,37 @@ typedef struct { short v, pad_; int i; } orc_short_int;
     }                                                                         \
   } while (0)
 
+/* MPICH 3.3.2 opsum.c / opprod.c on the C complex types: MPIR_LSUM /
+ * MPIR_LPROD on float _Complex / double _Complex, a = inout, b = in.  For
+ * finite operands gcc's complex product is (a.re b.re - a.im b.im) +
+ * (a.re b.im + a.im b.re) i, no FMA on x86-64; its Annex G NaN recovery
+ * (__mulsc3, both parts NaN) is not restated -- the vectors use finite values */
+typedef struct { float re, im; } orc_cfloat;
+typedef struct { double re, im; } orc_cdouble;
+#define RL_CPLX(T, V)                                                         \
+  do {                                                                        \
+    T *a = (T *)inout; const T *b = (const T *)in;                            \
+    switch (op) {                                                             \
+      case ORC_SUM:                                                           \
+        for (size_t i = 0; i < n; i++) { a[i].re = a[i].re + b[i].re; a[i].im = a[i].im + b[i].im; } \
+        break;                                                                \
+      case ORC_PROD:                                                          \
+        for (size_t i = 0; i < n; i++) {                                      \
+          const V re = a[i].re * b[i].re - a[i].im * b[i].im;                 \
+          const V im = a[i].re * b[i].im + a[i].im * b[i].re;                 \
+          a[i].re = re;                                                       \
+          a[i].im = im;                                                       \
+        }                                                                     \
+        break;                                                                \
+      default: return -1;                                                     \
+    }                                                                         \
+  } while (0)
+
 int orc_reduce_local(const void *in, void *inout, size_t n, int dtype, int op) {
   if (dtype < ORC_FLOAT_INT && (op == ORC_MAXLOC || op == ORC_MINLOC)) return -1;
   switch (dtype) {
+    case ORC_C_FLOAT_COMPLEX:  RL_CPLX(orc_cfloat, float); break;
+    case ORC_C_DOUBLE_COMPLEX: RL_CPLX(orc_cdouble, double); break;
     case ORC_FLOAT_INT:  RL_PAIR(orc_float_int); break;
     case ORC_DOUBLE_INT: RL_PAIR(orc_double_int); break;
     case ORC_LONG_INT:   RL_PAIR(orc_long_int); break;
@@ -152,6 +182,12 @@ int orc_fill(void *buf, int dtype, size_t n, unsigned int seed) {
     case ORC_LONG_INT:   FILL_PAIR(orc_long_int, long, 0);
     case ORC_2INT:       FILL_PAIR(orc_2int, int, 0);
     case ORC_SHORT_INT:  FILL_PAIR(orc_short_int, short, 0);
+    case ORC_C_FLOAT_COMPLEX:   /* pico_core's fp distribution, re then im */
+      for (size_t i = 0; i < 2 * n; i++) ((float *)buf)[i] = (float)rand_r(&seed) / (float)RAND_MAX * 100.0f;
+      return 0;
+    case ORC_C_DOUBLE_COMPLEX:
+      for (size_t i = 0; i < 2 * n; i++) ((double *)buf)[i] = (double)rand_r(&seed) / (double)RAND_MAX * 100.0;
+      return 0;
     default: break;
   }
   for (size_t i = 0; i < n; i++) {

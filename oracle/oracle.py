@@ -17,7 +17,8 @@ _LIB = os.path.join(_HERE, "liboracle.so")
 
 DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 5,
           "int64": 6, "uint64": 7, "float": 8, "double": 9,
-          "float_int": 10, "double_int": 11, "long_int": 12, "2int": 13, "short_int": 14}
+          "float_int": 10, "double_int": 11, "long_int": 12, "2int": 13, "short_int": 14,
+          "c_float_complex": 15, "c_double_complex": 16}
 
 
 def _pair(v: str, size: int) -> np.dtype:
@@ -31,7 +32,8 @@ NP_DTYPES = {"int8": np.int8, "uint8": np.uint8, "int16": np.int16, "uint16": np
              "int32": np.int32, "uint32": np.uint32, "int64": np.int64, "uint64": np.uint64,
              "float": np.float32, "double": np.float64,
              "float_int": _pair("<f4", 8), "double_int": _pair("<f8", 16), "long_int": _pair("<i8", 16),
-             "2int": _pair("<i4", 8), "short_int": _pair("<i2", 8)}
+             "2int": _pair("<i4", 8), "short_int": _pair("<i2", 8),
+             "c_float_complex": np.complex64, "c_double_complex": np.complex128}
 PAIRS = ("float_int", "double_int", "long_int", "2int", "short_int")
 OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9,
        "maxloc": 10, "minloc": 11}
@@ -109,6 +111,9 @@ def sparsify(x: np.ndarray, dtype: str, rank: int) -> np.ndarray:
     if dtype in ("float", "double", "float_int", "double_int"):
         v[j % 5 == 1] = -0.0
         v[j % 11 == 2] = np.nan
+    if dtype in ("c_float_complex", "c_double_complex"):
+        v.real[j % 5 == 1] = -0.0
+        v.imag[j % 7 == 3] = -0.0
     return x
 
 

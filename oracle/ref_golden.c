@@ -105,6 +105,8 @@ static int dtype_of(const char *s, MPI_Datatype *dt, size_t *sz) {
   if (!strcmp(s, "long_int"))   { *dt = MPI_LONG_INT;   *sz = sizeof(p_long_int); return 0; }
   if (!strcmp(s, "2int"))       { *dt = MPI_2INT;       *sz = sizeof(p_2int); return 0; }
   if (!strcmp(s, "short_int"))  { *dt = MPI_SHORT_INT;  *sz = sizeof(p_short_int); return 0; }
+  if (!strcmp(s, "c_float_complex"))  { *dt = MPI_C_FLOAT_COMPLEX;  *sz = 8; return 0; }
+  if (!strcmp(s, "c_double_complex")) { *dt = MPI_C_DOUBLE_COMPLEX; *sz = 16; return 0; }
   return -1;
 }
 
@@ -146,6 +148,14 @@ static void fill(void *buf, const char *dt, size_t n, unsigned int seed) {
   if (!strcmp(dt, "long_int"))   FILL_PAIR(p_long_int, long, 0);
   if (!strcmp(dt, "2int"))       FILL_PAIR(p_2int, int, 0);
   if (!strcmp(dt, "short_int"))  FILL_PAIR(p_short_int, short, 0);
+  if (!strcmp(dt, "c_float_complex")) {   /* pico_core's fp distribution, re then im */
+    for (size_t i = 0; i < 2 * n; i++) ((float *)buf)[i] = (float)rand_r(&seed) / (float)RAND_MAX * 100.0f;
+    return;
+  }
+  if (!strcmp(dt, "c_double_complex")) {
+    for (size_t i = 0; i < 2 * n; i++) ((double *)buf)[i] = (double)rand_r(&seed) / (double)RAND_MAX * 100.0;
+    return;
+  }
   for (size_t i = 0; i < n; i++) {
     if (!strcmp(dt, "int8"))        ((int8_t *)buf)[i] = (int8_t)((rand_r(&seed) % 256) - 128);
     else if (!strcmp(dt, "int16"))  ((int16_t *)buf)[i] = (int16_t)((rand_r(&seed) % 65536) - 32768);
@@ -191,6 +201,17 @@ static void sparsify(void *buf, const char *dt, size_t n, int rank) {
     } else if (!strcmp(dt, "long_int"))  { if (z) ((p_long_int *)buf)[i].v = 0; }
     else if (!strcmp(dt, "2int"))        { if (z) ((p_2int *)buf)[i].v = 0; }
     else if (!strcmp(dt, "short_int"))   { if (z) ((p_short_int *)buf)[i].v = 0; }
+    else if (!strcmp(dt, "c_float_complex")) {
+      float *f = (float *)buf + 2 * i;
+      if (z) f[0] = f[1] = 0.0f;
+      if (j % 5 == 1) f[0] = -0.0f;
+      if (j % 7 == 3) f[1] = -0.0f;
+    } else if (!strcmp(dt, "c_double_complex")) {
+      double *f = (double *)buf + 2 * i;
+      if (z) f[0] = f[1] = 0.0;
+      if (j % 5 == 1) f[0] = -0.0;
+      if (j % 7 == 3) f[1] = -0.0;
+    }
   }
 }
 

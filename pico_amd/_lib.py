@@ -17,10 +17,13 @@ SHIM = os.path.join(LIBDIR, "libbine.so")
 DTYPES = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 5,
           "int64": 6, "uint64": 7, "float": 8, "double": 9,
           # MPI's (value, index) pair types, MAXLOC / MINLOC only
-          "float_int": 10, "double_int": 11, "long_int": 12, "2int": 13, "short_int": 14}
+          "float_int": 10, "double_int": 11, "long_int": 12, "2int": 13, "short_int": 14,
+          # C99 complex, SUM / PROD only
+          "c_float_complex": 15, "c_double_complex": 16}
 DTYPE_SIZE = {"int8": 1, "uint8": 1, "int16": 2, "uint16": 2, "int32": 4, "uint32": 4,
               "int64": 8, "uint64": 8, "float": 4, "double": 8,
-              "float_int": 8, "double_int": 16, "long_int": 16, "2int": 8, "short_int": 8}
+              "float_int": 8, "double_int": 16, "long_int": 16, "2int": 8, "short_int": 8,
+              "c_float_complex": 8, "c_double_complex": 16}
 OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9,
        "maxloc": 10, "minloc": 11}
 STATUS = {0: "SUCCESS", 1: "ERR_ARG", 2: "ERR_SIZE", 3: "ERR_NO_MEM", 4: "ERR_HIP", 5: "ERR_RCCL",
@@ -142,6 +145,7 @@ def lib():
         "bine_comm_set_graphs": ([vp, i], i),
         "bine_comm_set_stripes": ([vp, i], i),
         "bine_comm_set_direct": ([vp, i], i),
+        "bine_comm_set_direct_wgs": ([vp, i], i),
         "bine_comm_set_profile": ([vp, i], i),
         "bine_comm_profile": ([vp, vp, ctypes.c_int64], ctypes.c_int64),
         "bine_exchange": ([vp, i, vp, vp, vp, i, vp, vp, vp, vp], i),

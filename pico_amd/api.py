@@ -7,7 +7,8 @@ buffers are device tensors (torch, ROCm) or raw device addresses, ``dtype`` is a
 libbine element-type name ("float", "double", "int32", ...) or a torch dtype,
 ``op`` is "sum" | "prod" | "max" | "min" | "land" | "lor" | "lxor" | "band" | "bor" | "bxor" |
 "maxloc" | "minloc" (MPICH semantics; bitwise ops on integer types only, the loc ops on
-the pair types "float_int" | "double_int" | "long_int" | "2int" | "short_int" only), and
+the pair types "float_int" | "double_int" | "long_int" | "2int" | "short_int" only; the
+complex types "c_float_complex" | "c_double_complex" under "sum" / "prod" only), and
 ``comm`` is a :class:`Comm`.
 Errors raise :class:`BineError` carrying the status the reference would return
 as an MPI error class.  The work runs in libbine_amd.so (HIP kernels + RCCL);
@@ -171,6 +172,11 @@ class Comm:
         """RCCL communicators on one node: exchanges through mapped peer memory
         (bine_comm_set_direct); bit-identical; the first enable is collective."""
         check(lib().bine_comm_set_direct(self.handle, int(on)), "bine_comm_set_direct")
+
+    def set_direct_wgs(self, wgs: int) -> None:
+        """workgroups per message of the direct transport (0 = default;
+        bine_comm_set_direct_wgs); local, drops cached graphs"""
+        check(lib().bine_comm_set_direct_wgs(self.handle, int(wgs)), "bine_comm_set_direct_wgs")
 
     def set_profile(self, on: bool) -> None:
         """Per-op device timing of the following collectives (bine_comm_set_profile)."""

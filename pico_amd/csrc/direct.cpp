@@ -167,6 +167,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (slot < (1 << 20)) slot = 1 << 20;
   slot = slot / 4096 * 4096;
   if (wgs < 1) wgs = 1;
+  env_wgs = wgs;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
   double secs = 10.0;

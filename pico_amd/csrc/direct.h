@@ -13,7 +13,8 @@ namespace bine {
 struct DirectState {
   int P = 1, rank = 0, device = 0;
   size_t slot = (size_t)16 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES)
-  int wgs = 32;                    // workgroups per message (BINE_DIRECT_WGS)
+  int wgs = 32;                    // workgroups per message (BINE_DIRECT_WGS; bine_comm_set_direct_wgs)
+  int env_wgs = 32;                // the value init() settled on (the setter's 0)
   int merge = 3;                   // launch structure (BINE_DIRECT_MERGE): 2 = pushes + pulls of a round in one
                                    // launch, 1 = round k-1's pulls with round k's pushes, 0 = separate launches,
                                    // 3 = 2 for one-round exchanges, else 1

@@ -151,6 +151,7 @@ struct RcclTransport final : Transport {
   // bine_comm_set_direct: exchanges through mapped peer memory (direct.cpp)
   std::unique_ptr<DirectState> dm;
   bool dm_on = false;
+  int dm_wgs = 0;  // workgroups per message of the direct transport (0: BINE_DIRECT_WGS / 32)
   uint64_t key = 0;  // hash of the unique id: names the direct transport's sockets
   // direct exchanges derive their sequence numbers on the device: capturable
   bool capturable() const override { return nstripe == 1; }
@@ -915,8 +916,9 @@ const char *bine_last_error(void) { return g_err.c_str(); }
 
 int bine_op_valid(int dtype, int op) {
   if (dtype < 0 || dtype >= BINE_NUM_DTYPES || op < 0 || op >= BINE_NUM_OPS) return 0;
-  const bool pair = dtype >= BINE_FLOAT_INT, loc = op == BINE_MAXLOC || op == BINE_MINLOC;
+  const bool pair = dtype >= BINE_FLOAT_INT && dtype <= BINE_SHORT_INT, loc = op == BINE_MAXLOC || op == BINE_MINLOC;
   if (pair != loc) return 0;  // pair types under MAXLOC / MINLOC only, and those ops on pairs only
+  if (dtype == BINE_C_FLOAT_COMPLEX || dtype == BINE_C_DOUBLE_COMPLEX) return op == BINE_SUM || op == BINE_PROD;
   if ((op == BINE_BAND || op == BINE_BOR || op == BINE_BXOR) && (dtype == BINE_FLOAT || dtype == BINE_DOUBLE))
     return 0;  // no bitwise ops on floating types
   return 1;
@@ -930,6 +932,8 @@ size_t bine_dtype_size(int dt) {
     case BINE_INT64: case BINE_UINT64: case BINE_DOUBLE: return 8;
     case BINE_FLOAT_INT: case BINE_2INT: case BINE_SHORT_INT: return 8;
     case BINE_DOUBLE_INT: case BINE_LONG_INT: return 16;
+    case BINE_C_FLOAT_COMPLEX: return 8;
+    case BINE_C_DOUBLE_COMPLEX: return 16;
     default: return 0;
   }
 }
@@ -1364,6 +1368,7 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
       set_err("direct transport unavailable on some rank: %s", err.empty() ? "(a peer failed)" : err.c_str());
       return BINE_ERR_UNSUPPORTED;
     }
+    if (r->dm_wgs) d->wgs = r->dm_wgs;
     r->dm = std::move(d);
   }
   if (on && r->dm->poisoned()) {
@@ -1371,6 +1376,20 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
     return BINE_ERR_INTERNAL;
   }
   r->dm_on = on != 0;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_direct_wgs(bine_comm_t c, int wgs) {
+  if (!c || wgs < 0 || wgs > 1024) return BINE_ERR_ARG;
+  auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (!r) return BINE_ERR_UNSUPPORTED;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (wgs == r->dm_wgs) return BINE_SUCCESS;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // no launch of the old shape may still run
+  c->drop_graphs();                 // captured direct launches carry the old grid
+  r->dm_wgs = wgs;
+  if (r->dm) r->dm->wgs = wgs ? wgs : r->dm->env_wgs;
   return BINE_SUCCESS;
 }
 

@@ -89,10 +89,35 @@ struct is_pair : std::false_type {};
 template <typename V>
 struct is_pair<Pair<V>> : std::true_type {};
 
+// C99 complex {re; im} (MPI_C_FLOAT_COMPLEX / MPI_C_DOUBLE_COMPLEX)
+template <typename V>
+struct Cplx {
+  V re, im;
+};
+template <typename T>
+struct is_cplx : std::false_type {};
+template <typename V>
+struct is_cplx<Cplx<V>> : std::true_type {};
+
 // MPICH's MPIR_OP_TYPE_REDUCE_CASE: a = inout, b = in, a = OP(a, b)
 template <typename T, int OP>
 __device__ __forceinline__ T apply(T io, T in) {
-  if constexpr (OP == BINE_SUM) {
+  if constexpr (is_cplx<T>::value) {
+    // MPICH's MPIR_LSUM / MPIR_LPROD on float/double _Complex: component-wise
+    // sum; for finite operands the product is (a.re b.re - a.im b.im) +
+    // (a.re b.im + a.im b.re) i (a = inout; no FMA: -ffp-contract=off)
+    if constexpr (OP == BINE_SUM) {
+      io.re = io.re + in.re;
+      io.im = io.im + in.im;
+    } else {
+      static_assert(OP == BINE_PROD, "complex types: SUM / PROD only");
+      const auto re = io.re * in.re - io.im * in.im;
+      const auto im = io.re * in.im + io.im * in.re;
+      io.re = re;
+      io.im = im;
+    }
+    return io;
+  } else if constexpr (OP == BINE_SUM) {
     if constexpr (std::is_integral_v<T>) return (T)((uint_of<T>)io + (uint_of<T>)in);
     else return io + in;
   } else if constexpr (OP == BINE_PROD) {
@@ -139,6 +164,8 @@ template <typename T>
 constexpr bool kBitsT = std::is_same_v<T, uint8_t>;
 template <typename T>
 constexpr bool kPairT = is_pair<T>::value;
+template <typename T>
+constexpr bool kCplxT = is_cplx<T>::value;
 
 // BINE_OP_SWITCH(T, CALL): `return CALL(OP)` for the op in variable `op`,
 // only for the (T, OP) pairs instantiated; hipErrorInvalidValue otherwise
@@ -155,6 +182,8 @@ constexpr bool kPairT = is_pair<T>::value;
 #else
 #define BINE_OP_SWITCH(T, CALL)                                      \
   switch (op) {                                                      \
+    case BINE_SUM: if constexpr (kCplxT<T>) return CALL(BINE_SUM); break;   \
+    case BINE_PROD: if constexpr (kCplxT<T>) return CALL(BINE_PROD); break; \
     case BINE_LAND: if constexpr (kLogicT<T>) return CALL(BINE_LAND); break; \
     case BINE_LOR: if constexpr (kLogicT<T>) return CALL(BINE_LOR); break;   \
     case BINE_LXOR: if constexpr (kLogicT<T>) return CALL(BINE_LXOR); break; \
@@ -168,7 +197,11 @@ constexpr bool kPairT = is_pair<T>::value;
   return hipErrorInvalidValue;
 #endif
 
-[[maybe_unused]] static bool logic_op(int op) { return op >= BINE_LAND && op < BINE_NUM_OPS; }
+// the (type, op) pairs the opset-1 compilation holds: the logical / bitwise /
+// loc ops, and the pair and complex types
+[[maybe_unused]] static bool ext_op(int dtype, int op) {
+  return (op >= BINE_LAND && op < BINE_NUM_OPS) || (dtype >= BINE_FLOAT_INT && dtype < BINE_NUM_DTYPES);
+}
 
 // the element type an op runs on (see kLogicT / kBitsT); *scale = elements
 // of the run type per element of `dtype`; -1: the op is not defined on the
@@ -351,7 +384,7 @@ static hipError_t reduce_op(const void *a, const void *b, void *out, size_t n, i
 int BINE_FN(launch_reduce)(const void *a, const void *b, void *out, size_t count, int dtype, int op, void *stream) {
   if (count == 0) return BINE_SUCCESS;
 #if BINE_OPSET == 0
-  if (logic_op(op)) return launch_reduce_logic(a, b, out, count, dtype, op, stream);
+  if (ext_op(dtype, op)) return launch_reduce_logic(a, b, out, count, dtype, op, stream);
 #endif
   size_t scale;
   dtype = canon_dtype(dtype, op, &scale);
@@ -377,6 +410,8 @@ int BINE_FN(launch_reduce)(const void *a, const void *b, void *out, size_t count
     case BINE_LONG_INT: e = reduce_op<Pair<long>>(a, b, out, count, op, st); break;
     case BINE_2INT: e = reduce_op<Pair<int>>(a, b, out, count, op, st); break;
     case BINE_SHORT_INT: e = reduce_op<Pair<short>>(a, b, out, count, op, st); break;
+    case BINE_C_FLOAT_COMPLEX: e = reduce_op<Cplx<float>>(a, b, out, count, op, st); break;
+    case BINE_C_DOUBLE_COMPLEX: e = reduce_op<Cplx<double>>(a, b, out, count, op, st); break;
 #endif
     default: return BINE_ERR_UNSUPPORTED;
   }
@@ -525,7 +560,7 @@ int BINE_FN(launch_reduce_batch)(int n, const void *const *a, const void *const 
                                  const size_t *count_in, int dtype, int op, void *stream) {
   if (n < 1 || n > kMaxBatch) return BINE_ERR_ARG;
 #if BINE_OPSET == 0
-  if (logic_op(op)) return launch_reduce_batch_logic(n, a, b, out, count_in, dtype, op, stream);
+  if (ext_op(dtype, op)) return launch_reduce_batch_logic(n, a, b, out, count_in, dtype, op, stream);
 #endif
   size_t scale;
   dtype = canon_dtype(dtype, op, &scale);
@@ -551,6 +586,8 @@ int BINE_FN(launch_reduce_batch)(int n, const void *const *a, const void *const 
     case BINE_LONG_INT: e = batch_op<Pair<long>>(n, a, b, out, count, op, st); break;
     case BINE_2INT: e = batch_op<Pair<int>>(n, a, b, out, count, op, st); break;
     case BINE_SHORT_INT: e = batch_op<Pair<short>>(n, a, b, out, count, op, st); break;
+    case BINE_C_FLOAT_COMPLEX: e = batch_op<Cplx<float>>(n, a, b, out, count, op, st); break;
+    case BINE_C_DOUBLE_COMPLEX: e = batch_op<Cplx<double>>(n, a, b, out, count, op, st); break;
 #endif
     default: return BINE_ERR_UNSUPPORTED;
   }
@@ -730,7 +767,7 @@ int BINE_FN(launch_reduce_tree)(int nl, const void *const *leaf, void *out, size
                                 void *stream, unsigned swap) {
   if (count == 0) return BINE_SUCCESS;
 #if BINE_OPSET == 0
-  if (logic_op(op)) return launch_reduce_tree_logic(nl, leaf, out, count, dtype, op, stream, swap);
+  if (ext_op(dtype, op)) return launch_reduce_tree_logic(nl, leaf, out, count, dtype, op, stream, swap);
 #endif
   if (nl < 2 || nl > kMaxLeaves || (nl & (nl - 1))) return BINE_ERR_ARG;
   size_t scale;
@@ -760,6 +797,8 @@ int BINE_FN(launch_reduce_tree)(int nl, const void *const *leaf, void *out, size
     case BINE_LONG_INT: e = tree_op<Pair<long>>(nl, t, op, st); break;
     case BINE_2INT: e = tree_op<Pair<int>>(nl, t, op, st); break;
     case BINE_SHORT_INT: e = tree_op<Pair<short>>(nl, t, op, st); break;
+    case BINE_C_FLOAT_COMPLEX: e = tree_op<Cplx<float>>(nl, t, op, st); break;
+    case BINE_C_DOUBLE_COMPLEX: e = tree_op<Cplx<double>>(nl, t, op, st); break;
 #endif
     default: return BINE_ERR_UNSUPPORTED;
   }

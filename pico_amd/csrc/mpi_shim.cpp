@@ -83,13 +83,17 @@ int map_dtype(MPI_Datatype d) {
   if (d == MPI_UINT16_T || d == MPI_UNSIGNED_SHORT) return BINE_UINT16;
   if (d == MPI_INT32_T || d == MPI_INT) return BINE_INT32;
   if (d == MPI_UINT32_T || d == MPI_UNSIGNED) return BINE_UINT32;
-  if (d == MPI_INT64_T || d == MPI_LONG || d == MPI_LONG_LONG) return BINE_INT64;
+  if (d == MPI_INT64_T || d == MPI_LONG || d == MPI_LONG_LONG || d == MPI_AINT || d == MPI_OFFSET || d == MPI_COUNT)
+    return BINE_INT64;
+  if (d == MPI_C_BOOL) return BINE_UINT8;  // logical ops only (map_op)
   if (d == MPI_UINT64_T || d == MPI_UNSIGNED_LONG || d == MPI_UNSIGNED_LONG_LONG) return BINE_UINT64;
   if (d == MPI_FLOAT_INT) return BINE_FLOAT_INT;
   if (d == MPI_DOUBLE_INT) return BINE_DOUBLE_INT;
   if (d == MPI_LONG_INT) return BINE_LONG_INT;
   if (d == MPI_2INT) return BINE_2INT;
   if (d == MPI_SHORT_INT) return BINE_SHORT_INT;
+  if (d == MPI_C_FLOAT_COMPLEX || d == MPI_C_COMPLEX) return BINE_C_FLOAT_COMPLEX;
+  if (d == MPI_C_DOUBLE_COMPLEX) return BINE_C_DOUBLE_COMPLEX;
   return -1;
 }
 
@@ -115,6 +119,7 @@ int map_op(MPI_Op o, MPI_Datatype d) {
   if (r < 0) return -1;
   const bool bits = r == BINE_BAND || r == BINE_BOR || r == BINE_BXOR;
   if (d == MPI_BYTE) return bits ? r : -1;
+  if (d == MPI_C_BOOL) return r == BINE_LAND || r == BINE_LOR || r == BINE_LXOR ? r : -1;
   const int dt = map_dtype(d);
   return dt < 0 || bine_op_valid(dt, r) ? r : -1;  // unknown types are reported as MPI_ERR_TYPE
 }

@@ -59,7 +59,8 @@ def test_dtype_sizes():
 def test_op_valid_matches_mpich_table():
     """bine_op_valid (host-only) against the (op, type) pairs MPICH 3.3.2's
     MPI_Reduce_local accepts (probed with it): no bitwise op on float /
-    double, MAXLOC / MINLOC exactly on the pair types"""
+    double, MAXLOC / MINLOC exactly on the pair types, SUM / PROD only on the
+    complex types"""
     import pico_amd
     from pico_amd._lib import DTYPES, OPS
     lib = pico_amd.lib()
@@ -67,5 +68,7 @@ def test_op_valid_matches_mpich_table():
         for o, ov in OPS.items():
             pair, loc = d in ("float_int", "double_int", "long_int", "2int", "short_int"), o in ("maxloc", "minloc")
             want = pair == loc and not (o in ("band", "bor", "bxor") and d in ("float", "double"))
+            if d.startswith("c_"):
+                want = o in ("sum", "prod")   # C99 complex: SUM / PROD only
             assert bool(lib.bine_op_valid(dv, ov)) == want, (d, o)
-    assert not lib.bine_op_valid(15, 0) and not lib.bine_op_valid(0, 12)
+    assert not lib.bine_op_valid(17, 0) and not lib.bine_op_valid(0, 12)

@@ -25,3 +25,9 @@ def test_pick_headline():
     assert bench.pick_headline(base, (slow, True, 1), best, (fast, False, 2))[0] == base
     assert bench.pick_headline(base, (fast, False, 1), best, (slow, None, 2))[0] == best
     assert bench.pick_headline(base, (fast, False, 1), best, (slow, False, 2))[0] == base
+
+
+def test_dm_wgs_mode_suffix():
+    assert bench.dm_wgs("flatrs+flat") is None and bench.dm_wgs("trees") is None
+    assert bench.dm_wgs("flatrs+flat+dm") == 0 and bench.dm_wgs("direct+dm") == 0
+    assert bench.dm_wgs("flatrs+flat+dm64") == 64 and bench.dm_wgs("relay+flat+dm16") == 16

@@ -269,3 +269,96 @@ def test_collectives_loc_pairs_every_algorithm(dev, P, mode):
             c.set_flat_ag(False)
             c.set_flat_rs(False)
     assert not bad, bad[:8]
+
+
+# ---- C99 complex types (SUM / PROD) -------------------------------------------------
+
+CPLX = ["c_float_complex", "c_double_complex"]
+
+
+@pytest.mark.parametrize("dtype", CPLX)
+@pytest.mark.parametrize("op", ["sum", "prod"])
+def test_reduce_local_complex(dev, dtype, op):
+    """MPICH's complex sum / product (a = inout; product re = a.re b.re -
+    a.im b.im, im = a.re b.im + a.im b.re, no FMA), zeros and -0.0 parts"""
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for n in (1, 3, 17, 1000, 100003):
+        for shift_a, shift_b in ((0, 0), (1, 1), (1, 0)):
+            a = O.sparsify(O.fill(dtype, n, 11 + n), dtype, 0)
+            b = O.sparsify(O.fill(dtype, n, 97 + n), dtype, 1)
+            ta = to_dev(np.concatenate([np.zeros(shift_a, a.dtype), a]))
+            tb = to_dev(np.concatenate([np.zeros(shift_b, b.dtype), b]))
+            pico_amd.reduce_local(ta.data_ptr() + shift_a * esz, tb.data_ptr() + shift_b * esz, n, dtype, op)
+            torch.cuda.synchronize()
+            exp = b.copy()
+            O.reduce_local(a, exp, dtype, op)
+            assert from_dev(tb, dtype, n, shift_b * esz).tobytes() == exp.tobytes(), (n, shift_a, shift_b)
+    with pytest.raises(pico_amd.BineError):
+        pico_amd.reduce_local(ta, tb.data_ptr(), 4, dtype, "max")
+
+
+@pytest.mark.parametrize("dtype", CPLX)
+def test_reduce_tree_and_batch_complex(dev, dtype):
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for op in ("sum", "prod"):
+        for nl in (2, 8, 16):
+            for n in (4099, 3):
+                host = [O.sparsify(O.fill(dtype, n, 300 + j), dtype, j) for j in range(nl)]
+                want = _host_tree(host, dtype, op)
+                leaves = [to_dev(h, pad=16) for h in host]
+                out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
+                assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
+                torch.cuda.synchronize()
+                assert sha(from_dev(out, dtype, n)) == sha(want), (op, nl, n)
+        counts = [5003, 16, 1]
+        ins = [O.fill(dtype, c, 40 + k) for k, c in enumerate(counts)]
+        ios = [O.fill(dtype, c, 50 + k) for k, c in enumerate(counts)]
+        tin, tio = [to_dev(x, pad=16) for x in ins], [to_dev(x, pad=16) for x in ios]
+        assert pico_amd.reduce_batch(tin, tio, counts, dtype, op) == 0
+        torch.cuda.synchronize()
+        for k, c in enumerate(counts):
+            exp = ios[k].copy()
+            O.reduce_local(ins[k], exp, dtype, op)
+            assert from_dev(tio[k], dtype, c).tobytes() == exp.tobytes(), (op, k)
+
+
+@pytest.mark.parametrize("mode", ["literal", "flat"])
+@pytest.mark.parametrize("P", [4, 8])
+def test_collectives_complex_every_algorithm(dev, P, mode):
+    """every reduce-family algorithm under complex SUM / PROD, literal schedule
+    and flat phases, bit-exact vs the oracle (pinned by the reference's
+    vectors on both complex types)"""
+    flat = mode == "flat"
+    for c in comms(P):
+        c.set_flat_ag(flat)
+        c.set_flat_rs(flat)
+    bad = []
+    try:
+        for op, dt in (("sum", "c_float_complex"), ("prod", "c_double_complex"), ("prod", "c_float_complex")):
+            n = 1003
+            sb = [O.sparsify(O.fill(dt, n, 1234 + r), dt, r) for r in range(P)]
+            for algo in AR_ALGOS:
+                want, rets = O.allreduce(algo, sb, dt, op)
+                outs, st = run_loopback("allreduce", algo, sb, dt, op)
+                if any(rets) or any(st):
+                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
+                        bad.append(("ar", algo, op, dt, st, rets))
+                    continue
+                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                    bad.append(("ar", algo, op, dt))
+            rc = [n // P] * P
+            sbr = [x[: sum(rc)] for x in sb]
+            for algo in RS_ALGOS:
+                want, rets = O.reduce_scatter(algo, sbr, rc, dt, op)
+                outs, st = run_loopback("reduce_scatter", algo, sbr, dt, op, rcounts=rc)
+                if any(rets) or any(st):
+                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
+                        bad.append(("rs", algo, op, dt, st, rets))
+                    continue
+                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                    bad.append(("rs", algo, op, dt))
+    finally:
+        for c in comms(P):
+            c.set_flat_ag(False)
+            c.set_flat_rs(False)
+    assert not bad, bad[:8]

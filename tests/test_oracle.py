@@ -70,7 +70,7 @@ def test_oracle_matches_reference_goldens(key, cs):
 
 def test_fill_matches_pico_core_generator():
     cs = G.select(coll="fill")
-    assert len(cs) == 18   # 7 dtypes x {plain, sparsified} inputs + 2 pair types x the same
+    assert len(cs) == 22   # 7 dtypes x {plain, sparsified} inputs + 2 pair and 2 complex types x the same
     for c in cs:
         exp = G.outputs(c)
         got = G.inputs(c)

@@ -35,7 +35,9 @@ OUT = os.path.join(ROOT, "tests", "golden")
 MPI = "/opt/conda/bin"
 SEED = 1234
 ESZ = {"float": 4, "double": 8, "int8": 1, "int16": 2, "int32": 4, "int64": 8, "uint8": 1,
-       "float_int": 8, "double_int": 16, "long_int": 16, "2int": 8, "short_int": 8}
+       "float_int": 8, "double_int": 16, "long_int": 16, "2int": 8, "short_int": 8,
+       "c_float_complex": 8, "c_double_complex": 16}
+CPLX_DT = ["c_float_complex", "c_double_complex"]
 # MPI's pair types whose size equals their extent: the reference's copy_buffer
 # copies MPI_Type_size x count bytes (libbine_utils.h:176-190), so for the
 # padded ones (double_int, long_int, short_int: size 12 / 12 / 6 < extent 16 /
@@ -148,8 +150,16 @@ def ops_jobs():
             for a in ("bine_permute_remap", "bine_block_by_block", "butterfly"):
                 jobs.append((P, "reduce_scatter", a, op, 0, "even_sparse", PAIR_DT, [P * 3, P * 250], True))
             jobs.append((P, "reduce", "bine_bdw", op, 0, "even_sparse", PAIR_DT, [13, 1000], True))
-    jobs.append((8, "fill", "-", "sum", 0, "even", PAIR_DT, [64], True))
-    jobs.append((8, "fill", "-", "sum", 0, "even_sparse", PAIR_DT, [64], True))
+        for op in ("sum", "prod"):
+            # C99 complex (SUM / PROD only); plain and sparsified (zeros, -0.0) inputs
+            for rk in ("even", "even_sparse"):
+                for a in ("bine_bdw_remap", "bine_lat", "ring"):
+                    jobs.append((P, "allreduce", a, op, 0, rk, CPLX_DT, [13, 1000], True))
+                for a in ("bine_permute_remap", "bine_block_by_block"):
+                    jobs.append((P, "reduce_scatter", a, op, 0, rk, CPLX_DT, [P * 3, P * 250], True))
+                jobs.append((P, "reduce", "bine_bdw", op, 0, rk, CPLX_DT, [13, 1000], True))
+    jobs.append((8, "fill", "-", "sum", 0, "even", PAIR_DT + CPLX_DT, [64], True))
+    jobs.append((8, "fill", "-", "sum", 0, "even_sparse", PAIR_DT + CPLX_DT, [64], True))
     for P in (3, 6):
         for op in ("land", "bxor", "max"):
             rk, dts = ("even", ["int32"]) if op == "bxor" else ("even_sparse", ["float", "int8"])
@@ -160,7 +170,7 @@ def ops_jobs():
 
 def _is_ops_case(c):
     return c["op"] in LOGIC_OPS + BIT_OPS + ["maxloc", "minloc"] or c["rcounts"].endswith("_sparse") or \
-        c["dtype"] in ("float_int", "double_int", "long_int", "2int", "short_int")
+        c["dtype"] in ("float_int", "double_int", "long_int", "2int", "short_int") + tuple(CPLX_DT)
 
 
 def main():
