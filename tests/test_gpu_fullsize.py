@@ -186,3 +186,65 @@ def test_c4_reduce_scatter_fullsize(dev, comms, mode):
         assert torch.equal(rb[r], want), r
     del sb, rb
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("algo,flat", [("bine_bdw_remap", False), ("bine_bdw_remap", True), ("ring", False)])
+def test_allreduce_beyond_int32_element_counts(dev, algo, flat):
+    """counts past 2^31 elements (the reference's reduce_scatter takes int
+    rcounts; its allreduce takes size_t counts): int8 SUM allreduce of
+    2^31 + 4099 elements per rank at P = 2 -- every 32-bit index or grid
+    computation in the planner, executor and kernels would show here.
+    Integer SUM is associative, so the wrapped element-wise sum is the exact
+    result of any schedule; it is computed on the device in int16."""
+    n = (1 << 31) + 4099
+    cs = pico_amd.Comm.loopback(2, 0)
+    try:
+        for c in cs:
+            c.set_flat_ag(flat)
+            c.set_flat_rs(flat)
+        sb = [torch.empty(n, dtype=torch.int8, device="cuda:0") for _ in range(2)]
+        for r, b in enumerate(sb):
+            pico_amd.fill_pico(b, n, "int8", 1234 + r)
+        rb = [torch.empty(n, dtype=torch.int8, device="cuda:0") for _ in range(2)]
+        torch.cuda.synchronize()
+        rc, st = pico_amd.loopback_allreduce(cs, algo, sb, rb, n, "int8")
+        assert rc == 0 and not any(st), st
+        torch.cuda.synchronize()
+        want = torch.empty(n, dtype=torch.int8, device="cuda:0")
+        step = 1 << 28
+        for s in range(0, n, step):   # (a + b) mod 2^8, in slabs to bound the int16 temporaries
+            want[s:s + step] = (sb[0][s:s + step].to(torch.int16) + sb[1][s:s + step].to(torch.int16)).to(torch.int8)
+        for r in range(2):
+            assert torch.equal(rb[r], want), r
+    finally:
+        for c in cs:
+            c.destroy()
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("algo", ["bine_permute_remap", "bine_block_by_block", "recursivehalving"])
+def test_reduce_scatter_beyond_int32_total(dev, algo):
+    """int rcounts (include/libbine.h REDUCE_SCATTER_ARGS) whose total passes
+    2^31 elements: int8 SUM at P = 2, blocks of 2^30 + 5, exact vs the
+    wrapped element-wise sum of each block"""
+    blk = (1 << 30) + 5
+    n = 2 * blk
+    cs = pico_amd.Comm.loopback(2, 0)
+    try:
+        sb = [torch.empty(n, dtype=torch.int8, device="cuda:0") for _ in range(2)]
+        for r, b in enumerate(sb):
+            pico_amd.fill_pico(b, n, "int8", 4321 + r)
+        rb = [torch.empty(blk, dtype=torch.int8, device="cuda:0") for _ in range(2)]
+        torch.cuda.synchronize()
+        rc, st = pico_amd.loopback_reduce_scatter(cs, algo, sb, rb, [blk, blk], "int8")
+        assert rc == 0 and not any(st), st
+        torch.cuda.synchronize()
+        for r in range(2):
+            lo = r * blk
+            want = (sb[0][lo:lo + blk].to(torch.int16) + sb[1][lo:lo + blk].to(torch.int16)).to(torch.int8)
+            assert torch.equal(rb[r], want), r
+            del want
+    finally:
+        for c in cs:
+            c.destroy()
+        torch.cuda.empty_cache()
