@@ -862,7 +862,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     st0 = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
     ok0, dig0 = parity("direct")
     provisional = headline(base_cfg, st0, ok0, dig0)
-    trial_budget = float(os.environ.get("BENCH_TRIAL_BUDGET_S", "300"))
+    trial_budget = float(os.environ.get("BENCH_TRIAL_BUDGET_S", "180"))
 
     def _provisional():
         if provisional is not None:
@@ -930,7 +930,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # (an RCCL or transport fault in a secondary configuration), every rank
     # stops at the same budget and rank 0 still prints the headline line with
     # what was measured so far -- a hang after the headline must not lose it
-    budget = float(os.environ.get("BENCH_SIDE_BUDGET_S", "300"))
+    budget = float(os.environ.get("BENCH_SIDE_BUDGET_S", "180"))
 
     def _partial():
         if out is not None:
