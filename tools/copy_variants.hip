@@ -65,6 +65,33 @@ __global__ __launch_bounds__(BS) void k_copy_tile(const u4 *__restrict__ a, u4 *
   }
 }
 
+// XCD-aware tile order (round 2 addition): workgroups are dispatched
+// round-robin over the 8 XCDs (blockIdx.x % 8 = XCD); MAP 1 gives each XCD one
+// contiguous eighth of the buffer, MAP 2 pairs of adjacent tiles to one XCD
+template <int BS, int U, int NTL, int NTS, int MAP>
+__global__ __launch_bounds__(BS) void k_copy_xcd(const u4 *__restrict__ a, u4 *__restrict__ o, size_t nvec,
+                                                  unsigned ntiles) {
+  const size_t tile = (size_t)BS * U;
+  const unsigned b = blockIdx.x, x = b % 8, i = b / 8, per = (ntiles + 7) / 8;
+  unsigned t = b;
+  if constexpr (MAP == 1) t = x * per + i;
+  if constexpr (MAP == 2) t = (i / 2) * 16 + x * 2 + (i % 2);
+  if (t >= ntiles) return;
+  const size_t base = (size_t)t * tile + threadIdx.x;
+  if (base + (U - 1) * (size_t)BS < nvec) {
+    u4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = ld<NTL>(a + base + (size_t)u * BS);
+#pragma unroll
+    for (int u = 0; u < U; u++) st<NTS>(v[u], o + base + (size_t)u * BS);
+  } else {
+    for (int u = 0; u < U; u++) {
+      const size_t j = base + (size_t)u * BS;
+      if (j < nvec) o[j] = a[j];
+    }
+  }
+}
+
 // grid-strided over a fixed grid (GRID workgroups), U vectors in flight
 template <int BS, int U, int NTL, int NTS>
 __global__ __launch_bounds__(BS) void k_copy_gs(const u4 *__restrict__ a, u4 *__restrict__ o, size_t nvec) {
@@ -204,6 +231,17 @@ int main(int argc, char **argv) {
     GS(512, 4, 1, 0, 4);
     GS(256, 4, 1, 1, 8);
     GS(1024, 4, 1, 0, 2);
+#define XCD(BS, U, NTL, NTS, MAP)                                                                          \
+  vars.push_back({"xcd bs" #BS " u" #U " ntl" #NTL " nts" #NTS " map" #MAP, [&, nvec](int k, hipStream_t st) {  \
+                    const unsigned tiles = (unsigned)((nvec + (size_t)BS * U - 1) / ((size_t)BS * U));      \
+                    const unsigned grid = MAP == 0 ? tiles : (tiles + 15) / 16 * 16;                       \
+                    hipLaunchKernelGGL((k_copy_xcd<BS, U, NTL, NTS, MAP>), dim3(grid), dim3(BS), 0, st, A[k], O[k], \
+                                       nvec, tiles);                                                        \
+                  }})
+    XCD(256, 8, 1, 1, 0);
+    XCD(256, 8, 1, 1, 1);
+    XCD(256, 8, 1, 1, 2);
+    XCD(256, 4, 1, 1, 1);
     vars.push_back({"hipMemcpyAsync D2D", [&](int k, hipStream_t st) {
                       (void)hipMemcpyAsync(O[k], A[k], bytes, hipMemcpyDeviceToDevice, st);
                     }});
