@@ -816,10 +816,16 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # correct one; the fastest pair is kept
     trials, verdicts = {}, {}
 
+    dm_dead = []   # the direct transport failed once (setup or a timed-out wait): not tried again
+
     def trial(cfg):
         # a setting the planner rejects fails identically on every rank before
         # any transfer (plans are a pure function of the arguments): skip it
         cfg = tuple(cfg) + (False, 1)[len(cfg) - 2:]
+        if dm_dead and dm_wgs(cfg[0]) is not None:
+            trials[cfg] = float("inf")
+            verdicts[cfg] = "error"
+            return
         try:
             # inside: enabling the direct transport fails on every rank alike
             # when peer memory cannot be mapped (BINE_ERR_UNSUPPORTED)
@@ -839,6 +845,10 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             comm.synchronize()
             trials[cfg] = float("inf")
             verdicts[cfg] = "error"
+            if dm_wgs(cfg[0]) is not None:
+                # symmetric: setup is agreed over RCCL and a poisoned transport
+                # reports on every rank, so every rank stops trying together
+                dm_dead.append(tname(cfg))
 
     mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
     S = nelem * 4
