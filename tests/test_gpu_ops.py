@@ -41,6 +41,75 @@ def _valid(dtype, op):
     return not (op in BITS and dtype in ("float", "double"))
 
 
+def _every_algorithm(P, mode, cases, make):
+    """every allreduce and reduce_scatter algorithm on loopback ranks for each
+    (op, dtype) in `cases`, literal schedule or flat phases, bit-exact vs the
+    oracle (statuses compared where the reference errs); make(dt, n, seed, r)
+    builds rank r's input.  Returns the mismatches."""
+    flat = mode == "flat"
+    for c in comms(P):
+        c.set_flat_ag(flat)
+        c.set_flat_rs(flat)
+    bad = []
+    try:
+        for op, dt in cases:
+            n = 1003
+            sb = [make(dt, n, 1234 + r, r) for r in range(P)]
+            rc = [n // P + (1 if i == 0 else 0) for i in range(P)]
+            sbr = [make(dt, sum(rc), 77 + r, r) for r in range(P)]
+            for coll, algos in (("allreduce", AR_ALGOS), ("reduce_scatter", RS_ALGOS)):
+                for algo in algos:
+                    if coll == "allreduce":
+                        want, rets = O.allreduce(algo, sb, dt, op)
+                        outs, st = run_loopback(coll, algo, sb, dt, op)
+                    else:
+                        # permute_remap needs equal blocks (DESIGN.md deviations)
+                        r_ = rc if algo != "bine_permute_remap" else [n // P] * P
+                        s_ = [x[: sum(r_)] for x in sbr]
+                        want, rets = O.reduce_scatter(algo, s_, r_, dt, op)
+                        outs, st = run_loopback(coll, algo, s_, dt, op, rcounts=r_)
+                    if any(rets) or any(st):
+                        if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
+                            bad.append((coll, algo, op, dt, st, rets))
+                    elif any(sha(o) != sha(w) for o, w in zip(outs, want)):
+                        bad.append((coll, algo, op, dt))
+    finally:
+        for c in comms(P):
+            c.set_flat_ag(False)
+            c.set_flat_rs(False)
+    return bad
+
+
+def _tree_and_batch(dtype, ops, make):
+    """bine_reduce_tree (2 / 8 / 16 leaves, vector body and a 3-element
+    scalar case) and bine_reduce_batch (three windows) vs the oracle"""
+    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
+    for op in ops:
+        for nl in (2, 8, 16):
+            for n in (4099, 3):
+                host = [make(dtype, n, 300 + j, j) for j in range(nl)]
+                want = _host_tree(host, dtype, op)
+                leaves = [to_dev(h, pad=16) for h in host]
+                out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
+                assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
+                torch.cuda.synchronize()
+                assert sha(from_dev(out, dtype, n)) == sha(want), (op, nl, n)
+        counts = [5003, 16, 1]
+        ins = [make(dtype, c, 40 + k, 0) for k, c in enumerate(counts)]
+        ios = [make(dtype, c, 50 + k, 2) for k, c in enumerate(counts)]
+        tin, tio = [to_dev(x, pad=16) for x in ins], [to_dev(x, pad=16) for x in ios]
+        assert pico_amd.reduce_batch(tin, tio, counts, dtype, op) == 0
+        torch.cuda.synchronize()
+        for k, c in enumerate(counts):
+            exp = ios[k].copy()
+            O.reduce_local(ins[k], exp, dtype, op)
+            assert sha(from_dev(tio[k], dtype, c)) == sha(exp), (op, k)
+
+
+def _sparse_pico(dt, n, seed, r):
+    return O.sparsify(O.fill(dt, n, seed), dt, r)
+
+
 @pytest.fixture(scope="module")
 def dev():
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
@@ -74,31 +143,12 @@ def test_reduce_local_logic_bits(dev, dtype, op):
 def test_reduce_tree_and_batch_logic_bits(dev, dtype):
     """the flat reduce-scatter's fused tree kernel and the multi-tree batch
     kernel under the new ops (bitwise ops run byte-wise on integer types)"""
-    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
-    for op in LOGIC + BITS:
-        if not _valid(dtype, op):
-            out = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    if dtype in ("float", "double"):
+        out = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+        for op in BITS:
             assert pico_amd.reduce_tree([out, out], out, 4, dtype, op) != 0
-            continue
-        for nl in (2, 8, 16):
-            for n in (4099, 3):
-                host = [sparse(dtype, n, 300 + j, rank=j) for j in range(nl)]
-                want = _host_tree(host, dtype, op)
-                leaves = [to_dev(h, pad=16) for h in host]
-                out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
-                assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
-                torch.cuda.synchronize()
-                assert sha(from_dev(out, dtype, n)) == sha(want), (op, nl, n)
-        counts = [5003, 16, 1]
-        ins = [sparse(dtype, c, 40 + k) for k, c in enumerate(counts)]
-        ios = [sparse(dtype, c, 50 + k, rank=2) for k, c in enumerate(counts)]
-        tin, tio = [to_dev(x, pad=16) for x in ins], [to_dev(x, pad=16) for x in ios]
-        assert pico_amd.reduce_batch(tin, tio, counts, dtype, op) == 0
-        torch.cuda.synchronize()
-        for k, c in enumerate(counts):
-            exp = ios[k].copy()
-            O.reduce_local(ins[k], exp, dtype, op)
-            assert from_dev(tio[k], dtype, c).tobytes() == exp.tobytes(), (op, k)
+    _tree_and_batch(dtype, [op for op in LOGIC + BITS if _valid(dtype, op)],
+                    lambda dt, n, seed, r: sparse(dt, n, seed, rank=r))
 
 
 AR_ALGOS = ["bine_bdw_remap", "bine_bdw_static", "bine_bdw_remap_segmented", "bine_lat",
@@ -110,46 +160,13 @@ RS_ALGOS = ["bine_permute_remap", "bine_send_remap", "bine_static", "bine_block_
 @pytest.mark.parametrize("mode", ["literal", "flat"])
 @pytest.mark.parametrize("P", [4, 8])
 def test_collectives_logic_bits_every_algorithm(dev, P, mode):
-    """every reduce-family algorithm under LAND / LXOR (int8, float, sparse
-    inputs) and BOR / BXOR (int16, int64), literal schedule and with the flat
-    phases (fused tree kernel) -- bit-exact vs the oracle"""
-    flat = mode == "flat"
-    for c in comms(P):
-        c.set_flat_ag(flat)
-        c.set_flat_rs(flat)
-    bad = []
-    try:
-        for op, dts in (("land", ("int8", "float")), ("lxor", ("double", "uint8")), ("bor", ("int16",)),
-                        ("bxor", ("int64", "int8"))):
-            for dt in dts:
-                n = 1003
-                sb = [sparse(dt, n, 1234 + r, rank=r) for r in range(P)]
-                for algo in AR_ALGOS:
-                    want, rets = O.allreduce(algo, sb, dt, op)
-                    outs, st = run_loopback("allreduce", algo, sb, dt, op)
-                    if any(rets) or any(st):
-                        if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
-                            bad.append(("ar", algo, op, dt, st, rets))
-                        continue
-                    if any(sha(o) != sha(w) for o, w in zip(outs, want)):
-                        bad.append(("ar", algo, op, dt))
-                rc = [n // P + (1 if i == 0 else 0) for i in range(P)]
-                sbr = [sparse(dt, sum(rc), 77 + r, rank=r) for r in range(P)]
-                for algo in RS_ALGOS:
-                    r_ = rc if algo != "bine_permute_remap" else [n // P] * P
-                    s_ = sbr if algo != "bine_permute_remap" else [x[: sum(r_)] for x in sbr]
-                    want, rets = O.reduce_scatter(algo, s_, r_, dt, op)
-                    outs, st = run_loopback("reduce_scatter", algo, s_, dt, op, rcounts=r_)
-                    if any(rets) or any(st):
-                        if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
-                            bad.append(("rs", algo, op, dt, st, rets))
-                        continue
-                    if any(sha(o) != sha(w) for o, w in zip(outs, want)):
-                        bad.append(("rs", algo, op, dt))
-    finally:
-        for c in comms(P):
-            c.set_flat_ag(False)
-            c.set_flat_rs(False)
+    """every reduce-family algorithm under LAND / LXOR (int8, float, double,
+    uint8, sparse inputs) and BOR / BXOR (int16, int64, int8), literal
+    schedule and with the flat phases (fused tree kernel) -- bit-exact vs the
+    oracle"""
+    cases = [("land", "int8"), ("land", "float"), ("lxor", "double"), ("lxor", "uint8"), ("bor", "int16"),
+             ("bxor", "int64"), ("bxor", "int8")]
+    bad = _every_algorithm(P, mode, cases, lambda dt, n, seed, r: sparse(dt, n, seed, rank=r))
     assert not bad, bad[:8]
 
 
@@ -203,27 +220,7 @@ def test_loc_ops_refuse_other_types(dev):
 
 @pytest.mark.parametrize("dtype", PAIRS)
 def test_reduce_tree_and_batch_loc_pairs(dev, dtype):
-    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
-    for op in ("maxloc", "minloc"):
-        for nl in (2, 8, 16):
-            for n in (4099, 3):
-                host = [O.sparsify(O.fill(dtype, n, 300 + j), dtype, j) for j in range(nl)]
-                want = _host_tree(host, dtype, op)
-                leaves = [to_dev(h, pad=16) for h in host]
-                out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
-                assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
-                torch.cuda.synchronize()
-                assert sha(from_dev(out, dtype, n)) == sha(want), (op, nl, n)
-        counts = [5003, 16, 1]
-        ins = [O.fill(dtype, c, 40 + k) for k, c in enumerate(counts)]
-        ios = [O.fill(dtype, c, 50 + k) for k, c in enumerate(counts)]
-        tin, tio = [to_dev(x, pad=16) for x in ins], [to_dev(x, pad=16) for x in ios]
-        assert pico_amd.reduce_batch(tin, tio, counts, dtype, op) == 0
-        torch.cuda.synchronize()
-        for k, c in enumerate(counts):
-            exp = ios[k].copy()
-            O.reduce_local(ins[k], exp, dtype, op)
-            assert sha(from_dev(tio[k], dtype, c)) == sha(exp), (op, k)
+    _tree_and_batch(dtype, ("maxloc", "minloc"), _sparse_pico)
 
 
 @pytest.mark.parametrize("mode", ["literal", "flat"])
@@ -234,40 +231,9 @@ def test_collectives_loc_pairs_every_algorithm(dev, P, mode):
     oracle is pinned by the reference's vectors for the unpadded pair types;
     for the padded ones the reference's copy_buffer copies MPI_Type_size x
     count bytes, libbine_utils.h:176-190, and its outputs are wrong)"""
-    flat = mode == "flat"
-    for c in comms(P):
-        c.set_flat_ag(flat)
-        c.set_flat_rs(flat)
-    bad = []
-    try:
-        for op, dt in (("maxloc", "float_int"), ("minloc", "double_int"), ("maxloc", "short_int"),
-                       ("minloc", "2int"), ("maxloc", "long_int")):
-            n = 1003
-            sb = [O.sparsify(O.fill(dt, n, 1234 + r), dt, r) for r in range(P)]
-            for algo in AR_ALGOS:
-                want, rets = O.allreduce(algo, sb, dt, op)
-                outs, st = run_loopback("allreduce", algo, sb, dt, op)
-                if any(rets) or any(st):
-                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
-                        bad.append(("ar", algo, op, dt, st, rets))
-                    continue
-                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
-                    bad.append(("ar", algo, op, dt))
-            rc = [n // P] * P
-            sbr = [x[: sum(rc)] for x in sb]
-            for algo in RS_ALGOS:
-                want, rets = O.reduce_scatter(algo, sbr, rc, dt, op)
-                outs, st = run_loopback("reduce_scatter", algo, sbr, dt, op, rcounts=rc)
-                if any(rets) or any(st):
-                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
-                        bad.append(("rs", algo, op, dt, st, rets))
-                    continue
-                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
-                    bad.append(("rs", algo, op, dt))
-    finally:
-        for c in comms(P):
-            c.set_flat_ag(False)
-            c.set_flat_rs(False)
+    cases = [("maxloc", "float_int"), ("minloc", "double_int"), ("maxloc", "short_int"), ("minloc", "2int"),
+             ("maxloc", "long_int")]
+    bad = _every_algorithm(P, mode, cases, _sparse_pico)
     assert not bad, bad[:8]
 
 
@@ -299,27 +265,7 @@ def test_reduce_local_complex(dev, dtype, op):
 
 @pytest.mark.parametrize("dtype", CPLX)
 def test_reduce_tree_and_batch_complex(dev, dtype):
-    esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
-    for op in ("sum", "prod"):
-        for nl in (2, 8, 16):
-            for n in (4099, 3):
-                host = [O.sparsify(O.fill(dtype, n, 300 + j), dtype, j) for j in range(nl)]
-                want = _host_tree(host, dtype, op)
-                leaves = [to_dev(h, pad=16) for h in host]
-                out = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0")
-                assert pico_amd.reduce_tree(leaves, out, n, dtype, op) == 0
-                torch.cuda.synchronize()
-                assert sha(from_dev(out, dtype, n)) == sha(want), (op, nl, n)
-        counts = [5003, 16, 1]
-        ins = [O.fill(dtype, c, 40 + k) for k, c in enumerate(counts)]
-        ios = [O.fill(dtype, c, 50 + k) for k, c in enumerate(counts)]
-        tin, tio = [to_dev(x, pad=16) for x in ins], [to_dev(x, pad=16) for x in ios]
-        assert pico_amd.reduce_batch(tin, tio, counts, dtype, op) == 0
-        torch.cuda.synchronize()
-        for k, c in enumerate(counts):
-            exp = ios[k].copy()
-            O.reduce_local(ins[k], exp, dtype, op)
-            assert from_dev(tio[k], dtype, c).tobytes() == exp.tobytes(), (op, k)
+    _tree_and_batch(dtype, ("sum", "prod"), _sparse_pico)
 
 
 @pytest.mark.parametrize("mode", ["literal", "flat"])
@@ -328,37 +274,6 @@ def test_collectives_complex_every_algorithm(dev, P, mode):
     """every reduce-family algorithm under complex SUM / PROD, literal schedule
     and flat phases, bit-exact vs the oracle (pinned by the reference's
     vectors on both complex types)"""
-    flat = mode == "flat"
-    for c in comms(P):
-        c.set_flat_ag(flat)
-        c.set_flat_rs(flat)
-    bad = []
-    try:
-        for op, dt in (("sum", "c_float_complex"), ("prod", "c_double_complex"), ("prod", "c_float_complex")):
-            n = 1003
-            sb = [O.sparsify(O.fill(dt, n, 1234 + r), dt, r) for r in range(P)]
-            for algo in AR_ALGOS:
-                want, rets = O.allreduce(algo, sb, dt, op)
-                outs, st = run_loopback("allreduce", algo, sb, dt, op)
-                if any(rets) or any(st):
-                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
-                        bad.append(("ar", algo, op, dt, st, rets))
-                    continue
-                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
-                    bad.append(("ar", algo, op, dt))
-            rc = [n // P] * P
-            sbr = [x[: sum(rc)] for x in sb]
-            for algo in RS_ALGOS:
-                want, rets = O.reduce_scatter(algo, sbr, rc, dt, op)
-                outs, st = run_loopback("reduce_scatter", algo, sbr, dt, op, rcounts=rc)
-                if any(rets) or any(st):
-                    if [int(x != 0) for x in st] != [int(x != 0) for x in rets]:
-                        bad.append(("rs", algo, op, dt, st, rets))
-                    continue
-                if any(sha(o) != sha(w) for o, w in zip(outs, want)):
-                    bad.append(("rs", algo, op, dt))
-    finally:
-        for c in comms(P):
-            c.set_flat_ag(False)
-            c.set_flat_rs(False)
+    cases = [("sum", "c_float_complex"), ("prod", "c_double_complex"), ("prod", "c_float_complex")]
+    bad = _every_algorithm(P, mode, cases, _sparse_pico)
     assert not bad, bad[:8]
