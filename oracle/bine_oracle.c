@@ -1202,6 +1202,13 @@ static int nb_partner(int r, int mask, int P) {
 /* reduce_scatter_bine_send_remap (:906-983) and _permute_remap (:985-1063) */
 static void rs_bine_remap(ctx_t *c, const int *rc, char **S, char **R, int *rets, int permute) {
   int P = c->P; size_t esz = c->esz;
+  if (!is_pow2(P)) {
+    /* the reference has no power-of-two check here and hangs or crashes at
+     * P = 3, 5, 6, 7 (no vector); reported as MPI_ERR_ARG,
+     * the status the device path returns (deviations) */
+    for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG;
+    return;
+  }
   if (permute)
     for (int i = 1; i < P; i++)
       if (rc[i] != rc[0]) {

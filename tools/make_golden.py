@@ -168,6 +168,27 @@ def ops_jobs():
     return jobs
 
 
+def odd_p_jobs():
+    """P = 5 and 7 (prime, odd: neither power of two nor even) for every
+    algorithm the reference runs at any P, both reduce-family collectives and
+    the allgather family's any-P algorithms"""
+    jobs = []
+    for P in (5, 7):
+        for a in ("ring", "rabenseifner", "recursivedoubling", "bine_lat", "bine_bdw_remap_segmented",
+                  "bine_bdw_remap", "bine_bdw_static"):   # the last two: MPI_ERR_ARG
+            seg = 64 if a == "bine_bdw_remap_segmented" else 0
+            jobs.append((P, "allreduce", a, "sum", seg, "even", FEW_DT, [1, 7, 13, 333, 4096], True))
+        for a in ("recursive_distance_doubling", "ring", "bine_send_remap", "bine_static", "butterfly"):
+            jobs.append((P, "reduce_scatter", a, "sum", 0, "even", FEW_DT, [P, P * 5, P * 1000], True))
+        for a in ("bine_lat", "bine_bdw"):
+            jobs.append((P, "reduce", a, "sum", 0, "even", ["float"], [13], True))
+    return jobs
+
+
+def _is_odd_p_case(c):
+    return c["P"] in (5, 7) and c["coll"] != "allgather"
+
+
 def _is_ops_case(c):
     return c["op"] in LOGIC_OPS + BIT_OPS + ["maxloc", "minloc"] or c["rcounts"].endswith("_sparse") or \
         c["dtype"] in ("float_int", "double_int", "long_int", "2int", "short_int") + tuple(CPLX_DT)
@@ -182,6 +203,11 @@ def main():
         # regenerate one collective's cases, keep everything else as it is
         old = json.load(open(os.path.join(OUT, "index.json")))["cases"]
         prev = dict(np.load(os.path.join(OUT, "outputs.npz")))
+        if only == "oddp":
+            index = [c for c in old if not _is_odd_p_case(c)]
+            keep = {c["id"] for c in index}
+            arrays = {k: v for k, v in prev.items() if k in keep}
+            return capture(odd_p_jobs(), index, arrays)
         if only == "ops":
             index = [c for c in old if not _is_ops_case(c)]
             keep = {c["id"] for c in index}
@@ -229,6 +255,7 @@ def main():
     jobs.append((8, "allreduce", "bine_bdw_remap", "sum", 0, "even", ["double", "int64"], [262147], False))
     jobs += allgather_jobs()
     jobs += ops_jobs()
+    jobs += odd_p_jobs()
     capture(jobs, [], {})
 
 
