@@ -185,6 +185,20 @@ def odd_p_jobs():
     return jobs
 
 
+def p16_jobs():
+    """P = 16 (four Bine steps) for the reduce family's main algorithms"""
+    jobs = []
+    for a in ("bine_bdw_remap", "bine_bdw_static", "bine_lat", "bine_bdw_remap_segmented", "ring", "rabenseifner",
+              "recursivedoubling", "bine_block_by_block_any_even"):
+        seg = 64 if a == "bine_bdw_remap_segmented" else 0
+        jobs.append((16, "allreduce", a, "sum", seg, "even", FEW_DT, [13, 4096, 65537], True))
+    for a in RS_BINE + RS_CLASSIC:
+        jobs.append((16, "reduce_scatter", a, "sum", 0, "even", FEW_DT, [16, 16 * 300], True))
+    for a in ("bine_lat", "bine_bdw"):
+        jobs.append((16, "reduce", a, "sum", 0, "even", FEW_DT, [13, 4096], True))
+    return jobs
+
+
 def _is_odd_p_case(c):
     return c["P"] in (5, 7) and c["coll"] != "allgather"
 
@@ -203,6 +217,11 @@ def main():
         # regenerate one collective's cases, keep everything else as it is
         old = json.load(open(os.path.join(OUT, "index.json")))["cases"]
         prev = dict(np.load(os.path.join(OUT, "outputs.npz")))
+        if only == "p16":
+            index = [c for c in old if not (c["P"] == 16 and c["coll"] != "allgather")]
+            keep = {c["id"] for c in index}
+            arrays = {k: v for k, v in prev.items() if k in keep}
+            return capture(p16_jobs(), index, arrays)
         if only == "oddp":
             index = [c for c in old if not _is_odd_p_case(c)]
             keep = {c["id"] for c in index}
@@ -256,6 +275,7 @@ def main():
     jobs += allgather_jobs()
     jobs += ops_jobs()
     jobs += odd_p_jobs()
+    jobs += p16_jobs()
     capture(jobs, [], {})
 
 
