@@ -20,6 +20,9 @@
  *                pico_core_utils.c:511-514), rbuf = P * N zeroed elements
  *   rcounts_kind even   -> rcounts[i] = N / P  (pico_core_utils.c:535-536)
  *                ragged -> rcounts[i] = N / P + (i % 3)   (exercises displs)
+ *                an "_inplace" suffix calls with MPI_IN_PLACE: the input is
+ *                copied into rbuf first (reduce: at the root; reduce_scatter:
+ *                the whole input, the result read from the start of rbuf)
  *                a "_sparse" suffix (e.g. even_sparse) post-processes the
  *                inputs so that the logical ops and MAX / MIN see zeros, -0.0
  *                and NaN (sparsify() below; tests/golden_util.py repeats it)
@@ -239,6 +242,7 @@ int main(int argc, char **argv) {
   int nn = split_csv(argv[9], ns, 32);
   MPI_Op op;
   if (op_of(ops, &op)) MPI_Abort(MPI_COMM_WORLD, 3);
+  const int inplace = strstr(rk, "_inplace") != NULL;
   bine_allreduce_segsize = segsize;
 
   for (int d = 0; d < ndt; d++) {
@@ -268,11 +272,13 @@ int main(int argc, char **argv) {
       } else if (!strcmp(coll, "allreduce")) {
         ar_fn f = pick_allreduce(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
-        ret = f(sbuf, rbuf, N, dt, op, MPI_COMM_WORLD);
+        if (inplace) memcpy(rbuf, sbuf, total * esz);
+        ret = f(inplace ? MPI_IN_PLACE : sbuf, rbuf, N, dt, op, MPI_COMM_WORLD);
       } else if (!strcmp(coll, "reduce_scatter")) {
         rs_fn f = pick_reduce_scatter(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
-        ret = f(sbuf, rbuf, rcounts, dt, op, MPI_COMM_WORLD);
+        if (inplace) memcpy(rbuf, sbuf, total * esz);
+        ret = f(inplace ? MPI_IN_PLACE : sbuf, rbuf, rcounts, dt, op, MPI_COMM_WORLD);
       } else if (!strcmp(coll, "allgather")) {
         ag_fn f = pick_allgather(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
@@ -281,7 +287,8 @@ int main(int argc, char **argv) {
         rd_fn f = pick_reduce(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
         /* pico_core passes rbuf = NULL on non-roots (pico_core_reduce_utils.c:24-31) */
-        ret = f(sbuf, rank == 0 ? rbuf : NULL, N, dt, op, 0, MPI_COMM_WORLD);
+        if (inplace && rank == 0) memcpy(rbuf, sbuf, total * esz);
+        ret = f(inplace && rank == 0 ? MPI_IN_PLACE : sbuf, rank == 0 ? rbuf : NULL, N, dt, op, 0, MPI_COMM_WORLD);
         if (rank != 0) outn = 0;
       } else {
         MPI_Abort(MPI_COMM_WORLD, 6);

@@ -199,6 +199,22 @@ def p16_jobs():
     return jobs
 
 
+def inplace_jobs():
+    """MPI_IN_PLACE through every reduce-family algorithm (the reference's own
+    in-place code paths, e.g. libbine_allreduce.c:849-852,
+    libbine_reduce_scatter.c:810-813)"""
+    jobs = []
+    for P in (1, 2, 4, 8):
+        for a in AR_BINE + AR_CLASSIC + ["bine_bdw_remap_segmented"]:
+            seg = 64 if a == "bine_bdw_remap_segmented" else 0
+            jobs.append((P, "allreduce", a, "sum", seg, "even_inplace", FEW_DT, [13, 4096], True))
+        for a in RS_BINE + RS_CLASSIC:
+            jobs.append((P, "reduce_scatter", a, "sum", 0, "even_inplace", FEW_DT, [P * 3, P * 1024], True))
+        for a in ("bine_lat", "bine_bdw"):
+            jobs.append((P, "reduce", a, "sum", 0, "even_inplace", FEW_DT, [13, 4096], True))
+    return jobs
+
+
 def _is_odd_p_case(c):
     return c["P"] in (5, 7) and c["coll"] != "allgather"
 
@@ -217,6 +233,11 @@ def main():
         # regenerate one collective's cases, keep everything else as it is
         old = json.load(open(os.path.join(OUT, "index.json")))["cases"]
         prev = dict(np.load(os.path.join(OUT, "outputs.npz")))
+        if only == "inplace":
+            index = [c for c in old if not c["rcounts"].endswith("_inplace")]
+            keep = {c["id"] for c in index}
+            arrays = {k: v for k, v in prev.items() if k in keep}
+            return capture(inplace_jobs(), index, arrays)
         if only == "p16":
             index = [c for c in old if not (c["P"] == 16 and c["coll"] != "allgather")]
             keep = {c["id"] for c in index}
@@ -276,6 +297,7 @@ def main():
     jobs += ops_jobs()
     jobs += odd_p_jobs()
     jobs += p16_jobs()
+    jobs += inplace_jobs()
     capture(jobs, [], {})
 
 
