@@ -1265,6 +1265,12 @@ static void rs_bine_remap(ctx_t *c, const int *rc, char **S, char **R, int *rets
 /* reduce_scatter_bine_block_by_block, :1066-1174 */
 static void rs_bine_bbb(ctx_t *c, const int *rc, char **S, char **R, int *rets) {
   int P = c->P; size_t esz = c->esz;
+  if (!is_pow2(P)) {
+    /* no power-of-two check in the reference: it hangs at P = 3 (measured)
+     * and indexes past its blocks; MPI_ERR_ARG, as the device path */
+    for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG;
+    return;
+  }
   int *displs = (int *)malloc(sizeof(int) * (size_t)P), *invr = (int *)malloc(sizeof(int) * (size_t)P), count = 0;
   for (int i = 0; i < P; i++) { displs[i] = count; count += rc[i]; invr[orc_remap_rank((uint32_t)P, (uint32_t)i)] = i; }
   char **tmp = alloc_ranks(P, (size_t)count * esz), **res = alloc_ranks(P, (size_t)count * esz);

@@ -1,0 +1,105 @@
+"""Randomized parity sweep of the device path (fixed seeds, so every run checks
+the same cases): collective x algorithm x P x count x element type x operator x
+transport setting (relay, flat allgather / reduce-scatter phases, pipelining
+chunk) x in place, on loopback ranks, bit-exact against the oracle (the CPU
+restatement pinned by the reference's vectors, tests/test_oracle.py).  Where
+the oracle reports an error (the reference's MPI_ERR_ARG / MPI_ERR_SIZE, or a
+reference assert / hang) the device path must return an error too.  The oracle itself
+reports MPI_ERR_ARG where the reference hangs or overruns (the remap and
+block-by-block reduce-scatters at non-power-of-two P), as the device path does."""
+import random
+
+import numpy as np
+import pytest
+
+import pico_amd  # noqa: E402  (after torch, via test_gpu)
+from oracle import oracle as O
+from test_gpu import comms, run_loopback, sha
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+PLAIN = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64", "float", "double"]
+OPS_OF = {
+    **{d: ["sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"] for d in PLAIN},
+    "float": ["sum", "prod", "max", "min", "land", "lor", "lxor"],
+    "double": ["sum", "prod", "max", "min", "land", "lor", "lxor"],
+    "float_int": ["maxloc", "minloc"], "double_int": ["maxloc", "minloc"], "2int": ["maxloc", "minloc"],
+    "c_float_complex": ["sum", "prod"], "c_double_complex": ["sum", "prod"],
+}
+COLLS = {"allreduce": list(pico_amd.ALGOS["allreduce"]), "reduce_scatter": list(pico_amd.ALGOS["reduce_scatter"]),
+         "reduce": list(pico_amd.ALGOS["reduce"])}
+
+
+def _case(rng):
+    coll = rng.choice(["allreduce"] * 3 + ["reduce_scatter"] * 2 + ["reduce"])
+    algo = rng.choice(COLLS[coll])
+    P = rng.choice([1, 2, 3, 4, 4, 5, 6, 8, 8, 16])
+    dt = rng.choice(list(OPS_OF))
+    op = rng.choice(OPS_OF[dt])
+    n = rng.choice([1, 2, 7, 64, 333, 1000, 4097, rng.randint(1, 30000)])
+    opts = {"relay": rng.choice([0, 0, 64, 4096]), "flat_ag": rng.random() < 0.4, "flat_rs": rng.random() < 0.4,
+            "chunk": rng.choice([0, 0, 256, 4096, 65536]), "in_place": rng.random() < 0.25,
+            "sparse": rng.random() < 0.5, "ragged": rng.random() < 0.5}
+    return coll, algo, P, dt, op, n, opts
+
+
+def _run(coll, algo, P, dt, op, n, o):
+    mk = (lambda r: O.sparsify(O.fill(dt, m, 99 + r), dt, r)) if o["sparse"] else (lambda r: O.fill(dt, m, 99 + r))
+    rk = None
+    if coll == "reduce_scatter":
+        rk = [n // P + ((i % 3) if o["ragged"] and algo != "bine_permute_remap" else 0) for i in range(P)]
+        m = sum(rk)
+    else:
+        m = n
+    sb = [mk(r) for r in range(P)]
+    if coll == "allreduce":
+        want, rets = O.allreduce(algo, sb, dt, op, 64 if algo == "bine_bdw_remap_segmented" else 0)
+    elif coll == "reduce_scatter":
+        want, rets = O.reduce_scatter(algo, sb, rk, dt, op)
+        if P == 1 and algo in ("butterfly", "bine_block_by_block"):
+            want = [sb[0][: rk[0]]]   # the P = 1 copy the reference omits (DESIGN.md deviations)
+    else:
+        w, rets = O.reduce(algo, sb, dt, op)
+        want = [w]
+    for c in comms(P):
+        c.set_flat_ag(o["flat_ag"])
+        c.set_flat_rs(o["flat_rs"])
+        c.set_chunk(o["chunk"])
+    outs, st = run_loopback(coll, algo, sb, dt, op, rk, 64 if algo == "bine_bdw_remap_segmented" else 0,
+                            in_place=o["in_place"], relay=o["relay"])
+    return want, rets, outs, st
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_configurations_bit_exact(dev_fuzz, seed):
+    rng = random.Random(1000 + seed)
+    bad = []
+    try:
+        for _ in range(60):
+            coll, algo, P, dt, op, n, o = _case(rng)
+            want, rets, outs, st = _run(coll, algo, P, dt, op, n, o)
+            if any(rets):
+                if not all(st):
+                    bad.append((coll, algo, P, dt, op, n, o, "expected an error", rets, st))
+                continue
+            if any(st):
+                bad.append((coll, algo, P, dt, op, n, o, "status", st))
+            elif any(sha(x) != sha(w) for x, w in zip(outs, want)):
+                bad.append((coll, algo, P, dt, op, n, o, "data"))
+    finally:
+        for P in (1, 2, 3, 4, 5, 6, 8, 16):
+            for c in comms(P):
+                c.set_relay(0)
+                c.set_flat_ag(False)
+                c.set_flat_rs(False)
+                c.set_chunk(0)
+    assert not bad, bad[:6]
+
+
+@pytest.fixture(scope="module")
+def dev_fuzz():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    np.seterr(all="ignore")
+    return torch.device("cuda:0")
