@@ -72,7 +72,7 @@ def _run(coll, algo, P, dt, op, n, o):
     return want, rets, outs, st
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(20))
 def test_random_configurations_bit_exact(dev_fuzz, seed):
     rng = random.Random(1000 + seed)
     bad = []
