@@ -1305,6 +1305,12 @@ static void rs_bine_bbb(ctx_t *c, const int *rc, char **S, char **R, int *rets) 
 /* reduce_scatter_bine_block_by_block_any_even, :1176-1298 */
 static void rs_bine_bbb_any_even(ctx_t *c, const int *rc, char **S, char **R, int *rets) {
   int P = c->P; size_t esz = c->esz;
+  if (P % 2 && P > 1) {
+    /* odd P: the reference hangs (no vector) and its
+     * partners leave the communicator; MPI_ERR_ARG, as the device path */
+    for (int r = 0; r < P; r++) rets[r] = ORC_ERR_ARG;
+    return;
+  }
   int *displs = (int *)malloc(sizeof(int) * (size_t)P), count = 0;
   for (int i = 0; i < P; i++) { displs[i] = count; count += rc[i]; }
   char **tmp = alloc_ranks(P, (size_t)count * esz), **res = alloc_ranks(P, (size_t)count * esz);

@@ -813,15 +813,19 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
 
 // chunk_bytes == kCommChunk: the communicator's setting (bine_comm_set_chunk)
 constexpr size_t kCommChunk = ~(size_t)0;
+// op of the data-movement collectives (allgather family): no reduction runs
+constexpr int kOpNone = -1;
 
 static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbuf, int dtype, int op,
                           size_t chunk_bytes, void *stream) {
   if (!c) return BINE_ERR_ARG;
   if (dtype < 0 || dtype >= BINE_NUM_DTYPES) return BINE_ERR_UNSUPPORTED;
-  if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
-  // (op, type) pairs MPICH's MPI_Reduce_local rejects (MPI_ERR_OP): refused
-  // before any exchange, identically on every rank
-  if (!bine_op_valid(dtype, op)) return BINE_ERR_ARG;
+  if (op != kOpNone) {
+    if (op < 0 || op >= BINE_NUM_OPS) return BINE_ERR_UNSUPPORTED;
+    // (op, type) pairs MPICH's MPI_Reduce_local rejects (MPI_ERR_OP): refused
+    // before any exchange, identically on every rank
+    if (!bine_op_valid(dtype, op)) return BINE_ERR_ARG;
+  }
   std::lock_guard<std::mutex> g(c->mu);
   if (chunk_bytes == kCommChunk) chunk_bytes = c->chunk_bytes ? c->chunk_bytes : default_chunk_bytes();
   HIP_TRY(hipSetDevice(c->device));
@@ -1173,7 +1177,8 @@ int bine_allgather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t
   PlanArgs a;
   a.algo = algo;
   a.count = count;
-  return run_collective(c, a, sbuf, rbuf, dtype, BINE_SUM, kCommChunk, stream);
+  // pure data movement: no operator applies (kOpNone skips the (type, op) check)
+  return run_collective(c, a, sbuf, rbuf, dtype, kOpNone, kCommChunk, stream);
 }
 
 int bine_exchange(bine_comm_t c, int nsend, const int *send_peers, const void *const *sbufs, const size_t *sbytes,

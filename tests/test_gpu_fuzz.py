@@ -29,11 +29,11 @@ OPS_OF = {
     "c_float_complex": ["sum", "prod"], "c_double_complex": ["sum", "prod"],
 }
 COLLS = {"allreduce": list(pico_amd.ALGOS["allreduce"]), "reduce_scatter": list(pico_amd.ALGOS["reduce_scatter"]),
-         "reduce": list(pico_amd.ALGOS["reduce"])}
+         "reduce": list(pico_amd.ALGOS["reduce"]), "allgather": list(pico_amd.ALGOS["allgather"])}
 
 
 def _case(rng):
-    coll = rng.choice(["allreduce"] * 3 + ["reduce_scatter"] * 2 + ["reduce"])
+    coll = rng.choice(["allreduce"] * 3 + ["reduce_scatter"] * 2 + ["reduce", "allgather"])
     algo = rng.choice(COLLS[coll])
     P = rng.choice([1, 2, 3, 4, 4, 5, 6, 8, 8, 16])
     dt = rng.choice(list(OPS_OF))
@@ -54,6 +54,16 @@ def _run(coll, algo, P, dt, op, n, o):
     else:
         m = n
     sb = [mk(r) for r in range(P)]
+    if coll == "allgather":   # pure data movement: any type, no operator, out of place
+        want, rets = O.allgather(algo, sb, dt)
+        if algo == "recursivedoubling" and P & (P - 1):
+            rets = [1] * P   # the reference gathers nothing and reports success; here MPI_ERR_ARG
+        if algo == "bine_block_by_block_any_even" and P % 2:
+            rets = [1] * P   # odd P (1 included) hangs / crashes in the reference (no vector); MPI_ERR_ARG here
+        for c in comms(P):
+            c.set_flat_ag(o["flat_ag"])
+        outs, st = run_loopback(coll, algo, sb, dt, relay=o["relay"])
+        return want, rets, outs, st
     if coll == "allreduce":
         want, rets = O.allreduce(algo, sb, dt, op, 64 if algo == "bine_bdw_remap_segmented" else 0)
     elif coll == "reduce_scatter":
