@@ -1,7 +1,7 @@
 """Randomized parity sweep of the device path (fixed seeds, so every run checks
 the same cases): collective x algorithm x P x count x element type x operator x
 transport setting (relay, flat allgather / reduce-scatter phases, pipelining
-chunk) x in place, on loopback ranks, bit-exact against the oracle (the CPU
+chunk, multi-tree mode on integer types) x in place, on loopback ranks, bit-exact against the oracle (the CPU
 restatement pinned by the reference's vectors, tests/test_oracle.py).  Where
 the oracle reports an error (the reference's MPI_ERR_ARG / MPI_ERR_SIZE, or a
 reference assert / hang) the device path must return an error too.  The oracle itself
@@ -20,7 +20,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-PLAIN = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64", "float", "double"]
+INTS = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64"]
+PLAIN = INTS + ["float", "double"]
 OPS_OF = {
     **{d: ["sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"] for d in PLAIN},
     "float": ["sum", "prod", "max", "min", "land", "lor", "lxor"],
@@ -41,7 +42,7 @@ def _case(rng):
     n = rng.choice([1, 2, 7, 64, 333, 1000, 4097, rng.randint(1, 30000)])
     opts = {"relay": rng.choice([0, 0, 64, 4096]), "flat_ag": rng.random() < 0.4, "flat_rs": rng.random() < 0.4,
             "chunk": rng.choice([0, 0, 256, 4096, 65536]), "in_place": rng.random() < 0.25,
-            "sparse": rng.random() < 0.5, "ragged": rng.random() < 0.5}
+            "sparse": rng.random() < 0.5, "ragged": rng.random() < 0.5, "trees": rng.random() < 0.25}
     return coll, algo, P, dt, op, n, opts
 
 
@@ -73,10 +74,15 @@ def _run(coll, algo, P, dt, op, n, o):
     else:
         w, rets = O.reduce(algo, sb, dt, op)
         want = [w]
+    # multi-tree mode (P = 4, 8) relabels ranks: bit-exact vs the reference's
+    # schedule only where the operator is associative and commutative in the
+    # element type -- the integer types
+    trees = o["trees"] and dt in INTS and P in (4, 8)
     for c in comms(P):
         c.set_flat_ag(o["flat_ag"])
         c.set_flat_rs(o["flat_rs"])
         c.set_chunk(o["chunk"])
+        c.set_trees(trees)
     outs, st = run_loopback(coll, algo, sb, dt, op, rk, 64 if algo == "bine_bdw_remap_segmented" else 0,
                             in_place=o["in_place"], relay=o["relay"])
     return want, rets, outs, st
@@ -105,6 +111,7 @@ def test_random_configurations_bit_exact(dev_fuzz, seed):
                 c.set_flat_ag(False)
                 c.set_flat_rs(False)
                 c.set_chunk(0)
+                c.set_trees(False)
     assert not bad, bad[:6]
 
 
