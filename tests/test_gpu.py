@@ -666,6 +666,25 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat)
     assert "Last Iter Time" in p.stdout
 
 
+OP_CHECK = os.path.join(ROOT, "integration", "_build", "op_check")
+
+
+@pytest.mark.skipif(not os.path.exists(OP_CHECK), reason="integration/op_check not built (integration/Makefile)")
+@pytest.mark.parametrize("np_,flat", [(1, False), (2, False), (2, True)])
+def test_mpi_typed_entry_points_match_mpich(dev, np_, flat):
+    """integration/op_check: libbine.so's MPI-typed entry points (allreduce,
+    reduce_scatter, reduce; host buffers) equal MPICH's own PMPI_* collectives
+    for every order-independent (type, op) pair, and return MPI_ERR_OP where
+    MPICH rejects the pair; 2 ranks share the GPU as above"""
+    import subprocess
+    env = dict(os.environ, BINE_FAKE_HOSTS="1")
+    if flat:
+        env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
+    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_)], env=env,
+                       capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0 and "OPCHECK ok" in p.stdout, (p.stdout[-1500:], p.stderr[-1500:])
+
+
 @pytest.mark.parametrize("relay", [0, 64, "flat"], ids=["direct", "relay", "flat"])
 @pytest.mark.parametrize("P", [2, 4, 6, 8])
 def test_allgather_family_matches_oracle(dev, P, relay):
