@@ -68,7 +68,8 @@ typedef enum {
   BINE_ERR_HIP = 4,          /* a HIP runtime call failed */
   BINE_ERR_RCCL = 5,         /* an RCCL call failed */
   BINE_ERR_UNSUPPORTED = 6,  /* algorithm / dtype / op not provided */
-  BINE_ERR_INTERNAL = 7
+  BINE_ERR_INTERNAL = 7,
+  BINE_ERR_ROOT = 8          /* reference returns MPI_ERR_ROOT (bcast_bine_lat: root != 0) */
 } bine_status_t;
 
 /* Algorithms.  Names are the libbine function names without the collective
@@ -110,7 +111,17 @@ typedef enum {
   BINE_AG_BINE_PERMUTE_REMAP = 56,    /* :725  */
   BINE_AG_BINE_SEND_REMAP = 57,       /* :811  */
   BINE_AG_BINE_2_BLOCKS = 58,         /* :892  */
-  BINE_AG_BINE_2_BLOCKS_DTYPE = 59    /* :999  */
+  BINE_AG_BINE_2_BLOCKS_DTYPE = 59,   /* :999  */
+  /* bcast, libbine_bcast.c (widening past section 8):
+   * the latency trees; the scatter-allgather and bandwidth variants are not
+   * provided yet (BINE_ERR_UNSUPPORTED) */
+  BINE_BC_SCATTER_ALLGATHER = 64,     /* :42   (not provided) */
+  BINE_BC_BINE_LAT = 65,              /* :189  */
+  BINE_BC_BINE_LAT_REVERSED = 66,     /* :281  */
+  BINE_BC_BINE_LAT_NEW = 67,          /* :373  */
+  BINE_BC_BINE_LAT_I_NEW = 68,        /* :408  */
+  BINE_BC_BINE_BDW_STATIC = 69,       /* :462  (not provided) */
+  BINE_BC_BINE_BDW_REMAP = 70         /* :649  (not provided) */
 } bine_algo_t;
 
 /* the reference's MPI_IN_PLACE (mpi.h: (void *)-1) */
@@ -372,6 +383,11 @@ int bine_reduce(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t
  * any_even variants have no in-place path (BINE_ERR_ARG). */
 int bine_allgather(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count,
                    int dtype, void *stream);
+/* bcast_* (libbine.h:54-60): `buf` (count elements) of `root` reaches every
+ * rank, whole-buffer transfers along the algorithm's tree.  Power-of-two P
+ * only (BINE_ERR_SIZE otherwise); bine_lat / bine_lat_reversed take root 0
+ * only (BINE_ERR_ROOT), as the reference. */
+int bine_bcast(bine_comm_t comm, int algo, void *buf, size_t count, int dtype, int root, void *stream);
 
 /* One group of point-to-point transfers on the communicator's transport (RCCL:
  * ncclSend / ncclRecv inside one ncclGroupStart/End) -- the MPI_Sendrecv /
@@ -407,6 +423,8 @@ int bine_loopback_run_reduce(bine_comm_t *comms, int nranks, int algo,
 int bine_loopback_run_allgather(bine_comm_t *comms, int nranks, int algo,
                                 const void *const *sbufs, void *const *rbufs, size_t count,
                                 int dtype, int *statuses);
+int bine_loopback_run_bcast(bine_comm_t *comms, int nranks, int algo, void *const *bufs,
+                            size_t count, int dtype, int root, int *statuses);
 
 /* ---- schedule introspection (host only, no GPU needed) ----------------------
  * A plan is the ordered list of primitives one rank executes. */

@@ -14,7 +14,8 @@
  * staged by the shim, compared byte for byte (pair types: field by field;
  * floats: by value)
  * with PMPI_Allreduce / PMPI_Reduce_scatter / PMPI_Reduce.  And the pairs
- * MPICH rejects come back as MPI_ERR_OP.
+ * MPICH rejects come back as MPI_ERR_OP.  Then the bcast latency trees
+ * (bine_lat, _reversed at root 0; _new, _i_new at every root) vs PMPI_Bcast.
  *   usage: mpiexec -n P op_check      (prints "OPCHECK ok <cases>" on rank 0)
  * P a power of two: the remap / block-by-block reduce-scatters report
  * MPI_ERR_ARG elsewhere (the reference hangs there; DESIGN.md deviations).
@@ -147,6 +148,32 @@ int main(int argc, char **argv) {
       }
     }
   }
+  /* bcast latency trees vs PMPI_Bcast (any type: pure data movement); the
+   * root-0-only variants at root 0, the _new ones at every root */
+  typedef int (*bc_fn)(void *, size_t, MPI_Datatype, int, MPI_Comm);
+  const struct { const char *name; bc_fn f; int any_root; } bcs[] = {
+      {"bine_lat", bcast_bine_lat, 0}, {"bine_lat_reversed", bcast_bine_lat_reversed, 0},
+      {"bine_lat_new", bcast_bine_lat_new, 1}, {"bine_lat_i_new", bcast_bine_lat_i_new, 1}};
+  for (size_t bi = 0; bi < sizeof bcs / sizeof *bcs; bi++)
+    for (size_t ti = 0; ti < sizeof types / sizeof *types; ti++)
+      for (size_t ci = 0; ci < sizeof counts / sizeof *counts; ci++)
+        for (int root = 0; root < (bcs[bi].any_root ? P : 1); root++) {
+          const type_t *t = &types[ti];
+          const size_t n = counts[ci];
+          char *r = malloc(n * t->esz), *w = malloc(n * t->esz);
+          fill(r, t, n, 99u + 13u * (unsigned)rank + (unsigned)(bi * 7 + ti * 3 + ci));
+          memcpy(w, r, n * t->esz);
+          int e = bcs[bi].f(r, n, t->dt, root, MPI_COMM_WORLD);
+          int ew = PMPI_Bcast(w, (int)n, t->dt, root, MPI_COMM_WORLD);
+          cases++;
+          if (e != MPI_SUCCESS || ew != MPI_SUCCESS || !same(r, w, t, n)) {
+            bad++;
+            if (bad <= 40)
+              fprintf(stderr, "rank %d MISMATCH bcast_%s %s n=%zu root=%d rc=%d (mpich rc %d)\n", rank,
+                      bcs[bi].name, t->name, n, root, e, ew);
+          }
+          free(r); free(w);
+        }
   int tot = 0;
   MPI_Allreduce(&bad, &tot, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
   if (rank == 0) printf(tot ? "OPCHECK FAILED %d of %d\n" : "OPCHECK ok %d cases\n", tot ? tot : cases, cases);

@@ -194,6 +194,58 @@ def allgather(algo, sbufs, dtype, in_place_rbufs=None):
     return rbufs, rets.tolist()
 
 
+ERR_ROOT = 7   # MPICH's MPI_ERR_ROOT
+
+
+def bcast(algo, sbufs, dtype, root=0):
+    """bcast latency trees, in place (each rank's buffer = its input); returns
+    (buffers after the broadcast, rets).  Message-level replay of the
+    reference: every step's transfers are applied in order, a rank forwards
+    only what it holds.
+      bine_lat / _reversed  libbine_bcast.c:189-279 / :281-371 (root 0 only)
+      bine_lat_new / _i_new :373-406 / :408-452 (negabinary partners, any root)
+    P = 1 with the _new variants: the reference shifts by -1 (:384, :421) and
+    crashes; here the broadcast of one rank is a no-op."""
+    P = len(sbufs)
+    bufs = [np.array(b, dtype=NP_DTYPES[dtype]).copy() for b in sbufs]
+    steps = P.bit_length() - 1
+    if P & (P - 1):
+        return bufs, [ERR_SIZE] * P
+    if algo in ("bine_lat", "bine_lat_reversed"):
+        if root != 0:
+            return bufs, [ERR_ROOT] * P
+        have = {0}
+        for s in range(steps):
+            ss = steps - s - 1 if algo == "bine_lat_reversed" else s
+            moves = [(x, pi(x, ss, P)) for x in sorted(have) if pi(x, ss, P) not in have]
+            for src, dst in moves:
+                bufs[dst][:] = bufs[src]
+            have |= {d for _, d in moves}
+        have = [r in have for r in range(P)]
+    elif algo in ("bine_lat_new", "bine_lat_i_new"):
+        M = 0xAAAAAAAA
+        have = [r == root for r in range(P)]
+        mask = 1 << (steps - 1) if steps else 0
+        while mask > 0:
+            lo = (mask << 1) - 1
+            moves = []
+            for r in range(P):
+                nb = (((r - root) % P) + M) & 0xFFFFFFFF ^ M
+                partner = (((((nb ^ lo) ^ M) - M) & 0xFFFFFFFF) + root) % P
+                lsbs = nb & lo
+                if not have[r] and (lsbs == 0 or lsbs == lo):
+                    moves.append((partner, r))
+            for src, dst in moves:
+                assert have[src], (algo, P, root, src, dst)
+                bufs[dst][:] = bufs[src]
+                have[dst] = True
+            mask >>= 1
+    else:
+        raise ValueError(algo)
+    assert all(have), (algo, P, root)
+    return bufs, [OK] * P
+
+
 def _mix64(x):
     x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
     x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)

@@ -15,7 +15,8 @@
  *
  * usage: ref_golden <outdir> <coll> <algo> <op> <segsize> <rcounts_kind>
  *                   <seed_base> <dtype,dtype,...> <N,N,...>
- *   coll         allreduce | reduce_scatter | reduce | allgather | fill (dump the inputs)
+ *   coll         allreduce | reduce_scatter | reduce | allgather | bcast | fill (dump the inputs)
+ *                bcast: in place on each rank's input; rcounts "root<k>" = root k
  *                allgather: N = elements per rank (scount = rcount, same type,
  *                pico_core_utils.c:511-514), rbuf = P * N zeroed elements
  *   rcounts_kind even   -> rcounts[i] = N / P  (pico_core_utils.c:535-536)
@@ -40,6 +41,7 @@ typedef int (*ar_fn)(const void *, void *, size_t, MPI_Datatype, MPI_Op, MPI_Com
 typedef int (*rs_fn)(const void *, void *, const int *, MPI_Datatype, MPI_Op, MPI_Comm);
 typedef int (*rd_fn)(const void *, void *, size_t, MPI_Datatype, MPI_Op, int, MPI_Comm);
 typedef int (*ag_fn)(const void *, size_t, MPI_Datatype, void *, size_t, MPI_Datatype, MPI_Comm);
+typedef int (*bc_fn)(void *, size_t, MPI_Datatype, int, MPI_Comm);
 
 static ar_fn pick_allreduce(const char *a) {
   if (!strcmp(a, "recursivedoubling")) return allreduce_recursivedoubling;
@@ -69,6 +71,14 @@ static rs_fn pick_reduce_scatter(const char *a) {
 static rd_fn pick_reduce(const char *a) {
   if (!strcmp(a, "bine_lat")) return reduce_bine_lat;
   if (!strcmp(a, "bine_bdw")) return reduce_bine_bdw;
+  return NULL;
+}
+
+static bc_fn pick_bcast(const char *a) {
+  if (!strcmp(a, "bine_lat")) return bcast_bine_lat;
+  if (!strcmp(a, "bine_lat_reversed")) return bcast_bine_lat_reversed;
+  if (!strcmp(a, "bine_lat_new")) return bcast_bine_lat_new;
+  if (!strcmp(a, "bine_lat_i_new")) return bcast_bine_lat_i_new;
   return NULL;
 }
 
@@ -283,6 +293,13 @@ int main(int argc, char **argv) {
         ag_fn f = pick_allgather(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
         ret = f(sbuf, N, dt, rbuf, N, dt, MPI_COMM_WORLD);
+      } else if (!strcmp(coll, "bcast")) {
+        /* in place on every rank's own input; root from "root<k>" (else 0) */
+        bc_fn f = pick_bcast(algo);
+        if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
+        const int root = !strncmp(rk, "root", 4) ? atoi(rk + 4) : 0;
+        memcpy(rbuf, sbuf, total * esz);
+        ret = f(rbuf, N, dt, root, MPI_COMM_WORLD);
       } else if (!strcmp(coll, "reduce")) {
         rd_fn f = pick_reduce(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);

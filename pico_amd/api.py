@@ -413,6 +413,20 @@ def loopback_allgather(comms, algo, sbufs, rbufs, count, dtype):
     return rc, list(st)
 
 
+def bcast(algo, buf, count: int, dtype, root: int, comm: Comm, stream=None) -> None:
+    """root's `count` elements of buf reach every rank (in place)."""
+    check(lib().bine_bcast(comm.handle, _algo("bcast", algo), _ptr(buf), count, _dtype(dtype, buf), root,
+                           _stream(stream, comm)), f"bcast_{algo}")
+
+
+def loopback_bcast(comms, algo, bufs, count, dtype, root):
+    st = (ctypes.c_int * len(comms))()
+    hs = (ctypes.c_void_p * len(comms))(*[c.handle.value for c in comms])
+    rc = lib().bine_loopback_run_bcast(hs, len(comms), _algo("bcast", algo), _ptrs(bufs), count,
+                                       _dtype(dtype, bufs[0]), root, st)
+    return rc, list(st)
+
+
 # ---- libbine-named entry points (include/libbine.h:30-78) --------------------------
 
 def _mk_ar(name):
@@ -447,6 +461,14 @@ def _mk_ag(name):
     return f
 
 
+def _mk_bc(name):
+    def f(buf, count, dtype, root, comm, stream=None):
+        bcast(name, buf, count, dtype, root, comm, stream=stream)
+    f.__name__ = "bcast_" + name
+    f.__doc__ = f"bcast_{name} (libbine_bcast.c) on MI355X."
+    return f
+
+
 ENTRY_POINTS = {}
 for _n in ALGOS["allreduce"]:
     ENTRY_POINTS["allreduce_" + _n] = _mk_ar(_n)
@@ -456,10 +478,12 @@ for _n in ALGOS["reduce"]:
     ENTRY_POINTS["reduce_" + _n] = _mk_rd(_n)
 for _n in ALGOS["allgather"]:
     ENTRY_POINTS["allgather_" + _n] = _mk_ag(_n)
+for _n in ALGOS["bcast"]:
+    ENTRY_POINTS["bcast_" + _n] = _mk_bc(_n)
 globals().update(ENTRY_POINTS)
 
 __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum", "copy",
            "rccl_version",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
-           "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "reduce_batch",
+           "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "bcast", "loopback_bcast", "reduce_batch",
            "exchange", "vendor_allreduce", "reduce_tree"] + list(ENTRY_POINTS)

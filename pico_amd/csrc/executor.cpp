@@ -912,6 +912,7 @@ const char *bine_status_string(int s) {
     case BINE_ERR_HIP: return "HIP runtime error";
     case BINE_ERR_RCCL: return "RCCL error";
     case BINE_ERR_UNSUPPORTED: return "unsupported algorithm, datatype or operator";
+    case BINE_ERR_ROOT: return "unsupported root (reference: MPI_ERR_ROOT)";
     default: return "internal error";
   }
 }
@@ -976,6 +977,14 @@ static const struct { int algo; const char *coll, *name, *selector; } kAlgos[] =
     {BINE_AG_BINE_SEND_REMAP, "allgather", "bine_send_remap", "bine_send_remap_over"},
     {BINE_AG_BINE_2_BLOCKS, "allgather", "bine_2_blocks", "bine_2_blocks_over"},
     {BINE_AG_BINE_2_BLOCKS_DTYPE, "allgather", "bine_2_blocks_dtype", "bine_2_blocks_dtype_over"},
+    // pico_core_utils.c:166-174
+    {BINE_BC_SCATTER_ALLGATHER, "bcast", "scatter_allgather", "scatter_allgather_over"},
+    {BINE_BC_BINE_LAT, "bcast", "bine_lat", "bine_lat_over"},
+    {BINE_BC_BINE_LAT_REVERSED, "bcast", "bine_lat_reversed", "bine_lat_reversed_over"},
+    {BINE_BC_BINE_LAT_NEW, "bcast", "bine_lat_new", "bine_lat_new_over"},
+    {BINE_BC_BINE_LAT_I_NEW, "bcast", "bine_lat_i_new", "bine_lat_i_new_over"},
+    {BINE_BC_BINE_BDW_STATIC, "bcast", "bine_bdw_static", "bine_bdw_static_over"},
+    {BINE_BC_BINE_BDW_REMAP, "bcast", "bine_bdw_remap", "bine_bdw_remap_over"},
 };
 
 int bine_algo_from_name(const char *coll, const char *name) {
@@ -1181,6 +1190,17 @@ int bine_allgather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t
   return run_collective(c, a, sbuf, rbuf, dtype, kOpNone, kCommChunk, stream);
 }
 
+int bine_bcast(bine_comm_t c, int algo, void *buf, size_t count, int dtype, int root, void *stream) {
+  if (algo < BINE_BC_SCATTER_ALLGATHER || algo > BINE_BC_BINE_BDW_REMAP) return BINE_ERR_UNSUPPORTED;
+  if (!c || root < 0 || root >= c->size) return BINE_ERR_ARG;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  a.root = root;
+  // in place on `buf`; pure data movement (no operator)
+  return run_collective(c, a, BINE_IN_PLACE, buf, dtype, kOpNone, kCommChunk, stream);
+}
+
 int bine_exchange(bine_comm_t c, int nsend, const int *send_peers, const void *const *sbufs, const size_t *sbytes,
                   int nrecv, const int *recv_peers, void *const *rbufs, const size_t *rbytes, void *stream) {
   if (!c || nsend < 0 || nrecv < 0) return BINE_ERR_ARG;
@@ -1253,6 +1273,14 @@ int bine_loopback_run_allgather(bine_comm_t *comms, int n, int algo, const void 
   return run_threads(comms, n, statuses, [&](int r) {
     (void)hipSetDevice(comms[r]->device);
     return bine_allgather(comms[r], algo, sbufs[r], rbufs[r], count, dtype, comms[r]->stream);  // one stream per virtual rank
+  });
+}
+
+int bine_loopback_run_bcast(bine_comm_t *comms, int n, int algo, void *const *bufs, size_t count, int dtype,
+                            int root, int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_bcast(comms[r], algo, bufs[r], count, dtype, root, comms[r]->stream);  // one stream per virtual rank
   });
 }
 

@@ -68,6 +68,7 @@ int to_mpi(int st) {
     case BINE_ERR_SIZE: return MPI_ERR_SIZE;
     case BINE_ERR_NO_MEM: return MPI_ERR_NO_MEM;
     case BINE_ERR_UNSUPPORTED: return MPI_ERR_UNSUPPORTED_OPERATION;
+    case BINE_ERR_ROOT: return MPI_ERR_ROOT;
     default:
       fprintf(stderr, "libbine(amd): %s: %s\n", bine_status_string(st), bine_last_error());
       return MPI_ERR_OTHER;
@@ -287,11 +288,26 @@ int do_allgather(int algo, const void *sbuf, size_t scount, MPI_Datatype sdtype,
   });
 }
 
+// bcast family: pure data movement on `buf` in place (read on the root,
+// written elsewhere), run on bytes whatever the type
+int do_bcast(int algo, void *buf, size_t count, MPI_Datatype dtype, int root, MPI_Comm comm) {
+  int sz = 0;
+  if (MPI_Type_size(dtype, &sz) != MPI_SUCCESS || sz <= 0) return MPI_ERR_TYPE;
+  const size_t bytes = count * (size_t)sz;
+  if (bytes == 0) return MPI_SUCCESS;
+  Entry *e;
+  int rc = get_entry(comm, &e);
+  if (rc) return rc;
+  return with_buffers(e, MPI_IN_PLACE, 0, buf, bytes, true, [&](const void *, void *r, void *st) {
+    return bine_bcast(e->comm, algo, r, bytes, BINE_UINT8, root, st);
+  });
+}
+
 int unsupported(const char *name) {
   static std::once_flag once;
   std::call_once(once, [&] {
     fprintf(stderr, "libbine(amd): %s is outside the reduce family this library provides "
-                    "(allreduce / reduce_scatter / reduce / allgather); returning "
+                    "(allreduce / reduce_scatter / reduce / allgather / the bcast latency trees); returning "
                     "MPI_ERR_UNSUPPORTED_OPERATION\n", name);
   });
   return MPI_ERR_UNSUPPORTED_OPERATION;
@@ -349,10 +365,13 @@ AG(allgather_bine_2_blocks_dtype, BINE_AG_BINE_2_BLOCKS_DTYPE)
 
 NA(alltoall_bine, BINE_ALLGATHER_ARGS)
 NA(bcast_scatter_allgather, BINE_BCAST_ARGS)
-NA(bcast_bine_lat, BINE_BCAST_ARGS)
-NA(bcast_bine_lat_reversed, BINE_BCAST_ARGS)
-NA(bcast_bine_lat_new, BINE_BCAST_ARGS)
-NA(bcast_bine_lat_i_new, BINE_BCAST_ARGS)
+#define BC(fn, id) \
+  int fn(BINE_BCAST_ARGS) { return do_bcast(id, buf, count, dtype, root, comm); }
+BC(bcast_bine_lat, BINE_BC_BINE_LAT)
+BC(bcast_bine_lat_reversed, BINE_BC_BINE_LAT_REVERSED)
+BC(bcast_bine_lat_new, BINE_BC_BINE_LAT_NEW)
+BC(bcast_bine_lat_i_new, BINE_BC_BINE_LAT_I_NEW)
+#undef BC
 NA(bcast_bine_bdw_static, BINE_BCAST_ARGS)
 NA(bcast_bine_bdw_remap, BINE_BCAST_ARGS)
 NA(gather_bine, BINE_GATHER_ARGS)

@@ -1565,6 +1565,56 @@ void ag_bine_2_blocks(Builder &b, const PlanArgs &a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// bcast, libbine_bcast.c: the latency trees.  Whole-buffer messages in RB
+// (in place); a rank receives once and then sends at every later step.
+// ---------------------------------------------------------------------------
+
+// bcast_bine_lat (:189-279) and _reversed (:281-371): root 0, power-of-two P;
+// the step at which each rank receives is found by replaying the tree from
+// the root (:221-234), step s of the reversed variant uses pi(., steps-1-s)
+void bc_bine_lat(Builder &b, const PlanArgs &a, bool reversed) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (!is_pow2(P)) { b.fail(BINE_ERR_SIZE); return; }
+  if (a.root != 0) { b.fail(BINE_ERR_ROOT); return; }
+  auto peer = [&](int x, int s) { return pi(x, reversed ? steps - s - 1 : s, P); };
+  std::vector<char> got((size_t)P);
+  got[0] = 1;
+  int recv_step = -1;
+  for (int s = 0; s < steps && !got[(size_t)r]; s++)
+    for (int x = 0; x < P; x++) {
+      if (!got[(size_t)x]) continue;
+      const int d = peer(x, s);
+      got[(size_t)d] = 1;
+      if (d == r) { recv_step = s; break; }
+    }
+  for (int s = 0; s < steps; s++) {
+    if (r != 0 && recv_step == s) b.recv(peer(r, s), RB, 0, a.count);
+    else if (recv_step < s) b.send(peer(r, s), RB, 0, a.count);
+    b.end();
+  }
+}
+
+// bcast_bine_lat_new (:373-406) and _i_new (:408-452, the same messages with
+// non-blocking sends): any root, power-of-two P; negabinary partner per step
+void bc_bine_lat_new(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (!is_pow2(P)) { b.fail(BINE_ERR_SIZE); return; }
+  if (a.root < 0 || a.root >= P) { b.fail(BINE_ERR_ROOT); return; }
+  const uint32_t nbm = 0xAAAAAAAAu;
+  const int vrank = pmod(r - a.root, P);
+  const uint32_t nb = ((uint32_t)vrank + nbm) ^ nbm;  // binary_to_negabinary, libbine_utils.h:509
+  bool have = r == a.root;
+  for (int mask = steps ? 1 << (steps - 1) : 0; mask > 0; mask >>= 1) {
+    const uint32_t lo = ((uint32_t)mask << 1) - 1;
+    const int partner = pmod((int32_t)(((nb ^ lo) ^ nbm) - nbm) + a.root, P);  // negabinary_to_binary
+    const uint32_t lsbs = nb & lo;
+    if (have) b.send(partner, RB, 0, a.count);
+    else if (lsbs == 0 || lsbs == lo) { b.recv(partner, RB, 0, a.count); have = true; }
+    b.end();
+  }
+}
+
 Plan make_plan(const PlanArgs &a) {
   Builder b(a.rank);
   if (a.P < 1 || a.rank < 0 || a.rank >= a.P || a.esz == 0) { b.fail(BINE_ERR_ARG); return b.p; }
@@ -1603,6 +1653,10 @@ Plan make_plan(const PlanArgs &a) {
     case BINE_AG_BINE_SEND_REMAP: ag_bine_remap(b, a, false); break;
     case BINE_AG_BINE_2_BLOCKS:
     case BINE_AG_BINE_2_BLOCKS_DTYPE: ag_bine_2_blocks(b, a); break;
+    case BINE_BC_BINE_LAT: bc_bine_lat(b, a, false); break;
+    case BINE_BC_BINE_LAT_REVERSED: bc_bine_lat(b, a, true); break;
+    case BINE_BC_BINE_LAT_NEW:
+    case BINE_BC_BINE_LAT_I_NEW: bc_bine_lat_new(b, a); break;
     default: b.fail(BINE_ERR_UNSUPPORTED); break;
   }
   if (!b.pend_send.empty() || !b.pend_recv.empty()) b.end();

@@ -41,6 +41,11 @@ def rcounts(c):
     return [N // P + ((i % 3) if c["rcounts"].startswith("ragged") else 0) for i in range(P)]
 
 
+def root(c):
+    """bcast cases: rcounts "root<k>" = root k, else 0 (oracle/ref_golden.c)"""
+    return int(c["rcounts"][4:]) if c["rcounts"].startswith("root") else 0
+
+
 def inputs(c, total=None):
     """every rank's send buffer of case c (pico_core's generator, seed_base +
     rank; sparsified for the "*_sparse" input kinds, oracle/ref_golden.c)"""

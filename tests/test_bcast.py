@@ -1,0 +1,91 @@
+"""bcast latency trees (libbine_bcast.c:189-452, widening past SURVEY.md §8):
+the planner's per-rank plans, run by the host rendezvous simulator
+(tests/plan_sim.py), deliver the root's buffer to every rank, deadlock-free,
+with the reference's message pattern: every non-root rank receives the whole
+buffer exactly once, from its tree parent, and log2(P) steps in all.  The
+reference's error returns: MPI_ERR_SIZE at non-power-of-two P, MPI_ERR_ROOT
+for bcast_bine_lat / _reversed at root != 0 (:198-210, :290-302, :381, :417)."""
+import numpy as np
+import pytest
+
+import pico_amd
+import plan_sim
+from oracle import oracle as O
+
+BC = list(pico_amd.ALGOS["bcast"])
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("algo", BC)
+def test_bcast_delivers_root_buffer(algo, P):
+    roots = [0] if algo in ("bine_lat", "bine_lat_reversed") else sorted({x for x in (0, 1, P - 1, P // 2) if x < P})
+    for dt, n in (("float", 37), ("int8", 5), ("double", 1)):
+        for root in roots:
+            bufs = O.inputs(dt, n, P)
+            got = plan_sim.run("bcast", algo, bufs, dt, root=root, in_place=True)
+            for r in range(P):
+                assert got[r].tobytes() == bufs[root].tobytes(), (algo, P, root, r)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+@pytest.mark.parametrize("algo", BC)
+def test_bcast_message_pattern(algo, P):
+    root = 0 if algo in ("bine_lat", "bine_lat_reversed") else P - 1
+    sends = 0
+    for r in range(P):
+        prims, _ = pico_amd.plan("bcast", algo, P, r, count=64, root=root, esz=4, in_place=True)
+        recv = [p for p in prims if p["type"] == "RECV"]
+        sends += sum(p["type"] == "SEND" for p in prims)
+        assert len(recv) == (0 if r == root else 1), (r, recv)
+        assert all(p["count"] == 64 for p in prims)
+        assert all(p["type"] in ("SEND", "RECV") for p in prims)   # in place: no copies
+        # a rank sends only after it has received (group order)
+        if recv:
+            assert all(p["group"] > recv[0]["group"] for p in prims if p["type"] == "SEND")
+        assert len({p["group"] for p in prims}) <= P.bit_length() - 1
+    assert sends == P - 1   # a tree: every rank reached once
+
+
+def test_bine_lat_tree_matches_reference_pi():
+    """bcast_bine_lat's parent at each step is pi(rank, step) (:247-249): check
+    the plan's peers against the schedule math directly"""
+    P, steps = 8, 3
+    for r in range(1, P):
+        prims, _ = pico_amd.plan("bcast", "bine_lat", P, r, count=8, root=0, esz=4, in_place=True)
+        recv = [p for p in prims if p["type"] == "RECV"][0]
+        sends = [p for p in prims if p["type"] == "SEND"]
+        assert all(p["peer"] != recv["peer"] for p in sends)
+    # the root sends at every step
+    prims, _ = pico_amd.plan("bcast", "bine_lat", P, 0, count=8, root=0, esz=4, in_place=True)
+    assert [p["type"] for p in prims] == ["SEND"] * steps
+
+
+@pytest.mark.parametrize("algo", BC)
+def test_bcast_errors(algo):
+    for P in (3, 5, 6, 12):
+        with pytest.raises(pico_amd.BineError) as e:
+            pico_amd.plan("bcast", algo, P, 0, count=8, root=0, esz=4, in_place=True)
+        assert e.value.status == 2   # ERR_SIZE (MPI_ERR_SIZE)
+    if algo in ("bine_lat", "bine_lat_reversed"):
+        with pytest.raises(pico_amd.BineError) as e:
+            pico_amd.plan("bcast", algo, 4, 1, count=8, root=1, esz=4, in_place=True)
+        assert e.value.status == 8   # ERR_ROOT (MPI_ERR_ROOT)
+
+
+def test_bcast_schedule_race_free():
+    from test_schedule import check_race_free
+    for algo in BC:
+        for P in (2, 4, 8):
+            for r in range(P):
+                ops, c_join, final_wait = pico_amd.schedule("bcast", algo, P, r, count=999, root=0, esz=4,
+                                                            in_place=True, chunk_bytes=256)
+                check_race_free(ops, c_join, final_wait, True)
+
+
+def test_unprovided_bcast_algorithms_report_unsupported():
+    for name in ("scatter_allgather", "bine_bdw_static", "bine_bdw_remap"):
+        a = pico_amd.lib().bine_algo_from_name(b"bcast", name.encode())
+        assert a > 0
+        with pytest.raises(pico_amd.BineError) as e:
+            pico_amd.plan("bcast", a, 4, 0, count=8, root=0, esz=4, in_place=True)
+        assert e.value.status == 6

@@ -24,7 +24,7 @@ import pico_amd  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALL_DT = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64", "float", "double"]
-STATUS_OF_MPI = {12: 1, 51: 2}   # MPI_ERR_ARG -> BINE_ERR_ARG, MPI_ERR_SIZE -> BINE_ERR_SIZE
+STATUS_OF_MPI = {12: 1, 51: 2, 7: 8}   # MPI_ERR_ARG / _SIZE / _ROOT -> BINE_ERR_ARG / _SIZE / _ROOT
 
 
 @pytest.fixture(scope="module")
@@ -163,6 +163,10 @@ def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, ro
         torch.cuda.synchronize()
         rc, st = pico_amd.loopback_allgather(comms(P), algo, ds, dr, n, dtype)
         outs = [from_dev(d, dtype, P * n) for d in dr]
+    elif coll == "bcast":   # in place: every rank's buffer holds its input
+        torch.cuda.synchronize()
+        rc, st = pico_amd.loopback_bcast(comms(P), algo, ds, n, dtype, root)
+        outs = [from_dev(d, dtype, n) for d in ds]
     else:
         dr = [torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0") if r == root else None for r in range(P)]
         if in_place:   # MPI_IN_PLACE at the root: its input already sits in its receive buffer
@@ -174,9 +178,11 @@ def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, ro
     return outs, st
 
 
-def oracle_outputs(coll, algo, sb, dt, op, rk, segsize):
+def oracle_outputs(coll, algo, sb, dt, op, rk, segsize, root=0):
     """the oracle's per-rank outputs of one collective (intended semantics:
     the reference's bugs are not reproduced)"""
+    if coll == "bcast":
+        return O.bcast(algo, sb, dt, root)[0]
     if coll == "allgather":
         return O.allgather(algo, sb, dt)[0]
     if coll == "reduce_scatter":
@@ -209,7 +215,8 @@ def test_collectives_match_reference_goldens(dev, key, cs, relay):
         rk = G.rcounts(c) if coll == "reduce_scatter" else None
         sb = G.inputs(c, sum(rk) if rk else N)
         ip = c["rcounts"].endswith("_inplace")   # MPI_IN_PLACE cases (the reference's in-place paths)
-        outs, st = run_loopback(coll, algo, sb, dt, c["op"], rk, c["segsize"], relay=relay, in_place=ip)
+        root = G.root(c) if coll == "bcast" else 0
+        outs, st = run_loopback(coll, algo, sb, dt, c["op"], rk, c["segsize"], root=root, relay=relay, in_place=ip)
         if coll == "allgather" and c["status"] == "ok" and not any(c["rets"]) and any(st) and (
                 (algo == "recursivedoubling" and P & (P - 1))):
             # deviation: the reference returns MPI_SUCCESS without
@@ -231,7 +238,7 @@ def test_collectives_match_reference_goldens(dev, key, cs, relay):
             else:
                 # the reference crashed (e.g. MPI_IN_PLACE in the block-by-block
                 # and remap variants, which read it as a buffer): vs the oracle
-                want = oracle_outputs(coll, algo, sb, dt, c["op"], rk, c["segsize"])
+                want = oracle_outputs(coll, algo, sb, dt, c["op"], rk, c["segsize"], root)
                 if coll == "reduce_scatter" and P == 1 and algo in ("butterfly", "bine_block_by_block"):
                     want = [sb[0][: rk[0]]]   # the P = 1 copy the reference omits (DESIGN.md deviations)
                 if any(sha(o) != sha(w) for o, w in zip(outs, want)):

@@ -34,6 +34,8 @@ def _run(c, ref_bugs=True):
     if c["coll"] == "allgather":
         sb = G.inputs(c)
         return O.allgather(c["algo"], sb, dt)
+    if c["coll"] == "bcast":
+        return O.bcast(c["algo"], G.inputs(c), dt, G.root(c))
     sb = G.inputs(c)
     o, rets = O.reduce(c["algo"], sb, dt, c["op"])
     return [o] + [np.zeros(0)] * (P - 1), rets

@@ -120,6 +120,19 @@ LOGIC_DT = ["float", "double", "int32", "int8", "uint8"]
 BIT_DT = ["int64", "int32", "int16", "int8", "uint8"]
 
 
+def bcast_jobs():
+    """bcast latency trees (libbine_bcast.c:189-452): in place on each rank's
+    own input; rcounts "root<k>" = root k ("even" = root 0); non-power-of-two
+    P pins the MPI_ERR_SIZE returns, root != 0 the MPI_ERR_ROOT ones"""
+    jobs = []
+    for P in (1, 2, 3, 4, 6, 8, 16):
+        for a in ("bine_lat", "bine_lat_reversed", "bine_lat_new", "bine_lat_i_new"):
+            roots = sorted({r for r in (1, P - 1, P // 2) if 0 < r < P})
+            for rk in ["even"] + [f"root{r}" for r in roots]:
+                jobs.append((P, "bcast", a, "sum", 0, rk, ["float", "int64", "int8"], [1, 7, 333, 4099], True))
+    return jobs
+
+
 def ops_jobs():
     """MPICH's logical and bitwise MPI_Ops through the reference's collectives
     (logical ops on sparsified inputs -- zeros, -0.0, NaN -- so that both truth
@@ -255,7 +268,7 @@ def main():
             return capture(ops_jobs(), index, arrays)
         index = [c for c in old if c["coll"] != only]
         arrays = {k: v for k, v in prev.items() if not k.startswith(only + ".")}
-        jobs = {"allgather": allgather_jobs}[only]()
+        jobs = {"allgather": allgather_jobs, "bcast": bcast_jobs}[only]()
         return capture(jobs, index, arrays)
     jobs = []  # (P, coll, algo, op, segsize, rk, dtypes, ns, store_small)
     # input generator pin
@@ -298,6 +311,7 @@ def main():
     jobs += odd_p_jobs()
     jobs += p16_jobs()
     jobs += inplace_jobs()
+    jobs += bcast_jobs()
     capture(jobs, [], {})
 
 
@@ -305,7 +319,7 @@ def capture(jobs, index, arrays):
     for (P, coll, algo, op, seg, rk, dts, ns, store) in jobs:
         # the reference hangs on some shapes (e.g. odd P in the any_even
         # variants): a short limit, then the cases are re-run one by one
-        recs = run_case(P, coll, algo, op, seg, rk, dts, ns, timeout=60 if coll == "allgather" else 120)
+        recs = run_case(P, coll, algo, op, seg, rk, dts, ns, timeout=60 if coll in ("allgather", "bcast") else 120)
         if any(r[2] is None for r in recs):
             # one crashing case (e.g. the static variant's tmp_buf overflow,
             # libbine_allreduce.c:724 vs :749-765) kills the whole mpiexec:
@@ -314,7 +328,7 @@ def capture(jobs, index, arrays):
             for rec in recs:
                 if rec[2] is None:
                     rec = run_case(P, coll, algo, op, seg, rk, [rec[0]], [rec[1]],
-                                   timeout=20 if coll == "allgather" else 120)[0]
+                                   timeout=20 if coll in ("allgather", "bcast") else 120)[0]
                 fixed.append(rec)
             recs = fixed
         for dt, n, rets, outs, failed in recs:
