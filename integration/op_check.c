@@ -15,7 +15,8 @@
  * floats: by value)
  * with PMPI_Allreduce / PMPI_Reduce_scatter / PMPI_Reduce.  And the pairs
  * MPICH rejects come back as MPI_ERR_OP.  Then the bcast latency trees
- * (bine_lat, _reversed at root 0; _new, _i_new at every root) vs PMPI_Bcast.
+ * (bine_lat, _reversed at root 0; _new, _i_new at every root) vs PMPI_Bcast,
+ * and four allgathers vs PMPI_Allgather, every type (P a power of two).
  *   usage: mpiexec -n P op_check      (prints "OPCHECK ok <cases>" on rank 0)
  * P a power of two: the remap / block-by-block reduce-scatters report
  * MPI_ERR_ARG elsewhere (the reference hangs there; DESIGN.md deviations).
@@ -174,6 +175,31 @@ int main(int argc, char **argv) {
           }
           free(r); free(w);
         }
+  /* allgather (pure data movement, every type incl. the padded pairs) vs PMPI_Allgather */
+  typedef int (*ag_fn)(const void *, size_t, MPI_Datatype, void *, size_t, MPI_Datatype, MPI_Comm);
+  /* (the Bine allgathers return MPI_ERR_ARG at P = 1, as the reference: golden-pinned) */
+  const struct { const char *name; ag_fn f; int p1; } ags[] = {
+      {"ring", allgather_ring, 1}, {"bine_block_by_block", allgather_bine_block_by_block, 0},
+      {"bine_permute_remap", allgather_bine_permute_remap, 0}, {"k_bruck", allgather_k_bruck, 1}};
+  for (size_t ai = 0; ai < sizeof ags / sizeof *ags; ai++)
+    for (size_t ti = 0; ti < sizeof types / sizeof *types; ti++)
+      for (size_t ci = 0; ci < sizeof counts / sizeof *counts; ci++) {
+        if (P == 1 && !ags[ai].p1) continue;
+        const type_t *t = &types[ti];
+        const size_t n = counts[ci];
+        char *s = malloc(n * t->esz), *r = calloc(n * (size_t)P, t->esz), *w = calloc(n * (size_t)P, t->esz);
+        fill(s, t, n, 555u + 31u * (unsigned)rank + (unsigned)(ai * 7 + ti * 3 + ci));
+        int e = ags[ai].f(s, n, t->dt, r, n, t->dt, MPI_COMM_WORLD);
+        int ew = PMPI_Allgather(s, (int)n, t->dt, w, (int)n, t->dt, MPI_COMM_WORLD);
+        cases++;
+        if (e != MPI_SUCCESS || ew != MPI_SUCCESS || !same(r, w, t, n * (size_t)P)) {
+          bad++;
+          if (bad <= 40)
+            fprintf(stderr, "rank %d MISMATCH allgather_%s %s n=%zu rc=%d (mpich rc %d)\n", rank, ags[ai].name,
+                    t->name, n, e, ew);
+        }
+        free(s); free(r); free(w);
+      }
   int tot = 0;
   MPI_Allreduce(&bad, &tot, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
   if (rank == 0) printf(tot ? "OPCHECK FAILED %d of %d\n" : "OPCHECK ok %d cases\n", tot ? tot : cases, cases);

@@ -270,14 +270,29 @@ int do_reduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype
 }
 
 // allgather family: pure data movement, so it runs on bytes whatever the type
+// bytes one element of `dt` spans in memory (its extent: MPI_DOUBLE_INT's
+// padding included, where MPI_Type_size counts 12 of its 16 bytes); 0 for a
+// type with a gap in front or holes a byte copy would not preserve
+size_t span(MPI_Datatype dt) {
+  MPI_Aint lb = 0, ext = 0;
+  int sz = 0;
+  if (MPI_Type_get_extent(dt, &lb, &ext) != MPI_SUCCESS || MPI_Type_size(dt, &sz) != MPI_SUCCESS) return 0;
+  if (lb != 0 || ext <= 0 || sz <= 0) return 0;
+  // predefined types only (derived types: MPI_ERR_TYPE, as map_dtype); the
+  // pair types' padding is the only gap allowed
+  if ((size_t)sz != (size_t)ext && map_dtype(dt) < 0) return 0;
+  return (size_t)ext;
+}
+
 int do_allgather(int algo, const void *sbuf, size_t scount, MPI_Datatype sdtype, void *rbuf, size_t rcount,
                  MPI_Datatype rdtype, MPI_Comm comm) {
-  int rsz = 0, ssz = 0;
-  if (MPI_Type_size(rdtype, &rsz) != MPI_SUCCESS || rsz <= 0) return MPI_ERR_TYPE;
-  const size_t bytes = rcount * (size_t)rsz;
+  const size_t rsz = span(rdtype);
+  if (!rsz) return MPI_ERR_TYPE;
+  const size_t bytes = rcount * rsz;
   if (sbuf != MPI_IN_PLACE) {
-    if (MPI_Type_size(sdtype, &ssz) != MPI_SUCCESS || ssz <= 0) return MPI_ERR_TYPE;
-    if (scount * (size_t)ssz != bytes) return MPI_ERR_ARG;  // unequal block sizes: not supported
+    const size_t ssz = span(sdtype);
+    if (!ssz) return MPI_ERR_TYPE;
+    if (scount * ssz != bytes) return MPI_ERR_ARG;  // unequal block sizes: not supported
   }
   if (bytes == 0) return MPI_SUCCESS;
   Entry *e;
@@ -291,9 +306,9 @@ int do_allgather(int algo, const void *sbuf, size_t scount, MPI_Datatype sdtype,
 // bcast family: pure data movement on `buf` in place (read on the root,
 // written elsewhere), run on bytes whatever the type
 int do_bcast(int algo, void *buf, size_t count, MPI_Datatype dtype, int root, MPI_Comm comm) {
-  int sz = 0;
-  if (MPI_Type_size(dtype, &sz) != MPI_SUCCESS || sz <= 0) return MPI_ERR_TYPE;
-  const size_t bytes = count * (size_t)sz;
+  const size_t sz = span(dtype);
+  if (!sz) return MPI_ERR_TYPE;
+  const size_t bytes = count * sz;
   if (bytes == 0) return MPI_SUCCESS;
   Entry *e;
   int rc = get_entry(comm, &e);
