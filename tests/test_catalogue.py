@@ -55,4 +55,4 @@ def test_entries_resolve_and_constraints_match_planner():
                 # rules out the single-rank copy of reduce_scatter any_even)
                 assert planned == allowed or (P == 1 and planned and not allowed), (coll, sel, P)
             n += 1
-    assert n == 31
+    assert n == 35   # 8 + 9 + 2 reduce family, 12 allgather, 4 bcast

@@ -74,6 +74,14 @@ ENTRIES = [
     ("ALLGATHER", "bine_2_blocks", "bine_2_blocks_over", [POW2_MIN2], ["bine"], "Bine two-block (:892)."),
     ("ALLGATHER", "bine_2_blocks_dtype", "bine_2_blocks_dtype_over", [POW2_MIN2], ["bine"],
      "Bine two-block, derived-datatype variant (:999)."),
+    ("BCAST", "bine_lat", "bine_lat_over", [POW2], ["bine", "latency_optimal"],
+     "Bine binomial tree, root 0 (libbine_bcast.c:189)."),
+    ("BCAST", "bine_lat_reversed", "bine_lat_reversed_over", [POW2], ["bine", "latency_optimal"],
+     "Bine binomial tree, steps reversed, root 0 (:281)."),
+    ("BCAST", "bine_lat_new", "bine_lat_new_over", [POW2], ["bine", "latency_optimal"],
+     "Bine binomial tree, negabinary partners, any root (:373)."),
+    ("BCAST", "bine_lat_i_new", "bine_lat_i_new_over", [POW2], ["bine", "latency_optimal"],
+     "Bine binomial tree, negabinary partners, non-blocking sends (:408)."),
 ]
 
 
