@@ -656,6 +656,8 @@ PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
     (2, "ALLREDUCE", "bine_lat_over", "double", True),
     (2, "REDUCE_SCATTER", "bine_permute_remap_over", "int64", True),
     (2, "REDUCE", "bine_bdw_over", "float", False),
+    (2, "BCAST", "bine_lat_over", "float", False),
+    (2, "BCAST", "bine_lat_new_over", "int64", False),
 ])
 def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat):
     """the reference's UNCHANGED pico_core (integration/Makefile links it against
