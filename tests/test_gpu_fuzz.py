@@ -30,7 +30,8 @@ OPS_OF = {
     "c_float_complex": ["sum", "prod"], "c_double_complex": ["sum", "prod"],
 }
 COLLS = {"allreduce": list(pico_amd.ALGOS["allreduce"]), "reduce_scatter": list(pico_amd.ALGOS["reduce_scatter"]),
-         "reduce": list(pico_amd.ALGOS["reduce"]), "allgather": list(pico_amd.ALGOS["allgather"])}
+         "reduce": list(pico_amd.ALGOS["reduce"]), "allgather": list(pico_amd.ALGOS["allgather"]),
+         "bcast": list(pico_amd.ALGOS["bcast"])}
 
 
 def _case(rng):
@@ -46,6 +47,10 @@ def _case(rng):
     return coll, algo, P, dt, op, n, opts
 
 
+def rng_root(P, n):
+    return (n * 7 + 3) % P   # deterministic from the case: 0 for about 1 in P cases
+
+
 def _run(coll, algo, P, dt, op, n, o):
     mk = (lambda r: O.sparsify(O.fill(dt, m, 99 + r), dt, r)) if o["sparse"] else (lambda r: O.fill(dt, m, 99 + r))
     rk = None
@@ -55,6 +60,13 @@ def _run(coll, algo, P, dt, op, n, o):
     else:
         m = n
     sb = [mk(r) for r in range(P)]
+    if coll == "bcast":   # pure data movement, in place; any root (the root-0-only trees: ERR_ROOT elsewhere)
+        root = rng_root(P, n)
+        want, rets = O.bcast(algo, sb, dt, root)
+        for c in comms(P):
+            c.set_flat_ag(o["flat_ag"])
+        outs, st = run_loopback(coll, algo, sb, dt, root=root, relay=o["relay"])
+        return want, rets, outs, st
     if coll == "allgather":   # pure data movement: any type, no operator, out of place
         want, rets = O.allgather(algo, sb, dt)
         if algo == "recursivedoubling" and P & (P - 1):
@@ -112,6 +124,36 @@ def test_random_configurations_bit_exact(dev_fuzz, seed):
                 c.set_flat_rs(False)
                 c.set_chunk(0)
                 c.set_trees(False)
+    assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_bcast_bit_exact(dev_fuzz, seed):
+    """bcast latency trees: random P (non-powers of two: MPI_ERR_SIZE), root
+    (root-0-only trees: MPI_ERR_ROOT elsewhere), type, count, relay, vs the
+    oracle's message-level replay (tests/test_oracle.py pins it)"""
+    rng = random.Random(5000 + seed)
+    bad = []
+    try:
+        for _ in range(40):
+            algo = rng.choice(COLLS["bcast"])
+            P = rng.choice([1, 2, 3, 4, 4, 6, 8, 8, 16])
+            dt = rng.choice(list(OPS_OF))
+            n = rng.choice([1, 2, 7, 64, 333, 1000, 4097, rng.randint(1, 30000)])
+            o = {"relay": rng.choice([0, 0, 64, 4096]), "flat_ag": rng.random() < 0.4, "sparse": rng.random() < 0.5}
+            want, rets, outs, st = _run("bcast", algo, P, dt, "sum", n, o)
+            if any(rets):
+                if not all(st):
+                    bad.append((algo, P, dt, n, o, "expected an error", rets, st))
+            elif any(st):
+                bad.append((algo, P, dt, n, o, "status", st))
+            elif any(sha(x) != sha(w) for x, w in zip(outs, want)):
+                bad.append((algo, P, dt, n, o, "data"))
+    finally:
+        for P in (1, 2, 3, 4, 6, 8, 16):
+            for c in comms(P):
+                c.set_relay(0)
+                c.set_flat_ag(False)
     assert not bad, bad[:6]
 
 
