@@ -73,12 +73,24 @@ def host_info():
     return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_usable": aff}
 
 
+def kernels_source_sha256():
+    import hashlib
+    with open(os.path.join(ROOT, "pico_amd", "csrc", "kernels.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def _pmc_traffic(kernel_prefix: str):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
-    (profiles/latest_pmc.json, written by tools/pmc_summary.py), or None."""
+    (profiles/latest_pmc.json, written by tools/pmc_summary.py), or None -- also
+    when those passes were taken on another build: the file carries the sha256
+    of the kernels.hip it measured, and a tree whose kernels.hip differs gets
+    None rather than a stale figure."""
     try:
         with open(os.path.join(ROOT, "profiles", "latest_pmc.json")) as f:
-            return float(json.load(f)["kernels"][kernel_prefix]["hbm_bytes_per_launch"])
+            pmc = json.load(f)
+        if pmc.get("kernels_hip_sha256") != kernels_source_sha256():
+            return None
+        return float(pmc["kernels"][kernel_prefix]["hbm_bytes_per_launch"])
     except Exception:
         return None
 
@@ -560,9 +572,8 @@ def dm_wgs(mode):
     return int(digits) if digits.isdigit() else 0
 
 
-def apply_transport(comm, mode, chunk, graphs=False, stripes=1):
+def apply_transport(comm, mode, chunk, graphs=False):
     comm.set_graphs(graphs)
-    comm.set_stripes(stripes)
     w = dm_wgs(mode)
     comm.set_direct(w is not None)
     if w is not None:
@@ -576,7 +587,7 @@ def apply_transport(comm, mode, chunk, graphs=False, stripes=1):
     comm.set_chunk(chunk)
 
 
-def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk, graphs=False, stripes=1):
+def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk, graphs=False):
     """BASELINE configs C1, C4 and C5 on the transport chosen for C3 (C1: the
     bit-exact flat phases instead of multi-tree mode, a large-message mode;
     eager and graph-replayed), each checked against the oracle's digests of
@@ -586,7 +597,7 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
     # libbine bine_bdw_remap_over 381.9 us at P = 4 through pico_core,
     # BASELINE.md section 2) -- latency-bound: the bandwidth and the
     # latency-optimal Bine variants are both timed
-    apply_transport(comm, "flatrs+flat" if mode == "trees" else mode, chunk, False, stripes)
+    apply_transport(comm, "flatrs+flat" if mode == "trees" else mode, chunk, False)
     n1 = C1_ELEMS
     sb = torch.empty(n1, dtype=torch.float32, device=dev)
     rb = torch.empty(n1, dtype=torch.float32, device=dev)
@@ -605,7 +616,7 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
                 "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
     comm.set_graphs(False)
     del sb, rb
-    apply_transport(comm, mode, chunk, graphs, stripes)
+    apply_transport(comm, mode, chunk, graphs)
     trees = mode == "trees"
     # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
     n = C4_ELEMS
@@ -743,8 +754,7 @@ def link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen):
 
 def tname(cfg):
     """trial label: transport/chunk[+sK][+graph]"""
-    return (f"{cfg[0]}/{cfg[1] >> 20}MiB" + (f"+s{cfg[3]}" if len(cfg) > 3 and cfg[3] > 1 else "")
-            + ("+graph" if len(cfg) > 2 and cfg[2] else ""))
+    return f"{cfg[0]}/{cfg[1] >> 20}MiB" + ("+graph" if len(cfg) > 2 and cfg[2] else "")
 
 
 def _best_of(trials, verdicts, nbytes, keep):
@@ -757,19 +767,25 @@ def _best_of(trials, verdicts, nbytes, keep):
     return {"transport": tname(c), "ms": round(v, 4), "algbw_per_rank_GBs": round(nbytes / (v * 1e-3) / 1e9, 2)}
 
 
+DEADLINE_EXIT = 3   # exit status of a run cut by a deadline (its JSON line says "cut_by_deadline")
+
+
 def arm_deadline(budget_s, payload, what):
     """A daemon timer: unless cancelled within budget_s seconds, print
-    payload() as the JSON line (when it is not None -- rank 0), say so on
-    stderr and end the process with status 0.  Every rank arms the same
-    budget, so all ranks stop together instead of waiting in a collective a
-    hung peer never joins."""
+    payload() as the JSON line (when it is not None -- rank 0) marked
+    "cut_by_deadline": <what>, say so on stderr and end the process with
+    status DEADLINE_EXIT, so that a hang is never mistaken for a clean run.
+    Every rank arms the same budget, so all ranks stop together instead of
+    waiting in a collective a hung peer never joins.  (os._exit: no re-exec,
+    nothing restarts a process that has touched the GPU.)"""
     def fire():
         line = payload()
         if line is not None:
+            line["cut_by_deadline"] = what
             print(json.dumps(line), flush=True)
-        sys.stderr.write(f"bench: {what} exceeded {budget_s:.0f} s; exiting\n")
+        sys.stderr.write(f"bench: {what} exceeded {budget_s:.0f} s; exiting with status {DEADLINE_EXIT}\n")
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(DEADLINE_EXIT)
 
     t = threading.Timer(budget_s, fire)
     t.daemon = True
@@ -778,7 +794,7 @@ def arm_deadline(budget_s, payload, what):
 
 
 def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, extras: bool = True,
-                    chunk_mib: int = 0, graph_trial: bool = True, stripe_trials=()):
+                    chunk_mib: int = 0, graph_trial: bool = True):
     import pico_amd
     import torch
     import torch.distributed as dist
@@ -827,7 +843,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     def trial(cfg):
         # a setting the planner rejects fails identically on every rank before
         # any transfer (plans are a pure function of the arguments): skip it
-        cfg = tuple(cfg) + (False, 1)[len(cfg) - 2:]
+        cfg = tuple(cfg) + (False,)[len(cfg) - 2:]
         if dm_dead and dm_wgs(cfg[0]) is not None:
             trials[cfg] = float("inf")
             verdicts[cfg] = "error"
@@ -872,7 +888,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # direct transport on the driver's node (configurations no one-GPU box can
     # rehearse over xGMI), every rank stops at the same budget and rank 0
     # prints this line instead of losing the run.
-    base_cfg = ("direct", mid, False, 1)
+    base_cfg = ("direct", mid, False)
     apply_transport(comm, *base_cfg)
     rbuf.fill_(float("nan"))
     st0 = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
@@ -890,29 +906,29 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     watchdog = arm_deadline(trial_budget, _provisional, "transport trials")
     if len(modes) > 1 or len(chunks) > 1:
         for m in modes:
-            trial((m, mid, False, 1))
+            trial((m, mid, False))
         finite = {c[0]: v for c, v in trials.items() if c[1] == mid and v != float("inf")}
         m_best = _prefer_exact(finite) if finite else "direct"
         for ch in chunks:
-            if (m_best, ch, False, 1) not in trials:
-                trial((m_best, ch, False, 1))
+            if (m_best, ch, False) not in trials:
+                trial((m_best, ch, False))
         cands = [c for c in trials if c[0] == m_best and trials[c] != float("inf")]
         best = min(cands, key=trials.get) if cands else base_cfg
         if dm_wgs(best[0]) == 0:
             # the direct transport's workgroups per message at the chosen chunk
             # (default 32): how many it takes to fill a link is the node's to say
             for w in DM_WGS_TRIALS:
-                trial((best[0] + str(w), best[1], False, 1))
+                trial((best[0] + str(w), best[1], False))
             cands = [c for c in trials if c[1] == best[1] and not c[2] and trials[c] != float("inf")
                      and (c[0] == best[0] or c[0] in [best[0] + str(w) for w in DM_WGS_TRIALS])]
             best = min(cands, key=trials.get)
     else:
-        best = (modes[0], chunks[0], False, 1)
+        best = (modes[0], chunks[0], False)
     if graph_trial:
         # the same transport x chunk issued as one HIP-graph replay per call
-        trial((best[0], best[1], True, 1))
-        if trials[(best[0], best[1], True, 1)] < trials.get(best, float("inf")):
-            best = (best[0], best[1], True, 1)
+        trial((best[0], best[1], True))
+        if trials[(best[0], best[1], True)] < trials.get(best, float("inf")):
+            best = (best[0], best[1], True)
     run1 = None
     if best != base_cfg:
         apply_transport(comm, *best)
@@ -920,8 +936,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         st1 = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
         run1 = (st1,) + parity(best[0])
     best, (st, ok_head, dig) = pick_headline(base_cfg, (st0, ok0, dig0), best, run1)
-    chosen, chunk, graphs, stripes = best
-    apply_transport(comm, chosen, chunk, graphs, stripes)
+    chosen, chunk, graphs = best
+    apply_transport(comm, chosen, chunk, graphs)
     ok_trees_tol = None
     if chosen == "trees":
         # fp results of multi-tree mode are the reference's schedule on
@@ -931,14 +947,14 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         run()
         torch.cuda.synchronize()
         tree_out = rbuf.clone()
-        apply_transport(comm, "flatrs+flat", chunk, graphs, stripes)
+        apply_transport(comm, "flatrs+flat", chunk, graphs)
         run()
         torch.cuda.synchronize()
         ok_exact, _ = parity("flatrs+flat")
         tol = world * 1e-6 * 100.0
         ok_trees_tol = all_ok(torch, dist, bool(ok_exact) and float((tree_out - rbuf).abs().max()) <= tol)
         del tree_out
-        apply_transport(comm, chosen, chunk, graphs, stripes)
+        apply_transport(comm, chosen, chunk, graphs)
     watchdog.cancel()
     ms = st["median_ms"]
     out = headline(best, st, ok_head, dig, ok_trees_tol)
@@ -957,27 +973,16 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
-                                                           chosen, chunk, graphs, stripes)) if extras else {}
-    apply_transport(comm, chosen, chunk, graphs, stripes)
+                                                           chosen, chunk, graphs)) if extras else {}
+    apply_transport(comm, chosen, chunk, graphs)
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}
     vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
                                                                       stream, world, ms)) if extras else {}
-    # striped exchanges (bine_comm_set_stripes) are trialled LAST and only
-    # reported: creating ncclCommSplit children slows the parent communicator
-    # for the rest of the process even after they are destroyed (measured on
-    # RCCL's socket transport, 103 -> 220-240 ms, profiles/r2_stripes_probe.txt),
-    # so they must not run before the headline
-    stripe_ms = {}
-    for k in stripe_trials if world > 1 else ():
-        cfg = (chosen, chunk, False, k)
-        trial(cfg)
-        stripe_ms[tname(cfg)] = {"ms": round(trials[cfg], 4), "parity_ok": verdicts.get(cfg)}
     watchdog.cancel()
     if out is not None:
         out["config"].update({"step_profile_rank0": steps_prof, "other_baseline_configs": extra,
                               "rccl_p2p_probe": probe, "rccl_allreduce_baseline": vendor,
-                              "striped_exchanges_after_headline": stripe_ms,
                               "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
                               "provisional_literal_rccl": {"ms": round(st0["median_ms"], 4),
                                                            "algbw_per_rank_GBs": round(S / (st0["median_ms"] * 1e-3) / 1e9, 2),
@@ -1019,8 +1024,8 @@ def pick_headline(base, run0, best, run1):
 def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, st, ok_head, dig, ok_trees_tol,
                    trials, verdicts):
     """the N > 1 JSON line for one timed configuration cfg = (transport, chunk,
-    graphs, stripes): per-rank algbw, busbw, schedule-aware link roofline"""
-    chosen, chunk, graphs, stripes = cfg
+    graphs): per-rank algbw, busbw, schedule-aware link roofline"""
+    chosen, chunk, graphs = cfg
     ms = st["median_ms"]
     S = nelem * 4
     algbw = S / (ms * 1e-3) / 1e9
@@ -1030,7 +1035,7 @@ def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, 
     # time allows at 153 GB/s per link (153 for the literal one-peer-per-step
     # schedule, up to 7 x 153 when every step loads all links)
     link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
-    achieved = egress / (st["mean_ms"] * 1e-3) / 1e9
+    achieved = egress / (ms * 1e-3) / 1e9   # the headline statistic (median), as value and ms_per_step
     out = {
         "metric": METRIC, "value": round(algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -1045,7 +1050,7 @@ def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, 
                    "algbw_per_rank_GBs": round(algbw, 2), "busbw_per_rank_GBs": round(busbw, 2),
                    "whole_job_GBs": round(world * algbw, 2),
                    "busbw_frac_of_target_1071": round(busbw / TARGET_BUSBW_GBS, 4),
-                   "transport": chosen, "graph_replay": graphs, "stripes": stripes,
+                   "transport": chosen, "graph_replay": graphs,
                    "bit_exact_vs_reference": chosen != "trees" or "integers only (fp: within rounding)",
                    "chunk_bytes": chunk,
                    "parity": {"headline_ok": ok_head, "digest": str(dig),
@@ -1063,7 +1068,6 @@ def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, 
                    "other_baseline_configs": None,
                    "rccl_p2p_probe": None,
                    "rccl_allreduce_baseline": None,
-                   "striped_exchanges_after_headline": None,
                    "rccl": pico_amd.rccl_version(), "host": host_info()},
         "roofline": {"bound": "xgmi", "achieved": round(achieved, 2), "peak": link_peak,
                      "unit": "GB/s", "frac": round(achieved / link_peak, 4),
@@ -1073,8 +1077,8 @@ def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, 
                      "traffic": None,
                      "egress_bytes": egress,
                      "link_time_bytes": L,
-                     "note": "achieved = this rank's xGMI egress bytes (executed schedule) / mean kept "
-                             "per-iteration time; peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
+                     "note": "achieved = this rank's xGMI egress bytes (executed schedule) / ms_per_step "
+                             "(the median that also gives value); peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
                              "of the busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "
                              "to 7 x 153 when every step loads all links; frac_of_target_1071_busbw = busbw / "
                              "(7 x 153), the BASELINE target's denominator"},
@@ -1096,17 +1100,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="N > 1: skip the C1/C4/C5 side measurements")
     ap.add_argument("--no-graph-trial", action="store_true", help="N > 1: do not trial HIP-graph replay")
-    # off by default: a striped flatrs+flat trial over 3 communicators hung in
-    # 2 of 4 one-GPU socket-transport runs inside RCCL's communicator split
-    # (profiles/r2_direct_transport.txt), and a hang there would lose the line
-    ap.add_argument("--stripes", default="", help="N > 1: stripe counts to trial after the headline (comma list, "
-                                                  "e.g. 2,4; default none)")
     ap.add_argument("--cpu-budget", type=float, default=5.0)
     args = ap.parse_args()
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
         res = bench_allreduce(args.steps, args.warmup, args.elems, args.algo, args.relay, not args.no_extras,
-                              args.chunk_mib, not args.no_graph_trial,
-                              tuple(int(x) for x in args.stripes.split(",") if x))
+                              args.chunk_mib, not args.no_graph_trial)
         if res is not None:
             print(json.dumps(res), flush=True)
         return

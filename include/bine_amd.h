@@ -289,19 +289,6 @@ int bine_comm_set_coll_a2a(bine_comm_t comm, int on);
  * (BINE_FLAT_RS=1 turns it on); collective. */
 int bine_comm_set_flat_rs(bine_comm_t comm, int on);
 
-/* Striped exchanges (RCCL communicators): every exchange group is split over
- * k communicators -- this one and k-1 children made once by ncclCommSplit
- * (same ranks, same order) -- each carrying part j of every message (bytes
- * [b*j/k, b*(j+1)/k), 16-B aligned cuts) on its own comm stream, forked from
- * and joined back into the exchange's stream.  More RCCL channels and proxy
- * work in flight per peer; same bytes in the same places, results
- * bit-identical.  k = 1..8 (1 = off, the default).  Collective: every rank
- * * calls it with the same k (it runs ncclCommSplit; children beyond k-1 are
- * destroyed, so k = 1 returns to one communicator); it synchronizes the
- * communicator's streams.  Exchanges then never use ncclAllToAllv, and graph
- * mode runs such collectives eagerly.  Loopback: BINE_ERR_UNSUPPORTED. */
-int bine_comm_set_stripes(bine_comm_t comm, int k);
-
 /* Direct peer-memory transport (RCCL communicators, one node): exchanges
  * move through device memory every rank maps from every peer (VMM
  * allocations exported as POSIX file descriptors and handed over Unix

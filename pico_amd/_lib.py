@@ -148,7 +148,6 @@ def lib():
         "bine_comm_set_coll_a2a": ([vp, i], i),
         "bine_comm_set_flat_rs": ([vp, i], i),
         "bine_comm_set_graphs": ([vp, i], i),
-        "bine_comm_set_stripes": ([vp, i], i),
         "bine_comm_set_direct": ([vp, i], i),
         "bine_comm_set_direct_wgs": ([vp, i], i),
         "bine_comm_set_profile": ([vp, i], i),

@@ -163,11 +163,6 @@ class Comm:
         stream must not be the NULL stream."""
         check(lib().bine_comm_set_graphs(self.handle, int(on)), "bine_comm_set_graphs")
 
-    def set_stripes(self, k: int) -> None:
-        """RCCL communicators: split every exchange over k communicators
-        (ncclCommSplit children) on k streams; bit-identical; collective."""
-        check(lib().bine_comm_set_stripes(self.handle, k), "bine_comm_set_stripes")
-
     def set_direct(self, on: bool) -> None:
         """RCCL communicators on one node: exchanges through mapped peer memory
         (bine_comm_set_direct); bit-identical; the first enable is collective."""

@@ -80,8 +80,6 @@ struct Transport {
     return BINE_ERR_UNSUPPORTED;
   }
   virtual void retire() {}
-  virtual int stripes() const { return 1; }
-  virtual bool capturable() const { return stripes() == 1; }
   // device-side transport state that must see every collective's exchanges
   // in one stream order (the direct transport's sequence bases)
   virtual bool stream_ordered() const { return false; }
@@ -118,20 +116,10 @@ struct RcclTransport final : Transport {
   void *stage = nullptr;
   size_t stage_bytes = 0;
   uint64_t stage_gen = 0;  // bumped when `stage` moves (graph mode drops graphs holding the old one)
-  // bine_comm_set_stripes: every exchange split over `nstripe` communicators
-  // (this one + ncclCommSplit children), each on its own stream
-  int nstripe = 1;
-  std::vector<ncclComm_t> extra;      // stripe j >= 1 uses extra[j - 1]
-  std::vector<hipStream_t> xstream;   // ... and xstream[j - 1]
-  std::vector<hipEvent_t> xev;        // [0]: fork, [j]: join of stripe j
   ~RcclTransport() override {
     if (stage) (void)hipFree(stage);
-    for (auto x : extra) ncclCommDestroy(x);
-    for (auto x : xstream) (void)hipStreamDestroy(x);
-    for (auto x : xev) (void)hipEventDestroy(x);
     if (comm) ncclCommDestroy(comm);
   }
-  int stripes() const override { return nstripe; }
   // *all = 1 iff every rank passes ok = true (an RCCL MIN reduction of one int)
   int agree(bool ok, int *all) {
     int *d = nullptr;
@@ -153,78 +141,12 @@ struct RcclTransport final : Transport {
   bool dm_on = false;
   int dm_wgs = 0;  // workgroups per message of the direct transport (0: BINE_DIRECT_WGS / 32)
   uint64_t key = 0;  // hash of the unique id: names the direct transport's sockets
-  // direct exchanges derive their sequence numbers on the device: capturable
-  bool capturable() const override { return nstripe == 1; }
   bool stream_ordered() const override { return dm_on; }
   int health() const override {
     if (dm_on && dm->poisoned()) {
       set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
       return BINE_ERR_INTERNAL;
     }
-    return BINE_SUCCESS;
-  }
-  // collective: every rank calls it with the same k, in the same order
-  int set_stripes(int k) {
-    if (k < 1 || k > 8) return BINE_ERR_ARG;
-    int lo = 0, hi = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    while ((int)extra.size() < k - 1) {
-      ncclComm_t x = nullptr;
-      NCCL_TRY(ncclCommSplit(comm, 0, rank, &x, nullptr));  // same ranks, same order; parent's config
-      extra.push_back(x);
-      hipStream_t st = nullptr;
-      HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi));
-      xstream.push_back(st);
-    }
-    // children beyond k - 1 are released: idle communicators keep RCCL proxy
-    // threads and connections alive (measured: a 4-rank socket run slowed
-    // 2.6x after a stripes-4 trial until they were destroyed)
-    while ((int)extra.size() > k - 1) {
-      NCCL_TRY(ncclCommDestroy(extra.back()));
-      extra.pop_back();
-      HIP_TRY(hipStreamDestroy(xstream.back()));
-      xstream.pop_back();
-    }
-    while ((int)xev.size() < k) {
-      hipEvent_t e = nullptr;
-      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      xev.push_back(e);
-    }
-    nstripe = k;
-    return BINE_SUCCESS;
-  }
-  // part j of a message of b bytes: [b * j / k, b * (j + 1) / k) rounded to
-  // 16 B -- a function of (b, j, k) only, so both ends cut identically
-  static void part(size_t b, int j, int k, size_t *off, size_t *len) {
-    const size_t a = (b * (size_t)j / (size_t)k) & ~(size_t)15;
-    const size_t z = j + 1 == k ? b : (b * (size_t)(j + 1) / (size_t)k) & ~(size_t)15;
-    *off = a;
-    *len = z > a ? z - a : 0;
-  }
-  int striped(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) {
-    const int k = nstripe;
-    HIP_TRY(hipEventRecord(xev[0], st));
-    for (int j = 0; j < k; j++) {
-      hipStream_t sj = j ? xstream[(size_t)j - 1] : st;
-      ncclComm_t cj = j ? extra[(size_t)j - 1] : comm;
-      if (j) HIP_TRY(hipStreamWaitEvent(sj, xev[0], 0));
-      NCCL_TRY(ncclGroupStart());
-      ncclResult_t r0 = ncclSuccess;
-      size_t off, len;
-      for (const auto &x : s) {
-        part(x.bytes, j, k, &off, &len);
-        if (len && r0 == ncclSuccess) r0 = ncclSend((const char *)x.ptr + off, len, ncclUint8, x.peer, cj, sj);
-      }
-      for (const auto &x : r) {
-        part(x.bytes, j, k, &off, &len);
-        if (len && r0 == ncclSuccess) r0 = ncclRecv((char *)x.ptr + off, len, ncclUint8, x.peer, cj, sj);
-      }
-      const ncclResult_t r1 = ncclGroupEnd();
-      NCCL_TRY(r0);
-      NCCL_TRY(r1);
-      if (j) HIP_TRY(hipEventRecord(xev[(size_t)j], sj));
-    }
-    for (int j = 1; j < k; j++) HIP_TRY(hipStreamWaitEvent(st, xev[(size_t)j], 0));
     return BINE_SUCCESS;
   }
   bool allgather_shape(const std::vector<XSend> &s, const std::vector<XRecv> &r) const {
@@ -275,7 +197,6 @@ struct RcclTransport final : Transport {
       return dm->exchange(s, r, st);
     }
     if (coll_ag && allgather_shape(s, r)) return allgather(s, r, st);
-    if (nstripe > 1) return striped(s, r, st);
     NCCL_TRY(ncclGroupStart());
     // the group is always closed, also when posting an operation failed
     ncclResult_t r0 = ncclSuccess;
@@ -424,6 +345,15 @@ struct bine_comm {
   bool coll_a2a = false;       // all-peers exchanges as ncclAllToAllv (no relay / trees)
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
   bool used_user = false;
+  // stream-ordered transports (the direct transport's device-side sequence
+  // bases): every exchange of a call must follow every exchange of the
+  // previous call, whichever caller stream that one ran on.  `order_ev` is
+  // recorded on the caller's stream at the end of each call (which by then
+  // follows all of the call's exchanges, single-stream or not, eager or graph);
+  // a call on another stream waits for it before issuing anything.
+  hipEvent_t order_ev = nullptr;
+  hipStream_t order_stream = nullptr;
+  bool order_valid = false;
   // bine_comm_set_graphs: each (plan, buffers, stream) is captured once into a
   // HIP graph -- both streams' work and the event hand-offs between them -- and
   // replayed with one hipGraphLaunch per call (RCCL communicators only)
@@ -459,6 +389,7 @@ struct bine_comm {
     for (int t = 0; t < 4; t++)
       if (tmp[t]) (void)hipFree(tmp[t]);
     for (auto e : ev) (void)hipEventDestroy(e);
+    if (order_ev) (void)hipEventDestroy(order_ev);
     for (auto &p : prof) {
       if (p.a) (void)hipEventDestroy(p.a);
       if (p.b) (void)hipEventDestroy(p.b);
@@ -478,6 +409,7 @@ static int comm_setup(bine_comm *c) {
   HIP_TRY(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi));
   c->ev.resize(1024);
   for (auto &e : c->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
   if (const char *e = getenv("BINE_RELAY_MIN_BYTES")) c->relay_min_bytes = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_TREES")) c->trees = atoi(e) != 0;
   if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) != 0;
@@ -512,6 +444,22 @@ static int stream_join(bine_comm *c, hipStream_t dst, hipStream_t src) {
   hipEvent_t e = next_event(c);
   HIP_TRY(hipEventRecord(e, src));
   HIP_TRY(hipStreamWaitEvent(dst, e, 0));
+  return BINE_SUCCESS;
+}
+
+// stream-ordered transports: K follows the previous call's exchanges (see
+// bine_comm::order_ev); order_end() marks this call's end on K
+static int order_begin(bine_comm *c, hipStream_t K) {
+  if (c->tx->stream_ordered() && c->order_valid && c->order_stream != K)
+    HIP_TRY(hipStreamWaitEvent(K, c->order_ev, 0));
+  return BINE_SUCCESS;
+}
+
+static int order_end(bine_comm *c, hipStream_t K) {
+  if (!c->tx->stream_ordered()) return BINE_SUCCESS;
+  HIP_TRY(hipEventRecord(c->order_ev, K));
+  c->order_stream = K;
+  c->order_valid = true;
   return BINE_SUCCESS;
 }
 
@@ -606,7 +554,8 @@ static int run_local(const std::vector<Prim> &prims, Ptr ptr, int dtype, int op,
 static bool a2a_shape(const bine_comm *c, const std::vector<XSend> &s, const std::vector<XRecv> &r) {
   const int P = c->size;
   if (!c->coll_a2a || c->hub || c->relay_min_bytes || c->trees || P < 3) return false;  // hub: loopback
-  if (!c->tx->capturable()) return false;  // striped / direct exchanges have their own path
+  const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
+  if (!rt || rt->dm_on) return false;  // direct exchanges have their own path
   if ((int)s.size() != P - 1 || (int)r.size() != P - 1) return false;
   const size_t b = s[0].bytes;
   std::vector<char> ss((size_t)P, 0), rs((size_t)P, 0);
@@ -862,12 +811,13 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     roctxRangePushA(lbl);
   }
   const bool single = bytes <= c->single_stream_bytes;
-  // graph mode captures RCCL on the capture's origin stream only: striped
-  // exchanges (RCCL on forked streams) run eagerly
-  if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && c->tx->capturable())
+  rc = order_begin(c, K);
+  if (rc) {
+  } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on())
     rc = run_graph(c, key, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
   else
     rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
+  if (!rc) rc = order_end(c, K);
   if (roctx_on()) roctxRangePop();
   return rc;
 }
@@ -1192,7 +1142,10 @@ int bine_allgather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t
 
 int bine_bcast(bine_comm_t c, int algo, void *buf, size_t count, int dtype, int root, void *stream) {
   if (algo < BINE_BC_SCATTER_ALLGATHER || algo > BINE_BC_BINE_BDW_REMAP) return BINE_ERR_UNSUPPORTED;
-  if (!c || root < 0 || root >= c->size) return BINE_ERR_ARG;
+  // the communicator size, then the root, are checked by the planner in the
+  // reference's order (libbine_bcast.c:198-210): MPI_ERR_SIZE before
+  // MPI_ERR_ROOT, also for count == 0
+  if (!c) return BINE_ERR_ARG;
   PlanArgs a;
   a.algo = algo;
   a.count = count;
@@ -1220,10 +1173,12 @@ int bine_exchange(bine_comm_t c, int nsend, const int *send_peers, const void *c
   hipStream_t K = (hipStream_t)stream;
   c->last_user = K;
   c->used_user = true;
-  int rc = stream_join(c, c->cstream, K);
+  int rc = order_begin(c, K);
+  if (!rc) rc = stream_join(c, c->cstream, K);
   if (rc) return rc;
   if ((rc = c->tx->exchange(xs, xr, c->cstream))) return rc;
-  return stream_join(c, K, c->cstream);
+  if ((rc = stream_join(c, K, c->cstream))) return rc;
+  return order_end(c, K);
 }
 
 int bine_vendor_allreduce(bine_comm_t c, const void *sbuf, void *rbuf, size_t count, int dtype, int op,
@@ -1424,16 +1379,6 @@ int bine_comm_set_direct_wgs(bine_comm_t c, int wgs) {
   r->dm_wgs = wgs;
   if (r->dm) r->dm->wgs = wgs ? wgs : r->dm->env_wgs;
   return BINE_SUCCESS;
-}
-
-int bine_comm_set_stripes(bine_comm_t c, int k) {
-  if (!c) return BINE_ERR_ARG;
-  auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
-  if (!r) return BINE_ERR_UNSUPPORTED;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipDeviceSynchronize());  // RCCL: one process per device; the caller's streams may be gone
-  return r->set_stripes(k);
 }
 
 int bine_comm_set_flat_ag(bine_comm_t c, int on) {

@@ -309,7 +309,9 @@ int do_bcast(int algo, void *buf, size_t count, MPI_Datatype dtype, int root, MP
   const size_t sz = span(dtype);
   if (!sz) return MPI_ERR_TYPE;
   const size_t bytes = count * sz;
-  if (bytes == 0) return MPI_SUCCESS;
+  // count == 0 still goes through the planner: the reference returns
+  // MPI_ERR_SIZE / MPI_ERR_ROOT before looking at the count
+  // (libbine_bcast.c:198-210)
   Entry *e;
   int rc = get_entry(comm, &e);
   if (rc) return rc;

@@ -1620,7 +1620,10 @@ Plan make_plan(const PlanArgs &a) {
   if (a.P < 1 || a.rank < 0 || a.rank >= a.P || a.esz == 0) { b.fail(BINE_ERR_ARG); return b.p; }
   const bool rs = a.algo >= BINE_RS_RECURSIVEHALVING && a.algo <= BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN;
   if (rs && (int)a.rcounts.size() != a.P) { b.fail(BINE_ERR_ARG); return b.p; }
-  if (!rs && a.count == 0) return b.p;  // nothing to move
+  const bool bc = a.algo >= BINE_BC_SCATTER_ALLGATHER && a.algo <= BINE_BC_BINE_BDW_REMAP;
+  // nothing to move; the bcast trees still return the reference's size / root
+  // errors at count 0 (their planners emit no zero-length message)
+  if (!rs && !bc && a.count == 0) return b.p;
   switch (a.algo) {
     case BINE_AR_RECURSIVEDOUBLING: ar_recursivedoubling(b, a); break;
     case BINE_AR_RING: ar_ring(b, a); break;

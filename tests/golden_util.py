@@ -1,12 +1,15 @@
 """Loaders for the golden vectors captured from the real reference libbine.
 
-The fixtures (tests/golden/index.json + outputs.npz) were produced by
+The fixtures (tests/golden/index.json.gz + outputs.npz) were produced by
 tools/make_golden.py from oracle/_ref (the reference's own libbine sources
-compiled against MPICH 3.3.2); see that script for the case matrix.
+compiled against MPICH 3.3.2); see that script for the case matrix.  Stored
+outputs are kept once per distinct content: a stored case names its npz
+member in "blob".
 """
 from __future__ import annotations
 
 import functools
+import gzip
 import hashlib
 import json
 import os
@@ -19,7 +22,7 @@ from oracle.oracle import NP_DTYPES as NP  # noqa: E402  (pair types: structured
 
 @functools.lru_cache(maxsize=None)
 def cases():
-    with open(os.path.join(GOLDEN, "index.json")) as f:
+    with gzip.open(os.path.join(GOLDEN, "index.json.gz"), "rt") as f:
         return json.load(f)["cases"]
 
 
@@ -63,7 +66,7 @@ def outputs(c):
     """Per-rank expected outputs of a stored case (list of arrays), else None."""
     if not c.get("stored"):
         return None
-    raw = _npz()[c["id"]].tobytes()
+    raw = _npz()[c["blob"]].tobytes()
     dt = NP[c["dtype"]]
     if c["stored"] == "rank0":
         a = np.frombuffer(raw, dtype=dt)

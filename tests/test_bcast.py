@@ -72,6 +72,29 @@ def test_bcast_errors(algo):
         assert e.value.status == 8   # ERR_ROOT (MPI_ERR_ROOT)
 
 
+@pytest.mark.parametrize("algo", BC)
+def test_bcast_error_order_and_zero_count(algo):
+    """the reference checks the size first, then the root
+    (libbine_bcast.c:198-210), before it looks at the count: P = 3 with an
+    out-of-range root is MPI_ERR_SIZE, a power-of-two P with root >= P is
+    MPI_ERR_ROOT (bine_lat / _reversed: any root != 0; the _new variants hang
+    in the reference there -- no rank is the root -- and report MPI_ERR_ROOT
+    here), and count = 0 reports the same errors"""
+    for count in (0, 8):
+        with pytest.raises(pico_amd.BineError) as e:
+            pico_amd.plan("bcast", algo, 3, 0, count=count, root=5, esz=4, in_place=True)
+        assert e.value.status == 2, (algo, count)
+        with pytest.raises(pico_amd.BineError) as e:
+            pico_amd.plan("bcast", algo, 4, 0, count=count, root=4, esz=4, in_place=True)
+        assert e.value.status == 8, (algo, count)
+        with pytest.raises(pico_amd.BineError) as e:
+            pico_amd.plan("bcast", algo, 6, 1, count=count, root=0, esz=4, in_place=True)
+        assert e.value.status == 2, (algo, count)
+    # count = 0 with valid arguments: success, nothing moves
+    prims, _ = pico_amd.plan("bcast", algo, 4, 1, count=0, root=0, esz=4, in_place=True)
+    assert prims == []
+
+
 def test_bcast_schedule_race_free():
     from test_schedule import check_race_free
     for algo in BC:

@@ -105,7 +105,9 @@ def test_all_ok_without_dist():
 
 def test_arm_deadline_prints_partial_line_and_exits(tmp_path):
     """a side measurement that hangs past the budget: the line measured so far
-    is printed and the process ends with status 0 (bench.arm_deadline)"""
+    is printed, marked cut_by_deadline, and the process ends with the distinct
+    status bench.DEADLINE_EXIT (bench.arm_deadline), so a hang never looks
+    like a clean run"""
     import subprocess
     import sys
     script = (
@@ -119,9 +121,10 @@ def test_arm_deadline_prints_partial_line_and_exits(tmp_path):
         "time.sleep(30)\n"
         "print('not reached')\n" % ROOT)
     r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0
+    assert r.returncode == bench.DEADLINE_EXIT != 0
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-    assert lines == [{"metric": "m", "value": 1.0, "config": {"side_measurements_cut_after_s": 0.3}}]
+    assert lines == [{"metric": "m", "value": 1.0, "config": {"side_measurements_cut_after_s": 0.3},
+                      "cut_by_deadline": "side measurements"}]
     assert "not reached" not in r.stdout and "exceeded" in r.stderr
 
 
@@ -134,12 +137,28 @@ def test_arm_deadline_cancelled_is_silent():
 
 def test_best_of_picks_fastest_verified_rccl_trial():
     inf = float("inf")
-    trials = {("direct", 16 << 20, False, 1): 3.0, ("flat", 16 << 20, False, 1): 2.0,
-              ("flatrs+flat", 16 << 20, False, 1): 1.0, ("direct+dm", 16 << 20, False, 1): 0.5,
-              ("relay", 16 << 20, False, 1): inf}
-    verdicts = {("direct", 16 << 20, False, 1): True, ("flat", 16 << 20, False, 1): True,
-                ("flatrs+flat", 16 << 20, False, 1): False, ("direct+dm", 16 << 20, False, 1): True,
-                ("relay", 16 << 20, False, 1): "error"}
+    trials = {("direct", 16 << 20, False): 3.0, ("flat", 16 << 20, False): 2.0,
+              ("flatrs+flat", 16 << 20, False): 1.0, ("direct+dm", 16 << 20, False): 0.5,
+              ("relay", 16 << 20, False): inf}
+    verdicts = {("direct", 16 << 20, False): True, ("flat", 16 << 20, False): True,
+                ("flatrs+flat", 16 << 20, False): False, ("direct+dm", 16 << 20, False): True,
+                ("relay", 16 << 20, False): "error"}
     b = bench._best_of(trials, verdicts, 1 << 28, lambda c: "+dm" not in c[0])
     assert b == {"transport": "flat/16MiB", "ms": 2.0, "algbw_per_rank_GBs": round((1 << 28) / 2e-3 / 1e9, 2)}
     assert bench._best_of(trials, verdicts, 1 << 28, lambda c: False) is None
+
+
+def test_pmc_traffic_only_for_the_measured_kernel_source(tmp_path, monkeypatch):
+    """traffic comes from profiles/latest_pmc.json only while the tree's
+    kernels.hip hashes to the source those counters were taken on"""
+    pmc = {"kernels_hip_sha256": bench.kernels_source_sha256(),
+           "kernels": {"k_copy": {"hbm_bytes_per_launch": 123.0}}}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "pico_amd" / "csrc").mkdir(parents=True)
+    with open(os.path.join(ROOT, "pico_amd", "csrc", "kernels.hip"), "rb") as f:
+        (tmp_path / "pico_amd" / "csrc" / "kernels.hip").write_bytes(f.read())
+    (tmp_path / "profiles" / "latest_pmc.json").write_text(json.dumps(pmc))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench._pmc_traffic("k_copy") == 123.0
+    (tmp_path / "pico_amd" / "csrc" / "kernels.hip").write_bytes(b"// another build\n")
+    assert bench._pmc_traffic("k_copy") is None

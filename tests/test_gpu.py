@@ -675,6 +675,29 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat)
     assert "Last Iter Time" in p.stdout
 
 
+@pytest.mark.skipif(not os.path.exists(PICO_CORE), reason="reference pico_core not built (integration/Makefile)")
+@pytest.mark.parametrize("algo,flat", [("bine_bdw_remap_over", False), ("bine_bdw_remap_over", True),
+                                       ("bine_lat_over", False)])
+def test_reference_pico_core_c1(dev, tmp_path, algo, flat):
+    """BASELINE configs[0] (C1) through the GPU path exactly as the reference
+    runs it: the unchanged pico_core, 4 ranks, 262,144 fp32 elements (1 MiB)
+    per rank, allreduce SUM (pico_core_utils.h:262), 20 iterations, every one
+    checked by pico_core against MPICH's PMPI_Allreduce (pico_core_utils.c:
+    553-610, 960-992); the 4 ranks share the GPU through RCCL's socket
+    transport (distinct NCCL_HOSTIDs); host buffers, staged by libbine.so"""
+    import subprocess
+    env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
+    if flat:
+        env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
+    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), "4", "ALLREDUCE", "262144",
+                        "20", algo, "float"], env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
+    assert "Last Iter Time" in p.stdout
+    csv = tmp_path / "data" / f"262144_{algo}_float.csv"
+    lines = csv.read_text().splitlines()
+    assert lines[0].startswith("highest,rank0,rank1,rank2,rank3") and len(lines) == 21
+
+
 OP_CHECK = os.path.join(ROOT, "integration", "_build", "op_check")
 
 

@@ -136,3 +136,42 @@ def test_graph_mode_size1_comm(dev):
         comm.set_graphs(False)
     finally:
         comm.destroy()
+
+
+# ---- C1 at its own shape (BASELINE configs[0]) --------------------------------------
+
+C1_N, C1_P = 262_144, 4
+
+
+@pytest.mark.parametrize("mode", ["direct", "flat", "flatrs+flat", "relay"])
+@pytest.mark.parametrize("algo", ["bine_bdw_remap", "bine_lat"])
+def test_c1_allreduce_own_shape_vs_committed_digests(dev, algo, mode):
+    """C1 itself: fp32 SUM allreduce, 262,144 elements (1 MiB) per rank, P = 4,
+    pico_core's inputs (seed 1234 + rank, generated on the device) -- the
+    reference's own CPU configuration (pico_core bine_bdw_remap_over,
+    libbine_allreduce.c:820-923; bine_lat, :321-439).  Four loopback ranks on
+    one MI355X through the same planner and executor as RCCL, literal
+    schedule, flat allgather, flat reduce-scatter + flat allgather (the
+    one-shot form for bine_lat) and relay; every rank's output digest must
+    equal the committed oracle digest (tools/make_bench_digests.py) --
+    bine_lat's result differs per rank, as in the reference.  0 ulp."""
+    cs = pico_amd.Comm.loopback(C1_P, 0)
+    try:
+        for c in cs:
+            c.set_relay(256 << 10 if mode == "relay" else 0)
+            c.set_flat_ag("flat" in mode)
+            c.set_flat_rs("flatrs" in mode)
+        sb = [torch.empty(C1_N, dtype=torch.float32, device=dev) for _ in range(C1_P)]
+        for r, b in enumerate(sb):
+            pico_amd.fill_pico(b, C1_N, "float", 1234 + r)
+        rb = [torch.full((C1_N,), float("nan"), dtype=torch.float32, device=dev) for _ in range(C1_P)]
+        torch.cuda.synchronize()
+        for _ in range(3):   # repeated calls reuse the cached plan and workspace
+            rc, st = pico_amd.loopback_allreduce(cs, algo, sb, rb, C1_N, "float")
+            assert rc == 0 and not any(st), st
+        got = [pico_amd.checksum(b, C1_N, "float") for b in rb]
+        want = [int(x) for x in GOLD[f"C1/allreduce/{algo}/float/N{C1_N}/P{C1_P}"]]
+        assert got == want
+    finally:
+        for c in cs:
+            c.destroy()

@@ -12,11 +12,17 @@ chunks -- i.e. the exact schedules bench.py times.
 * C5 int64 allreduce 256 MiB/rank: exact vs the element-wise wrapped int64 sum
   (integer SUM is associative, so any correct schedule gives these bits); fp64
   vs the oracle's digests.
-* C4 fp32 reduce_scatter 1 GiB/rank: integer-valued fp32 inputs (sums of eight
-  values < 2^24 are exact in any association order), so every block can be
-  checked bit-exact against a device-side sum at full size; the association
-  order itself is pinned against the oracle at smaller sizes in test_gpu.py.
+* C4 fp32 reduce_scatter 1 GiB/rank on pico_core's own inputs (seed 1234 +
+  rank): every rank's output digest equals the committed oracle digest
+  (tests/golden/bench_digests.json), i.e. the reference's association order
+  at full size, 0 ulp; direct and flat reduce-scatter (the fused tree
+  kernel).  Beside it, integer-valued fp32 inputs (sums of eight values <
+  2^24 are exact in any association order) checked element for element
+  against a device-side sum, for every transport incl. multi-tree mode.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -28,6 +34,9 @@ torch = pytest.importorskip("torch")
 import pico_amd  # noqa: E402
 
 P = 8
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+with open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")) as _f:
+    GOLD = json.load(_f)["digests"]
 C3_N = 67_108_864
 C4_N = 268_435_456
 C5_N = 33_554_432
@@ -159,6 +168,35 @@ def test_c5_double_allreduce_fullsize(dev, comms, c5_double_digest, mode):
     finally:
         _mode(comms, "direct")
     assert got == [expect] * P
+
+
+@pytest.mark.parametrize("mode", ["direct", "flatrs", "relay"])
+def test_c4_reduce_scatter_fullsize_pico_inputs(dev, comms, mode):
+    """C4 exactly as bench.py runs it: reduce_scatter_bine_permute_remap, fp32
+    SUM, 268,435,456 elements (1 GiB) per rank at P = 8, pico_core's
+    distribution (rand_r / RAND_MAX * 100, seed 1234 + rank,
+    pico_core_utils.c:903-916) -- every rank's 128 MiB block digest equals the
+    oracle's digest of the reference's association order
+    (libbine_reduce_scatter.c:985-1063), committed in
+    tests/golden/bench_digests.json.  (pico_core's generator repeats every
+    2^27 elements, so blocks r and r + 4 carry equal digests; the element-wise
+    test below uses non-repeating inputs.)"""
+    per = C4_N // P
+    want = [int(x) for x in GOLD[f"C4/reduce_scatter/bine_permute_remap/float/N{C4_N}/P{P}"]]
+    sb = _device_inputs("float", torch.float32, C4_N)
+    rb = [torch.full((per,), float("nan"), dtype=torch.float32, device="cuda:0") for _ in range(P)]
+    torch.cuda.synchronize()
+    _mode(comms, mode)
+    try:
+        rc, st = pico_amd.loopback_reduce_scatter(comms, "bine_permute_remap", sb, rb, [per] * P, "float")
+        assert rc == 0 and not any(st), st
+        torch.cuda.synchronize()
+        got = [pico_amd.checksum(b, per, "float") for b in rb]
+    finally:
+        _mode(comms, "direct")
+        del sb, rb
+        torch.cuda.empty_cache()
+    assert got == want
 
 
 @pytest.mark.parametrize("mode", ["direct", "relay", "trees", "flatrs"])

@@ -47,3 +47,18 @@ def test_rccl_matrix_4_ranks():
     tail = "\n".join(r.stdout.splitlines()[-12:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=4" in r.stdout
+
+
+@pytest.mark.timeout(300)
+def test_direct_transport_orders_calls_across_streams():
+    """direct peer-memory transport, 2 processes: small (single-stream) and
+    large (two-stream) allreduce calls alternate over two caller streams with
+    no host synchronisation in between; every output equals the oracle's
+    digest (tools/dm_order.py) -- the sequence bases the calls share are
+    reached in call order (executor.cpp order_begin / order_end)"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_order.py"), "2", "8"], env=env,
+                       capture_output=True, text=True, timeout=280)
+    tail = "\n".join(r.stdout.splitlines()[-8:])
+    assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
+    assert "RESULT P=2" in r.stdout

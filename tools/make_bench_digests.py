@@ -107,7 +107,7 @@ def main():
     d.update(small())
     if not quick:
         d.update(big())
-    doc = {"generator": "tools/make_bench_digests.py (oracle/bine_oracle.c, pinned by tests/golden/index.json)",
+    doc = {"generator": "tools/make_bench_digests.py (oracle/bine_oracle.c, pinned by tests/golden/index.json.gz)",
            "inputs": "pico_core rand_r distribution, seed 1234 + rank (C2: in 1234, inout 1235; tree: leaf j "
                      f"seed {TREE_SEED} + j)",
            "digest": "sum_i mix64(bits(x[i]) + i * 0x9E3779B97F4A7C15) mod 2^64 (bine_checksum)",

@@ -5,7 +5,7 @@ Runs ``oracle/_ref/ref_golden`` (built by ``make -C oracle ref`` from the source
 under /root/reference, against the image's MPICH 3.3.2) under ``mpiexec -n P``
 and writes:
 
-* ``tests/golden/index.json`` -- one record per (collective, algorithm, op,
+* ``tests/golden/index.json.gz`` -- one record per (collective, algorithm, op,
   dtype, P, N, segsize, rcounts kind): per-rank return codes, output lengths and
   SHA-256 digests of the outputs;
 * ``tests/golden/outputs.npz`` -- the full per-rank outputs of the small cases
@@ -18,6 +18,7 @@ in the build container only; the fixtures it writes are what travels.
 """
 from __future__ import annotations
 
+import gzip
 import hashlib
 import itertools
 import json
@@ -244,8 +245,7 @@ def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     if only:
         # regenerate one collective's cases, keep everything else as it is
-        old = json.load(open(os.path.join(OUT, "index.json")))["cases"]
-        prev = dict(np.load(os.path.join(OUT, "outputs.npz")))
+        old, prev = load_fixtures()
         if only == "inplace":
             index = [c for c in old if not c["rcounts"].endswith("_inplace")]
             keep = {c["id"] for c in index}
@@ -351,11 +351,37 @@ def capture(jobs, index, arrays):
                 rec["stored"] = ("rank0" if same else "all") if small else None
             index.append(rec)
         print(f"P={P} {coll} {algo} {op} seg={seg} {rk}: {len(recs)} cases", flush=True)
-    with open(os.path.join(OUT, "index.json"), "w") as f:
-        json.dump({"generator": "tools/make_golden.py", "reference": "HLC-Lab/pico libbine @ 2025-07-25",
-                   "mpi": "MPICH 3.3.2 (ch3:nemesis)", "cases": index}, f, separators=(",", ":"))
-    np.savez_compressed(os.path.join(OUT, "outputs.npz"), **arrays)
-    print(len(index), "cases,", len(arrays), "stored")
+    write_fixtures(index, arrays)
+
+
+def write_fixtures(index, arrays):
+    """tests/golden/index.json.gz + outputs.npz.  Stored outputs are kept once
+    per distinct content (many algorithms, in- and out-of-place runs give the
+    same bytes): npz members are named by a content hash, and each stored case
+    names its member in "blob"."""
+    blobs = {}
+    for rec in index:
+        a = arrays.get(rec["id"])
+        if a is None:
+            continue
+        name = "b" + hashlib.sha256(a.tobytes()).hexdigest()[:24]
+        blobs[name] = a
+        rec["blob"] = name
+    doc = {"generator": "tools/make_golden.py", "reference": "HLC-Lab/pico libbine @ 2025-07-25",
+           "mpi": "MPICH 3.3.2 (ch3:nemesis)", "cases": index}
+    with gzip.GzipFile(os.path.join(OUT, "index.json.gz"), "wb", mtime=0) as f:
+        f.write(json.dumps(doc, separators=(",", ":")).encode())
+    np.savez_compressed(os.path.join(OUT, "outputs.npz"), **blobs)
+    print(len(index), "cases,", len(arrays), "stored,", len(blobs), "distinct")
+
+
+def load_fixtures():
+    """(index, {case id: stored bytes}) of the committed fixtures"""
+    with gzip.open(os.path.join(OUT, "index.json.gz"), "rt") as f:
+        index = json.load(f)["cases"]
+    npz = np.load(os.path.join(OUT, "outputs.npz"), allow_pickle=False)
+    arrays = {c["id"]: npz[c["blob"]] for c in index if c.get("blob")}
+    return index, arrays
 
 
 if __name__ == "__main__":

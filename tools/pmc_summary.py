@@ -16,6 +16,7 @@ usage: python tools/pmc_summary.py TAG
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
@@ -86,7 +87,11 @@ def main():
         kernels[name] = dict(by_grid[g], grid_size=g,
                              all_stats_avg_ns=stats.get(name, {}).get("avg_ns"),
                              shapes={str(x): {f: v for f, v in by_grid[x].items() if f != "name"} for x in sorted(by_grid)})
-    res = {"tag": tag, "kernels": kernels}
+    # the kernel source these counters belong to: bench.py reports `traffic`
+    # only while the tree's kernels.hip still hashes to this
+    with open(os.path.join(ROOT, "pico_amd", "csrc", "kernels.hip"), "rb") as f:
+        src = hashlib.sha256(f.read()).hexdigest()
+    res = {"tag": tag, "kernels_hip_sha256": src, "kernels": kernels}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     for name in (f"{tag}_pmc.json", "latest_pmc.json"):
         with open(os.path.join(ROOT, "profiles", name), "w") as f:

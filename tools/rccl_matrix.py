@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 CASES = (("float", 4099), ("int64", 1001), ("int8", 333), ("float", 4096))  # 4096: equal blocks up to P = 16
 # (name, relay_min_bytes, chunk_bytes, flat phases (1: allgather, 2: reduce-scatter, 4: one-to-all
 # exchanges as ncclAllGather, 8: all-peers exchanges as ncclAllToAllv, 16: HIP-graph mode,
-# 32 / 64: exchanges striped over 2 / 3 communicators, 128: direct peer-memory transport),
+# 128: direct peer-memory transport),
 # run each collective twice on a side stream)
 SETTINGS = (("direct", 0, 0, 0, 0), ("chunk4KiB", 0, 4096, 0, 0), ("relay", 64, 1024, 0, 0),
             ("relay+flat", 64, 1024, 1, 0), ("flatrs+flat", 0, 1024, 3, 0), ("side-stream x2", 64, 1024, 1, 1),
@@ -36,8 +36,6 @@ SETTINGS = (("direct", 0, 0, 0, 0), ("chunk4KiB", 0, 4096, 0, 0), ("relay", 64, 
             # graph mode (bit 16): the first call runs eagerly and is captured, the
             # second (into a zeroed output) is the HIP-graph replay
             ("graphs chunk1KiB x2", 0, 1024, 16, 1), ("graphs relay+flatrs+flat x2", 64, 1024, 16 | 3, 1),
-            # exchanges striped over 2 / 3 RCCL communicators (bits 32 / 64)
-            ("stripes2 chunk1KiB", 0, 1024, 32, 0), ("stripes3 relay+flatrs+flat x2", 64, 1024, 64 | 3, 1),
             # the direct peer-memory transport (bit 128) instead of RCCL send/recv
             ("direct-mem", 0, 0, 128, 0), ("direct-mem relay chunk1KiB", 64, 1024, 128, 0),
             ("direct-mem flatrs+flat x2", 0, 1024, 128 | 3, 1))
@@ -102,7 +100,6 @@ def worker(rank, P, port, q):
         comm.set_coll_ag(bool(flat & 4))
         comm.set_coll_a2a(bool(flat & 8))
         comm.set_graphs(bool(flat & 16))
-        comm.set_stripes(3 if flat & 64 else 2 if flat & 32 else 1)
         comm.set_direct(bool(flat & 128))
         ctx = torch.cuda.stream(side) if twice else contextlib.nullcontext()
         ctx.__enter__()
