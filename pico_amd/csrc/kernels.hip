@@ -918,9 +918,14 @@ __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
     const uint32_t old = __hip_atomic_fetch_add(cnt_ptr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
     if (old + 1 == (uint32_t)a.wgs) {
       __hip_atomic_store(cnt_ptr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use: a later launch
+      // system-scope release (buffer_wbl2 sc0 sc1), its write-back waited for
+      // explicitly (the compiler may drop the wait after buffer_wbl2 when the
+      // vmcnt scoreboard is provably empty, MI355X_MICROARCH.md "Compiler
+      // hazard"), then a relaxed system-scope flag store (sc0 sc1): the
+      // flag cannot overtake the data (ISA: profiles/r3_dm_move_isa.txt)
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(sig_ptr, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(sig_ptr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     uint32_t *lc = reinterpret_cast<uint32_t *>(own + kLaunchCntOff);
     const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);

@@ -9,11 +9,16 @@
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <set>
+#include <utility>
 #include <vector>
 
 #include "bine_amd.h"
@@ -31,7 +36,45 @@ struct Entry {
   // staging for host buffers
   void *dev[2] = {nullptr, nullptr};
   size_t dev_bytes[2] = {0, 0};
+  // host->device and device->host copy streams (PCIe is full duplex: the two
+  // directions overlap) and the events that hand chunks between them and the
+  // collective's stream
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  std::vector<hipEvent_t> ev;
+  size_t ev_next = 0;
 };
+
+// Host buffers the shim has page-locked (hipHostRegister), so that the
+// staging copies are DMA straight from / to the caller's memory and run
+// asynchronously on the copy streams.  pico_core keeps its buffers for the
+// whole run (pico_core_allreduce_utils.c:13-25); each is registered once, on
+// first use, and released at MPI_Finalize (MPI_COMM_SELF's delete callback).
+// BINE_HOST_REGISTER=0 turns it off (pageable copies).
+std::vector<std::pair<uintptr_t, uintptr_t>> g_pinned;  // [lo, hi), page-rounded
+constexpr size_t kPinMinBytes = 1 << 20;
+
+bool pin_host(const void *p, size_t n) {
+  static const bool on = !getenv("BINE_HOST_REGISTER") || atoi(getenv("BINE_HOST_REGISTER")) != 0;
+  if (!on || n < kPinMinBytes) return false;
+  const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+  const uintptr_t lo = (uintptr_t)p & ~(pg - 1), hi = ((uintptr_t)p + n + pg - 1) & ~(pg - 1);
+  for (const auto &r : g_pinned) {
+    if (lo >= r.first && hi <= r.second) return true;
+    if (lo < r.second && r.first < hi) return false;  // overlaps another registration: stay pageable
+  }
+  if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  g_pinned.emplace_back(lo, hi);
+  return true;
+}
+
+void unpin_all() {
+  for (const auto &r : g_pinned) (void)hipHostUnregister((void *)r.first);
+  (void)hipGetLastError();
+  g_pinned.clear();
+}
 
 int g_keyval = MPI_KEYVAL_INVALID;
 int g_self_keyval = MPI_KEYVAL_INVALID;
@@ -45,6 +88,9 @@ void release(Entry *e) {
   }
   for (int i = 0; i < 2; i++)
     if (e->dev[i]) (void)hipFree(e->dev[i]);
+  if (e->h2d) (void)hipStreamDestroy(e->h2d);
+  if (e->d2h) (void)hipStreamDestroy(e->d2h);
+  for (auto x : e->ev) (void)hipEventDestroy(x);
   delete e;
 }
 
@@ -58,6 +104,7 @@ int comm_delete(MPI_Comm, int, void *val, void *) {
 int self_delete(MPI_Comm, int, void *, void *) {
   for (auto *e : g_entries) release(e);
   g_entries.clear();
+  unpin_all();
   return MPI_SUCCESS;
 }
 
@@ -187,9 +234,48 @@ int stage(Entry *e, int slot, size_t bytes, void **dev) {
   return MPI_SUCCESS;
 }
 
-// Run `body(dev_sbuf, dev_rbuf, stream)` with host buffers staged.
+int copy_streams(Entry *e) {
+  if (e->h2d) return MPI_SUCCESS;
+  if (hipStreamCreateWithFlags(&e->h2d, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->d2h, hipStreamNonBlocking) != hipSuccess)
+    return MPI_ERR_OTHER;
+  e->ev.resize(64);
+  for (auto &x : e->ev)
+    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return MPI_ERR_OTHER;
+  return MPI_SUCCESS;
+}
+
+// `dst` stream waits for everything enqueued so far on `src`
+int follow(Entry *e, hipStream_t dst, hipStream_t src) {
+  hipEvent_t x = e->ev[e->ev_next];
+  e->ev_next = (e->ev_next + 1) % e->ev.size();
+  if (hipEventRecord(x, src) != hipSuccess || hipStreamWaitEvent(dst, x, 0) != hipSuccess) return MPI_ERR_OTHER;
+  return MPI_SUCCESS;
+}
+
+// staging chunk of the pipelined path (BINE_STAGE_CHUNK_BYTES, default 16 MiB)
+size_t stage_chunk_bytes() {
+  static const size_t v = [] {
+    const char *x = getenv("BINE_STAGE_CHUNK_BYTES");
+    const size_t b = x ? (size_t)strtoull(x, nullptr, 10) : (size_t)16 << 20;
+    return std::max<size_t>(b, 1 << 20) & ~(size_t)255;
+  }();
+  return v;
+}
+
+// Run `body(dev_sbuf, dev_rbuf, first_elem, elems, stream)` with host buffers
+// staged through the device.  Host->device copies run on the h2d stream,
+// device->host copies on the d2h stream, the collective on the communicator's
+// stream, chained by events.  `esz` > 0 declares the collective separable by
+// element (element i of the result depends only on element i of the inputs,
+// through a reduction whose result bits do not depend on how the buffer is
+// cut -- see do_allreduce): then the buffer is cut into chunks and chunk k's
+// host->device copy, collective and device->host copy are pipelined, so the
+// two PCIe directions and the device work overlap.  Otherwise one collective
+// over the whole buffer, between the two staged copies.
 template <typename F>
-int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes, bool read_rbuf, F body) {
+int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes, bool read_rbuf, size_t esz,
+                 size_t count, F body) {
   hipStream_t st = (hipStream_t)bine_comm_stream(e->comm);
   (void)hipSetDevice(bine_comm_device(e->comm));
   const bool in_place = sbuf == MPI_IN_PLACE;
@@ -198,23 +284,61 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
   bool stage_s = !in_place && sbuf && sbytes && !on_device(sbuf);
   bool stage_r = rbuf && rbytes && !on_device(rbuf);
   int rc;
+  if (!stage_s && !stage_r) {  // device buffers: the collective as it is (the CUDA_AWARE-style path)
+    int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st);
+    if (bst != BINE_SUCCESS) return to_mpi(bst);
+    if (hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
+    return to_mpi(bine_comm_synchronize(e->comm));
+  }
+  if ((rc = copy_streams(e))) return rc;
   if (stage_s) {
     void *d;
     if ((rc = stage(e, 0, sbytes, &d))) return rc;
-    if (hipMemcpyAsync(d, sbuf, sbytes, hipMemcpyHostToDevice, st) != hipSuccess) return MPI_ERR_OTHER;
     ds = d;
+    pin_host(sbuf, sbytes);
   }
   if (stage_r) {
     void *d;
     if ((rc = stage(e, 1, rbytes, &d))) return rc;
-    if ((in_place || read_rbuf) && hipMemcpyAsync(d, rbuf, rbytes, hipMemcpyHostToDevice, st) != hipSuccess)
-      return MPI_ERR_OTHER;
     dr = d;
+    pin_host(rbuf, rbytes);
   }
-  int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (void *)st);
-  if (bst != BINE_SUCCESS) return to_mpi(bst);
-  if (stage_r && hipMemcpyAsync(rbuf, dr, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess) return MPI_ERR_OTHER;
-  if (hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
+  const bool fill_r = stage_r && (in_place || read_rbuf);  // (every earlier call has drained all three streams)
+  const size_t ch = esz ? stage_chunk_bytes() / esz * esz : 0;
+  const size_t total = count * esz;
+  if (ch && total >= 2 * ch && (!stage_s || sbytes == total) && (!stage_r || rbytes == total)) {
+    for (size_t off = 0; off < total; off += ch) {
+      const size_t len = std::min(ch, total - off);
+      if (stage_s && hipMemcpyAsync((char *)ds + off, (const char *)sbuf + off, len, hipMemcpyHostToDevice,
+                                    e->h2d) != hipSuccess)
+        return MPI_ERR_OTHER;
+      if (fill_r && hipMemcpyAsync((char *)dr + off, (char *)rbuf + off, len, hipMemcpyHostToDevice, e->h2d) !=
+                        hipSuccess)
+        return MPI_ERR_OTHER;
+      if ((rc = follow(e, st, e->h2d))) return rc;
+      const void *cs = in_place ? BINE_IN_PLACE : (const void *)((const char *)ds + off);
+      int bst = body(cs, (char *)dr + off, off / esz, len / esz, (void *)st);
+      if (bst != BINE_SUCCESS) return to_mpi(bst);
+      if (stage_r) {
+        if ((rc = follow(e, e->d2h, st))) return rc;
+        if (hipMemcpyAsync((char *)rbuf + off, (char *)dr + off, len, hipMemcpyDeviceToHost, e->d2h) != hipSuccess)
+          return MPI_ERR_OTHER;
+      }
+    }
+  } else {
+    if (stage_s && hipMemcpyAsync((void *)ds, sbuf, sbytes, hipMemcpyHostToDevice, e->h2d) != hipSuccess)
+      return MPI_ERR_OTHER;
+    if (fill_r && hipMemcpyAsync(dr, rbuf, rbytes, hipMemcpyHostToDevice, e->h2d) != hipSuccess)
+      return MPI_ERR_OTHER;
+    if ((rc = follow(e, st, e->h2d))) return rc;
+    int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st);
+    if (bst != BINE_SUCCESS) return to_mpi(bst);
+    if (stage_r) {
+      if ((rc = follow(e, e->d2h, st))) return rc;
+      if (hipMemcpyAsync(rbuf, dr, rbytes, hipMemcpyDeviceToHost, e->d2h) != hipSuccess) return MPI_ERR_OTHER;
+    }
+  }
+  if (hipStreamSynchronize(e->d2h) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
   return to_mpi(bine_comm_synchronize(e->comm));
 }
 
@@ -227,11 +351,22 @@ int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datat
   Entry *e;
   int rc = get_entry(comm, &e);
   if (rc) return rc;
-  const size_t bytes = count * bine_dtype_size(dt);
+  const size_t esz = bine_dtype_size(dt);
+  const size_t bytes = count * esz;
   const size_t seg = bine_allreduce_segsize;
-  return with_buffers(e, sbuf, bytes, rbuf, bytes, false, [&](const void *s, void *r, void *st) {
-    return bine_allreduce(e->comm, algo, s, r, count, dt, o, algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? seg : 0, st);
-  });
+  // separable by element, so the staged path may pipeline it chunk by chunk:
+  // at P = 1 every algorithm is the copy sbuf -> rbuf (libbine_allreduce.c:
+  // 849-852); on the plain integer types every MPI_Op is associative and
+  // commutative in the element type, so the result bits do not depend on the
+  // reduction tree, i.e. on how the buffer is cut.  Floating-point results
+  // depend on the tree (block ownership follows the count): one collective.
+  const bool integer = dt <= BINE_UINT64;
+  const bool separable = e->size == 1 || integer;
+  return with_buffers(e, sbuf, bytes, rbuf, bytes, false, separable ? esz : 0, count,
+                      [&](const void *s, void *r, size_t, size_t n, void *st) {
+                        return bine_allreduce(e->comm, algo, s, r, n, dt, o,
+                                              algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? seg : 0, st);
+                      });
 }
 
 int do_reduce_scatter(int algo, const void *sbuf, void *rbuf, const int rcounts[], MPI_Datatype dtype, MPI_Op op,
@@ -248,9 +383,10 @@ int do_reduce_scatter(int algo, const void *sbuf, void *rbuf, const int rcounts[
   const bool in_place = sbuf == MPI_IN_PLACE;
   // MPI_IN_PLACE: the input is the whole rbuf
   const size_t rbytes = (in_place ? total : (size_t)rcounts[e->rank]) * esz;
-  return with_buffers(e, sbuf, total * esz, rbuf, rbytes, false, [&](const void *s, void *r, void *st) {
-    return bine_reduce_scatter(e->comm, algo, s, r, rcounts, dt, o, st);
-  });
+  return with_buffers(e, sbuf, total * esz, rbuf, rbytes, false, 0, total,
+                      [&](const void *s, void *r, size_t, size_t, void *st) {
+                        return bine_reduce_scatter(e->comm, algo, s, r, rcounts, dt, o, st);
+                      });
 }
 
 int do_reduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype dtype, MPI_Op op, int root,
@@ -264,9 +400,10 @@ int do_reduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype
   if (rc) return rc;
   const size_t bytes = count * bine_dtype_size(dt);
   void *r = e->rank == root ? rbuf : nullptr;
-  return with_buffers(e, sbuf, bytes, r, r ? bytes : 0, false, [&](const void *s, void *rr, void *st) {
-    return bine_reduce(e->comm, algo, s, rr, count, dt, o, root, st);
-  });
+  return with_buffers(e, sbuf, bytes, r, r ? bytes : 0, false, 0, count,
+                      [&](const void *s, void *rr, size_t, size_t, void *st) {
+                        return bine_reduce(e->comm, algo, s, rr, count, dt, o, root, st);
+                      });
 }
 
 // allgather family: pure data movement, so it runs on bytes whatever the type
@@ -298,9 +435,10 @@ int do_allgather(int algo, const void *sbuf, size_t scount, MPI_Datatype sdtype,
   Entry *e;
   int rc = get_entry(comm, &e);
   if (rc) return rc;
-  return with_buffers(e, sbuf, bytes, rbuf, bytes * (size_t)e->size, false, [&](const void *s, void *r, void *st) {
-    return bine_allgather(e->comm, algo, s, r, bytes, BINE_UINT8, st);
-  });
+  return with_buffers(e, sbuf, bytes, rbuf, bytes * (size_t)e->size, false, 0, bytes,
+                      [&](const void *s, void *r, size_t, size_t, void *st) {
+                        return bine_allgather(e->comm, algo, s, r, bytes, BINE_UINT8, st);
+                      });
 }
 
 // bcast family: pure data movement on `buf` in place (read on the root,
@@ -315,9 +453,10 @@ int do_bcast(int algo, void *buf, size_t count, MPI_Datatype dtype, int root, MP
   Entry *e;
   int rc = get_entry(comm, &e);
   if (rc) return rc;
-  return with_buffers(e, MPI_IN_PLACE, 0, buf, bytes, true, [&](const void *, void *r, void *st) {
-    return bine_bcast(e->comm, algo, r, bytes, BINE_UINT8, root, st);
-  });
+  return with_buffers(e, MPI_IN_PLACE, 0, buf, bytes, true, 0, bytes,
+                      [&](const void *, void *r, size_t, size_t, void *st) {
+                        return bine_bcast(e->comm, algo, r, bytes, BINE_UINT8, root, st);
+                      });
 }
 
 int unsupported(const char *name) {

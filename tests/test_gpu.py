@@ -650,16 +650,21 @@ PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
 
 
 @pytest.mark.skipif(not os.path.exists(PICO_CORE), reason="reference pico_core not built (integration/Makefile)")
-@pytest.mark.parametrize("np_,coll,algo,dtype,flat", [
-    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", False),
-    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", True),
-    (2, "ALLREDUCE", "bine_lat_over", "double", True),
-    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "int64", True),
-    (2, "REDUCE", "bine_bdw_over", "float", False),
-    (2, "BCAST", "bine_lat_over", "float", False),
-    (2, "BCAST", "bine_lat_new_over", "int64", False),
+@pytest.mark.parametrize("np_,coll,algo,dtype,flat,count", [
+    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "1048576"),
+    # staged in pipelined chunks (libbine.so with_buffers): P = 1 is a copy, int64
+    # SUM is exact in any association -- both cut the buffer into 16 MiB chunks
+    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "67108864"),
+    (2, "ALLREDUCE", "bine_bdw_remap_over", "int64", False, "8388608"),
+    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "16777216"),
+    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", True, "1048576"),
+    (2, "ALLREDUCE", "bine_lat_over", "double", True, "1048576"),
+    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "int64", True, "1048576"),
+    (2, "REDUCE", "bine_bdw_over", "float", False, "1048576"),
+    (2, "BCAST", "bine_lat_over", "float", False, "1048576"),
+    (2, "BCAST", "bine_lat_new_over", "int64", False, "1048576"),
 ])
-def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat):
+def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat, count):
     """the reference's UNCHANGED pico_core (integration/Makefile links it against
     libbine.so) drives the GPU path through the libbine.h symbols and checks
     every result against MPICH's own PMPI_* collective (pico_core_utils.c:
@@ -669,7 +674,7 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat)
     env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
     if flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
-    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, "1048576",
+    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, count,
                         "5", algo, dtype], env=env, capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
     assert "Last Iter Time" in p.stdout

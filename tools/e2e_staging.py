@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""End-to-end rate with host buffers (north_star: "the end-to-end rate
+including H2D and D2H copies"): the reference's UNCHANGED pico_core
+(integration/_build/pico_core) through libbine.so, allreduce
+bine_bdw_remap_over, 256 MiB per rank, host (malloc) buffers -- per
+configuration the median of pico_core's own per-iteration times (its CSV,
+max over ranks, first 20 % dropped), every iteration checked by pico_core
+against PMPI_Allreduce.  Configurations: the staging pipeline's chunk
+(BINE_STAGE_CHUNK_BYTES) and page-locking on / off (BINE_HOST_REGISTER).
+usage: python tools/e2e_staging.py [NP] [DTYPE] [COUNT] [ITERS]"""
+import json
+import os
+import statistics
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(np_, dtype, count, iters, env_extra):
+    with tempfile.TemporaryDirectory() as tmp:
+        env = dict(os.environ, PICO_OUT=tmp, **env_extra)
+        if np_ > 1:
+            env["BINE_FAKE_HOSTS"] = "1"
+        p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), "ALLREDUCE",
+                            str(count), str(iters), "bine_bdw_remap_over", dtype], env=env, capture_output=True,
+                           text=True, timeout=300)
+        if p.returncode != 0:
+            return {"error": (p.stdout[-400:] + p.stderr[-400:])}
+        rows = open(os.path.join(tmp, "data", f"{count}_bine_bdw_remap_over_{dtype}.csv")).read().splitlines()[1:]
+        hi = [int(r.split(",")[0]) * 1e-6 for r in rows]   # ns -> ms
+        kept = hi[int(len(hi) * 0.2):]
+        return {"ms_median": round(statistics.median(kept), 3), "ms_min": round(min(kept), 3), "iters": len(hi),
+                "pico_core_check": "passed"}
+
+
+if __name__ == "__main__":
+    np_ = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    dtype = sys.argv[2] if len(sys.argv) > 2 else "float"
+    count = int(sys.argv[3]) if len(sys.argv) > 3 else 67108864
+    iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+    esz = {"float": 4, "double": 8, "int64": 8, "int32": 4}[dtype]
+    S = count * esz
+    out = {"np": np_, "dtype": dtype, "count": count, "bytes_per_rank": S}
+    cfgs = [("pageable, one collective (round-2 path)", {"BINE_HOST_REGISTER": "0", "BINE_STAGE_CHUNK_BYTES": str(1 << 40)}),
+            ("page-locked, one collective", {"BINE_STAGE_CHUNK_BYTES": str(1 << 40)}),
+            ("page-locked, 4 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(4 << 20)}),
+            ("page-locked, 8 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(8 << 20)}),
+            ("page-locked, 16 MiB chunks (default)", {}),
+            ("page-locked, 32 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(32 << 20)})]
+    for name, env in cfgs:
+        r = run(np_, dtype, count, iters, env)
+        if "ms_median" in r:
+            r["algbw_GBs"] = round(S / (r["ms_median"] * 1e-3) / 1e9, 2)
+            r["pcie_bytes_GBs"] = round(2 * S / (r["ms_median"] * 1e-3) / 1e9, 2)
+        out[name] = r
+        print(name, json.dumps(r), flush=True)
+    print(json.dumps(out))
