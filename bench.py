@@ -587,7 +587,7 @@ def apply_transport(comm, mode, chunk, graphs=False):
     comm.set_chunk(chunk)
 
 
-def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk, graphs=False):
+def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, chunk, graphs=False, dm_ok=False):
     """BASELINE configs C1, C4 and C5 on the transport chosen for C3 (C1: the
     bit-exact flat phases instead of multi-tree mode, a large-message mode;
     eager and graph-replayed), each checked against the oracle's digests of
@@ -615,6 +615,25 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
                 "algbw_per_rank_GBs": round(n1 * 4 / (st["median_ms"] * 1e-3) / 1e9, 2),
                 "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
     comm.set_graphs(False)
+    if dm_ok and "+dm" not in mode and world > 1:
+        # C1 also over the direct peer-memory transport with the flat phases:
+        # one k_dm_fused launch per call (the whole flat collective in one
+        # kernel), beside the RCCL path chosen for C3
+        try:
+            apply_transport(comm, "flatrs+flat+dm", chunk, False)
+            for algo in ("bine_bdw_remap", "bine_lat"):
+                rb.fill_(float("nan"))
+                st = timed(torch, stream,
+                           lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
+                           50, 10, dist, (comm.synchronize,))
+                ok, _ = check_digest(pico_amd, rb, n1, "float", gkey("C1", "allreduce", algo, "float", n1, world),
+                                     rank)
+                out[f"C1_allreduce_{algo}_f32_1MiB_direct_fused"] = {
+                    "us": round(st["median_ms"] * 1e3, 2),
+                    "algbw_per_rank_GBs": round(n1 * 4 / (st["median_ms"] * 1e-3) / 1e9, 2),
+                    "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
+        except pico_amd.BineError as e:   # symmetric: setup is agreed over RCCL
+            out["C1_direct_fused"] = {"error": str(e)}
     del sb, rb
     apply_transport(comm, mode, chunk, graphs)
     trees = mode == "trees"
@@ -973,7 +992,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
-                                                           chosen, chunk, graphs)) if extras else {}
+                                                           chosen, chunk, graphs, not dm_dead)) if extras else {}
     apply_transport(comm, chosen, chunk, graphs)
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}

@@ -163,6 +163,39 @@ struct DmArgs {
   DmMsg m[kMaxDm];
 };
 int launch_dm_move(const DmArgs &a, void *stream);
+
+// The whole flat-form small collective in ONE launch over the direct
+// transport (k_dm_fused): phase A pushes this rank's blocks into the peers'
+// inboxes; phase B waits for the peers' blocks and evaluates the reference's
+// reduction tree (the REDUCE_TREE primitive: own leaf at `pos`, the received
+// blocks read straight out of the inbox slots, `swap` per level) into `out`;
+// phase C pushes `out` to the peers and copies theirs out of the inbox (the
+// flat allgather; absent for the one-shot latency form).  Workgroup w handles
+// the same 1/wgs slice of every message in every phase, so a workgroup only
+// ever reads back what it wrote itself: no grid-wide barrier.  Messages use
+// the same slots, flags, counters and device-side sequence bases as
+// k_dm_move (j = the message's index among this launch's messages of its kind
+// to / from its peer).
+constexpr int kMaxFusedPeers = 15;  // P <= 16
+struct DmFusedArgs {
+  int wgs = 1, rank = 0;
+  uint64_t slot = 0;
+  uint8_t *own = nullptr;
+  uint32_t *poison_host = nullptr;
+  uint64_t timeout_ticks = 0;
+  int na = 0, nb = 0, nc = 0, nd = 0;  // phase A pushes, A pulls (tree leaves), C pushes, C pulls
+  DmMsg m[4 * kMaxFusedPeers];         // in that order
+  int nl = 0, pos = 0;
+  unsigned swap = 0;
+  int leaf[kMaxLeaves];                // leaf j != pos: index in m of the A pull carrying it
+  const void *own_leaf = nullptr;
+  void *out = nullptr;
+  uint64_t nvec = 0;                   // 16-B vectors per leaf / of out
+};
+// BINE_ERR_UNSUPPORTED: (dtype, op) has no fused instantiation (the caller
+// issues the primitives one by one)
+int launch_dm_fused(const DmFusedArgs &a, int dtype, int op, void *stream);
+bool dm_fused_supported(int dtype, int op);
 int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
 
 }  // namespace bine

@@ -570,6 +570,118 @@ static bool a2a_shape(const bine_comm *c, const std::vector<XSend> &s, const std
   return true;
 }
 
+// BINE_DIRECT_FUSED=0: small direct-transport collectives issue their
+// primitives one by one instead of k_dm_fused
+static bool fused_on() {
+  static const bool on = !getenv("BINE_DIRECT_FUSED") || atoi(getenv("BINE_DIRECT_FUSED")) != 0;
+  return on;
+}
+
+// The flat form of a small collective over the direct transport as ONE
+// launch (k_dm_fused, bine_internal.h DmFusedArgs) when its schedule is
+//   [exchange A][REDUCE_TREE over A's received blocks + the own leaf][exchange C]?
+// with exchange C (optional) sending the tree's output block and receiving
+// into the caller's buffer -- allreduce_bine_bdw_remap / _static / segmented
+// / rabenseifner ... with the flat phases, and the one-shot bine_lat.  The
+// kernel's workgroups each own the same slice of every message, so it is
+// correct only when no workgroup writes bytes another one may still read:
+// the tree's output overlaps no block exchange A sends, and every block
+// exchange C receives is disjoint from A's sends or exactly one of them (the
+// same slice then belongs to the same workgroup in both phases).  Returns -1
+// when the schedule or the arguments do not qualify (the caller then issues
+// the primitives).
+template <typename Ptr>
+static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, hipStream_t K) {
+  auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (!rt || !rt->dm_on || !rt->dm || c->profile || !fused_on() || op < 0 || !dm_fused_supported(dtype, op))
+    return -1;
+  const auto &ops = sc.ops;
+  if (ops.size() < 2 || ops.size() > 3 || !ops[0].xchg || ops[1].xchg || ops[1].prims.size() != 1 ||
+      ops[1].prims[0].type != BINE_PRIM_REDUCE_TREE || (ops.size() == 3 && !ops[2].xchg))
+    return -1;
+  const DirectState &d = *rt->dm;
+  const Prim &t = ops[1].prims[0];
+  const uint64_t tbytes = t.count * esz;
+  if (t.peer < 2 || t.peer > kMaxLeaves || t.pos < 0 || t.pos >= t.peer || tbytes % 16 || !tbytes) return -1;
+  DmFusedArgs a;
+  a.wgs = d.wgs;
+  a.rank = c->rank;
+  a.slot = d.slot;
+  a.own = (uint8_t *)d.own;
+  a.poison_host = d.hpoison_dev;
+  a.timeout_ticks = d.timeout_ticks;
+  a.nl = t.peer;
+  a.pos = t.pos;
+  a.swap = (unsigned)t.flags >> 8;
+  a.own_leaf = ptr(t.aux_buf, t.aux_off);
+  a.out = ptr(t.dst_buf, t.dst_off);
+  a.nvec = tbytes / 16;
+  for (int j = 0; j < kMaxLeaves; j++) a.leaf[j] = -1;
+  std::vector<int> js((size_t)c->size, 0), jr((size_t)c->size, 0);
+  struct Range { const char *lo, *hi; };
+  std::vector<Range> a_src;
+  auto overlap = [](Range x, Range y) { return x.lo < y.hi && y.lo < x.hi; };
+  const Range out_r{(const char *)a.out, (const char *)a.out + tbytes};
+  int n = 0;
+  auto add = [&](const Prim &x, bool push, const void *src, void *dst) -> bool {
+    if (n >= 4 * kMaxFusedPeers || x.peer < 0 || x.peer >= c->size || x.count * esz > d.slot) return false;
+    int &j = push ? js[(size_t)x.peer] : jr[(size_t)x.peer];
+    if (j >= dm::kSlots) return false;
+    DmMsg &m = a.m[n++];
+    m.src = (const uint8_t *)src;
+    m.dst = (uint8_t *)dst;
+    m.bytes = x.count * esz;
+    m.push = push ? 1 : 0;
+    m.peer = x.peer;
+    m.j = j++;
+    return true;
+  };
+  // exchange A: sends (any source but the tree's output), receives = the
+  // tree's non-own leaves (leaf k of the staging area: k-th leaf != pos)
+  for (const Prim &x : ops[0].prims)
+    if (x.type == BINE_PRIM_SEND) {
+      const char *p = ptr(x.src_buf, x.src_off);
+      const Range r{p, p + x.count * esz};
+      if (overlap(r, out_r) || !add(x, true, p, nullptr)) return -1;
+      a_src.push_back(r);
+      a.na++;
+    }
+  for (const Prim &x : ops[0].prims)
+    if (x.type == BINE_PRIM_RECV) {
+      if (x.dst_buf != t.src_buf || x.count != t.count || x.dst_off < t.src_off ||
+          (x.dst_off - t.src_off) % t.count)
+        return -1;
+      const uint64_t k = (x.dst_off - t.src_off) / t.count;
+      if (k >= (uint64_t)t.peer - 1) return -1;
+      const int leaf = (int)k < t.pos ? (int)k : (int)k + 1;
+      if (a.leaf[leaf] >= 0) return -1;
+      a.leaf[leaf] = n;
+      if (!add(x, false, nullptr, ptr(x.dst_buf, x.dst_off))) return -1;
+      a.nb++;
+    }
+  if (a.nb != t.peer - 1) return -1;
+  if (ops.size() == 3) {
+    for (const Prim &x : ops[2].prims)
+      if (x.type == BINE_PRIM_SEND) {  // the tree's output, re-read by the workgroup that wrote it
+        if (ptr(x.src_buf, x.src_off) != a.out || x.count != t.count || !add(x, true, a.out, nullptr)) return -1;
+        a.nc++;
+      }
+    for (const Prim &x : ops[2].prims)
+      if (x.type == BINE_PRIM_RECV) {
+        char *p = ptr(x.dst_buf, x.dst_off);
+        const Range r{p, p + x.count * esz};
+        if (overlap(r, out_r) || overlap(r, Range{(const char *)a.own_leaf, (const char *)a.own_leaf + tbytes}))
+          return -1;
+        for (const Range &y : a_src)
+          if (overlap(r, y) && (r.lo != y.lo || r.hi != y.hi)) return -1;
+        if (!add(x, false, nullptr, p)) return -1;
+        a.nd++;
+      }
+  }
+  const int rc = launch_dm_fused(a, dtype, op, K);
+  return rc == BINE_ERR_ARG || rc == BINE_ERR_UNSUPPORTED ? -1 : rc;  // not co-aligned etc.: the primitives
+}
+
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
                    hipStream_t K, bool single = false, bool joined = false) {
   char *base[6];
@@ -578,6 +690,10 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
   base[BINE_BUF_STAGE] = (char *)c->tmp[3];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
+  if (single) {  // a small collective over the direct transport: one launch when its form allows
+    const int rc = try_fused(c, sc, ptr, esz, dtype, op, K);
+    if (rc >= 0) return rc;
+  }
   hipStream_t C = single ? K : c->cstream;
   // stream-ordered transports (direct: sequence bases in device memory) need
   // every exchange of this call after every exchange of the previous one,

@@ -954,6 +954,235 @@ int launch_dm_move(const DmArgs &a, void *stream) {
 }
 
 // ----------------------------------------------------------------------------
+// k_dm_fused: a flat-form small collective in one launch (bine_internal.h
+// DmFusedArgs).  Flags, counters, slots and sequence bases are k_dm_move's.
+
+namespace dmf {
+using namespace dm;
+
+// where message m of this launch reads, writes, waits and publishes
+struct Msg {
+  const u32x4 *src;
+  u32x4 *dst;
+  const uint64_t *wait;  // nullptr: nothing to wait for
+  uint64_t wait_val;
+  uint64_t *sig;
+  uint32_t *cnt;
+  uint64_t seq, nvec;
+};
+
+__device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
+  Msg r;
+  uint8_t *own = a.own;
+  const uint64_t *base = reinterpret_cast<const uint64_t *>(own + (m.push ? kBaseSendOff : kBaseRecvOff)) + m.peer;
+  r.seq = __hip_atomic_load(base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
+  const size_t k = (size_t)(r.seq % kSlots);
+  uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
+  r.nvec = m.bytes / 16;
+  if (m.push) {
+    r.src = reinterpret_cast<const u32x4 *>(m.src);
+    r.dst = reinterpret_cast<u32x4 *>(remote + kFlagsBytes + ((size_t)a.rank * kSlots + k) * a.slot);
+    r.wait = r.seq > (uint64_t)kSlots
+                 ? reinterpret_cast<const uint64_t *>(own + kAckOff + ((size_t)m.peer * kSlots + k) * kFlagStride)
+                 : nullptr;
+    r.wait_val = r.seq - kSlots;
+    r.sig = reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
+    r.cnt = reinterpret_cast<uint32_t *>(own + kCntPushOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+  } else {
+    r.src = reinterpret_cast<const u32x4 *>(own + kFlagsBytes + ((size_t)m.peer * kSlots + k) * a.slot);
+    r.dst = reinterpret_cast<u32x4 *>(m.dst);
+    r.wait = reinterpret_cast<const uint64_t *>(own + kReadyOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+    r.wait_val = r.seq;
+    r.sig = reinterpret_cast<uint64_t *>(remote + kAckOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
+    r.cnt = reinterpret_cast<uint32_t *>(own + kCntPullOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+  }
+  return r;
+}
+
+// the whole workgroup: thread 0 polls (system-scope acquire loads, bounded),
+// everyone then acquires.  false: the transport is poisoned (now or earlier)
+__device__ __forceinline__ bool wait_flag(const DmFusedArgs &a, const uint64_t *p, uint64_t v) {
+  __shared__ int go;
+  uint32_t *poison = reinterpret_cast<uint32_t *>(a.own + kPoisonOff);
+  if (threadIdx.x == 0) {
+    int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
+    if (ok && p) {
+      const long long t0 = wall_clock64();
+      while (ld_acq_sys(p) < v) {
+        if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
+          __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ok = 0;
+          break;
+        }
+        if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    go = ok;
+  }
+  __syncthreads();
+  const bool ok = go != 0;
+  __syncthreads();  // `go` is reused by the next wait
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return ok;
+}
+
+// the whole workgroup, after its share of message m: release, count in; the
+// last workgroup of the message publishes seq (k_dm_move's protocol)
+__device__ __forceinline__ void arrive(const DmFusedArgs &a, const Msg &m) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(m.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == (uint32_t)a.wgs) {
+      __hip_atomic_store(m.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(m.sig, m.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// this workgroup's slice of a message of n vectors
+__device__ __forceinline__ void slice(uint64_t n, int wgs, uint64_t *lo, uint64_t *hi) {
+  *lo = n * blockIdx.x / (uint64_t)wgs;
+  *hi = n * (blockIdx.x + 1) / (uint64_t)wgs;
+}
+
+__device__ __forceinline__ void copy_slice(const Msg &m, int wgs) {
+  uint64_t lo, hi;
+  slice(m.nvec, wgs, &lo, &hi);
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) __builtin_nontemporal_store(__builtin_nontemporal_load(m.src + i), m.dst + i);
+}
+}  // namespace dmf
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
+  using namespace dmf;
+  const int nm = a.na + a.nb + a.nc + a.nd;
+  // phase A: our blocks into the peers' inboxes
+  for (int i = 0; i < a.na; i++) {
+    const Msg m = resolve(a, a.m[i]);
+    if (!wait_flag(a, m.wait, m.wait_val)) return;
+    copy_slice(m, a.wgs);
+    arrive(a, m);
+  }
+  // phase B: the peers' blocks, read in place in our inbox as the tree's leaves
+  const u32x4 *lp[kMaxLeaves];
+  for (int i = 0; i < a.nb; i++) {
+    const Msg m = resolve(a, a.m[a.na + i]);
+    if (!wait_flag(a, m.wait, m.wait_val)) return;
+  }
+#pragma unroll
+  for (int j = 0; j < kMaxLeaves; j++)
+    lp[j] = j >= a.nl ? nullptr
+            : j == a.pos ? reinterpret_cast<const u32x4 *>(a.own_leaf)
+                         : resolve(a, a.m[a.leaf[j]]).src;
+  {
+    u32x4 *out = reinterpret_cast<u32x4 *>(a.out);
+    uint64_t lo, hi;
+    slice(a.nvec, a.wgs, &lo, &hi);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+      u32x4 v[kMaxLeaves];
+#pragma unroll
+      for (int j = 0; j < kMaxLeaves; j++)
+        if (j < a.nl) v[j] = j == a.pos ? lp[j][i] : __builtin_nontemporal_load(lp[j] + i);
+      int lvl = 0;
+#pragma unroll
+      for (int w = 1; w < kMaxLeaves; w <<= 1, lvl++)
+#pragma unroll
+        for (int j = 0; j < kMaxLeaves; j += 2 * w)
+          if (j + w < a.nl) v[j] = comb16<T, OP>(v[j], v[j + w], (a.swap >> lvl) & 1);
+      out[i] = v[0];
+    }
+  }
+  // every leaf slice is read: the slots may be reused by their senders
+  for (int i = 0; i < a.nb; i++) arrive(a, resolve(a, a.m[a.na + i]));
+  // phase C: our result to the peers (this workgroup re-reads only what it
+  // wrote itself above), theirs out of our inbox
+  for (int i = 0; i < a.nc; i++) {
+    const Msg m = resolve(a, a.m[a.na + a.nb + i]);
+    if (!wait_flag(a, m.wait, m.wait_val)) return;
+    copy_slice(m, a.wgs);
+    arrive(a, m);
+  }
+  for (int i = 0; i < a.nd; i++) {
+    const Msg m = resolve(a, a.m[a.na + a.nb + a.nc + i]);
+    if (!wait_flag(a, m.wait, m.wait_val)) return;
+    copy_slice(m, a.wgs);
+    arrive(a, m);
+  }
+  // the launch's last workgroup advances the sequence bases (every workgroup
+  // has read them: each resolve() happened before its launch-counter add)
+  if (threadIdx.x == 0) {
+    uint32_t *lc = reinterpret_cast<uint32_t *>(a.own + dm::kLaunchCntOff);
+    const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (ol + 1 == gridDim.x) {
+      __hip_atomic_store(lc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = 0; i < nm; i++) {
+        uint64_t *bp = reinterpret_cast<uint64_t *>(a.own + (a.m[i].push ? dm::kBaseSendOff : dm::kBaseRecvOff)) +
+                       a.m[i].peer;
+        __hip_atomic_store(bp, __hip_atomic_load(bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+template <typename T, int OP>
+static hipError_t fused_launch(const DmFusedArgs &a, hipStream_t st) {
+  hipLaunchKernelGGL((k_dm_fused<T, OP>), dim3((unsigned)a.wgs), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t fused_t(const DmFusedArgs &a, int op, hipStream_t st) {
+#define CALL(OP) fused_launch<T, OP>(a, st)
+  BINE_OP_SWITCH(T, CALL)
+#undef CALL
+}
+
+bool dm_fused_supported(int dtype, int op) {
+  const bool t = dtype == BINE_FLOAT || dtype == BINE_DOUBLE || dtype == BINE_INT32 || dtype == BINE_INT64 ||
+                 dtype == BINE_UINT32 || dtype == BINE_UINT64;
+  return t && op >= BINE_SUM && op <= BINE_MIN;
+}
+
+int launch_dm_fused(const DmFusedArgs &a, int dtype, int op, void *stream) {
+  if (!dm_fused_supported(dtype, op)) return BINE_ERR_UNSUPPORTED;
+  const int nm = a.na + a.nb + a.nc + a.nd;
+  if (a.wgs < 1 || !a.own || !a.slot || a.nl < 2 || a.nl > kMaxLeaves || a.pos < 0 || a.pos >= a.nl ||
+      a.nb != a.nl - 1 || nm > 4 * kMaxFusedPeers || !a.out || !a.own_leaf)
+    return BINE_ERR_ARG;
+  for (int i = 0; i < nm; i++) {
+    const DmMsg &m = a.m[i];
+    if (m.peer < 0 || m.peer >= dm::kMaxPeers || m.j < 0 || m.j >= dm::kSlots || m.bytes > a.slot ||
+        m.bytes % 16 || ((uintptr_t)(m.push ? (const void *)m.src : (const void *)m.dst) & 15))
+      return BINE_ERR_ARG;
+  }
+  for (int j = 0; j < a.nl; j++)
+    if (j != a.pos && (a.leaf[j] < a.na || a.leaf[j] >= a.na + a.nb || a.m[a.leaf[j]].bytes != a.nvec * 16))
+      return BINE_ERR_ARG;
+  if (((uintptr_t)a.out & 15) || ((uintptr_t)a.own_leaf & 15)) return BINE_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case BINE_FLOAT: e = fused_t<float>(a, op, st); break;
+    case BINE_DOUBLE: e = fused_t<double>(a, op, st); break;
+    case BINE_INT32: e = fused_t<int32_t>(a, op, st); break;
+    case BINE_INT64: e = fused_t<int64_t>(a, op, st); break;
+    case BINE_UINT32: e = fused_t<uint32_t>(a, op, st); break;
+    case BINE_UINT64: e = fused_t<uint64_t>(a, op, st); break;
+    default: return BINE_ERR_UNSUPPORTED;
+  }
+  return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
 // pico_core input generator (glibc rand_r, LCG jump-ahead)
 // ----------------------------------------------------------------------------
 

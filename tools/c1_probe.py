@@ -38,7 +38,9 @@ def worker(rank, P, iters, port, q):
     pico_amd.fill_pico(sb, n, "float", 1234 + rank)
     stream = torch.cuda.current_stream()
     res = {}
-    for mode in ("direct", "flatrs+flat"):
+    # +dm: the direct peer-memory transport; with the flat phases a C1 call is
+    # then ONE k_dm_fused launch (BINE_DIRECT_FUSED=0: the primitives one by one)
+    for mode in ("direct", "flatrs+flat", "direct+dm", "flatrs+flat+dm"):
         bench.apply_transport(comm, mode, 0)
         for algo in ("bine_bdw_remap", "bine_lat"):
             st = bench.timed(torch, stream,

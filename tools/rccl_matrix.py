@@ -24,7 +24,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CASES = (("float", 4099), ("int64", 1001), ("int8", 333), ("float", 4096))  # 4096: equal blocks up to P = 16
+CASES = (("float", 4099), ("int64", 1001), ("int8", 333), ("float", 4096),  # 4096: equal blocks up to P = 16
+         ("int64", 2048))  # 16-B multiples per block: the one-launch direct form (k_dm_fused) applies
 # (name, relay_min_bytes, chunk_bytes, flat phases (1: allgather, 2: reduce-scatter, 4: one-to-all
 # exchanges as ncclAllGather, 8: all-peers exchanges as ncclAllToAllv, 16: HIP-graph mode,
 # 128: direct peer-memory transport),
@@ -38,7 +39,11 @@ SETTINGS = (("direct", 0, 0, 0, 0), ("chunk4KiB", 0, 4096, 0, 0), ("relay", 64, 
             ("graphs chunk1KiB x2", 0, 1024, 16, 1), ("graphs relay+flatrs+flat x2", 64, 1024, 16 | 3, 1),
             # the direct peer-memory transport (bit 128) instead of RCCL send/recv
             ("direct-mem", 0, 0, 128, 0), ("direct-mem relay chunk1KiB", 64, 1024, 128, 0),
-            ("direct-mem flatrs+flat x2", 0, 1024, 128 | 3, 1))
+            ("direct-mem flatrs+flat x2", 0, 1024, 128 | 3, 1),
+            # unchunked flat phases over the direct transport: small allreduces
+            # whose blocks are 16-B multiples run as ONE k_dm_fused launch
+            ("direct-mem flatrs+flat unchunked (fused)", 0, 0, 128 | 3, 0),
+            ("direct-mem flatrs+flat unchunked (fused) x2", 0, 0, 128 | 3, 1))
 
 
 def worker(rank, P, port, q):

@@ -118,6 +118,26 @@ __global__ __launch_bounds__(BS) void k_read8(Leaves L, f4 *sink, size_t nvec) {
   if (s.x == 12345.f) sink[threadIdx.x] = s;
 }
 
+// read-only ceiling of 8 / 9 streams with U vectors of each in flight per lane
+template <int BS, int U, int NS>
+__global__ __launch_bounds__(BS) void k_readn(Leaves L, const f4 *extra, f4 *sink, size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * BS * U + threadIdx.x;
+  f4 s = {0, 0, 0, 0};
+  f4 v[U][NS];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+      const size_t i = base + (size_t)u * BS;
+      v[u][j] = i < nvec ? __builtin_nontemporal_load((j < NL ? L.p[j] : extra) + i) : f4{0, 0, 0, 0};
+    }
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int j = 0; j < NS; j++) s += v[u][j];
+  if (s.x == 12345.f) sink[threadIdx.x] = s;
+}
+
 struct Var {
   std::string name;
   double bytes_per_elem;
@@ -201,6 +221,29 @@ int main() {
        [](const Leaves &L, f4 *, f4 *sk, size_t nv, hipStream_t st) {
          hipLaunchKernelGGL((k_read8<256, 1>), dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, L, sk, nv);
        }},
+      // r3: read-only ceilings with more in flight, and of all 9 streams the
+      // tree touches (the output buffer read instead of written)
+      {"read8 u2 (8S read only)", 4.0 * NL,
+       [](const Leaves &L, f4 *o, f4 *sk, size_t nv, hipStream_t st) {
+         hipLaunchKernelGGL((k_readn<256, 2, 8>), dim3((unsigned)((nv + 511) / 512)), dim3(256), 0, st, L, o, sk, nv);
+       }},
+      {"read8 u4 (8S read only)", 4.0 * NL,
+       [](const Leaves &L, f4 *o, f4 *sk, size_t nv, hipStream_t st) {
+         hipLaunchKernelGGL((k_readn<256, 4, 8>), dim3((unsigned)((nv + 1023) / 1024)), dim3(256), 0, st, L, o, sk,
+                            nv);
+       }},
+      {"read9 u2 (9S read only)", 4.0 * (NL + 1),
+       [](const Leaves &L, f4 *o, f4 *sk, size_t nv, hipStream_t st) {
+         hipLaunchKernelGGL((k_readn<256, 2, 9>), dim3((unsigned)((nv + 511) / 512)), dim3(256), 0, st, L, o, sk, nv);
+       }},
+      {"read9 u4 (9S read only)", 4.0 * (NL + 1),
+       [](const Leaves &L, f4 *o, f4 *sk, size_t nv, hipStream_t st) {
+         hipLaunchKernelGGL((k_readn<256, 4, 9>), dim3((unsigned)((nv + 1023) / 1024)), dim3(256), 0, st, L, o, sk,
+                            nv);
+       }},
+      mk<256, 4, 0, 1, 1, 0, 1>("bs256 u4 ntL ntO"),
+      mk<256, 4, 1, 1, 1, 0, 1>("bs256 u4 ntAll ntO"),
+      mk<256, 4, 0, 1, 0, 1, 2>("bs256 u4 ntL half 2tiles/wg"),
   };
   const int rounds = 7, iters = 40;
   std::vector<std::vector<float>> ms(vars.size());
