@@ -684,7 +684,10 @@ __device__ __forceinline__ void tree_tile(const u32x4 *const *lp, u32x4 *vo, siz
 #pragma unroll
       for (int g = 0; g < NG; g += 2 * w) part[u][g] = comb16<T, OP>(part[u][g], part[u][g + w], (swap >> lvl) & 1);
     const size_t i = base + (size_t)u * kBlock;
-    if (!GUARD || i < nvec) vo[i] = part[u][0];
+    // non-temporal stores: 23.91 vs 24.12 us at the C3 chunk shape, 0.99 of
+    // the 9 streams' read-only ceiling (profiles/r3_tree_variants.txt); nt
+    // stores keep the line in the XCD's L2 for the allgather that sends it
+    if (!GUARD || i < nvec) __builtin_nontemporal_store(part[u][0], vo + i);
   }
 }
 
@@ -1071,17 +1074,23 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
     copy_slice(m, a.wgs);
     arrive(a, m);
   }
-  // phase B: the peers' blocks, read in place in our inbox as the tree's leaves
-  const u32x4 *lp[kMaxLeaves];
-  for (int i = 0; i < a.nb; i++) {
+  // phase B: the peers' blocks, read in place in our inbox as the tree's
+  // leaves; each result vector goes to `out` and, for the flat allgather
+  // (phase C's pushes), straight from registers into every peer's slot --
+  // whose previous use must have been acknowledged first
+  for (int i = 0; i < a.nb + a.nc; i++) {
     const Msg m = resolve(a, a.m[a.na + i]);
     if (!wait_flag(a, m.wait, m.wait_val)) return;
   }
+  const u32x4 *lp[kMaxLeaves];
 #pragma unroll
   for (int j = 0; j < kMaxLeaves; j++)
     lp[j] = j >= a.nl ? nullptr
             : j == a.pos ? reinterpret_cast<const u32x4 *>(a.own_leaf)
                          : resolve(a, a.m[a.leaf[j]]).src;
+  u32x4 *cp[kMaxFusedPeers];
+#pragma unroll
+  for (int i = 0; i < kMaxFusedPeers; i++) cp[i] = i < a.nc ? resolve(a, a.m[a.na + a.nb + i]).dst : nullptr;
   {
     u32x4 *out = reinterpret_cast<u32x4 *>(a.out);
     uint64_t lo, hi;
@@ -1098,18 +1107,15 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
         for (int j = 0; j < kMaxLeaves; j += 2 * w)
           if (j + w < a.nl) v[j] = comb16<T, OP>(v[j], v[j + w], (a.swap >> lvl) & 1);
       out[i] = v[0];
+#pragma unroll
+      for (int c = 0; c < kMaxFusedPeers; c++)
+        if (c < a.nc) __builtin_nontemporal_store(v[0], cp[c] + i);
     }
   }
-  // every leaf slice is read: the slots may be reused by their senders
-  for (int i = 0; i < a.nb; i++) arrive(a, resolve(a, a.m[a.na + i]));
-  // phase C: our result to the peers (this workgroup re-reads only what it
-  // wrote itself above), theirs out of our inbox
-  for (int i = 0; i < a.nc; i++) {
-    const Msg m = resolve(a, a.m[a.na + a.nb + i]);
-    if (!wait_flag(a, m.wait, m.wait_val)) return;
-    copy_slice(m, a.wgs);
-    arrive(a, m);
-  }
+  // every leaf slice is read (the senders may reuse their slots) and every
+  // result slice is in the peers' inboxes
+  for (int i = 0; i < a.nb + a.nc; i++) arrive(a, resolve(a, a.m[a.na + i]));
+  // phase C: the peers' results out of our inbox
   for (int i = 0; i < a.nd; i++) {
     const Msg m = resolve(a, a.m[a.na + a.nb + a.nc + i]);
     if (!wait_flag(a, m.wait, m.wait_val)) return;

@@ -62,7 +62,7 @@ bool pin_host(const void *p, size_t n) {
     if (lo >= r.first && hi <= r.second) return true;
     if (lo < r.second && r.first < hi) return false;  // overlaps another registration: stay pageable
   }
-  if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterDefault) != hipSuccess) {
+  if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterMapped) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
@@ -253,6 +253,15 @@ int follow(Entry *e, hipStream_t dst, hipStream_t src) {
   return MPI_SUCCESS;
 }
 
+// device->host copies of the pipelined path: "dma" (hipMemcpyAsync, the
+// copy engines) or "kernel" (k_copy storing straight into the page-locked,
+// device-mapped host buffer, so host->device DMA and device->host stores run
+// on different engines); BINE_STAGE_D2H, default dma
+bool d2h_kernel() {
+  static const bool v = getenv("BINE_STAGE_D2H") && !strcmp(getenv("BINE_STAGE_D2H"), "kernel");
+  return v;
+}
+
 // staging chunk of the pipelined path (BINE_STAGE_CHUNK_BYTES, default 16 MiB)
 size_t stage_chunk_bytes() {
   static const size_t v = [] {
@@ -297,11 +306,15 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
     ds = d;
     pin_host(sbuf, sbytes);
   }
+  void *rbuf_dev = nullptr;  // rbuf as the device addresses it (page-locked and mapped), for d2h_kernel()
   if (stage_r) {
     void *d;
     if ((rc = stage(e, 1, rbytes, &d))) return rc;
     dr = d;
-    pin_host(rbuf, rbytes);
+    if (pin_host(rbuf, rbytes) && d2h_kernel() && hipHostGetDevicePointer(&rbuf_dev, rbuf, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      rbuf_dev = nullptr;
+    }
   }
   const bool fill_r = stage_r && (in_place || read_rbuf);  // (every earlier call has drained all three streams)
   const size_t ch = esz ? stage_chunk_bytes() / esz * esz : 0;
@@ -321,8 +334,13 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
       if (bst != BINE_SUCCESS) return to_mpi(bst);
       if (stage_r) {
         if ((rc = follow(e, e->d2h, st))) return rc;
-        if (hipMemcpyAsync((char *)rbuf + off, (char *)dr + off, len, hipMemcpyDeviceToHost, e->d2h) != hipSuccess)
+        if (rbuf_dev) {
+          if (bine_copy((char *)rbuf_dev + off, (char *)dr + off, len, (void *)e->d2h) != BINE_SUCCESS)
+            return MPI_ERR_OTHER;
+        } else if (hipMemcpyAsync((char *)rbuf + off, (char *)dr + off, len, hipMemcpyDeviceToHost, e->d2h) !=
+                   hipSuccess) {
           return MPI_ERR_OTHER;
+        }
       }
     }
   } else {

@@ -62,3 +62,16 @@ def test_direct_transport_orders_calls_across_streams():
     tail = "\n".join(r.stdout.splitlines()[-8:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=2" in r.stdout
+
+
+@pytest.mark.timeout(300)
+def test_c1_four_processes_every_transport():
+    """C1 (fp32 allreduce, 262,144 elements per rank, P = 4) in 4 real
+    processes: bine_bdw_remap and bine_lat over RCCL (literal and flat) and
+    over the direct transport (literal, and flat = ONE k_dm_fused launch per
+    call), every output vs the committed oracle digests (tools/c1_probe.py)"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "c1_probe.py"), "4", "30"], env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + "\n" + r.stderr[-2000:]
+    assert '"exitcodes": [0, 0, 0, 0]' in r.stdout

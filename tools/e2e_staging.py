@@ -48,7 +48,10 @@ if __name__ == "__main__":
             ("page-locked, 4 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(4 << 20)}),
             ("page-locked, 8 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(8 << 20)}),
             ("page-locked, 16 MiB chunks (default)", {}),
-            ("page-locked, 32 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(32 << 20)})]
+            ("page-locked, 32 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(32 << 20)}),
+            ("page-locked, 16 MiB chunks, device->host by kernel stores", {"BINE_STAGE_D2H": "kernel"}),
+            ("page-locked, 8 MiB chunks, device->host by kernel stores",
+             {"BINE_STAGE_D2H": "kernel", "BINE_STAGE_CHUNK_BYTES": str(8 << 20)})]
     for name, env in cfgs:
         r = run(np_, dtype, count, iters, env)
         if "ms_median" in r:
