@@ -239,8 +239,36 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
  * The allgather family (out of place) becomes one all-peers exchange after
  * its own plan has decided the status.  Pure data movement: results
  * identical bit for bit.  Off by default (the literal schedule;
- * BINE_FLAT_AG=1 turns it on); collective. */
+ * BINE_FLAT_AG=1 turns it on); collective.  on = 2 (BINE_FLAT_AG=2): with
+ * the flat reduce-scatter too, the allreduces' allgather is cut with the
+ * reduce-scatter's chunks, chunk k's results leaving right after chunk k+1's
+ * reduce-scatter exchange, so the output completes chunk by chunk. */
 int bine_comm_set_flat_ag(bine_comm_t comm, int on);
+
+/* Host-buffer collectives with the host<->device staging pipelined into the
+ * collective (libbine.so's path for pico_core's host buffers,
+ * pico_core_allreduce_utils.c:13-25).  `host_sbuf` / `host_rbuf` are host
+ * memory (page-locked for the copies to be asynchronous), `dev_sbuf` /
+ * `dev_rbuf` their device counterparts (workspaces of the same sizes).
+ * host_sbuf = BINE_IN_PLACE: in place, the input is host_rbuf (dev_sbuf
+ * unused).  The input is copied host -> device piece by piece on `h2d_stream`,
+ * each piece just before the first operation that touches it, and the output
+ * device -> host on `d2h_stream` piece by piece, each right after the
+ * operation that writes it last; the collective runs on `stream` (and the
+ * communicator's comm stream), which ends after the last copy back, so
+ * synchronizing `stream` completes the call.  For this call the flat forms
+ * are on (bine_comm_set_flat_rs, bine_comm_set_flat_ag(2)) where the algorithm
+ * has them: the same result bits as the reference (block ownership and every
+ * reduction tree follow the whole count, whatever the chunking), while the
+ * output completes chunk by chunk, so the two PCIe directions overlap each
+ * other and the exchanges.  `chunk_bytes` = bytes one exchange round carries
+ * over all blocks (0: 16 MiB).  Never graph-captured. */
+int bine_allreduce_staged(bine_comm_t comm, int algo, const void *host_sbuf, void *host_rbuf, void *dev_sbuf,
+                          void *dev_rbuf, size_t count, int dtype, int op, size_t segsize, size_t chunk_bytes,
+                          void *h2d_stream, void *d2h_stream, void *stream);
+int bine_reduce_scatter_staged(bine_comm_t comm, int algo, const void *host_sbuf, void *host_rbuf,
+                               void *dev_sbuf, void *dev_rbuf, const int *rcounts, int dtype, int op,
+                               size_t chunk_bytes, void *h2d_stream, void *d2h_stream, void *stream);
 
 /* Transport option for RCCL communicators (P >= 3): an exchange in which
  * every rank sends ONE buffer to all P-1 others and receives one message of
@@ -464,8 +492,10 @@ int64_t bine_plan(int algo, int nranks, int rank, size_t count, const int *rcoun
  * relay staging buffer the schedule uses.
  * relay_min_bytes > 0 selects relay mode as bine_comm_set_relay does; `mode`
  * bit 0 = multi-tree mode (bine_comm_set_trees), bit 1 = flat allgather
- * (bine_comm_set_flat_ag), bit 2 = flat reduce-scatter (bine_comm_set_flat_rs).  Returns the number of entries (may exceed cap) or
- * -status. */
+ * (bine_comm_set_flat_ag), bit 2 = flat reduce-scatter (bine_comm_set_flat_rs),
+ * bit 3 = the allgather cut with the flat reduce-scatter's chunks
+ * (bine_comm_set_flat_ag(2)).  Returns the number of entries (may exceed cap)
+ * or -status. */
 typedef struct {
   int32_t op;
   int32_t xchg;
@@ -477,6 +507,17 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
                            size_t esz, size_t segsize, int in_place, size_t chunk_bytes,
                            size_t relay_min_bytes, int mode, bine_sched_entry_t *out, int64_t cap,
                            int *c_join, int64_t *final_wait, uint64_t *workspace);
+
+/* The host staging of that schedule (bine_allreduce_staged, no relay):
+ * kind 0 = host->device pieces (op, lo, hi) in elements of the input buffer,
+ * copied before op; kind 1 = device->host pieces (op, lo, hi) of RBUF,
+ * copied after op; kind 2 = (op, h2d_wait): the newest op whose host->device
+ * batch op waits for (-1 as UINT64_MAX: none).  `out` holds 3 (kinds 0, 1)
+ * or 2 (kind 2) words per entry.  Returns the number of entries (may exceed
+ * cap) or -status. */
+int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                        size_t segsize, int in_place, size_t chunk_bytes, int mode, int kind, uint64_t *out,
+                        int64_t cap);
 
 #ifdef __cplusplus
 }

@@ -147,9 +147,11 @@ class Comm:
         allgather phase) as ncclAllGather + device copies; bit-identical."""
         check(lib().bine_comm_set_coll_ag(self.handle, int(on)), "bine_comm_set_coll_ag")
 
-    def set_flat_ag(self, on: bool) -> None:
+    def set_flat_ag(self, on) -> None:
         """Allreduce (remap / static, power-of-two P): one all-peers allgather
-        exchange after the Bine reduce-scatter; bit-identical; collective."""
+        exchange after the Bine reduce-scatter; bit-identical; collective.
+        on = 2: with the flat reduce-scatter, the allgather is cut with its
+        chunks (outputs complete chunk by chunk)."""
         check(lib().bine_comm_set_flat_ag(self.handle, int(on)), "bine_comm_set_flat_ag")
 
     def set_flat_rs(self, on: bool) -> None:
@@ -269,6 +271,28 @@ def reduce_scatter(algo, sbuf, rbuf, rcounts: Sequence[int], dtype, op: str, com
                                     _dtype(dtype, rbuf), OPS[op], _stream(stream, comm)), f"reduce_scatter_{algo}")
 
 
+def allreduce_staged(algo, host_sbuf, host_rbuf, dev_sbuf, dev_rbuf, count: int, dtype, op: str, comm: Comm,
+                     h2d_stream, d2h_stream, segsize: int = 0, chunk_bytes: int = 0, stream=None) -> None:
+    """bine_allreduce_staged: host buffers (page-locked) staged through the
+    device buffers piece by piece, pipelined with the collective; synchronize
+    `stream` to complete the call."""
+    check(lib().bine_allreduce_staged(comm.handle, _algo("allreduce", algo), _ptr(host_sbuf), _ptr(host_rbuf),
+                                      _ptr(dev_sbuf), _ptr(dev_rbuf), count, _dtype(dtype, dev_rbuf), OPS[op],
+                                      segsize, chunk_bytes, _stream(h2d_stream, comm), _stream(d2h_stream, comm),
+                                      _stream(stream, comm)), f"allreduce_staged_{algo}")
+
+
+def reduce_scatter_staged(algo, host_sbuf, host_rbuf, dev_sbuf, dev_rbuf, rcounts: Sequence[int], dtype, op: str,
+                          comm: Comm, h2d_stream, d2h_stream, chunk_bytes: int = 0, stream=None) -> None:
+    """bine_reduce_scatter_staged (see allreduce_staged)."""
+    rc = (ctypes.c_int * len(rcounts))(*rcounts)
+    check(lib().bine_reduce_scatter_staged(comm.handle, _algo("reduce_scatter", algo), _ptr(host_sbuf),
+                                           _ptr(host_rbuf), _ptr(dev_sbuf), _ptr(dev_rbuf), rc,
+                                           _dtype(dtype, dev_rbuf), OPS[op], chunk_bytes,
+                                           _stream(h2d_stream, comm), _stream(d2h_stream, comm),
+                                           _stream(stream, comm)), f"reduce_scatter_staged_{algo}")
+
+
 def reduce(algo, sbuf, rbuf, count: int, dtype, op: str, root: int, comm: Comm, stream=None) -> None:
     check(lib().bine_reduce(comm.handle, _algo("reduce", algo), _ptr(sbuf), _ptr(rbuf), count,
                             _dtype(dtype, sbuf if rbuf is None else rbuf), OPS[op], root, _stream(stream, comm)),
@@ -337,7 +361,7 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
     rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
     cj, fw, ws = ctypes.c_int(), ctypes.c_int64(), (ctypes.c_uint64 * 4)()
     args = (a, nranks, rank, count, rc, root, esz, segsize, int(in_place), chunk_bytes, relay_min_bytes,
-            int(trees) | (2 if flat_ag else 0) | (4 if flat_rs else 0))
+            int(trees) | (2 if flat_ag else 0) | (4 if flat_rs else 0) | (8 if flat_ag == 2 else 0))
     n = lib().bine_plan_schedule(*args, None, 0, ctypes.byref(cj), ctypes.byref(fw), ws)
     if n < 0:
         raise BineError(int(-n), f"schedule {coll}_{algo}")
@@ -355,6 +379,33 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
         return ops, bool(cj.value), int(fw.value), {"tmp_elems": [int(x) for x in ws[:3]],
                                                      "stage_elems": int(ws[3])}
     return ops, bool(cj.value), int(fw.value)
+
+
+def stage_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, esz: int = 4,
+               segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0, flat_ag=False, flat_rs: bool = False):
+    """The host staging of rank `rank`'s schedule (bine_plan_stage; host only):
+    (h2d, d2h, h2d_wait) with h2d / d2h = {op: [(lo, hi), ...]} element ranges
+    copied before / after op, h2d_wait = [newest op whose h2d batch op i waits
+    for, or -1]."""
+    a = _algo(coll, algo)
+    rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
+    mode = (2 if flat_ag else 0) | (4 if flat_rs else 0) | (8 if flat_ag == 2 else 0)
+    res = []
+    for kind, w in ((0, 3), (1, 3), (2, 2)):
+        args = (a, nranks, rank, count, rc, 0, esz, segsize, int(in_place), chunk_bytes, mode, kind)
+        n = lib().bine_plan_stage(*args, None, 0)
+        if n < 0:
+            raise BineError(int(-n), f"stage_plan {coll}_{algo}")
+        arr = (ctypes.c_uint64 * max(int(n) * w, 1))()
+        lib().bine_plan_stage(*args, arr, n)
+        if kind < 2:
+            d = {}
+            for k in range(int(n)):
+                d.setdefault(int(arr[3 * k]), []).append((int(arr[3 * k + 1]), int(arr[3 * k + 2])))
+            res.append(d)
+        else:
+            res.append([ctypes.c_int64(arr[2 * k + 1]).value for k in range(int(n))])
+    return tuple(res)
 
 
 def reduce_batch(ins, inouts, counts, dtype, op: str = "sum", stream=None) -> int:
@@ -481,4 +532,5 @@ __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3
            "rccl_version",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "bcast", "loopback_bcast", "reduce_batch",
-           "exchange", "vendor_allreduce", "reduce_tree"] + list(ENTRY_POINTS)
+           "exchange", "vendor_allreduce", "reduce_tree", "allreduce_staged", "reduce_scatter_staged",
+           "stage_plan"] + list(ENTRY_POINTS)

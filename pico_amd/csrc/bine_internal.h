@@ -46,6 +46,12 @@ struct PlanArgs {
   // elements (0: one chunk): chunk k's transfer overlaps chunk k-1's tree.
   bool flat_rs = false;
   size_t flat_chunk = 0;
+  // with flat_rs and flat_ag (allreduce): the allgather exchange cut with the
+  // reduce-scatter's chunks, chunk k's results sent right after chunk k+1's
+  // reduce-scatter exchange, so the outputs complete chunk by chunk (the staged
+  // host-buffer pipeline copies each chunk back as soon as it is final).  Pure
+  // data movement: result bits unchanged.
+  bool flat_ag_chunked = false;
 };
 
 Plan make_plan(const PlanArgs &a);
@@ -92,6 +98,20 @@ struct SchedCfg {
   bool in_place = false;
   size_t relay_min = 0;   // relay mode: smallest relayed part, elements (0: off)
 };
+
+// Host staging of a schedule (bine_allreduce_staged / bine_reduce_scatter_staged):
+// the input buffer (SBUF, or RBUF in place) is copied host -> device piece by
+// piece just before the first op that touches each piece, and the output
+// (RBUF) device -> host piece by piece right after the op that writes it last.
+// h2d[i] = input element ranges first touched by op i (copied before it);
+// h2d_wait[i] = the newest op whose h2d batch op i must wait for (-1: none);
+// d2h[i] = output element ranges op i writes last (copied after it).
+using Ivl = std::pair<uint64_t, uint64_t>;  // [lo, hi) in elements
+struct StageRanges {
+  std::vector<std::vector<Ivl>> h2d, d2h;
+  std::vector<int64_t> h2d_wait;
+};
+void stage_ranges(const Schedule &sc, bool in_place, StageRanges &out);
 
 // issue.cpp.  `all` = the plans of every rank (same arguments, rank varied);
 // needed only for relay mode (null: no relay).

@@ -340,7 +340,7 @@ struct bine_comm {
   bool trees = false;          // multi-tree mode (allreduce, P = 4 / 8)
   size_t chunk_bytes = 0;      // pipelining chunk (0: default_chunk_bytes())
   size_t single_stream_bytes = 1 << 20;  // collectives up to this size run on the caller's stream only
-  bool flat_ag = false;        // allreduce: one-step all-peers allgather phase
+  int flat_ag = 0;             // allreduce: one-step all-peers allgather phase (2: cut with the flat RS chunks)
   bool flat_rs = false;        // one-step all-peers reduce-scatter phase + tree kernel
   bool coll_a2a = false;       // all-peers exchanges as ncclAllToAllv (no relay / trees)
   hipStream_t last_user = nullptr;  // caller's stream of the latest collective
@@ -364,7 +364,9 @@ struct bine_comm {
   std::vector<hipEvent_t> ev;
   size_t ev_next = 0;
   std::map<std::string, std::pair<bine::Plan, bine::Schedule>> plans;
+  std::map<std::string, bine::StageRanges> stage_cache;  // host staging ranges per plan key
   std::vector<hipEvent_t> op_ev;  // scratch of execute()
+  std::vector<hipEvent_t> stage_ev;  // scratch of execute(): host staging batches
   // per-op device timing of the latest collective (bine_comm_set_profile)
   bool profile = false;
   struct OpTime { hipEvent_t a = nullptr, b = nullptr; int xchg = 0, nprims = 0; uint64_t bytes = 0; };
@@ -412,7 +414,7 @@ static int comm_setup(bine_comm *c) {
   HIP_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
   if (const char *e = getenv("BINE_RELAY_MIN_BYTES")) c->relay_min_bytes = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_TREES")) c->trees = atoi(e) != 0;
-  if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) != 0;
+  if (const char *e = getenv("BINE_FLAT_AG")) c->flat_ag = atoi(e) < 0 ? 0 : std::min(atoi(e), 2);
   if (const char *e = getenv("BINE_FLAT_RS")) c->flat_rs = atoi(e) != 0;
   if (const char *e = getenv("BINE_COLL_A2A")) c->coll_a2a = atoi(e) != 0;
   if (const char *e = getenv("BINE_GRAPHS")) c->graphs = atoi(e) != 0;
@@ -682,15 +684,25 @@ static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int 
   return rc == BINE_ERR_ARG || rc == BINE_ERR_UNSUPPORTED ? -1 : rc;  // not co-aligned etc.: the primitives
 }
 
+// Host staging of one call (bine_*_staged): the input buffer comes from
+// `in_host` piece by piece on the h2d stream, the output goes back to
+// `out_host` piece by piece on the d2h stream (StageRanges)
+struct Staging {
+  const char *in_host = nullptr;
+  char *out_host = nullptr;
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  const StageRanges *rg = nullptr;
+};
+
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
-                   hipStream_t K, bool single = false, bool joined = false) {
+                   hipStream_t K, bool single = false, bool joined = false, const Staging *stg = nullptr) {
   char *base[6];
   base[BINE_BUF_SBUF] = (char *)sbuf;
   base[BINE_BUF_RBUF] = (char *)rbuf;
   for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
   base[BINE_BUF_STAGE] = (char *)c->tmp[3];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
-  if (single) {  // a small collective over the direct transport: one launch when its form allows
+  if (single && !stg) {  // a small collective over the direct transport: one launch when its form allows
     const int rc = try_fused(c, sc, ptr, esz, dtype, op, K);
     if (rc >= 0) return rc;
   }
@@ -713,12 +725,34 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   }
   std::vector<XSend> &sends = c->xs;
   std::vector<XRecv> &recvs = c->xr;
+  // staging: the input buffer's device copy (SBUF, or RBUF in place) and the
+  // h2d batches' events; per stream, the newest batch already waited for
+  char *in_dev = sbuf == rbuf ? base[BINE_BUF_RBUF] : base[BINE_BUF_SBUF];
+  std::vector<hipEvent_t> &hev = c->stage_ev;
+  if (stg) hev.assign(sc.ops.size(), nullptr);
+  int64_t h_waited[2] = {-1, -1};
   for (size_t i = 0; i < sc.ops.size(); i++) {
     const SOp &o = sc.ops[i];
     hipStream_t st = o.xchg ? C : K;
     if (trace_on())
       fprintf(stderr, "bine[%d] op %zu/%zu %s wait %lld prims %zu\n", c->rank, i, sc.ops.size(),
               o.xchg ? "xchg" : "local", (long long)o.wait, o.prims.size());
+    if (stg) {
+      const StageRanges &g = *stg->rg;
+      if (!g.h2d[i].empty()) {
+        for (const Ivl &r : g.h2d[i])
+          HIP_TRY(hipMemcpyAsync(in_dev + r.first * esz, stg->in_host + r.first * esz, (r.second - r.first) * esz,
+                                 hipMemcpyHostToDevice, stg->h2d));
+        hev[i] = next_event(c);
+        HIP_TRY(hipEventRecord(hev[i], stg->h2d));
+      }
+      const int64_t w = g.h2d_wait[i];
+      int64_t &hw = h_waited[st == K ? 0 : 1];
+      if (w > hw) {
+        HIP_TRY(hipStreamWaitEvent(st, hev[(size_t)w], 0));
+        hw = w;
+      }
+    }
     if (o.wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
     if (roctx_on()) {
       char lbl[64];
@@ -763,6 +797,15 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       evs[i] = next_event(c);
       HIP_TRY(hipEventRecord(evs[i], st));
     }
+    if (stg && !stg->rg->d2h[i].empty()) {  // pieces of the output this op wrote last
+      if (int rc = stream_join(c, stg->d2h, st)) return rc;
+      for (const Ivl &r : stg->rg->d2h[i])
+        HIP_TRY(hipMemcpyAsync(stg->out_host + r.first * esz, base[BINE_BUF_RBUF] + r.first * esz,
+                               (r.second - r.first) * esz, hipMemcpyDeviceToHost, stg->d2h));
+    }
+  }
+  if (stg) {  // the caller's stream ends after the last copy back
+    if (int rc = stream_join(c, K, stg->d2h)) return rc;
   }
   if (sc.final_wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
   if (ordered) return stream_join(c, K, C);
@@ -780,8 +823,8 @@ static size_t chunk_elems(size_t chunk_bytes, size_t esz) {
 static std::string plan_key(const PlanArgs &a) {
   std::string k;
   char buf[160];
-  snprintf(buf, sizeof buf, "%d|%zu|%zu|%zu|%d|%d|%d|%d|", a.algo, a.count, a.esz, a.segsize, (int)a.in_place, a.root,
-           (int)a.flat_ag, (int)a.flat_rs);
+  snprintf(buf, sizeof buf, "%d|%zu|%zu|%zu|%d|%d|%d|%d|%d|", a.algo, a.count, a.esz, a.segsize, (int)a.in_place,
+           a.root, (int)a.flat_ag, (int)a.flat_ag_chunked, (int)a.flat_rs);
   k = buf;
   for (int x : a.rcounts) { k += std::to_string(x); k += ','; }
   return k;
@@ -881,8 +924,11 @@ constexpr size_t kCommChunk = ~(size_t)0;
 // op of the data-movement collectives (allgather family): no reduction runs
 constexpr int kOpNone = -1;
 
+// `stg` (host staging, bine_*_staged): the flat forms are forced on for the
+// call (bit-identical; the allgather cut with the reduce-scatter's chunks, so
+// the output completes chunk by chunk), never graph-captured
 static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbuf, int dtype, int op,
-                          size_t chunk_bytes, void *stream) {
+                          size_t chunk_bytes, void *stream, Staging *stg = nullptr) {
   if (!c) return BINE_ERR_ARG;
   if (dtype < 0 || dtype >= BINE_NUM_DTYPES) return BINE_ERR_UNSUPPORTED;
   if (op != kOpNone) {
@@ -898,8 +944,9 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   a.rank = c->rank;
   a.esz = bine_dtype_size(dtype);
   a.in_place = sbuf == BINE_IN_PLACE;
-  a.flat_ag = c->flat_ag;
-  a.flat_rs = c->flat_rs;
+  a.flat_ag = c->flat_ag != 0 || stg;
+  a.flat_ag_chunked = c->flat_ag == 2 || stg;
+  a.flat_rs = c->flat_rs || stg;
   const size_t ch = chunk_elems(chunk_bytes, a.esz);
   const std::string key = plan_key(a) + "|" + std::to_string(ch) + "|" + std::to_string(c->relay_min_bytes) +
                           (c->trees ? "|T" : "");
@@ -927,12 +974,21 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     roctxRangePushA(lbl);
   }
   const bool single = bytes <= c->single_stream_bytes;
+  if (stg) {
+    auto sit = c->stage_cache.find(key);
+    if (sit == c->stage_cache.end()) {
+      StageRanges g;
+      stage_ranges(sc, a.in_place, g);
+      sit = c->stage_cache.emplace(key, std::move(g)).first;
+    }
+    stg->rg = &sit->second;
+  }
   rc = order_begin(c, K);
   if (rc) {
-  } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on())
+  } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && !stg)
     rc = run_graph(c, key, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
   else
-    rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
+    rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single, false, stg);
   if (!rc) rc = order_end(c, K);
   if (roctx_on()) roctxRangePop();
   return rc;
@@ -1231,6 +1287,46 @@ int bine_reduce_scatter(bine_comm_t c, int algo, const void *sbuf, void *rbuf, c
   return run_collective(c, a, sbuf, rbuf, dtype, op, kCommChunk, stream);
 }
 
+// host staging: `per` = flat pipeline chunk per block piece, from the bytes one
+// exchange round carries over all blocks
+static int run_staged(bine_comm_t c, PlanArgs &a, const void *host_sbuf, void *host_rbuf, void *dev_sbuf,
+                      void *dev_rbuf, int dtype, int op, size_t chunk_bytes, void *h2d, void *d2h, void *stream) {
+  if (!c || !host_rbuf || !dev_rbuf || !h2d || !d2h) return BINE_ERR_ARG;
+  const bool in_place = host_sbuf == BINE_IN_PLACE;
+  if (!in_place && (!host_sbuf || !dev_sbuf)) return BINE_ERR_ARG;
+  Staging g;
+  g.in_host = (const char *)(in_place ? host_rbuf : host_sbuf);
+  g.out_host = (char *)host_rbuf;
+  g.h2d = (hipStream_t)h2d;
+  g.d2h = (hipStream_t)d2h;
+  const size_t per = std::max<size_t>((chunk_bytes ? chunk_bytes : (size_t)16 << 20) / (size_t)c->size, 64 << 10);
+  return run_collective(c, a, in_place ? BINE_IN_PLACE : dev_sbuf, dev_rbuf, dtype, op, per, stream, &g);
+}
+
+int bine_allreduce_staged(bine_comm_t c, int algo, const void *host_sbuf, void *host_rbuf, void *dev_sbuf,
+                          void *dev_rbuf, size_t count, int dtype, int op, size_t segsize, size_t chunk_bytes,
+                          void *h2d_stream, void *d2h_stream, void *stream) {
+  if (algo < BINE_AR_RECURSIVEDOUBLING || algo > BINE_AR_BINE_BLOCK_BY_BLOCK_ANY_EVEN) return BINE_ERR_UNSUPPORTED;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  a.segsize = segsize;
+  return run_staged(c, a, host_sbuf, host_rbuf, dev_sbuf, dev_rbuf, dtype, op, chunk_bytes, h2d_stream,
+                    d2h_stream, stream);
+}
+
+int bine_reduce_scatter_staged(bine_comm_t c, int algo, const void *host_sbuf, void *host_rbuf, void *dev_sbuf,
+                               void *dev_rbuf, const int *rcounts, int dtype, int op, size_t chunk_bytes,
+                               void *h2d_stream, void *d2h_stream, void *stream) {
+  if (algo < BINE_RS_RECURSIVEHALVING || algo > BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_EVEN) return BINE_ERR_UNSUPPORTED;
+  if (!c || !rcounts) return BINE_ERR_ARG;
+  PlanArgs a;
+  a.algo = algo;
+  a.rcounts.assign(rcounts, rcounts + c->size);
+  return run_staged(c, a, host_sbuf, host_rbuf, dev_sbuf, dev_rbuf, dtype, op, chunk_bytes, h2d_stream,
+                    d2h_stream, stream);
+}
+
 int bine_reduce(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int op, int root,
                 void *stream) {
   if (algo != BINE_RD_BINE_LAT && algo != BINE_RD_BINE_BDW) return BINE_ERR_UNSUPPORTED;
@@ -1391,6 +1487,7 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
   PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
   a.flat_ag = (mode & 2) != 0;
   a.flat_rs = (mode & 4) != 0;
+  a.flat_ag_chunked = (mode & 8) != 0;
   Plan p;
   Schedule sc;
   build(a, chunk_elems(chunk_bytes, esz), relay_min_bytes, (mode & 1) != 0, p, sc);
@@ -1406,6 +1503,35 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
   if (workspace) {
     for (int t = 0; t < 3; t++) workspace[t] = p.tmp_elems[t];
     workspace[3] = sc.stage_elems;
+  }
+  return n;
+}
+
+int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                        size_t segsize, int in_place, size_t chunk_bytes, int mode, int kind, uint64_t *out,
+                        int64_t cap) {
+  if (!esz || kind < 0 || kind > 2) return -(int64_t)BINE_ERR_ARG;
+  PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, segsize, in_place);
+  a.flat_ag = (mode & 2) != 0;
+  a.flat_rs = (mode & 4) != 0;
+  a.flat_ag_chunked = (mode & 8) != 0;
+  Plan p;
+  Schedule sc;
+  build(a, chunk_elems(chunk_bytes, esz), 0, (mode & 1) != 0, p, sc);
+  if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
+  StageRanges g;
+  stage_ranges(sc, a.in_place, g);
+  int64_t n = 0;
+  for (size_t i = 0; i < sc.ops.size(); i++) {
+    if (kind == 2) {  // (op, h2d_wait)
+      if (n < cap) { out[2 * n] = i; out[2 * n + 1] = (uint64_t)g.h2d_wait[i]; }
+      n++;
+      continue;
+    }
+    for (const Ivl &r : kind == 0 ? g.h2d[i] : g.d2h[i]) {  // (op, lo, hi)
+      if (n < cap) { out[3 * n] = i; out[3 * n + 1] = r.first; out[3 * n + 2] = r.second; }
+      n++;
+    }
   }
   return n;
 }
@@ -1500,7 +1626,8 @@ int bine_comm_set_direct_wgs(bine_comm_t c, int wgs) {
 int bine_comm_set_flat_ag(bine_comm_t c, int on) {
   if (!c) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  c->flat_ag = on != 0;
+  if (on < 0 || on > 2) return BINE_ERR_ARG;
+  c->flat_ag = on;
   return BINE_SUCCESS;
 }
 

@@ -413,4 +413,125 @@ void make_schedule(const Plan &plan, const std::vector<Plan> *all, int rank, con
   if (out.final_wait >= 0) out.signals[(size_t)out.final_wait] = 1;
 }
 
+// ---- host staging -------------------------------------------------------------
+
+namespace {
+
+// element ranges op `o` reads (rd) and writes (wr) in buffer `buf` (SBUF
+// counts as RBUF in place, as in the dependency pass above)
+void touched(const SOp &o, int buf, bool in_place, std::vector<Ivl> *rd, std::vector<Ivl> *wr) {
+  auto add = [&](std::vector<Ivl> *v, int b, uint64_t off, uint64_t n) {
+    if (in_place && b == BINE_BUF_SBUF) b = BINE_BUF_RBUF;
+    if (v && b == buf && n) v->push_back({off, off + n});
+  };
+  for (const Prim &p : o.prims) {
+    switch (p.type) {
+      case BINE_PRIM_SEND: add(rd, p.src_buf, p.src_off, p.count); break;
+      case BINE_PRIM_RECV: add(wr, p.dst_buf, p.dst_off, p.count); break;
+      case BINE_PRIM_REDUCE:
+        add(rd, p.src_buf, p.src_off, p.count);
+        add(rd, p.dst_buf, p.dst_off, p.count);
+        add(wr, p.dst_buf, p.dst_off, p.count);
+        break;
+      case BINE_PRIM_REDUCE3:
+        add(rd, p.src_buf, p.src_off, p.count);
+        add(rd, p.aux_buf, p.aux_off, p.count);
+        add(wr, p.dst_buf, p.dst_off, p.count);
+        break;
+      case BINE_PRIM_REDUCE_TREE:
+        add(rd, p.aux_buf, p.aux_off, p.count);
+        add(rd, p.src_buf, p.src_off, (uint64_t)(p.peer - 1) * p.count);
+        add(wr, p.dst_buf, p.dst_off, p.count);
+        break;
+      default:  // COPY
+        add(rd, p.src_buf, p.src_off, p.count);
+        add(wr, p.dst_buf, p.dst_off, p.count);
+    }
+  }
+}
+
+// sorted, disjoint, merged interval set
+struct IvlSet {
+  std::vector<Ivl> v;
+  // pieces of [lo, hi) not in the set
+  void minus(uint64_t lo, uint64_t hi, std::vector<Ivl> &out) const {
+    auto it = std::upper_bound(v.begin(), v.end(), Ivl{lo, ~(uint64_t)0});
+    if (it != v.begin() && std::prev(it)->second > lo) --it;
+    uint64_t at = lo;
+    for (; it != v.end() && it->first < hi; ++it) {
+      if (it->first > at) out.push_back({at, it->first});
+      at = std::max(at, it->second);
+    }
+    if (at < hi) out.push_back({at, hi});
+  }
+  void add(uint64_t lo, uint64_t hi) {
+    if (lo >= hi) return;
+    auto it = std::lower_bound(v.begin(), v.end(), Ivl{lo, 0});
+    if (it != v.begin() && std::prev(it)->second >= lo) --it;
+    auto end = it;
+    while (end != v.end() && end->first <= hi) {
+      lo = std::min(lo, end->first);
+      hi = std::max(hi, end->second);
+      ++end;
+    }
+    it = v.erase(it, end);
+    v.insert(it, {lo, hi});
+  }
+};
+
+void merge_adjacent(std::vector<Ivl> &x) {
+  std::sort(x.begin(), x.end());
+  std::vector<Ivl> m;
+  for (const Ivl &r : x) {
+    if (!m.empty() && r.first <= m.back().second) m.back().second = std::max(m.back().second, r.second);
+    else m.push_back(r);
+  }
+  x.swap(m);
+}
+
+}  // namespace
+
+void stage_ranges(const Schedule &sc, bool in_place, StageRanges &out) {
+  const size_t n = sc.ops.size();
+  const int in_buf = in_place ? BINE_BUF_RBUF : BINE_BUF_SBUF;
+  out.h2d.assign(n, {});
+  out.d2h.assign(n, {});
+  out.h2d_wait.assign(n, -1);
+  // forward: first touch of every input piece; `who` remembers which op's
+  // batch staged each piece (a later toucher waits for that batch)
+  IvlSet covered;
+  std::vector<std::pair<Ivl, int64_t>> who;
+  std::vector<Ivl> rd, wr, fresh;
+  for (size_t i = 0; i < n; i++) {
+    rd.clear();
+    wr.clear();
+    touched(sc.ops[i], in_buf, in_place, &rd, &wr);
+    rd.insert(rd.end(), wr.begin(), wr.end());
+    int64_t w = -1;
+    for (const Ivl &r : rd) {
+      fresh.clear();
+      covered.minus(r.first, r.second, fresh);
+      for (const Ivl &f : fresh) {
+        covered.add(f.first, f.second);
+        out.h2d[i].push_back(f);
+        who.push_back({f, (int64_t)i});
+        w = (int64_t)i;
+      }
+      for (const auto &q : who)  // pieces staged by earlier batches
+        if (q.first.first < r.second && r.first < q.first.second) w = std::max(w, q.second);
+    }
+    merge_adjacent(out.h2d[i]);
+    out.h2d_wait[i] = w;
+  }
+  // backward: the last write of every output piece
+  IvlSet later;
+  for (size_t i = n; i-- > 0;) {
+    wr.clear();
+    touched(sc.ops[i], BINE_BUF_RBUF, in_place, nullptr, &wr);
+    for (const Ivl &r : wr) later.minus(r.first, r.second, out.d2h[i]);
+    for (const Ivl &r : wr) later.add(r.first, r.second);
+    merge_adjacent(out.d2h[i]);
+  }
+}
+
 }  // namespace bine

@@ -206,6 +206,16 @@ int get_entry(MPI_Comm comm, Entry **out) {
   MPI_Bcast(id, BINE_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
   st = bine_comm_init_rccl(&e->comm, e->size, e->rank, id, device);
   if (st != BINE_SUCCESS) { delete e; return to_mpi(st); }
+  // BINE_DIRECT=1: exchanges over the direct peer-memory transport instead of
+  // RCCL P2P (bine_comm_set_direct; collective, and every rank of a pico_core
+  // run sees the same environment).  Setup is agreed over RCCL, so a failure
+  // is the same on every rank: then the communicator keeps RCCL.
+  const char *dm = getenv("BINE_DIRECT");
+  if (e->size > 1 && dm && atoi(dm) > 0) {
+    const int dst = bine_comm_set_direct(e->comm, 1);
+    if (dst != BINE_SUCCESS && e->rank == 0)
+      fprintf(stderr, "libbine(amd): BINE_DIRECT=1 but the direct transport is unavailable (%d); using RCCL\n", dst);
+  }
   MPI_Comm_set_attr(comm, g_keyval, e);
   g_entries.insert(e);
   *out = e;
@@ -360,6 +370,46 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
   return to_mpi(bine_comm_synchronize(e->comm));
 }
 
+// The staging pipelined into the collective itself (bine_*_staged): for
+// collectives whose result bits follow the whole count's block ownership
+// (floating point at P > 1), so they cannot be cut into independent calls.
+// The core copies each input piece in just before the first operation that
+// touches it and each output piece back right after its last writer, with the
+// flat forms on (bit-identical) so the output completes chunk by chunk.  Used
+// when both buffers are on the host and the input spans at least two staging
+// chunks; BINE_STAGE_PIPELINE=0 keeps the serial H2D -> collective -> D2H.
+bool staged_pipeline_on() {
+  static const bool v = !getenv("BINE_STAGE_PIPELINE") || atoi(getenv("BINE_STAGE_PIPELINE")) != 0;
+  return v;
+}
+
+template <typename G>
+int with_staged(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes, G body) {
+  hipStream_t st = (hipStream_t)bine_comm_stream(e->comm);
+  (void)hipSetDevice(bine_comm_device(e->comm));
+  const bool in_place = sbuf == MPI_IN_PLACE;
+  int rc;
+  if ((rc = copy_streams(e))) return rc;
+  void *ds = nullptr, *dr = nullptr;
+  if (!in_place) {
+    if ((rc = stage(e, 0, sbytes, &ds))) return rc;
+    pin_host(sbuf, sbytes);
+  }
+  if ((rc = stage(e, 1, rbytes, &dr))) return rc;
+  pin_host(rbuf, rbytes);
+  const int bst = body(in_place ? BINE_IN_PLACE : sbuf, rbuf, ds, dr, (void *)e->h2d, (void *)e->d2h, (void *)st);
+  if (bst != BINE_SUCCESS) return to_mpi(bst);
+  if (hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
+  return to_mpi(bine_comm_synchronize(e->comm));
+}
+
+// both buffers on the host and large enough for the pipeline to pay
+bool use_staged(const void *sbuf, size_t sbytes, const void *rbuf, size_t rbytes) {
+  if (!staged_pipeline_on() || !rbuf || !rbytes || on_device(rbuf)) return false;
+  if (sbuf != MPI_IN_PLACE && (!sbuf || on_device(sbuf))) return false;
+  return std::max(sbytes, rbytes) >= 2 * stage_chunk_bytes();
+}
+
 int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype dtype, MPI_Op op,
                  MPI_Comm comm) {
   const int dt = map_dtype(dtype), o = map_op(op, dtype);
@@ -380,6 +430,13 @@ int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datat
   // depend on the tree (block ownership follows the count): one collective.
   const bool integer = dt <= BINE_UINT64;
   const bool separable = e->size == 1 || integer;
+  if (!separable && use_staged(sbuf, bytes, rbuf, bytes))
+    return with_staged(e, sbuf, bytes, rbuf, bytes,
+                       [&](const void *hs, void *hr, void *ds, void *dr, void *h2d, void *d2h, void *st) {
+                         return bine_allreduce_staged(e->comm, algo, hs, hr, ds, dr, count, dt, o,
+                                                      algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? seg : 0,
+                                                      stage_chunk_bytes(), h2d, d2h, st);
+                       });
   return with_buffers(e, sbuf, bytes, rbuf, bytes, false, separable ? esz : 0, count,
                       [&](const void *s, void *r, size_t, size_t n, void *st) {
                         return bine_allreduce(e->comm, algo, s, r, n, dt, o,
@@ -401,6 +458,12 @@ int do_reduce_scatter(int algo, const void *sbuf, void *rbuf, const int rcounts[
   const bool in_place = sbuf == MPI_IN_PLACE;
   // MPI_IN_PLACE: the input is the whole rbuf
   const size_t rbytes = (in_place ? total : (size_t)rcounts[e->rank]) * esz;
+  if (e->size > 1 && use_staged(sbuf, total * esz, rbuf, rbytes))
+    return with_staged(e, sbuf, total * esz, rbuf, rbytes,
+                       [&](const void *hs, void *hr, void *ds, void *dr, void *h2d, void *d2h, void *st) {
+                         return bine_reduce_scatter_staged(e->comm, algo, hs, hr, ds, dr, rcounts, dt, o,
+                                                           stage_chunk_bytes(), h2d, d2h, st);
+                       });
   return with_buffers(e, sbuf, total * esz, rbuf, rbytes, false, 0, total,
                       [&](const void *s, void *r, size_t, size_t, void *st) {
                         return bine_reduce_scatter(e->comm, algo, s, r, rcounts, dt, o, st);

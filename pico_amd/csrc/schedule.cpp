@@ -260,16 +260,42 @@ bool flat_rs_fits(const PlanArgs &a) { return a.flat_rs && a.P >= 2 && a.P <= kM
 // chunk with one REDUCE_TREE into (out, out_off).  `leaves` = the tree of the
 // block this rank computes (this rank's own contribution is one of them, not
 // necessarily the first: send_remap / static hand the block to another rank).
-void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &boff,
+//
+// `ag`: the caller's flat allgather follows (every rank sends the block it
+// computed, RB[boff[x], bcnt[x]], to every other).  With
+// PlanArgs::flat_ag_chunked that allgather is cut with the same chunks and
+// emitted here, chunk k's results leaving right after chunk k+1's
+// reduce-scatter exchange (so the comm stream never waits for a tree with
+// nothing else to move); returns true when it did (the caller then skips its
+// own).  Pure data movement: the same bytes in the same places.
+static bool flat_ag_here(const PlanArgs &a, bool ag, int out, uint64_t out_off, uint64_t own_off) {
+  return ag && a.flat_ag && a.flat_ag_chunked && out == RB && out_off == own_off;
+}
+
+static void flat_ag_chunk(Builder &b, const PlanArgs &a, const std::vector<uint64_t> &boff,
+                          const std::vector<uint64_t> &bcnt, uint64_t o, uint64_t ch) {
+  const int P = a.P, r = a.rank;
+  const uint64_t mine = bcnt[(size_t)r];
+  const uint64_t cl = o < mine ? std::min(ch, mine - o) : 0;
+  for (int x = 0; x < P; x++)
+    if (x != r) b.send(x, RB, boff[(size_t)r] + o, cl);
+  for (int x = 0; x < P; x++)
+    if (x != r && o < bcnt[(size_t)x]) b.recv(x, RB, boff[(size_t)x] + o, std::min(ch, bcnt[(size_t)x] - o));
+  b.end();
+}
+
+bool flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &boff,
              const std::vector<uint64_t> &bcnt, const std::vector<int> &leaves, int out, uint64_t out_off,
-             unsigned swap = 0) {
+             unsigned swap = 0, bool ag = false) {
   const int P = a.P, r = a.rank;
   uint64_t cmax = 0;
   for (int x = 0; x < P; x++) cmax = std::max(cmax, bcnt[(size_t)x]);
   const uint64_t mine = bcnt[(size_t)r];
   const uint64_t ch = a.flat_chunk ? a.flat_chunk : std::max<uint64_t>(cmax, 1);
+  const bool agc = flat_ag_here(a, ag, out, out_off, boff[(size_t)r]);
   b.tmp(T0, (uint64_t)(P - 1) * mine);
-  for (uint64_t k = 0; k * ch < cmax; k++) {
+  uint64_t k = 0;
+  for (; k * ch < cmax; k++) {
     const uint64_t o = k * ch;
     for (int x = 0; x < P; x++)
       if (x != r && o < bcnt[(size_t)x]) b.send(x, src, boff[(size_t)x] + o, std::min(ch, bcnt[(size_t)x] - o));
@@ -280,8 +306,11 @@ void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t>
       b.recv(leaves[(size_t)j], T0, base + (uint64_t)slot++ * cl, cl);
     }
     b.end();
+    if (agc && k > 0) flat_ag_chunk(b, a, boff, bcnt, o - ch, ch);
     b.reduce_tree(P, pos, src, boff[(size_t)r] + o, T0, base, out, out_off + o, cl, swap);
   }
+  if (agc && k > 0) flat_ag_chunk(b, a, boff, bcnt, (k - 1) * ch, ch);
+  return agc;
 }
 
 // The rings' reduction is a chain, not a balanced tree: block b travels the
@@ -290,24 +319,30 @@ void flat_rs(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t>
 // chain folded over the staged leaves (`order` = leaf ranks in chain order,
 // this rank's own leaf last) with P-1 pairwise reductions, each on a staged
 // slot, the last one into (out, out_off).
-void flat_chain(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &boff,
-                const std::vector<uint64_t> &bcnt, const std::vector<int> &order, int out, uint64_t out_off) {
+bool flat_chain(Builder &b, const PlanArgs &a, int src, const std::vector<uint64_t> &boff,
+                const std::vector<uint64_t> &bcnt, const std::vector<int> &order, int out, uint64_t out_off,
+                bool ag = false) {
   const int P = a.P, r = a.rank;
   uint64_t cmax = 0;
   for (int x = 0; x < P; x++) cmax = std::max(cmax, bcnt[(size_t)x]);
   const uint64_t mine = bcnt[(size_t)r];
   const uint64_t ch = a.flat_chunk ? a.flat_chunk : std::max<uint64_t>(cmax, 1);
+  const bool agc = flat_ag_here(a, ag, out, out_off, boff[(size_t)r]);
   b.tmp(T0, (uint64_t)(P - 1) * mine);
-  for (uint64_t k = 0; k * ch < cmax; k++) {
+  uint64_t k = 0;
+  for (; k * ch < cmax; k++) {
     const uint64_t o = k * ch;
     for (int x = 0; x < P; x++)
       if (x != r && o < bcnt[(size_t)x]) b.send(x, src, boff[(size_t)x] + o, std::min(ch, bcnt[(size_t)x] - o));
     const uint64_t base = (uint64_t)(P - 1) * o, cl = o < mine ? std::min(ch, mine - o) : 0;
     for (int j = 0; j + 1 < P; j++) b.recv(order[(size_t)j], T0, base + (uint64_t)j * cl, cl);
     b.end();
+    if (agc && k > 0) flat_ag_chunk(b, a, boff, bcnt, o - ch, ch);
     for (int j = 1; j + 1 < P; j++) b.reduce(T0, base + (uint64_t)(j - 1) * cl, T0, base + (uint64_t)j * cl, cl);
     b.reduce3(T0, base + (uint64_t)(P - 2) * cl, src, boff[(size_t)r] + o, out, out_off + o, cl);
   }
+  if (agc && k > 0) flat_ag_chunk(b, a, boff, bcnt, (k - 1) * ch, ch);
+  return agc;
 }
 
 // ---------------------------------------------------------------------------
@@ -379,7 +414,8 @@ void ar_ring(Builder &b, const PlanArgs &a) {
     for (int x = 0; x < P; x++) { boff[(size_t)x] = bl.off((x + 1) % P); bcnt[(size_t)x] = bl.cnt((x + 1) % P); }
     std::vector<int> order;
     for (int j = 1; j <= P; j++) order.push_back((r + j) % P);
-    flat_chain(b, a, src, boff, bcnt, order, RB, boff[(size_t)r]);
+    const bool agd = flat_chain(b, a, src, boff, bcnt, order, RB, boff[(size_t)r], true);
+    if (agd) return;
     if (a.flat_ag) {
       for (int x = 0; x < P; x++)
         if (x != r) b.send(x, RB, boff[(size_t)r], bcnt[(size_t)r]);
@@ -436,6 +472,7 @@ void ar_rabenseifner(Builder &b, const PlanArgs &a) {
   if (!a.in_place && !flat) b.copy(SB, 0, RB, 0, n);
   const uint64_t lh = n / 2, rh = n - lh;
   int vrank;
+  bool agd = false;  // flat_rs emitted the chunked allgather
   if (r < 2 * rem) {
     if (r % 2) {
       b.send(r - 1, RB, 0, lh); b.recv(r - 1, T0, lh, rh); b.end(PIPE);
@@ -466,10 +503,11 @@ void ar_rabenseifner(Builder &b, const PlanArgs &a) {
     if (flat && steps >= 1) {  // partners x ^ 2^s, acc = acc (op) received
       std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
       for (int x = 0; x < P; x++) owned(x, &boff[(size_t)x], &bcnt[(size_t)x]);
-      flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, flat_leaves(P, steps, r, [](int x, int s) { return x ^ (1 << s); }),
-              RB, boff[(size_t)r]);
+      agd = flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt,
+                    flat_leaves(P, steps, r, [](int x, int s) { return x ^ (1 << s); }), RB, boff[(size_t)r], 0, true);
     }
-    if (a.flat_ag && rem == 0 && steps >= 1) {
+    if (agd) {
+    } else if (a.flat_ag && rem == 0 && steps >= 1) {
       // one all-peers exchange: rank x's block after the halving
       for (int x = 0; x < P; x++)
         if (x != r) b.send(x, RB, ri[steps - 1], rc[steps - 1]);
@@ -551,7 +589,7 @@ void ar_bine_bdw_static(Builder &b, const PlanArgs &a) {
     std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
     for (int x = 0; x < P; x++) { boff[(size_t)x] = bl.off(perm[(size_t)x]); bcnt[(size_t)x] = bl.wcnt(perm[(size_t)x], 1); }
     const auto leaves = flat_leaves(P, steps, r, [&](int x, int s) { return pi(x, s, P); });
-    flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, leaves, RB, boff[(size_t)r]);
+    if (flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, leaves, RB, boff[(size_t)r], 0, true)) return;
     w = 1;
   }
   for (int s = 0; s < steps && w > 1; s++) {
@@ -640,6 +678,7 @@ void ar_bine_remap(Builder &b, const PlanArgs &a, bool segmented) {
     uint64_t w = n;
     const uint32_t vrank = remap_rank((uint32_t)adj, (uint32_t)nr);
     const bool flat = pw2 && flat_rs_fits(a);
+    bool agd = false;  // flat_rs emitted the chunked allgather
     for (int s = 0; s < steps; s++) {
       const int vd = pi(nr, s, adj);
       dst[s] = pw2 ? vd : (vd < extra ? (vd << 1) + 1 : vd + extra);
@@ -658,9 +697,10 @@ void ar_bine_remap(Builder &b, const PlanArgs &a, bool segmented) {
       std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
       for (int x = 0; x < P; x++) remap_owned(P, x, n, &boff[(size_t)x], &bcnt[(size_t)x]);
       const auto leaves = flat_leaves(P, steps, r, [&](int x, int s) { return pi(x, s, P); });
-      flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, leaves, RB, ri[steps - 1]);
+      agd = flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt, leaves, RB, ri[steps - 1], 0, true);
     }
-    if (a.flat_ag && pw2 && steps >= 1) {
+    if (agd) {
+    } else if (a.flat_ag && pw2 && steps >= 1) {
       for (int x = 0; x < P; x++)
         if (x != r) b.send(x, RB, ri[steps - 1], rc[steps - 1]);
       for (int x = 0; x < P; x++) {
@@ -694,8 +734,10 @@ void ar_bine_bbb_any_even(Builder &b, const PlanArgs &a) {
     // as the block-by-block reduce-scatter's first levels; tests/test_flat_symbolic.py)
     std::vector<uint64_t> boff((size_t)P), bcnt((size_t)P);
     for (int x = 0; x < P; x++) { boff[(size_t)x] = bl.off(x); bcnt[(size_t)x] = bl.cnt(x); }
-    flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt,
-            flat_leaves(P, log2_ceil(P), r, [P](int x, int s) { return nb_partner(x, 1 << s, P); }), RB, boff[(size_t)r]);
+    if (flat_rs(b, a, a.in_place ? RB : SB, boff, bcnt,
+                flat_leaves(P, log2_ceil(P), r, [P](int x, int s) { return nb_partner(x, 1 << s, P); }), RB,
+                boff[(size_t)r], 0, true))
+      return;
     if (a.flat_ag) {
       for (int x = 0; x < P; x++)
         if (x != r) b.send(x, RB, boff[(size_t)r], bcnt[(size_t)r]);

@@ -41,14 +41,28 @@ def scheduled_prims(coll, algo, P, r, chunk_bytes, relay=0, trees=False, flat_ag
     return out, info
 
 
+def poison(a):
+    """a recognisable non-value for the device copies the staging must fill"""
+    if a.dtype.kind == "f":
+        a[:] = np.nan
+    else:
+        a.view(np.uint8)[:] = 0xA5
+    return a
+
+
 def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_place=False,
-        rbufs=None, chunk_bytes=None, relay=0, trees=False, flat_ag=False, flat_rs=False):
+        rbufs=None, chunk_bytes=None, relay=0, trees=False, flat_ag=False, flat_rs=False, stage=False):
     """chunk_bytes != None: run the executor's chunked issue schedule instead of
-    the plan itself (same semantics when ops run in issue order)."""
+    the plan itself (same semantics when ops run in issue order).
+    stage=True (allreduce / reduce_scatter, chunk_bytes given): host staging
+    (pico_amd.stage_plan) -- the device input buffer starts poisoned and is
+    filled from the host input only by the h2d pieces, each applied just before
+    the op it belongs to; the result returned is the HOST output, assembled only
+    from the d2h pieces, each copied right after its op completed."""
     P = len(sbufs)
     esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
     count = sbufs[0].size
-    plans, bufs = [], []
+    plans, bufs, stg, host_in, host_out = [], [], [], [], []
     for r in range(P):
         prims, tmp = pico_amd.plan(coll, algo, P, r, count=count, rcounts=rcounts, root=root, esz=esz,
                                    segsize=segsize, in_place=in_place)
@@ -58,6 +72,10 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
                                           count=count, rcounts=rcounts, root=root,
                                     esz=esz, segsize=segsize, in_place=in_place)
         plans.append(prims)
+        if stage:
+            stg.append(pico_amd.stage_plan(coll, algo, P, r, count=count, rcounts=rcounts, esz=esz,
+                                           segsize=segsize, in_place=in_place, chunk_bytes=chunk_bytes,
+                                           flat_ag=flat_ag, flat_rs=flat_rs))
         if coll == "allgather":
             # in place: rbufs[r] already holds the rank's block where the
             # algorithm expects it (P * count elements)
@@ -83,6 +101,13 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         # relay staging (BINE_BUF_STAGE), exactly as large as the executor allocates
         tbufs.append(np.zeros(info["stage_elems"] if chunk_bytes is not None else 0, O.NP_DTYPES[dtype]))
         bufs.append([sb, rb] + tbufs)
+        if stage:
+            dev_in = rb if in_place else sb
+            host_in.append(dev_in.copy())
+            poison(dev_in)
+            if not in_place:
+                poison(rb)
+            host_out.append(poison(rb.copy()))
     pc = [0] * P
     sendq = collections.defaultdict(collections.deque)  # (src, dst) -> [(rank, idx)]
     recvq = collections.defaultdict(collections.deque)
@@ -128,6 +153,25 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
                 lvl += 1
             view(r, p["dst_buf"], p["dst_off"], n)[:] = v[0]
 
+    started = [set() for _ in range(P)]
+
+    def begin(r, g):  # op g of rank r is about to run: its h2d pieces land first
+        if stage and g not in started[r]:
+            started[r].add(g)
+            dev_in = bufs[r][RB if in_place else SB]
+            for lo, hi in stg[r][0].get(g, []):
+                dev_in[lo:hi] = host_in[r][lo:hi]
+
+    def finish(r, old_pc):  # ops between old_pc and pc[r] are complete: their d2h pieces
+        if not stage:
+            return
+        for j in range(old_pc, pc[r]):
+            g = plans[r][j]["group"]
+            last = j + 1 >= len(plans[r]) or plans[r][j + 1]["group"] != g
+            if last:
+                for lo, hi in stg[r][1].get(g, []):
+                    host_out[r][lo:hi] = bufs[r][RB][lo:hi]
+
     def try_transfer(key):
         moved = False
         while sendq[key] and recvq[key]:
@@ -151,6 +195,8 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         for r in range(P):
             while pc[r] < len(plans[r]) and posted[r] is None:
                 p = plans[r][pc[r]]
+                if "group" in p:
+                    begin(r, p["group"])
                 if p["type"] in ("SEND", "RECV"):
                     j = pc[r]
                     while j < len(plans[r]) and plans[r][j]["type"] in ("SEND", "RECV") and \
@@ -167,12 +213,14 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
                 else:
                     local(r, p)
                     pc[r] += 1
+                    finish(r, pc[r] - 1)
                     progress = True
         for key in list(sendq.keys()):
             progress |= try_transfer(key)
         for r in range(P):
             if posted[r] is not None and pending[r] == 0:
                 pc[r] = posted[r][1]
+                finish(r, posted[r][0])
                 posted[r] = None
                 progress = True
         if all(pc[r] >= len(plans[r]) and posted[r] is None for r in range(P)):
@@ -181,7 +229,7 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             raise PlanError(f"deadlock: pcs={pc}")
     outs = []
     for r in range(P):
-        rb = bufs[r][RB]
+        rb = host_out[r] if stage else bufs[r][RB]
         if coll == "reduce_scatter":
             outs.append(rb[:rcounts[r]])
         elif coll == "allgather":

@@ -657,6 +657,12 @@ PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
     (1, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "67108864"),
     (2, "ALLREDUCE", "bine_bdw_remap_over", "int64", False, "8388608"),
     (2, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "16777216"),
+    # floating point at P > 1: the staging pipelined into the collective
+    # (bine_allreduce_staged / bine_reduce_scatter_staged), over RCCL and over
+    # the direct peer-memory transport (BINE_DIRECT=1)
+    (4, "ALLREDUCE", "bine_bdw_remap_over", "float", "dm", "16777216"),
+    (4, "ALLREDUCE", "bine_bdw_static_over", "double", "dm", "8388608"),
+    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "float", False, "16777216"),
     (2, "ALLREDUCE", "bine_bdw_remap_over", "float", True, "1048576"),
     (2, "ALLREDUCE", "bine_lat_over", "double", True, "1048576"),
     (2, "REDUCE_SCATTER", "bine_permute_remap_over", "int64", True, "1048576"),
@@ -672,7 +678,9 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat,
     socket transport (distinct NCCL_HOSTIDs), optionally with the flat phases"""
     import subprocess
     env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
-    if flat:
+    if flat == "dm":
+        env.update(BINE_DIRECT="1")
+    elif flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
     p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, count,
                         "5", algo, dtype], env=env, capture_output=True, text=True, timeout=150)

@@ -42,8 +42,11 @@ def test_bench_two_ranks_one_gpu():
     assert c["parity"]["headline_ok"] is True
     assert c["provisional_literal_rccl"]["parity_ok"] is True
     trials = c["parity"]["trials"]
-    assert trials and all(v in (True, "error") for v in trials.values()), trials
-    assert any(v is True for v in trials.values())
+    # every transport the bench trials runs and matches the oracle's digests
+    # here (direct peer memory included: two processes on one device); an
+    # "error" verdict is a transport that failed to run, not a pass
+    assert trials and all(v is True for v in trials.values()), trials
+    assert any("+dm" in k.split("/")[0] for k in trials), trials
     others = c["other_baseline_configs"]
     assert others and all(v.get("parity_ok") is True for v in others.values()), others
     assert d["roofline"]["bound"] == "xgmi" and d["roofline"]["achieved"] > 0

@@ -286,3 +286,21 @@ def test_reduce_scatter_beyond_int32_total(dev, algo):
         for c in cs:
             c.destroy()
         torch.cuda.empty_cache()
+
+
+@pytest.mark.timeout(700)
+def test_full_size_configs_eight_processes():
+    """C3 (fp32 256 MiB/rank), C4 (reduce_scatter 1 GiB/rank) and C5 (fp64,
+    int64 256 MiB/rank) at P = 8 in eight real processes -- the transports the
+    driver's 8-GPU bench picks from (flat phases and the literal schedule over
+    the direct peer-memory transport, the flat phases over RCCL P2P) -- every
+    rank's output digest equal to the committed oracle digest of pico_core's
+    inputs (tools/fullsize_multirank.py)"""
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "fullsize_multirank.py"), "8"], env=env,
+                       capture_output=True, text=True, timeout=680)
+    tail = "\n".join(r.stdout.splitlines()[-20:])
+    assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
+    assert "RESULT P=8: ok" in r.stdout

@@ -75,3 +75,19 @@ def test_c1_four_processes_every_transport():
                        capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + "\n" + r.stderr[-2000:]
     assert '"exitcodes": [0, 0, 0, 0]' in r.stdout
+
+
+@pytest.mark.timeout(400)
+def test_staged_host_buffers_4_ranks():
+    """host buffers with the staging pipelined into the collective
+    (bine_allreduce_staged / bine_reduce_scatter_staged): 4 processes, RCCL and
+    the direct transport, 13 cases (allreduce / reduce_scatter algorithms x
+    dtypes x in place x chunk) bit-exact vs the oracle with the device input
+    NaN-poisoned, plus C3's 256 MiB per rank vs the committed digest
+    (tools/staged_check.py)"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "staged_check.py"), "4", "1"], env=env,
+                       capture_output=True, text=True, timeout=380)
+    tail = "\n".join(r.stdout.splitlines()[-16:])
+    assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
+    assert "RESULT P=4: ok" in r.stdout

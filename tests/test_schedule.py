@@ -425,7 +425,7 @@ def test_flat_reduce_scatter_matches_oracle(coll, algo, P):
                          ("float", 1001, "max"), ("int32", 515, "prod")):
         for chunk in (0, 64):
             for in_place in (False, True):
-                for flat_ag in ((False, True) if coll != "reduce_scatter" else (False,)):
+                for flat_ag in ((False, True, 2) if coll != "reduce_scatter" else (False,)):
                     assert _flat_rs_case(coll, algo, P, dtype, n, op, chunk, in_place, flat_ag), \
                         (dtype, n, op, chunk, in_place, flat_ag)
 
@@ -454,6 +454,45 @@ def test_flat_reduce_scatter_race_free_and_one_hop(coll, algo, P):
                 assert sends == ({0} if rank else set())
             else:
                 assert sends == set(range(P)) - {rank}
+
+
+FLAT_AG_CHUNKED = [a for c, a in FLAT_RS if c == "allreduce" and a not in ("bine_lat", "recursivedoubling")]
+
+
+@pytest.mark.parametrize("algo", FLAT_AG_CHUNKED)
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_flat_ag_chunked_race_free_and_interleaved(algo, P):
+    """flat_ag = 2: the allgather is cut with the reduce-scatter's chunks.
+    Race-free; every allgather exchange moves one chunk of every block (all
+    P-1 peers); the k-th allgather exchange follows the (k+1)-th reduce-scatter
+    exchange; the allgather moves exactly the bytes of the one-exchange form"""
+    n, ch = 4099, 1024
+    for rank in range(P):
+        for in_place in (False, True):
+            kw = dict(count=n, esz=4, segsize=256, chunk_bytes=ch, in_place=in_place, flat_rs=True)
+            ops, cj, fw = pico_amd.schedule("allreduce", algo, P, rank, flat_ag=2, **kw)
+            check_race_free(ops, cj, fw, in_place)
+            one, _, _ = pico_amd.schedule("allreduce", algo, P, rank, flat_ag=True, **kw)
+            def ag_sends(o_):  # (peer, elements) of every RBUF -> RBUF send
+                return [(p["peer"], p["count"]) for x in o_ if x["xchg"] for p in x["prims"]
+                        if p["type"] == "SEND" and p["src_buf"] == RB]
+            if in_place:  # the input is RBUF too: compare the totals only
+                continue
+            per_peer = lambda L: {q: sum(c for p_, c in L if p_ == q) for q, _ in L}
+            assert per_peer(ag_sends(ops)) == per_peer(ag_sends(one))
+            xs = [o for o in ops if o["xchg"]]
+            # reduce-scatter exchanges send SBUF; allgather exchanges only move RBUF
+            rs = [i for i, o in enumerate(xs) if any(p["type"] == "SEND" and p["src_buf"] == SB
+                                                     for p in o["prims"])]
+            ag = [i for i in range(len(xs)) if i not in rs]
+            assert len(rs) >= 2 and len(ag) == len(rs)
+            for k in range(len(rs) - 1):
+                assert rs[k + 1] < ag[k]
+            for i in ag:
+                assert all(p["src_buf" if p["type"] == "SEND" else "dst_buf"] == RB for p in xs[i]["prims"])
+                got = {p["peer"] for p in xs[i]["prims"] if p["type"] == "RECV"}
+                assert got and got <= set(range(P)) - {rank}  # (ragged blocks: a short block may be done)
+            assert {p["peer"] for p in xs[ag[0]]["prims"] if p["type"] == "RECV"} == set(range(P)) - {rank}
 
 
 def test_flat_reduce_scatter_not_applied_where_it_does_not_fit():

@@ -7,7 +7,11 @@ configuration the median of pico_core's own per-iteration times (its CSV,
 max over ranks, first 20 % dropped), every iteration checked by pico_core
 against PMPI_Allreduce.  Configurations: the staging pipeline's chunk
 (BINE_STAGE_CHUNK_BYTES) and page-locking on / off (BINE_HOST_REGISTER).
-usage: python tools/e2e_staging.py [NP] [DTYPE] [COUNT] [ITERS]"""
+Configuration set "pipeline" (5th argument; floating point at P > 1): the
+serial path (BINE_STAGE_PIPELINE=0: H2D, then the collective, then D2H)
+against the staging pipelined into the collective (bine_allreduce_staged)
+at several chunks.
+usage: python tools/e2e_staging.py [NP] [DTYPE] [COUNT] [ITERS] [chunks|pipeline]"""
 import json
 import os
 import statistics
@@ -52,6 +56,14 @@ if __name__ == "__main__":
             ("page-locked, 16 MiB chunks, device->host by kernel stores", {"BINE_STAGE_D2H": "kernel"}),
             ("page-locked, 8 MiB chunks, device->host by kernel stores",
              {"BINE_STAGE_D2H": "kernel", "BINE_STAGE_CHUNK_BYTES": str(8 << 20)})]
+    if len(sys.argv) > 5 and sys.argv[5] == "pipeline":
+        cfgs = [("serial: H2D, collective, D2H (BINE_STAGE_PIPELINE=0)", {"BINE_STAGE_PIPELINE": "0"}),
+                ("pipelined into the collective, 16 MiB rounds (default)", {}),
+                ("pipelined, 4 MiB rounds", {"BINE_STAGE_CHUNK_BYTES": str(4 << 20)}),
+                ("pipelined, 8 MiB rounds", {"BINE_STAGE_CHUNK_BYTES": str(8 << 20)}),
+                ("pipelined, 32 MiB rounds", {"BINE_STAGE_CHUNK_BYTES": str(32 << 20)}),
+                ("pipelined, 64 MiB rounds", {"BINE_STAGE_CHUNK_BYTES": str(64 << 20)})]
+        out["transport"] = "direct peer memory (BINE_DIRECT=1)" if os.environ.get("BINE_DIRECT") == "1" else "RCCL"
     for name, env in cfgs:
         r = run(np_, dtype, count, iters, env)
         if "ms_median" in r:
