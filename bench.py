@@ -635,7 +635,14 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
         except pico_amd.BineError as e:   # symmetric: setup is agreed over RCCL
             out["C1_direct_fused"] = {"error": str(e)}
     del sb, rb
-    apply_transport(comm, mode, chunk, graphs)
+    # C4 / C5 are bandwidth-bound (1 GiB / 256 MiB per rank): issued eagerly on
+    # the chosen transport and chunk, whatever graph replay did for C3 -- a
+    # replay saves host issue time only, and a fault in a replay of a shape
+    # no test replays must not cost the headline line (one-GPU rehearsal with
+    # GPU_MAX_HW_QUEUES=1: hipGraphLaunch of the captured C4 reduce_scatter
+    # segfaulted inside HIP 7.0; eager, and with the default queues, it runs
+    # bit-exactly -- profiles/r3_rs_graph_probe.txt)
+    apply_transport(comm, mode, chunk, False)
     trees = mode == "trees"
     # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
     n = C4_ELEMS
@@ -651,7 +658,7 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
     S = n * 4
     out["C4_reduce_scatter_bine_permute_remap_f32_1GiB"] = {
         "ms": round(st["median_ms"], 4), "busbw_per_rank_GBs": round((world - 1) / world * S / (st["median_ms"] * 1e-3) / 1e9, 2),
-        "parity_ok": all_ok(torch, dist, ok)}
+        "graph_replay": False, "parity_ok": all_ok(torch, dist, ok)}
     del sb, rb
     # C5: allreduce_bine_bdw_remap fp64 / int64 SUM, 256 MiB per rank
     n = C5_ELEMS
@@ -668,7 +675,7 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
         out[f"C5_allreduce_bine_bdw_remap_{dt}_256MiB"] = {
             "ms": round(ms, 4), "algbw_per_rank_GBs": round(S / (ms * 1e-3) / 1e9, 2),
             "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2),
-            "parity_ok": all_ok(torch, dist, ok)}
+            "graph_replay": False, "parity_ok": all_ok(torch, dist, ok)}
         del sb, rb
     torch.cuda.empty_cache()
     return out
@@ -989,6 +996,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         return out
 
     watchdog = arm_deadline(budget, _partial, "side measurements")
+    if rank == 0:
+        print(f"bench: headline {tname(best)} {ms:.4f} ms; side measurements next", file=sys.stderr, flush=True)
     steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,

@@ -15,8 +15,11 @@
 //     This is the device form of the segmented variant's double-buffered
 //     Irecv/Reduce_local loop (libbine_allreduce.c:1218-1253).
 //   * workspace (TMP0..2), plans and their schedules are cached per communicator.
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <signal.h>
+#include <unistd.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
@@ -403,7 +406,38 @@ struct bine_comm {
 
 namespace bine {
 
+// BINE_SEGV_TRACE=1 (diagnostics): a host-side SIGSEGV / SIGABRT prints the
+// native call stack to stderr -- which HIP / RCCL call of which library
+// function faulted -- and then passes the signal on to the handler installed
+// before (Python's faulthandler prints its frames) or the default action
+static struct sigaction g_prev_segv, g_prev_abrt;
+static void segv_trace(int sig, siginfo_t *si, void *uc) {
+  static const char hdr[] = "bine: fatal signal, native stack:\n";
+  (void)!write(2, hdr, sizeof hdr - 1);
+  void *fr[64];
+  backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
+  struct sigaction &prev = sig == SIGSEGV ? g_prev_segv : g_prev_abrt;
+  sigaction(sig, &prev, nullptr);
+  if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) prev.sa_sigaction(sig, si, uc);
+  else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN) prev.sa_handler(sig);
+  else raise(sig);
+}
+static void install_segv_trace() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char *e = getenv("BINE_SEGV_TRACE");
+    if (!e || atoi(e) == 0) return;
+    struct sigaction sa {};
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGABRT, &sa, &g_prev_abrt);
+  });
+}
+
 static int comm_setup(bine_comm *c) {
+  install_segv_trace();
   HIP_TRY(hipSetDevice(c->device));
   int lo = 0, hi = 0;
   HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));

@@ -12,7 +12,8 @@ relay, flat, flatrs+flat, +ag, +a2a, trees; and over the direct peer-memory
 transport "+dm"), each eagerly and in graph mode
 (bine_comm_set_graphs: one eager call + capture, then replays), plus
 reduce_scatter_bine_permute_remap
-on a 64 MiB input per rank (direct, flatrs).  Every rank's output digest is
+on a 64 MiB input per rank (direct, flatrs, flatrs over the direct transport;
+eagerly and in graph mode).  Every rank's output digest is
 compared with the oracle's (trees: the relabelled schedule's), computed once
 in the parent.
 usage: python tools/rccl_large.py [P]   (exit 0 = every rank, every case ok)
@@ -27,7 +28,7 @@ N32 = 16_777_216   # 64 MiB fp32
 N64 = 8_388_608    # 64 MiB fp64
 MODES = ("direct", "relay", "flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+flat+a2a", "trees",
          "direct+dm", "flatrs+flat+dm", "relay+flat+dm", "trees+dm")
-RS_MODES = ("direct", "flatrs")
+RS_MODES = ("direct", "flatrs", "flatrs+flat+dm")
 
 
 def expected(P):
@@ -96,15 +97,22 @@ def worker(rank, P, port, want, q):
     r = torch.empty(N32 // P, dtype=torch.float32, device="cuda:0")
     pico_amd.fill_pico(s, N32, "float", 1234 + rank)
     for m in RS_MODES:
-        bench.apply_transport(comm, m, 0, False)
-        r.fill_(float("nan"))
-        pico_amd.reduce_scatter("bine_permute_remap", s, r, [N32 // P] * P, "float", "sum", comm)
-        torch.cuda.synchronize()
-        comm.synchronize()
-        if pico_amd.checksum(r, N32 // P, "float") == want[("rs", "float", False)][rank]:
-            n_ok += 1
-        else:
-            bad.append(f"reduce_scatter {m}")
+        for g in (False, True):
+            # graph mode as bench.py's C4 side measurement runs it when the C3
+            # trials pick graph replay: one eager call + capture, then replays
+            print(f"rank {rank} reduce_scatter {m} graphs={g} ...", flush=True)
+            bench.apply_transport(comm, m, 0, g)
+            for it in range(3 if g else 1):
+                with torch.cuda.stream(side):
+                    r.fill_(float("nan"))
+                    pico_amd.reduce_scatter("bine_permute_remap", s, r, [N32 // P] * P, "float", "sum", comm)
+                torch.cuda.synchronize()
+                comm.synchronize()
+                if pico_amd.checksum(r, N32 // P, "float") == want[("rs", "float", False)][rank]:
+                    n_ok += 1
+                else:
+                    bad.append(f"reduce_scatter {m} graphs={g} iter {it}")
+            comm.set_graphs(False)
     for b in bad:
         print(f"rank {rank} MISMATCH {b}", flush=True)
     print(f"rank {rank} rccl {pico_amd.rccl_version()}", flush=True)
