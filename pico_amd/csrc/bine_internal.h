@@ -171,6 +171,8 @@ struct DmMsg {
   int push;            // 1: into the peer's inbox, 0: out of our own
   int peer;
   int j;               // this launch's j-th message of this kind to / from `peer`: seq = base[peer] + j + 1
+  int leaf = -1;       // k_dm_move_tree: >= 0 -- a pull whose slot is a leaf of the launch's tree (read in
+                       // place, never copied); -1 -- copied by its own workgroups
 };
 struct DmArgs {
   int nmsg = 0;
@@ -183,6 +185,33 @@ struct DmArgs {
   DmMsg m[kMaxDm];
 };
 int launch_dm_move(const DmArgs &a, void *stream);
+
+// The flat reduce-scatter's tree evaluated INSIDE the exchange launch that
+// receives its leaves (k_dm_move_tree<T, OP, NL>): the launch's copy messages
+// (pushes, and pulls that are not leaves) run as in k_dm_move on their
+// `wgs` workgroups each; `twgs` further workgroups wait for the leaf pulls'
+// ready marks, evaluate the reference's tree (own leaf at `pos`, per-level
+// swap bits) reading the received leaves in place in the inbox slots, write
+// `out`, and acknowledge every leaf slot -- the pull copy into a staging area
+// and the separate tree launch of the unfused form are gone (one HBM pass
+// over every received byte less).  Slots, flags, counters and sequence bases
+// are k_dm_move's; a leaf pull is counted and acknowledged like a copied one,
+// so both ends see the same protocol.
+struct DmTree {
+  int nl = 0, pos = 0;
+  unsigned swap = 0;
+  int twgs = 0;                 // tree workgroups (dispatched after the copy workgroups)
+  int ncopy = 0;                // copy messages, by index into DmArgs::m
+  int cidx[kMaxDm] = {};
+  int leaf_msg[kMaxLeaves] = {};  // tree position -> DmArgs::m index (-1 at pos)
+  const void *own_leaf = nullptr;
+  void *out = nullptr;
+  uint64_t nvec = 0;            // 16-B vectors per leaf and of `out`
+};
+// BINE_ERR_UNSUPPORTED: no instantiation for (dtype, op, nl) -- the caller
+// issues the unfused form
+int launch_dm_move_tree(const DmArgs &a, const DmTree &t, int dtype, int op, void *stream);
+bool dm_tree_supported(int dtype, int op, int nl);
 
 // The whole flat-form small collective in ONE launch over the direct
 // transport (k_dm_fused): phase A pushes this rank's blocks into the peers'

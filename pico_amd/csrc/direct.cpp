@@ -164,6 +164,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
+  if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
   if (slot < (1 << 20)) slot = 1 << 20;
   slot = slot / 4096 * 4096;
   if (wgs < 1) wgs = 1;
@@ -337,7 +338,23 @@ void DirectState::dump() const {
   }
 }
 
-int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) {
+bool DirectState::tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &t) const {
+  if (!dm_tree_supported(t.dtype, t.op, t.nl) || t.pos < 0 || t.pos >= t.nl || (int)r.size() != t.nl - 1 ||
+      (int)t.leaf_of_recv.size() != (int)r.size() || !t.leaf_bytes || t.leaf_bytes % 16 || slot % 16 ||
+      ((uintptr_t)t.own_leaf & 15) || ((uintptr_t)t.out & 15) || s.size() + r.size() > (size_t)kMaxDm)
+    return false;
+  unsigned seen = 1u << t.pos;
+  for (size_t i = 0; i < r.size(); i++) {
+    const int j = t.leaf_of_recv[i];
+    if (j < 0 || j >= t.nl || (seen >> j & 1) || r[i].bytes != t.leaf_bytes) return false;
+    seen |= 1u << j;
+  }
+  return true;
+}
+
+int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st,
+                          const TreeSpec *tree) {
+  if (tree && !tree_ok(s, r, *tree)) return BINE_ERR_UNSUPPORTED;
   // more messages to (or from) one peer in one exchange than slots per pair
   // would make a push wait for a pull of the same exchange: refuse
   std::vector<int> ns((size_t)P, 0), nr((size_t)P, 0);
@@ -359,8 +376,31 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   // j = index of a message among this launch's messages of its kind to / from
   // its peer (the kernel adds it to the device-side base)
   std::vector<int> js((size_t)P, 0), jr((size_t)P, 0);
+  // a launch holding leaf pulls (all of one round: tree_ok) evaluates that
+  // round's tree in place of copying them
+  int tree_round = -1;
   auto flush = [&]() -> int {
-    const int rc = launch_dm_move(a, st);
+    int rc;
+    if (tree_round >= 0) {
+      DmTree t;
+      t.nl = tree->nl;
+      t.pos = tree->pos;
+      t.swap = tree->swap;
+      t.twgs = tree_wgs;
+      const size_t off = (size_t)tree_round * slot, len = std::min(slot, tree->leaf_bytes - off);
+      t.own_leaf = tree->own_leaf + off;
+      t.out = tree->out + off;
+      t.nvec = len / 16;
+      for (int j = 0; j < kMaxLeaves; j++) t.leaf_msg[j] = -1;
+      for (int i = 0; i < a.nmsg; i++) {
+        if (a.m[i].leaf >= 0) t.leaf_msg[a.m[i].leaf] = i;
+        else t.cidx[t.ncopy++] = i;
+      }
+      rc = launch_dm_move_tree(a, t, tree->dtype, tree->op, st);
+      tree_round = -1;
+    } else {
+      rc = launch_dm_move(a, st);
+    }
     a.nmsg = 0;
     std::fill(js.begin(), js.end(), 0);
     std::fill(jr.begin(), jr.end(), 0);
@@ -379,6 +419,7 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.push = 1;
       m.peer = x.peer;
       m.j = js[(size_t)x.peer]++;
+      m.leaf = -1;
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }
@@ -386,7 +427,8 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   };
   // round k's pulls: out of our own slot once the sender marked it ready
   auto pulls = [&](size_t k) -> int {
-    for (const auto &x : r) {
+    for (size_t i = 0; i < r.size(); i++) {
+      const auto &x = r[i];
       if (x.bytes <= k * slot) continue;
       const size_t off = k * slot, len = std::min(slot, x.bytes - off);
       DmMsg &m = a.m[a.nmsg++];
@@ -396,6 +438,8 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.push = 0;
       m.peer = x.peer;
       m.j = jr[(size_t)x.peer]++;
+      m.leaf = tree ? tree->leaf_of_recv[i] : -1;
+      if (tree) tree_round = (int)k;
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }

@@ -10,6 +10,20 @@
 
 namespace bine {
 
+// The flat reduce-scatter's tree fed by an exchange's receives, evaluated in
+// the exchange's own launches (k_dm_move_tree): every receive is a leaf
+// (`leaf_of_recv[i]` = its tree position), all of `leaf_bytes`; the tree of
+// round r covers bytes [r * slot, ...) of every leaf, of `own_leaf` and of `out`.
+struct TreeSpec {
+  int nl = 0, pos = 0;
+  unsigned swap = 0;
+  std::vector<int> leaf_of_recv;
+  const char *own_leaf = nullptr;
+  char *out = nullptr;
+  size_t leaf_bytes = 0;
+  int dtype = 0, op = 0;
+};
+
 struct DirectState {
   int P = 1, rank = 0, device = 0;
   size_t slot = (size_t)16 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES)
@@ -34,7 +48,12 @@ struct DirectState {
   // phase 2, collective over the P ranks of the node (same key on all):
   // exchange descriptors over Unix sockets, map every peer's inbox
   int connect_peers(uint64_t key, std::string &err);
-  int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st);
+  int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st,
+               const TreeSpec *tree = nullptr);
+  // whether exchange() can take `tree` for these sends / receives (all of one
+  // round's messages in one launch, 16-B vectors, an instantiated tree)
+  bool tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &tree) const;
+  int tree_wgs = 256;  // tree workgroups per launch (BINE_DIRECT_TREE_WGS)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }
   // stderr: this rank's flags and device-side sequence bases (after a timeout)
   void dump() const;

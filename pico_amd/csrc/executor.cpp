@@ -88,6 +88,14 @@ struct Transport {
   virtual bool stream_ordered() const { return false; }
   // non-success: the transport is unusable (checked before a graph replay)
   virtual int health() const { return BINE_SUCCESS; }
+  // an exchange whose receives are the leaves of the following tree, the
+  // tree evaluated inside the exchange (direct transport, k_dm_move_tree)
+  virtual bool tree_ok(const std::vector<XSend> &, const std::vector<XRecv> &, const TreeSpec &) const {
+    return false;
+  }
+  virtual int exchange_tree(const std::vector<XSend> &, const std::vector<XRecv> &, const TreeSpec &, hipStream_t) {
+    return BINE_ERR_UNSUPPORTED;
+  }
 };
 
 static bool nccl_type(int dtype, ncclDataType_t *t) {
@@ -185,6 +193,18 @@ struct RcclTransport final : Transport {
       if (rc) return rc;
     }
     return BINE_SUCCESS;
+  }
+  bool tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &t) const override {
+    return dm_on && dm && dm->tree_ok(s, r, t);
+  }
+  int exchange_tree(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &t,
+                    hipStream_t st) override {
+    if (!dm_on) return BINE_ERR_UNSUPPORTED;
+    if (dm->poisoned()) {
+      set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
+      return BINE_ERR_INTERNAL;
+    }
+    return dm->exchange(s, r, st, &t);
   }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
     if (dm_on) {
@@ -370,6 +390,10 @@ struct bine_comm {
   std::map<std::string, bine::StageRanges> stage_cache;  // host staging ranges per plan key
   std::vector<hipEvent_t> op_ev;  // scratch of execute()
   std::vector<hipEvent_t> stage_ev;  // scratch of execute(): host staging batches
+  // scratch of execute(): trees evaluated inside their exchange (plan_dm_trees)
+  std::vector<int> tree_of, tree_at;
+  std::vector<bine::TreeSpec> tree_spec;
+  std::vector<hipEvent_t> tree_ev;
   // per-op device timing of the latest collective (bine_comm_set_profile)
   bool profile = false;
   struct OpTime { hipEvent_t a = nullptr, b = nullptr; int xchg = 0, nprims = 0; uint64_t bytes = 0; };
@@ -728,6 +752,93 @@ struct Staging {
   const StageRanges *rg = nullptr;
 };
 
+// BINE_DIRECT_TREE=0: the flat reduce-scatter's trees stay separate launches
+// (pull copies into the staging area + k_reduce_tree) over the direct transport
+static bool dm_tree_on() {
+  static const bool on = !getenv("BINE_DIRECT_TREE") || atoi(getenv("BINE_DIRECT_TREE")) != 0;
+  return on;
+}
+
+// Exchange i whose receives are exactly the leaves of the tree op j that
+// follows it -- the flat reduce-scatter's [exchange A][REDUCE_TREE] pair, with
+// only exchanges in between and j waiting for i -- is issued over the direct
+// transport as ONE exchange that evaluates the tree in its own launches,
+// reading the leaves in place in the inbox slots (TreeSpec, k_dm_move_tree).
+// Conditions: the staging buffer the leaves were received into is referenced
+// by nothing but receives and trees (no one else reads what is no longer
+// written), the tree's output overlaps no block the exchange sends (it is
+// written while the pushes still read), and the transport takes the shape
+// (tree_ok).  Fills tree_of[i] = j and tree_at[j] = i; false: none.
+template <typename Ptr>
+static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op,
+                          std::vector<int> &tree_of, std::vector<int> &tree_at, std::vector<TreeSpec> &spec) {
+  const size_t n = sc.ops.size();
+  tree_of.assign(n, -1);
+  tree_at.assign(n, -1);
+  if (!c->tx->stream_ordered() || !dm_tree_on() || op < 0 || c->profile) return false;
+  bool any = false;
+  std::vector<XSend> s;
+  std::vector<XRecv> r;
+  for (size_t i = 0; i < n; i++) {
+    if (!sc.ops[i].xchg) continue;
+    size_t j = i + 1;
+    while (j < n && sc.ops[j].xchg) j++;
+    if (j >= n || sc.ops[j].wait != (int64_t)i || sc.ops[j].prims.size() != 1 ||
+        sc.ops[j].prims[0].type != BINE_PRIM_REDUCE_TREE || tree_at[j] >= 0)
+      continue;
+    const Prim &t = sc.ops[j].prims[0];
+    // the staging buffer: only receives write it, only trees read it
+    bool clean = true;
+    for (const SOp &o : sc.ops)
+      for (const Prim &x : o.prims) {
+        const bool tree = x.type == BINE_PRIM_REDUCE_TREE, recv = x.type == BINE_PRIM_RECV;
+        if ((!tree && x.src_buf == t.src_buf && x.type != BINE_PRIM_RECV) || (!tree && x.aux_buf == t.src_buf) ||
+            (!recv && x.dst_buf == t.src_buf) || (tree && x.aux_buf == t.src_buf))
+          clean = false;
+      }
+    if (!clean) continue;
+    TreeSpec ts;
+    ts.nl = t.peer;
+    ts.pos = t.pos;
+    ts.swap = (unsigned)t.flags >> 8;
+    ts.own_leaf = ptr(t.aux_buf, t.aux_off);
+    ts.out = ptr(t.dst_buf, t.dst_off);
+    ts.leaf_bytes = t.count * esz;
+    ts.dtype = dtype;
+    ts.op = op;
+    s.clear();
+    r.clear();
+    bool ok = t.peer >= 2;
+    const char *olo = ts.out, *ohi = ts.out + ts.leaf_bytes;
+    for (const Prim &x : sc.ops[i].prims) {
+      if (x.type == BINE_PRIM_SEND) {
+        const char *p = ptr(x.src_buf, x.src_off);
+        if (p < ohi && olo < p + x.count * esz) ok = false;
+        s.push_back({x.peer, p, x.count * esz});
+      } else {
+        if (x.dst_buf != t.src_buf || x.count != t.count || x.dst_off < t.src_off ||
+            (x.dst_off - t.src_off) % t.count) {
+          ok = false;
+          break;
+        }
+        const uint64_t k = (x.dst_off - t.src_off) / t.count;
+        if (k >= (uint64_t)t.peer - 1) {
+          ok = false;
+          break;
+        }
+        ts.leaf_of_recv.push_back((int)k < t.pos ? (int)k : (int)k + 1);
+        r.push_back({x.peer, ptr(x.dst_buf, x.dst_off), x.count * esz});
+      }
+    }
+    if (!ok || !c->tx->tree_ok(s, r, ts)) continue;
+    tree_of[i] = (int)j;
+    tree_at[j] = (int)i;
+    spec[i] = std::move(ts);
+    any = true;
+  }
+  return any;
+}
+
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
                    hipStream_t K, bool single = false, bool joined = false, const Staging *stg = nullptr) {
   char *base[6];
@@ -765,9 +876,23 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   std::vector<hipEvent_t> &hev = c->stage_ev;
   if (stg) hev.assign(sc.ops.size(), nullptr);
   int64_t h_waited[2] = {-1, -1};
+  // trees evaluated inside their exchange (direct transport): tree_of[i] = j
+  std::vector<int> &tree_of = c->tree_of, &tree_at = c->tree_at;
+  std::vector<TreeSpec> &tspec = c->tree_spec;
+  tspec.resize(sc.ops.size());
+  const bool dm_trees = !single && !stg && plan_dm_trees(c, sc, ptr, esz, dtype, op, tree_of, tree_at, tspec);
+  std::vector<hipEvent_t> &tev = c->tree_ev;
+  if (dm_trees) tev.assign(sc.ops.size(), nullptr);
   for (size_t i = 0; i < sc.ops.size(); i++) {
     const SOp &o = sc.ops[i];
     hipStream_t st = o.xchg ? C : K;
+    if (dm_trees && tree_at[i] >= 0) {
+      // this tree ran inside exchange tree_at[i]: K takes up its place in K's
+      // order (later local ops follow it as they followed the tree)
+      HIP_TRY(hipStreamWaitEvent(K, tev[i], 0));
+      if (sc.signals[i]) evs[i] = tev[i];
+      continue;
+    }
     if (trace_on())
       fprintf(stderr, "bine[%d] op %zu/%zu %s wait %lld prims %zu\n", c->rank, i, sc.ops.size(),
               o.xchg ? "xchg" : "local", (long long)o.wait, o.prims.size());
@@ -816,7 +941,17 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
         if (x.type == BINE_PRIM_SEND) sends.push_back({x.peer, ptr(x.src_buf, x.src_off), x.count * esz});
         else recvs.push_back({x.peer, ptr(x.dst_buf, x.dst_off), x.count * esz});
       }
-      rc = a2a_shape(c, sends, recvs) ? c->tx->alltoallv(sends, recvs, C) : c->tx->exchange(sends, recvs, C);
+      if (dm_trees && tree_of[i] >= 0) {
+        // the tree reads the own leaf and writes its output where K's earlier
+        // ops may still be writing / reading: C follows K first
+        if (int rj = stream_join(c, C, K)) return rj;
+        rc = c->tx->exchange_tree(sends, recvs, tspec[i], C);
+        if (rc) return rc;
+        tev[(size_t)tree_of[i]] = next_event(c);
+        HIP_TRY(hipEventRecord(tev[(size_t)tree_of[i]], C));
+      } else {
+        rc = a2a_shape(c, sends, recvs) ? c->tx->alltoallv(sends, recvs, C) : c->tx->exchange(sends, recvs, C);
+      }
       if (rc) return rc;
     } else {
       rc = run_local(o.prims, ptr, dtype, op, esz, K);

@@ -830,9 +830,11 @@ __device__ __forceinline__ uint64_t ld_acq_sys(const uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
+// one workgroup's share of message mi (workgroup wi of a.wgs): wait, copy,
+// release, count in; the last workgroup of the message publishes.  false: the
+// transport is poisoned (the workgroup must leave the launch at once)
+__device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi) {
   using namespace dm;
-  const int mi = (int)(blockIdx.x / (unsigned)a.wgs), wi = (int)(blockIdx.x % (unsigned)a.wgs);
   const DmMsg &m = a.m[mi];
   uint8_t *own = a.own;
   uint32_t *poison = reinterpret_cast<uint32_t *>(own + kPoisonOff);
@@ -885,7 +887,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
     go = ok;
   }
   __syncthreads();
-  if (!go) return;  // poisoned: the transport is dead, counters and bases no longer matter
+  if (!go) return false;  // poisoned: the transport is dead, counters and bases no longer matter
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the peer released before its mark
   // grid-strided 16-B vectors (src / dst co-aligned mod 16: slots and plan
   // offsets are), bytes before the first boundary and after the last vector
@@ -914,7 +916,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
     }
   }
   // release this workgroup's stores, count it in; the last one of the message
-  // publishes, the last one of the launch advances the sequence bases
+  // publishes
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -930,19 +932,32 @@ __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(sig_ptr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    uint32_t *lc = reinterpret_cast<uint32_t *>(own + kLaunchCntOff);
-    const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (ol + 1 == gridDim.x) {
-      // every workgroup has read its base: advance them for the next launch
-      // (stream-ordered after this one)
-      __hip_atomic_store(lc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int i = 0; i < a.nmsg; i++) {
-        uint64_t *bp = reinterpret_cast<uint64_t *>(own + (a.m[i].push ? kBaseSendOff : kBaseRecvOff)) + a.m[i].peer;
-        __hip_atomic_store(bp, __hip_atomic_load(bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+  }
+  return true;
+}
+
+// thread 0, after its workgroup's share of the launch: the last workgroup of
+// the launch advances the sequence bases of every message (every workgroup has
+// read them; the next launch is stream-ordered after this one)
+__device__ __forceinline__ void dm_launch_done(const DmArgs &a) {
+  using namespace dm;
+  if (threadIdx.x != 0) return;
+  uint8_t *own = a.own;
+  uint32_t *lc = reinterpret_cast<uint32_t *>(own + kLaunchCntOff);
+  const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (ol + 1 == gridDim.x) {
+    __hip_atomic_store(lc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < a.nmsg; i++) {
+      uint64_t *bp = reinterpret_cast<uint64_t *>(own + (a.m[i].push ? kBaseSendOff : kBaseRecvOff)) + a.m[i].peer;
+      __hip_atomic_store(bp, __hip_atomic_load(bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
+  if (!dm_copy_msg(a, (int)(blockIdx.x / (unsigned)a.wgs), (int)(blockIdx.x % (unsigned)a.wgs))) return;
+  dm_launch_done(a);
 }
 
 int launch_dm_move(const DmArgs &a, void *stream) {
@@ -954,6 +969,156 @@ int launch_dm_move(const DmArgs &a, void *stream) {
       return BINE_ERR_ARG;
   hipLaunchKernelGGL(k_dm_move, dim3((unsigned)(a.nmsg * a.wgs)), dim3(kBlock), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// k_dm_move_tree<T, OP, NL> (bine_internal.h DmTree): the copy messages as in
+// k_dm_move, then `twgs` workgroups that evaluate the flat reduce-scatter's
+// tree straight out of the leaf pulls' inbox slots
+template <typename T, int OP, int NL>
+__global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
+  using namespace dm;
+  const unsigned ncw = (unsigned)t.ncopy * (unsigned)a.wgs;
+  if (blockIdx.x < ncw) {
+    if (!dm_copy_msg(a, t.cidx[blockIdx.x / (unsigned)a.wgs], (int)(blockIdx.x % (unsigned)a.wgs))) return;
+    dm_launch_done(a);
+    return;
+  }
+  uint8_t *own = a.own;
+  uint32_t *poison = reinterpret_cast<uint32_t *>(own + kPoisonOff);
+  // every leaf: its slot in our inbox, the sender's ready mark to wait for
+  const u32x4 *lp[NL];
+  __shared__ int go;
+  if (threadIdx.x == 0) go = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NL; j++) {
+    if (j == t.pos) {
+      lp[j] = reinterpret_cast<const u32x4 *>(t.own_leaf);
+      continue;
+    }
+    const DmMsg &m = a.m[t.leaf_msg[j]];
+    const uint64_t seq = __hip_atomic_load(reinterpret_cast<const uint64_t *>(own + kBaseRecvOff) + m.peer,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
+    const size_t k = (size_t)(seq % kSlots);
+    lp[j] = reinterpret_cast<const u32x4 *>(own + kFlagsBytes + ((size_t)m.peer * kSlots + k) * a.slot);
+    if (threadIdx.x == 0 && go) {
+      const uint64_t *w = reinterpret_cast<const uint64_t *>(own + kReadyOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+      const long long t0 = wall_clock64();
+      while (ld_acq_sys(w) < seq) {
+        if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
+          __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          go = 0;
+          break;
+        }
+        if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          go = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  __syncthreads();
+  if (!go) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the senders released before their marks
+  // the tree over this workgroup's tiles (k_reduce_tree's tile body)
+  constexpr int U = NL == 2 ? 8 : NL <= 8 ? 4 : 2;
+  const int tw = (int)(blockIdx.x - ncw);
+  u32x4 *vo = reinterpret_cast<u32x4 *>(t.out);
+  const size_t tile = (size_t)kBlock * U, ntiles = (t.nvec + tile - 1) / tile;
+  for (size_t ti = (size_t)tw; ti < ntiles; ti += (size_t)t.twgs) {
+    const size_t b = ti * tile + threadIdx.x;
+    if ((ti + 1) * tile <= t.nvec) tree_tile<T, OP, NL, U, false>(lp, vo, b, t.nvec, t.swap);
+    else tree_tile<T, OP, NL, U, true>(lp, vo, b, t.nvec, t.swap);
+  }
+  // every leaf slice read: count in per leaf; the last tree workgroup of a
+  // leaf acknowledges its slot to the sender (as a pull's last workgroup does)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+      if (j == t.pos) continue;
+      const DmMsg &m = a.m[t.leaf_msg[j]];
+      const uint64_t seq = __hip_atomic_load(reinterpret_cast<const uint64_t *>(own + kBaseRecvOff) + m.peer,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
+      const size_t k = (size_t)(seq % kSlots);
+      uint32_t *cnt = reinterpret_cast<uint32_t *>(own + kCntPullOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+      const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (old + 1 == (uint32_t)t.twgs) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
+        uint64_t *sig = reinterpret_cast<uint64_t *>(remote + kAckOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(sig, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  dm_launch_done(a);
+}
+
+bool dm_tree_supported(int dtype, int op, int nl) {
+  return dm_fused_supported(dtype, op) && (nl == 2 || nl == 4 || nl == 8 || nl == 16);
+}
+
+template <typename T, int OP>
+static hipError_t dmt_launch(const DmArgs &a, const DmTree &t, hipStream_t st) {
+  const dim3 g((unsigned)(t.ncopy * a.wgs + t.twgs));
+  switch (t.nl) {
+    case 2: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 2>), g, dim3(kBlock), 0, st, a, t); break;
+    case 4: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 4>), g, dim3(kBlock), 0, st, a, t); break;
+    case 8: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 8>), g, dim3(kBlock), 0, st, a, t); break;
+    case 16: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 16>), g, dim3(kBlock), 0, st, a, t); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t dmt_t(const DmArgs &a, const DmTree &t, int op, hipStream_t st) {
+#define CALL(OP) dmt_launch<T, OP>(a, t, st)
+  BINE_OP_SWITCH(T, CALL)
+#undef CALL
+}
+
+int launch_dm_move_tree(const DmArgs &a, const DmTree &t, int dtype, int op, void *stream) {
+  if (!dm_tree_supported(dtype, op, t.nl)) return BINE_ERR_UNSUPPORTED;
+  if (a.nmsg <= 0 || a.nmsg > kMaxDm || a.wgs < 1 || !a.own || !a.slot || t.twgs < 1 || t.ncopy < 0 ||
+      t.ncopy + t.nl - 1 != a.nmsg || t.pos < 0 || t.pos >= t.nl || !t.nvec || t.nvec * 16 > a.slot || !t.out ||
+      !t.own_leaf || ((uintptr_t)t.out & 15) || ((uintptr_t)t.own_leaf & 15))
+    return BINE_ERR_ARG;
+  for (int i = 0; i < a.nmsg; i++)
+    if (a.m[i].peer < 0 || a.m[i].peer >= dm::kMaxPeers || a.m[i].j < 0 || a.m[i].j >= dm::kSlots ||
+        a.m[i].bytes > a.slot)
+      return BINE_ERR_ARG;
+  // every copy message once, every leaf position but pos once, by a leaf pull of nvec vectors
+  unsigned seen = 0;
+  for (int c = 0; c < t.ncopy; c++) {
+    const int i = t.cidx[c];
+    if (i < 0 || i >= a.nmsg || a.m[i].leaf >= 0 || (seen >> i & 1)) return BINE_ERR_ARG;
+    seen |= 1u << i;
+  }
+  for (int j = 0; j < t.nl; j++) {
+    if (j == t.pos) continue;
+    const int i = t.leaf_msg[j];
+    if (i < 0 || i >= a.nmsg || (seen >> i & 1) || a.m[i].push || a.m[i].leaf != j || a.m[i].bytes != t.nvec * 16)
+      return BINE_ERR_ARG;
+    seen |= 1u << i;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case BINE_FLOAT: e = dmt_t<float>(a, t, op, st); break;
+    case BINE_DOUBLE: e = dmt_t<double>(a, t, op, st); break;
+    case BINE_INT32: e = dmt_t<int32_t>(a, t, op, st); break;
+    case BINE_INT64: e = dmt_t<int64_t>(a, t, op, st); break;
+    case BINE_UINT32: e = dmt_t<uint32_t>(a, t, op, st); break;
+    case BINE_UINT64: e = dmt_t<uint64_t>(a, t, op, st); break;
+    default: return BINE_ERR_UNSUPPORTED;
+  }
+  return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
 // ----------------------------------------------------------------------------
