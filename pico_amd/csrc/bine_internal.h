@@ -154,7 +154,7 @@ int launch_fill_pico(void *buf, size_t count, int dtype, uint32_t seed, void *st
 // device (per peer and direction, in the rank's own inbox) and every address
 // and flag is derived from them in the kernel, so launches carry no host-side
 // state and can be captured into a graph and replayed.
-constexpr int kMaxDm = 16;
+constexpr int kMaxDm = 32;
 // the inbox layout (bytes from its base): flags region, then the data slots
 namespace dm {
 constexpr size_t kFlagStride = 128;  // one flag / counter per 128-B line

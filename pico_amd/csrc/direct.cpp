@@ -352,9 +352,22 @@ bool DirectState::tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> 
   return true;
 }
 
+bool DirectState::defer_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r,
+                           const std::vector<XRecv> &dl, const TreeSpec &t) const {
+  if (!tree_ok({}, dl, t) || t.leaf_bytes > slot) return false;
+  // the first launch holds the deferred leaves, every send's and (one round,
+  // or merge 2) every receive's first sub-message
+  size_t maxb = 0;
+  for (const auto &x : s) maxb = std::max(maxb, x.bytes);
+  for (const auto &x : r) maxb = std::max(maxb, x.bytes);
+  const bool pulls_first = merge == 2 || (merge == 3 && maxb <= slot);
+  return dl.size() + s.size() + (pulls_first ? r.size() : 0) <= (size_t)kMaxDm;
+}
+
 int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st,
-                          const TreeSpec *tree) {
+                          const TreeSpec *tree, const std::vector<XRecv> *dleaves, const TreeSpec *dtree) {
   if (tree && !tree_ok(s, r, *tree)) return BINE_ERR_UNSUPPORTED;
+  if (dleaves && (tree || !dtree || !defer_ok(s, r, *dleaves, *dtree))) return BINE_ERR_UNSUPPORTED;
   // more messages to (or from) one peer in one exchange than slots per pair
   // would make a push wait for a pull of the same exchange: refuse
   std::vector<int> ns((size_t)P, 0), nr((size_t)P, 0);
@@ -379,25 +392,27 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   // a launch holding leaf pulls (all of one round: tree_ok) evaluates that
   // round's tree in place of copying them
   int tree_round = -1;
+  const TreeSpec *ltree = tree;  // the tree of the launch being built
   auto flush = [&]() -> int {
     int rc;
     if (tree_round >= 0) {
       DmTree t;
-      t.nl = tree->nl;
-      t.pos = tree->pos;
-      t.swap = tree->swap;
+      t.nl = ltree->nl;
+      t.pos = ltree->pos;
+      t.swap = ltree->swap;
       t.twgs = tree_wgs;
-      const size_t off = (size_t)tree_round * slot, len = std::min(slot, tree->leaf_bytes - off);
-      t.own_leaf = tree->own_leaf + off;
-      t.out = tree->out + off;
+      const size_t off = (size_t)tree_round * slot, len = std::min(slot, ltree->leaf_bytes - off);
+      t.own_leaf = ltree->own_leaf + off;
+      t.out = ltree->out + off;
       t.nvec = len / 16;
       for (int j = 0; j < kMaxLeaves; j++) t.leaf_msg[j] = -1;
       for (int i = 0; i < a.nmsg; i++) {
         if (a.m[i].leaf >= 0) t.leaf_msg[a.m[i].leaf] = i;
         else t.cidx[t.ncopy++] = i;
       }
-      rc = launch_dm_move_tree(a, t, tree->dtype, tree->op, st);
+      rc = launch_dm_move_tree(a, t, ltree->dtype, ltree->op, st);
       tree_round = -1;
+      ltree = tree;
     } else {
       rc = launch_dm_move(a, st);
     }
@@ -445,6 +460,24 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
     }
     return BINE_SUCCESS;
   };
+  // the deferred leaves (one sub-message each, defer_ok): pulled first --
+  // their sender pushed them before anything of this exchange -- and
+  // evaluated by the first launch's tree workgroups
+  if (dleaves) {
+    for (size_t i = 0; i < dleaves->size(); i++) {
+      const auto &x = (*dleaves)[i];
+      DmMsg &m = a.m[a.nmsg++];
+      m.src = nullptr;
+      m.dst = (uint8_t *)x.ptr;
+      m.bytes = x.bytes;
+      m.push = 0;
+      m.peer = x.peer;
+      m.j = jr[(size_t)x.peer]++;
+      m.leaf = dtree->leaf_of_recv[i];
+    }
+    tree_round = 0;
+    ltree = dtree;
+  }
   // merge = 2: launch k carries round k's pushes and then round k's pulls --
   // one launch per round, a pull's workgroups waiting for the peer's push of
   // the same round.  The pushes come first in workgroup order, so they

@@ -48,11 +48,20 @@ struct DirectState {
   // phase 2, collective over the P ranks of the node (same key on all):
   // exchange descriptors over Unix sockets, map every peer's inbox
   int connect_peers(uint64_t key, std::string &err);
+  // tree: the receives r are the leaves of `tree`, evaluated in this
+  // exchange's launches; dleaves + dtree: the receives of an EARLIER exchange
+  // (issued there without them) are the leaves of `dtree`, pulled and
+  // evaluated in this exchange's first launch, beside its own messages
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st,
-               const TreeSpec *tree = nullptr);
+               const TreeSpec *tree = nullptr, const std::vector<XRecv> *dleaves = nullptr,
+               const TreeSpec *dtree = nullptr);
   // whether exchange() can take `tree` for these sends / receives (all of one
   // round's messages in one launch, 16-B vectors, an instantiated tree)
   bool tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &tree) const;
+  // whether an exchange with these sends / receives can host the deferred
+  // leaves of `dtree` (one slot each, all in its first launch)
+  bool defer_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const std::vector<XRecv> &dleaves,
+                const TreeSpec &dtree) const;
   int tree_wgs = 256;  // tree workgroups per launch (BINE_DIRECT_TREE_WGS)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }
   // stderr: this rank's flags and device-side sequence bases (after a timeout)

@@ -93,7 +93,13 @@ struct Transport {
   virtual bool tree_ok(const std::vector<XSend> &, const std::vector<XRecv> &, const TreeSpec &) const {
     return false;
   }
-  virtual int exchange_tree(const std::vector<XSend> &, const std::vector<XRecv> &, const TreeSpec &, hipStream_t) {
+  virtual bool defer_ok(const std::vector<XSend> &, const std::vector<XRecv> &, const std::vector<XRecv> &,
+                        const TreeSpec &) const {
+    return false;
+  }
+  // DirectState::exchange's tree / deferred-leaves forms
+  virtual int exchange_tree(const std::vector<XSend> &, const std::vector<XRecv> &, const TreeSpec *,
+                            const std::vector<XRecv> *, const TreeSpec *, hipStream_t) {
     return BINE_ERR_UNSUPPORTED;
   }
 };
@@ -197,14 +203,18 @@ struct RcclTransport final : Transport {
   bool tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &t) const override {
     return dm_on && dm && dm->tree_ok(s, r, t);
   }
-  int exchange_tree(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &t,
-                    hipStream_t st) override {
+  bool defer_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const std::vector<XRecv> &dl,
+                const TreeSpec &t) const override {
+    return dm_on && dm && dm->defer_ok(s, r, dl, t);
+  }
+  int exchange_tree(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec *t,
+                    const std::vector<XRecv> *dl, const TreeSpec *dt, hipStream_t st) override {
     if (!dm_on) return BINE_ERR_UNSUPPORTED;
     if (dm->poisoned()) {
       set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
       return BINE_ERR_INTERNAL;
     }
-    return dm->exchange(s, r, st, &t);
+    return dm->exchange(s, r, st, t, dl, dt);
   }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
     if (dm_on) {
@@ -345,6 +355,14 @@ struct LoopbackTransport final : Transport {
   }
 };
 
+// the trees plan_dm_trees (below) fuses into exchange launches
+struct DmTreePlan {
+  std::vector<int> tree_at, host, hosted;
+  std::vector<char> defer;
+  std::vector<TreeSpec> spec;                // by tree op j
+  std::vector<std::vector<XRecv>> leaves;    // by tree op j: exchange i's receives
+};
+
 }  // namespace bine
 
 // ---------------------------------------------------------------------------
@@ -391,9 +409,9 @@ struct bine_comm {
   std::vector<hipEvent_t> op_ev;  // scratch of execute()
   std::vector<hipEvent_t> stage_ev;  // scratch of execute(): host staging batches
   // scratch of execute(): trees evaluated inside their exchange (plan_dm_trees)
-  std::vector<int> tree_of, tree_at;
-  std::vector<bine::TreeSpec> tree_spec;
+  bine::DmTreePlan tree_plan;
   std::vector<hipEvent_t> tree_ev;
+  std::vector<char> tree_pending;
   // per-op device timing of the latest collective (bine_comm_set_profile)
   bool profile = false;
   struct OpTime { hipEvent_t a = nullptr, b = nullptr; int xchg = 0, nprims = 0; uint64_t bytes = 0; };
@@ -759,32 +777,57 @@ static bool dm_tree_on() {
   return on;
 }
 
-// Exchange i whose receives are exactly the leaves of the tree op j that
-// follows it -- the flat reduce-scatter's [exchange A][REDUCE_TREE] pair, with
-// only exchanges in between and j waiting for i -- is issued over the direct
-// transport as ONE exchange that evaluates the tree in its own launches,
-// reading the leaves in place in the inbox slots (TreeSpec, k_dm_move_tree).
-// Conditions: the staging buffer the leaves were received into is referenced
-// by nothing but receives and trees (no one else reads what is no longer
-// written), the tree's output overlaps no block the exchange sends (it is
-// written while the pushes still read), and the transport takes the shape
-// (tree_ok).  Fills tree_of[i] = j and tree_at[j] = i; false: none.
+// Trees of the flat reduce-scatter over the direct transport, evaluated
+// inside an exchange launch instead of as pull copies into the staging area
+// plus a separate k_reduce_tree launch (TreeSpec, k_dm_move_tree).  A pair
+// [exchange i][...exchanges...][tree j] -- j the first local op after i,
+// waiting for i, its non-own leaves exactly i's receives -- is hosted
+//   * deferred (preferred): by the NEXT exchange i2 after i, whose first
+//     launch pulls i's receives (issued at i without them) and evaluates the
+//     tree beside i2's own messages -- tree k then overlaps the pushes of
+//     chunk k + 1, as the separate tree launch on the caller's stream did.
+//     Needs: i2 = i + 1 before j, or i2 = j + 1 (no op of either stream
+//     between the tree's place and its host); i2 neither reads the tree's
+//     output nor writes its output or own leaf, nor waits for j; leaves of
+//     one slot each; i2 hosts no other tree;
+//   * in its own exchange i otherwise (the last chunk's tree): the tree
+//     workgroups of round r beside the pushes of round r + 1 (merge 1), or of
+//     the one round; its output must overlap no block i sends;
+//   * not at all (the unfused form) when neither applies.
+// Always: the staging buffer is referenced by receives and trees only (no one
+// else reads what is no longer written there).  host[j] = the hosting
+// exchange, hosted[x] = the tree exchange x evaluates, tree_at[j] = i,
+// defer[i]: i's receives are pulled by the host; false: no fused tree at all.
 template <typename Ptr>
-static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op,
-                          std::vector<int> &tree_of, std::vector<int> &tree_at, std::vector<TreeSpec> &spec) {
+static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, DmTreePlan &pl) {
   const size_t n = sc.ops.size();
-  tree_of.assign(n, -1);
-  tree_at.assign(n, -1);
+  pl.tree_at.assign(n, -1);
+  pl.host.assign(n, -1);
+  pl.hosted.assign(n, -1);
+  pl.defer.assign(n, 0);
+  pl.spec.resize(n);
+  pl.leaves.resize(n);
   if (!c->tx->stream_ordered() || !dm_tree_on() || op < 0 || c->profile) return false;
+  auto sends_of = [&](size_t x, std::vector<XSend> &s) {
+    s.clear();
+    for (const Prim &p : sc.ops[x].prims)
+      if (p.type == BINE_PRIM_SEND) s.push_back({p.peer, ptr(p.src_buf, p.src_off), p.count * esz});
+  };
+  auto recvs_of = [&](size_t x, std::vector<XRecv> &r) {
+    r.clear();
+    for (const Prim &p : sc.ops[x].prims)
+      if (p.type == BINE_PRIM_RECV) r.push_back({p.peer, ptr(p.dst_buf, p.dst_off), p.count * esz});
+  };
+  auto overlaps = [](const char *a, size_t na, const char *b, size_t nb) { return a < b + nb && b < a + na; };
   bool any = false;
-  std::vector<XSend> s;
-  std::vector<XRecv> r;
+  std::vector<XSend> s, s2;
+  std::vector<XRecv> r, r2;
   for (size_t i = 0; i < n; i++) {
     if (!sc.ops[i].xchg) continue;
     size_t j = i + 1;
     while (j < n && sc.ops[j].xchg) j++;
     if (j >= n || sc.ops[j].wait != (int64_t)i || sc.ops[j].prims.size() != 1 ||
-        sc.ops[j].prims[0].type != BINE_PRIM_REDUCE_TREE || tree_at[j] >= 0)
+        sc.ops[j].prims[0].type != BINE_PRIM_REDUCE_TREE)
       continue;
     const Prim &t = sc.ops[j].prims[0];
     // the staging buffer: only receives write it, only trees read it
@@ -792,8 +835,7 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
     for (const SOp &o : sc.ops)
       for (const Prim &x : o.prims) {
         const bool tree = x.type == BINE_PRIM_REDUCE_TREE, recv = x.type == BINE_PRIM_RECV;
-        if ((!tree && x.src_buf == t.src_buf && x.type != BINE_PRIM_RECV) || (!tree && x.aux_buf == t.src_buf) ||
-            (!recv && x.dst_buf == t.src_buf) || (tree && x.aux_buf == t.src_buf))
+        if ((!tree && !recv && x.src_buf == t.src_buf) || x.aux_buf == t.src_buf || (!recv && x.dst_buf == t.src_buf))
           clean = false;
       }
     if (!clean) continue;
@@ -806,34 +848,52 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
     ts.leaf_bytes = t.count * esz;
     ts.dtype = dtype;
     ts.op = op;
-    s.clear();
-    r.clear();
     bool ok = t.peer >= 2;
-    const char *olo = ts.out, *ohi = ts.out + ts.leaf_bytes;
     for (const Prim &x : sc.ops[i].prims) {
-      if (x.type == BINE_PRIM_SEND) {
-        const char *p = ptr(x.src_buf, x.src_off);
-        if (p < ohi && olo < p + x.count * esz) ok = false;
-        s.push_back({x.peer, p, x.count * esz});
-      } else {
-        if (x.dst_buf != t.src_buf || x.count != t.count || x.dst_off < t.src_off ||
-            (x.dst_off - t.src_off) % t.count) {
-          ok = false;
-          break;
-        }
-        const uint64_t k = (x.dst_off - t.src_off) / t.count;
-        if (k >= (uint64_t)t.peer - 1) {
-          ok = false;
-          break;
-        }
-        ts.leaf_of_recv.push_back((int)k < t.pos ? (int)k : (int)k + 1);
-        r.push_back({x.peer, ptr(x.dst_buf, x.dst_off), x.count * esz});
+      if (x.type != BINE_PRIM_RECV) continue;
+      if (x.dst_buf != t.src_buf || x.count != t.count || x.dst_off < t.src_off || (x.dst_off - t.src_off) % t.count) {
+        ok = false;
+        break;
       }
+      const uint64_t k = (x.dst_off - t.src_off) / t.count;
+      if (k >= (uint64_t)t.peer - 1) {
+        ok = false;
+        break;
+      }
+      ts.leaf_of_recv.push_back((int)k < t.pos ? (int)k : (int)k + 1);
     }
-    if (!ok || !c->tx->tree_ok(s, r, ts)) continue;
-    tree_of[i] = (int)j;
-    tree_at[j] = (int)i;
-    spec[i] = std::move(ts);
+    if (!ok) continue;
+    sends_of(i, s);
+    recvs_of(i, r);
+    // deferred into the next exchange i2
+    size_t i2 = i + 1;
+    while (i2 < n && !sc.ops[i2].xchg) i2++;
+    bool dfr = i2 < n && ((i2 == i + 1 && i2 < j) || i2 == j + 1) && pl.hosted[i2] < 0 &&
+               sc.ops[i2].wait != (int64_t)j;
+    if (dfr) {
+      sends_of(i2, s2);
+      recvs_of(i2, r2);
+      for (const XSend &x : s2) dfr = dfr && !overlaps((const char *)x.ptr, x.bytes, ts.out, ts.leaf_bytes);
+      for (const XRecv &x : r2)
+        dfr = dfr && !overlaps((const char *)x.ptr, x.bytes, ts.out, ts.leaf_bytes) &&
+              !overlaps((const char *)x.ptr, x.bytes, ts.own_leaf, ts.leaf_bytes);
+      dfr = dfr && c->tx->defer_ok(s2, r2, r, ts);
+    }
+    size_t hx = n;
+    if (dfr) {
+      hx = i2;
+      pl.defer[i] = 1;
+    } else if (pl.hosted[i] < 0) {
+      bool own = true;  // in its own exchange: the output is written while the pushes still read
+      for (const XSend &x : s) own = own && !overlaps((const char *)x.ptr, x.bytes, ts.out, ts.leaf_bytes);
+      if (own && c->tx->tree_ok(s, r, ts)) hx = i;
+    }
+    if (hx == n) continue;
+    pl.tree_at[j] = (int)i;
+    pl.host[j] = (int)hx;
+    pl.hosted[hx] = (int)j;
+    pl.leaves[j] = r;
+    pl.spec[j] = std::move(ts);
     any = true;
   }
   return any;
@@ -876,21 +936,28 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   std::vector<hipEvent_t> &hev = c->stage_ev;
   if (stg) hev.assign(sc.ops.size(), nullptr);
   int64_t h_waited[2] = {-1, -1};
-  // trees evaluated inside their exchange (direct transport): tree_of[i] = j
-  std::vector<int> &tree_of = c->tree_of, &tree_at = c->tree_at;
-  std::vector<TreeSpec> &tspec = c->tree_spec;
-  tspec.resize(sc.ops.size());
-  const bool dm_trees = !single && !stg && plan_dm_trees(c, sc, ptr, esz, dtype, op, tree_of, tree_at, tspec);
+  // trees evaluated inside an exchange launch (direct transport; plan_dm_trees)
+  DmTreePlan &tp = c->tree_plan;
+  const bool dm_trees = !single && !stg && plan_dm_trees(c, sc, ptr, esz, dtype, op, tp);
   std::vector<hipEvent_t> &tev = c->tree_ev;
-  if (dm_trees) tev.assign(sc.ops.size(), nullptr);
+  std::vector<char> &tpend = c->tree_pending;
+  if (dm_trees) {
+    tev.assign(sc.ops.size(), nullptr);
+    tpend.assign(sc.ops.size(), 0);
+  }
   for (size_t i = 0; i < sc.ops.size(); i++) {
     const SOp &o = sc.ops[i];
     hipStream_t st = o.xchg ? C : K;
-    if (dm_trees && tree_at[i] >= 0) {
-      // this tree ran inside exchange tree_at[i]: K takes up its place in K's
-      // order (later local ops follow it as they followed the tree)
-      HIP_TRY(hipStreamWaitEvent(K, tev[i], 0));
-      if (sc.signals[i]) evs[i] = tev[i];
+    if (dm_trees && tp.host[i] >= 0) {
+      // this tree runs inside exchange host[i]: K takes up its place in K's
+      // order (later local ops follow it as they followed the tree) -- now,
+      // or right after the host is issued when that comes next
+      if (tev[i]) {
+        HIP_TRY(hipStreamWaitEvent(K, tev[i], 0));
+        if (sc.signals[i]) evs[i] = tev[i];
+      } else {
+        tpend[i] = 1;
+      }
       continue;
     }
     if (trace_on())
@@ -941,14 +1008,23 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
         if (x.type == BINE_PRIM_SEND) sends.push_back({x.peer, ptr(x.src_buf, x.src_off), x.count * esz});
         else recvs.push_back({x.peer, ptr(x.dst_buf, x.dst_off), x.count * esz});
       }
-      if (dm_trees && tree_of[i] >= 0) {
+      const int hj = dm_trees ? tp.hosted[i] : -1;
+      if (dm_trees && tp.defer[i]) recvs.clear();  // pulled by the next exchange, for its tree
+      if (hj >= 0) {
         // the tree reads the own leaf and writes its output where K's earlier
         // ops may still be writing / reading: C follows K first
         if (int rj = stream_join(c, C, K)) return rj;
-        rc = c->tx->exchange_tree(sends, recvs, tspec[i], C);
+        const bool own = tp.tree_at[(size_t)hj] == (int)i;
+        rc = own ? c->tx->exchange_tree(sends, recvs, &tp.spec[(size_t)hj], nullptr, nullptr, C)
+                 : c->tx->exchange_tree(sends, recvs, nullptr, &tp.leaves[(size_t)hj], &tp.spec[(size_t)hj], C);
         if (rc) return rc;
-        tev[(size_t)tree_of[i]] = next_event(c);
-        HIP_TRY(hipEventRecord(tev[(size_t)tree_of[i]], C));
+        hipEvent_t e = next_event(c);
+        HIP_TRY(hipEventRecord(e, C));
+        tev[(size_t)hj] = e;
+        if (tpend[(size_t)hj]) {  // the tree's place in K's order came first
+          HIP_TRY(hipStreamWaitEvent(K, e, 0));
+          if (sc.signals[(size_t)hj]) evs[(size_t)hj] = e;
+        }
       } else {
         rc = a2a_shape(c, sends, recvs) ? c->tx->alltoallv(sends, recvs, C) : c->tx->exchange(sends, recvs, C);
       }

@@ -1022,8 +1022,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
   __syncthreads();
   if (!go) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the senders released before their marks
-  // the tree over this workgroup's tiles (k_reduce_tree's tile body)
-  constexpr int U = NL == 2 ? 8 : NL <= 8 ? 4 : 2;
+  // the tree over this workgroup's tiles (k_reduce_tree's tile body).  Fewer
+  // vectors in flight per lane than k_reduce_tree: the copy workgroups of the
+  // launch get this kernel's register allocation too
+  constexpr int U = NL <= 4 ? 4 : NL == 8 ? 2 : 1;
   const int tw = (int)(blockIdx.x - ncw);
   u32x4 *vo = reinterpret_cast<u32x4 *>(t.out);
   const size_t tile = (size_t)kBlock * U, ntiles = (t.nvec + tile - 1) / tile;
@@ -1094,18 +1096,18 @@ int launch_dm_move_tree(const DmArgs &a, const DmTree &t, int dtype, int op, voi
         a.m[i].bytes > a.slot)
       return BINE_ERR_ARG;
   // every copy message once, every leaf position but pos once, by a leaf pull of nvec vectors
-  unsigned seen = 0;
+  uint64_t seen = 0;
   for (int c = 0; c < t.ncopy; c++) {
     const int i = t.cidx[c];
     if (i < 0 || i >= a.nmsg || a.m[i].leaf >= 0 || (seen >> i & 1)) return BINE_ERR_ARG;
-    seen |= 1u << i;
+    seen |= 1ull << i;
   }
   for (int j = 0; j < t.nl; j++) {
     if (j == t.pos) continue;
     const int i = t.leaf_msg[j];
     if (i < 0 || i >= a.nmsg || (seen >> i & 1) || a.m[i].push || a.m[i].leaf != j || a.m[i].bytes != t.nvec * 16)
       return BINE_ERR_ARG;
-    seen |= 1u << i;
+    seen |= 1ull << i;
   }
   hipStream_t st = (hipStream_t)stream;
   hipError_t e;

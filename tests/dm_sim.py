@@ -18,12 +18,17 @@ import pico_amd
 SLOTS = 4
 
 
-def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3):
+def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3, deferred=()):
     """DirectState::exchange for one exchange: list of launches, each a list
-    of messages {kind, peer, seq}"""
+    of messages {kind, peer, seq}.  `deferred`: an earlier exchange's leaf
+    receives (one slot each) pulled at the start of the first launch"""
     maxb = max([b for _, b in sends] + [b for _, b in recvs] + [0])
     rounds = (maxb + slot - 1) // slot
     out = []
+    pre = []
+    for p, _ in deferred:
+        seq_r[p] += 1
+        pre.append({"kind": "pull", "peer": p, "seq": seq_r[p]})
     ns, nr = [0] * P, [0] * P
     for p, _ in sends:
         ns[p] += 1
@@ -52,12 +57,14 @@ def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3):
     # (the library's default): 2 for one round, else 1
     if merge == 2 or (merge == 3 and rounds == 1):
         for k in range(rounds):
-            launch = pushes(k) + pulls(k)
+            launch = (pre if k == 0 else []) + pushes(k) + pulls(k)
             if launch:
                 out.append(launch)
+        if rounds == 0 and pre:
+            out.append(pre)
         return out
     for k in range(rounds + 1):
-        launch = pulls(k - 1) if k > 0 else []
+        launch = pulls(k - 1) if k > 0 else list(pre)
         if not merge and launch:
             out.append(launch)
             launch = []
@@ -68,10 +75,78 @@ def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3):
     return out
 
 
+def dm_tree_src(ops, i):
+    """the tree op fed by exchange i: the first local op after it"""
+    j = i + 1
+    while j < len(ops) and ops[j]["xchg"]:
+        j += 1
+    return j
+
+
+def dm_tree_plan(ops, esz, slot, kmax=32):
+    """tests' restatement of the executor's plan_dm_trees (executor.cpp) on
+    symbolic ranges (buffer, element offset, count): {tree op j: host
+    exchange}, {exchange i: deferred}"""
+    n = len(ops)
+
+    def ranges(o, kind):
+        return [(p["src_buf"] if kind == "SEND" else p["dst_buf"],
+                 p["src_off"] if kind == "SEND" else p["dst_off"], p["count"]) for p in o["prims"]
+                if p["type"] == kind]
+
+    def ov(a, b):
+        return a[0] == b[0] and a[1] < b[1] + b[2] and b[1] < a[1] + a[2]
+
+    host, hosted, defer = {}, {}, set()
+    for i in range(n):
+        if not ops[i]["xchg"]:
+            continue
+        j = i + 1
+        while j < n and ops[j]["xchg"]:
+            j += 1
+        if j >= n or ops[j]["wait"] != i or len(ops[j]["prims"]) != 1 or ops[j]["prims"][0]["type"] != "REDUCE_TREE":
+            continue
+        t = ops[j]["prims"][0]
+        clean = all(not ((x["type"] not in ("REDUCE_TREE", "RECV") and x["src_buf"] == t["src_buf"])
+                         or x["aux_buf"] == t["src_buf"] or (x["type"] != "RECV" and x["dst_buf"] == t["src_buf"]))
+                    for o in ops for x in o["prims"])
+        recvs = [p for p in ops[i]["prims"] if p["type"] == "RECV"]
+        ok = clean and t["peer"] >= 2 and len(recvs) == t["peer"] - 1 and all(
+            p["dst_buf"] == t["src_buf"] and p["count"] == t["count"] and p["dst_off"] >= t["src_off"]
+            and (p["dst_off"] - t["src_off"]) % t["count"] == 0 for p in recvs)
+        if not ok:
+            continue
+        out = (t["dst_buf"], t["dst_off"], t["count"])
+        own = (t["aux_buf"], t["aux_off"], t["count"])
+        i2 = i + 1
+        while i2 < n and not ops[i2]["xchg"]:
+            i2 += 1
+        lb = t["count"] * esz
+        dfr = (i2 < n and ((i2 == i + 1 and i2 < j) or i2 == j + 1) and i2 not in hosted and ops[i2]["wait"] != j
+               and lb <= slot and lb % 16 == 0)
+        if dfr:
+            s2, r2 = ranges(ops[i2], "SEND"), ranges(ops[i2], "RECV")
+            dfr = not any(ov(x, out) for x in s2) and not any(ov(x, out) or ov(x, own) for x in r2)
+            maxb = max([x[2] * esz for x in s2 + r2] + [0])
+            dfr = dfr and len(recvs) + len(s2) + (len(r2) if maxb <= slot else 0) <= kmax
+        if dfr:
+            host[j] = i2
+            hosted[i2] = j
+            defer.add(i)
+        elif i not in hosted:
+            s1 = ranges(ops[i], "SEND")
+            if not any(ov(x, out) for x in s1) and len(s1) + len(recvs) <= kmax and lb % 16 == 0:
+                host[j] = i
+                hosted[i] = j
+    return host, hosted, defer
+
+
 def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay_min_bytes=0, trees=False,
-        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20, merge=3):
+        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20, merge=3, dm_trees=False, stats=None):
     """simulate `calls` consecutive collectives on all ranks; returns None if
-    every one completes, else a description of the deadlock"""
+    every one completes, else a description of the deadlock.  dm_trees: the
+    flat reduce-scatter's trees fused into exchange launches as the executor
+    does over the direct transport (deferred leaf pulls; `stats` counts them)"""
     seq_s = [[0] * P for _ in range(P)]
     seq_r = [[0] * P for _ in range(P)]
     # ready[owner][from][slot], ack[owner][from][slot]: plain stores, as the
@@ -86,6 +161,13 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                                                     trees=trees, flat_ag=flat_ag, flat_rs=flat_rs)
         seq = []
         base = 0
+        host, hosted, defer = dm_tree_plan(ops, esz, slot) if dm_trees else ({}, {}, set())
+        if stats is not None:
+            stats.setdefault("deferred", 0)
+            stats.setdefault("in_exchange", 0)
+            stats["deferred"] += len(defer)
+            stats["in_exchange"] += len(host) - len(defer)
+        held = {}
         for _call in range(calls):
             first_c = None
             for i, o in enumerate(ops):
@@ -94,10 +176,25 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                 if o["wait"] >= 0:
                     deps.append(base + o["wait"])
                 launches = []
-                if o["xchg"]:
+                if i in host:
+                    # the tree runs inside exchange host[i]: K waits for it there
+                    stream, deps = "K", [base + host[i]]
+                elif o["xchg"]:
                     sends = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "SEND" and p["count"]]
                     recvs = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "RECV" and p["count"]]
-                    launches = exchange_launches(r, sends, recvs, seq_s[r], seq_r[r], slot, P, merge)
+                    if i in defer:
+                        held[i] = recvs
+                        recvs = []
+                    dl = ()
+                    if i in hosted:
+                        j = hosted[i]
+                        # a deferred tree: the leaves of the exchange that feeds it
+                        srcs = [x for x in defer if x < i and dm_tree_src(ops, x) == j]
+                        if srcs:
+                            dl = held.pop(srcs[0])
+                        # stream_join(C, K): the comm stream follows every K op issued so far
+                        deps.append(("K-before-host", base + i, base + j))
+                    launches = exchange_launches(r, sends, recvs, seq_s[r], seq_r[r], slot, P, merge, dl)
                     if first_c is None and c_join:
                         first_c = base + i
                         # c_join: the comm stream waits for the caller's stream's prior work
@@ -113,6 +210,8 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
 
     def dep_done(r, d):
         seq = ranks[r]
+        if isinstance(d, tuple) and d[0] == "K-before-host":  # K ops issued before the host (not its tree)
+            return all(seq[j]["done"] for j in range(d[1]) if seq[j]["stream"] == "K" and j != d[2])
         if isinstance(d, tuple):  # all K ops before index d
             return all(seq[j]["done"] for j in range(d[1]) if seq[j]["stream"] == "K")
         return seq[d]["done"]

@@ -43,3 +43,30 @@ def test_multi_round_exchanges(mode, merge):
 def test_reduce_scatter_protocol_completes():
     res = dm_sim.run("reduce_scatter", "bine_send_remap", 8, rcounts=[1 << 16] * 8, flat_rs=True)
     assert res is None, res["stuck"][:8]
+
+
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+@pytest.mark.parametrize("chunk", [1 << 20, 4 << 20])
+def test_fused_trees_protocol_completes(P, chunk):
+    # the flat reduce-scatter's trees fused into exchange launches
+    # (executor.cpp plan_dm_trees): leaf pulls deferred into the next
+    # exchange's first launch
+    st = {}
+    res = dm_sim.run("allreduce", "bine_bdw_remap", P, count=P << 20, chunk_bytes=chunk, flat_ag=2, flat_rs=True,
+                     slot=1 << 20, dm_trees=True, stats=st)
+    assert res is None, res["stuck"][:8]
+    # leaves of several slots (chunk > slot), or P = 16 (15 deferred leaves +
+    # 15 sends + 15 receives exceed one launch's 32 messages): every tree
+    # runs inside its own exchange instead
+    assert (st["deferred"] if P <= 8 and chunk <= 1 << 20 else st["in_exchange"]) > 0, st
+
+
+@pytest.mark.parametrize("merge", [3, 2, 1, 0])
+def test_fused_trees_multi_round(merge):
+    # leaves of several slot rounds: trees inside their own exchange, round
+    # r's tree beside round r + 1's pushes
+    st = {}
+    res = dm_sim.run("reduce_scatter", "bine_permute_remap", 4, rcounts=[1 << 20] * 4, chunk_bytes=4 << 20,
+                     flat_rs=True, slot=256 << 10, merge=merge, dm_trees=True, stats=st)
+    assert res is None, res["stuck"][:8]
+    assert st["in_exchange"] > 0, st
