@@ -564,12 +564,20 @@ def step_profile(torch, comm, call):
 
 def dm_wgs(mode):
     """the direct transport's workgroups per message a mode names: "+dm" ->
-    0 (the default, 32), "+dm64" -> 64; None when the mode does not use it"""
+    0 (the default, 32), "+dm64" / "+dmt64" -> 64; None when the mode does not
+    use it"""
     i = mode.find("+dm")
     if i < 0:
         return None
-    digits = mode[i + 3:].split("+")[0]
+    digits = mode[i + 3:].split("+")[0].lstrip("t")
     return int(digits) if digits.isdigit() else 0
+
+
+def dm_tree(mode):
+    """"+dmt": the direct transport with the flat reduce-scatter's trees
+    inside the exchange launches (bine_comm_set_direct_tree)"""
+    i = mode.find("+dm")
+    return i >= 0 and mode[i + 3:].startswith("t")
 
 
 def apply_transport(comm, mode, chunk, graphs=False):
@@ -578,6 +586,7 @@ def apply_transport(comm, mode, chunk, graphs=False):
     comm.set_direct(w is not None)
     if w is not None:
         comm.set_direct_wgs(w)
+        comm.set_direct_tree(dm_tree(mode))
     comm.set_relay(RELAY_MIN_BYTES if "relay" in mode else 0)
     comm.set_trees(mode.startswith("trees"))
     comm.set_flat_ag("flat" in mode)
@@ -730,9 +739,11 @@ CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining c
 MODES = {"off": ["direct"],
          # "+a2a" is not tried: RCCL runs ncclAllToAllv as the same grouped P2P kernel
          # (rcclGenericKernel) as P-1 ncclSend/ncclRecv pairs (profiles/r2_a2a_vs_p2p_kernels.txt)
-         # "+dm": the direct peer-memory transport (bine_comm_set_direct) instead of RCCL
+         # "+dm": the direct peer-memory transport (bine_comm_set_direct) instead of RCCL;
+         # "+dmt": the same with the flat reduce-scatter's trees inside its exchange
+         # launches (bine_comm_set_direct_tree: no pull copies of the leaves)
          "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag", "trees",
-                  "direct+dm", "flatrs+flat+dm", "relay+flat+dm"]}
+                  "direct+dm", "flatrs+flat+dm", "flatrs+flat+dmt", "relay+flat+dm"]}
 
 
 def transport_modes(relay: str, world: int):

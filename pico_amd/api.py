@@ -175,6 +175,12 @@ class Comm:
         bine_comm_set_direct_wgs); local, drops cached graphs"""
         check(lib().bine_comm_set_direct_wgs(self.handle, int(wgs)), "bine_comm_set_direct_wgs")
 
+    def set_direct_tree(self, on) -> None:
+        """direct transport: the flat reduce-scatter's trees inside the exchange
+        launches (bine_comm_set_direct_tree; -1 = BINE_DIRECT_TREE); every rank
+        alike; bit-identical"""
+        check(lib().bine_comm_set_direct_tree(self.handle, int(on)), "bine_comm_set_direct_tree")
+
     def set_profile(self, on: bool) -> None:
         """Per-op device timing of the following collectives (bine_comm_set_profile)."""
         check(lib().bine_comm_set_profile(self.handle, int(on)), "bine_comm_set_profile")

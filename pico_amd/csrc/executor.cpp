@@ -409,6 +409,7 @@ struct bine_comm {
   std::vector<hipEvent_t> op_ev;  // scratch of execute()
   std::vector<hipEvent_t> stage_ev;  // scratch of execute(): host staging batches
   // scratch of execute(): trees evaluated inside their exchange (plan_dm_trees)
+  bool dm_tree = false;  // bine_comm_set_direct_tree
   bine::DmTreePlan tree_plan;
   std::vector<hipEvent_t> tree_ev;
   std::vector<char> tree_pending;
@@ -478,8 +479,16 @@ static void install_segv_trace() {
   });
 }
 
+// BINE_DIRECT_TREE=1: new communicators start with the direct transport's
+// fused trees on (bine_comm_set_direct_tree)
+static bool dm_tree_env() {
+  static const bool on = getenv("BINE_DIRECT_TREE") && atoi(getenv("BINE_DIRECT_TREE")) != 0;
+  return on;
+}
+
 static int comm_setup(bine_comm *c) {
   install_segv_trace();
+  c->dm_tree = dm_tree_env();
   HIP_TRY(hipSetDevice(c->device));
   int lo = 0, hi = 0;
   HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -770,12 +779,6 @@ struct Staging {
   const StageRanges *rg = nullptr;
 };
 
-// BINE_DIRECT_TREE=0: the flat reduce-scatter's trees stay separate launches
-// (pull copies into the staging area + k_reduce_tree) over the direct transport
-static bool dm_tree_on() {
-  static const bool on = !getenv("BINE_DIRECT_TREE") || atoi(getenv("BINE_DIRECT_TREE")) != 0;
-  return on;
-}
 
 // Trees of the flat reduce-scatter over the direct transport, evaluated
 // inside an exchange launch instead of as pull copies into the staging area
@@ -807,7 +810,7 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
   pl.defer.assign(n, 0);
   pl.spec.resize(n);
   pl.leaves.resize(n);
-  if (!c->tx->stream_ordered() || !dm_tree_on() || op < 0 || c->profile) return false;
+  if (!c->tx->stream_ordered() || !c->dm_tree || op < 0 || c->profile) return false;
   auto sends_of = [&](size_t x, std::vector<XSend> &s) {
     s.clear();
     for (const Prim &p : sc.ops[x].prims)
@@ -1865,6 +1868,18 @@ int bine_comm_set_direct_wgs(bine_comm_t c, int wgs) {
   c->drop_graphs();                 // captured direct launches carry the old grid
   r->dm_wgs = wgs;
   if (r->dm) r->dm->wgs = wgs ? wgs : r->dm->env_wgs;
+  return BINE_SUCCESS;
+}
+
+int bine_comm_set_direct_tree(bine_comm_t c, int on) {
+  if (!c || on < -1 || on > 1) return BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  const int v = on < 0 ? (dm_tree_env() ? 1 : 0) : on;
+  if (v == (c->dm_tree ? 1 : 0)) return BINE_SUCCESS;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  c->drop_graphs();  // captured exchanges carry the other launch structure
+  c->dm_tree = v != 0;
   return BINE_SUCCESS;
 }
 

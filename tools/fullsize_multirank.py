@@ -4,7 +4,8 @@
 P = 8 in the GPU suite).  The 8 processes share the box's one GPU (distinct
 NCCL_HOSTIDs); the transports are the ones bench.py picks from on the
 driver's 8-GPU node: the bit-exact flat phases over the direct peer-memory
-transport (flatrs+flat+dm), the literal Bine schedule over it (direct+dm),
+transport (flatrs+flat+dm; +dmt: its reduce-scatter trees inside the
+exchange launches), the literal Bine schedule over it (direct+dm),
 and the flat phases over RCCL P2P (flatrs+flat; RCCL's socket transport
 here).  Inputs are pico_core's distribution generated on the device (seed
 1234 + rank, exactly bench.py's); every rank's output digest is compared with
@@ -27,8 +28,8 @@ CASES = [("C3", "allreduce", "bine_bdw_remap", "float", 67_108_864),
          ("C5", "allreduce", "bine_bdw_remap", "double", 33_554_432),
          ("C5", "allreduce", "bine_bdw_remap", "int64", 33_554_432)]
 # (transport, which configs)
-TRANSPORTS = [("flatrs+flat+dm", ("C3", "C4", "C5")), ("direct+dm", ("C3", "C4", "C5")),
-              ("flatrs+flat", ("C3", "C4"))]
+TRANSPORTS = [("flatrs+flat+dm", ("C3", "C4", "C5")), ("flatrs+flat+dmt", ("C3", "C4", "C5")),
+              ("direct+dm", ("C3", "C4", "C5")), ("flatrs+flat", ("C3", "C4"))]
 
 
 def worker(rank, P, port, gold, q):

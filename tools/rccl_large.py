@@ -27,8 +27,8 @@ sys.path.insert(0, ROOT)
 N32 = 16_777_216   # 64 MiB fp32
 N64 = 8_388_608    # 64 MiB fp64
 MODES = ("direct", "relay", "flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+flat+a2a", "trees",
-         "direct+dm", "flatrs+flat+dm", "relay+flat+dm", "trees+dm")
-RS_MODES = ("direct", "flatrs", "flatrs+flat+dm")
+         "direct+dm", "flatrs+flat+dm", "flatrs+flat+dmt", "relay+flat+dm", "trees+dm")
+RS_MODES = ("direct", "flatrs", "flatrs+flat+dm", "flatrs+flat+dmt")
 
 
 def expected(P):
