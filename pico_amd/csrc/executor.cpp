@@ -822,6 +822,17 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
       if (p.type == BINE_PRIM_RECV) r.push_back({p.peer, ptr(p.dst_buf, p.dst_off), p.count * esz});
   };
   auto overlaps = [](const char *a, size_t na, const char *b, size_t nb) { return a < b + nb && b < a + na; };
+  // buffers only receives write and only trees read (staging areas)
+  bool clean_buf[8];
+  for (int b = 0; b < 8; b++) clean_buf[b] = true;
+  for (const SOp &o : sc.ops)
+    for (const Prim &x : o.prims) {
+      const bool tree = x.type == BINE_PRIM_REDUCE_TREE, recv = x.type == BINE_PRIM_RECV;
+      auto dirty = [&](int b) { if (b >= 0 && b < 8) clean_buf[b] = false; };
+      if (!tree && !recv) dirty(x.src_buf);
+      dirty(x.aux_buf);
+      if (!recv) dirty(x.dst_buf);
+    }
   bool any = false;
   std::vector<XSend> s, s2;
   std::vector<XRecv> r, r2;
@@ -834,14 +845,7 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
       continue;
     const Prim &t = sc.ops[j].prims[0];
     // the staging buffer: only receives write it, only trees read it
-    bool clean = true;
-    for (const SOp &o : sc.ops)
-      for (const Prim &x : o.prims) {
-        const bool tree = x.type == BINE_PRIM_REDUCE_TREE, recv = x.type == BINE_PRIM_RECV;
-        if ((!tree && !recv && x.src_buf == t.src_buf) || x.aux_buf == t.src_buf || (!recv && x.dst_buf == t.src_buf))
-          clean = false;
-      }
-    if (!clean) continue;
+    if (t.src_buf < 0 || t.src_buf >= 8 || !clean_buf[t.src_buf]) continue;
     TreeSpec ts;
     ts.nl = t.peer;
     ts.pos = t.pos;
