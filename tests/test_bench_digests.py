@@ -88,11 +88,16 @@ def test_overlap_fraction():
 
 
 def test_transport_modes():
-    assert bench.transport_modes("auto", 2) == ["direct", "flat", "flatrs+flat", "direct+dm", "flatrs+flat+dm"]
+    assert bench.transport_modes("auto", 2) == ["direct", "flat", "flatrs+flat", "direct+dm", "flatrs+flat+dm",
+                                                "flatrs+flat+dmt"]
     assert "trees" in bench.transport_modes("auto", 8) and "flatrs+flat+ag" in bench.transport_modes("auto", 8)
     assert bench.transport_modes("flatrs+flat+a2a", 8) == ["flatrs+flat+a2a"]
     assert bench.transport_modes("auto", 6) == ["direct", "relay", "direct+dm"]
     assert "relay+flat+dm" in bench.transport_modes("auto", 8)
+    assert "flatrs+flat+dmt" in bench.transport_modes("auto", 8)
+    assert bench.dm_wgs("flatrs+flat+dmt16") == 16 and bench.dm_tree("flatrs+flat+dmt16")
+    assert bench.dm_wgs("flatrs+flat+dm64") == 64 and not bench.dm_tree("flatrs+flat+dm64")
+    assert bench.dm_wgs("flatrs+flat") is None and not bench.dm_tree("direct")
     assert bench.transport_modes("off", 8) == ["direct"]
     assert bench.transport_modes("trees", 2) == ["direct"]
 

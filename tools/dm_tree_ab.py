@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
 """Trees inside the exchange vs pull copies + separate tree launches over the
-direct transport (BINE_DIRECT_TREE=1 / 0), P processes on the one GPU
-(distinct NCCL_HOSTIDs; GPU_MAX_HW_QUEUES as the caller sets it): C3
+direct transport (flatrs+flat+dmt / flatrs+flat+dm, i.e.
+bine_comm_set_direct_tree 1 / 0), P processes on the one GPU (distinct
+NCCL_HOSTIDs; GPU_MAX_HW_QUEUES as the caller sets it): C3
 (allreduce_bine_bdw_remap fp32 256 MiB per rank) and C4
-(reduce_scatter_bine_permute_remap fp32 1 GiB input per rank) on
-flatrs+flat+dm at each chunk, per-iteration events (bench.timed: max over
-ranks, median after dropping 20 %), every output digest-checked against the
-committed oracle digests.  One process group per setting (the library reads
-BINE_DIRECT_TREE once).  On one GPU all ranks share one HBM, so the figures
-rank the two forms by the HBM traffic they cause -- not an xGMI measurement.
+(reduce_scatter_bine_permute_remap fp32 1 GiB input per rank) at each chunk,
+per-iteration events (bench.timed: max over ranks, median after dropping
+20 %), every output digest-checked against the committed oracle digests.
+One process group per setting.  On one GPU all ranks share one HBM, so the
+figures rank the two forms by the HBM traffic they cause -- not an xGMI
+measurement.
 usage: python tools/dm_tree_ab.py P [CHUNK_MIB,...] [ITERS] [WGS]
 """
 import json
@@ -36,7 +37,7 @@ def worker(rank, P, tree, chunks, iters, wgs, port, q):
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     res = {}
-    mode = "flatrs+flat+dm" + (str(wgs) if wgs else "")
+    mode = ("flatrs+flat+dmt" if tree else "flatrs+flat+dm") + (str(wgs) if wgs else "")
     for cfg, n, coll in (("C3", bench.C3_ELEMS, "allreduce"), ("C4", bench.C4_ELEMS, "reduce_scatter")):
         sb = torch.empty(n, dtype=torch.float32, device="cuda:0")
         nout = n if coll == "allreduce" else n // P
