@@ -562,22 +562,32 @@ def step_profile(torch, comm, call):
                       for o in ls[:24]]}
 
 
+def _dm_token(mode):
+    i = mode.find("+dm")
+    return None if i < 0 else mode[i + 3:].split("+")[0]
+
+
 def dm_wgs(mode):
     """the direct transport's workgroups per message a mode names: "+dm" ->
-    0 (the default, 32), "+dm64" / "+dmt64" -> 64; None when the mode does not
-    use it"""
-    i = mode.find("+dm")
-    if i < 0:
+    0 (the default, 32), "+dm64" / "+dmt64" / "+dmt64x128" -> 64; None when the
+    mode does not use it"""
+    tok = _dm_token(mode)
+    if tok is None:
         return None
-    digits = mode[i + 3:].split("+")[0].lstrip("t")
+    digits = tok.lstrip("t").split("x")[0]
     return int(digits) if digits.isdigit() else 0
 
 
 def dm_tree(mode):
-    """"+dmt": the direct transport with the flat reduce-scatter's trees
-    inside the exchange launches (bine_comm_set_direct_tree)"""
-    i = mode.find("+dm")
-    return i >= 0 and mode[i + 3:].startswith("t")
+    """the direct transport's fused trees (bine_comm_set_direct_tree) a mode
+    names: "+dm" -> 0 (off: pull copies + a separate tree launch), "+dmt" ->
+    1 (on, the default tree workgroups), "+dmtxT" / "+dmtWxT" -> T tree
+    workgroups per launch"""
+    tok = _dm_token(mode)
+    if tok is None or not tok.startswith("t"):
+        return 0
+    t = tok.split("x")
+    return int(t[1]) if len(t) > 1 and t[1].isdigit() else 1
 
 
 def apply_transport(comm, mode, chunk, graphs=False):
@@ -735,6 +745,7 @@ def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, wo
 
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
 DM_WGS_TRIALS = (16, 64)       # direct transport: workgroups per message tried beside the default 32
+TREE_WGS_TRIALS = (128, 256)   # fused trees ("+dmt"): tree workgroups per launch tried beside the default 64
 CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 MODES = {"off": ["direct"],
          # "+a2a" is not tried: RCCL runs ncclAllToAllv as the same grouped P2P kernel
@@ -958,6 +969,15 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                 trial((best[0] + str(w), best[1], False))
             cands = [c for c in trials if c[1] == best[1] and not c[2] and trials[c] != float("inf")
                      and (c[0] == best[0] or c[0] in [best[0] + str(w) for w in DM_WGS_TRIALS])]
+            best = min(cands, key=trials.get)
+        if dm_tree(best[0]) == 1:
+            # the fused trees' workgroups per launch (default 64): on a node each
+            # GPU's CUs serve one rank, so more of them may pay there
+            names = [best[0] + "x" + str(t) for t in TREE_WGS_TRIALS]
+            for nm in names:
+                trial((nm, best[1], False))
+            cands = [c for c in trials if c[1] == best[1] and not c[2] and trials[c] != float("inf")
+                     and (c[0] == best[0] or c[0] in names)]
             best = min(cands, key=trials.get)
     else:
         best = (modes[0], chunks[0], False)

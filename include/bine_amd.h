@@ -344,13 +344,15 @@ int bine_comm_set_direct(bine_comm_t comm, int on);
  * (their launches carry the old grid).  bench.py trials it on the node. */
 int bine_comm_set_direct_wgs(bine_comm_t comm, int wgs);
 /* Direct transport: the flat reduce-scatter's trees evaluated inside the
- * exchange launches (on = 1: the leaves read in place in the inbox slots,
+ * exchange launches (on >= 1: the leaves read in place in the inbox slots,
  * each tree in the first launch of the exchange after the one that receives
- * its leaves, or in its own; 0: pull copies into the staging area + a
- * separate tree launch, the default; -1: BINE_DIRECT_TREE).  Bit-identical
- * either way.  Collective: every rank must use the same setting (it decides
- * in which launch a leaf is pulled).  Local call; drops cached graphs.
- * bench.py trials it on the node ("+dmt" transports). */
+ * its leaves, or in its own -- the default; on >= 2 also sets the tree
+ * workgroups per launch (1: BINE_DIRECT_TREE_WGS, 64); 0: pull copies into
+ * the staging area + a separate tree launch; -1: BINE_DIRECT_TREE, default
+ * on).  Bit-identical either way.  Collective: every rank must use the same
+ * setting (it decides in which launch a leaf is pulled).  Local call; drops
+ * cached graphs.  bench.py trials it on the node ("+dm" vs "+dmt"
+ * transports, "+dmtxT" for T tree workgroups). */
 int bine_comm_set_direct_tree(bine_comm_t comm, int on);
 
 /* Graph mode (RCCL communicators): the first collective call for a given

@@ -165,6 +165,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
   if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
+  tree_wgs_env = tree_wgs;
   if (slot < (1 << 20)) slot = 1 << 20;
   slot = slot / 4096 * 4096;
   if (wgs < 1) wgs = 1;

@@ -62,7 +62,8 @@ struct DirectState {
   // leaves of `dtree` (one slot each, all in its first launch)
   bool defer_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const std::vector<XRecv> &dleaves,
                 const TreeSpec &dtree) const;
-  int tree_wgs = 64;   // tree workgroups per launch (BINE_DIRECT_TREE_WGS; 64 measured best of 64 / 128 / 256)
+  int tree_wgs = 64;   // tree workgroups per launch (BINE_DIRECT_TREE_WGS; bine_comm_set_direct_tree)
+  int tree_wgs_env = 64;  // the value init() settled on
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }
   // stderr: this rank's flags and device-side sequence bases (after a timeout)
   void dump() const;

@@ -410,6 +410,7 @@ struct bine_comm {
   std::vector<hipEvent_t> stage_ev;  // scratch of execute(): host staging batches
   // scratch of execute(): trees evaluated inside their exchange (plan_dm_trees)
   bool dm_tree = false;  // bine_comm_set_direct_tree
+  int dm_tree_wgs = 0;   // its tree workgroups per launch (0: the transport's default)
   bine::DmTreePlan tree_plan;
   std::vector<hipEvent_t> tree_ev;
   std::vector<char> tree_pending;
@@ -479,10 +480,10 @@ static void install_segv_trace() {
   });
 }
 
-// BINE_DIRECT_TREE=1: new communicators start with the direct transport's
-// fused trees on (bine_comm_set_direct_tree)
+// BINE_DIRECT_TREE=0: new communicators start with the direct transport's
+// fused trees off (bine_comm_set_direct_tree; on by default)
 static bool dm_tree_env() {
-  static const bool on = getenv("BINE_DIRECT_TREE") && atoi(getenv("BINE_DIRECT_TREE")) != 0;
+  static const bool on = !getenv("BINE_DIRECT_TREE") || atoi(getenv("BINE_DIRECT_TREE")) != 0;
   return on;
 }
 
@@ -1851,6 +1852,7 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
       return BINE_ERR_UNSUPPORTED;
     }
     if (r->dm_wgs) d->wgs = r->dm_wgs;
+    if (c->dm_tree_wgs) d->tree_wgs = c->dm_tree_wgs;
     r->dm = std::move(d);
   }
   if (on && r->dm->poisoned()) {
@@ -1876,14 +1878,18 @@ int bine_comm_set_direct_wgs(bine_comm_t c, int wgs) {
 }
 
 int bine_comm_set_direct_tree(bine_comm_t c, int on) {
-  if (!c || on < -1 || on > 1) return BINE_ERR_ARG;
+  if (!c || on < -1 || on > 1024) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  const int v = on < 0 ? (dm_tree_env() ? 1 : 0) : on;
-  if (v == (c->dm_tree ? 1 : 0)) return BINE_SUCCESS;
+  const bool v = on < 0 ? dm_tree_env() : on != 0;
+  const int w = on > 1 ? on : 0;  // tree workgroups per launch (0: BINE_DIRECT_TREE_WGS / 64)
+  if (v == c->dm_tree && w == c->dm_tree_wgs) return BINE_SUCCESS;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
   c->drop_graphs();  // captured exchanges carry the other launch structure
-  c->dm_tree = v != 0;
+  c->dm_tree = v;
+  c->dm_tree_wgs = w;
+  if (auto *r = dynamic_cast<RcclTransport *>(c->tx.get()))
+    if (r->dm) r->dm->tree_wgs = w ? w : r->dm->tree_wgs_env;
   return BINE_SUCCESS;
 }
 

@@ -95,9 +95,11 @@ def test_transport_modes():
     assert bench.transport_modes("auto", 6) == ["direct", "relay", "direct+dm"]
     assert "relay+flat+dm" in bench.transport_modes("auto", 8)
     assert "flatrs+flat+dmt" in bench.transport_modes("auto", 8)
-    assert bench.dm_wgs("flatrs+flat+dmt16") == 16 and bench.dm_tree("flatrs+flat+dmt16")
-    assert bench.dm_wgs("flatrs+flat+dm64") == 64 and not bench.dm_tree("flatrs+flat+dm64")
-    assert bench.dm_wgs("flatrs+flat") is None and not bench.dm_tree("direct")
+    assert bench.dm_wgs("flatrs+flat+dmt16") == 16 and bench.dm_tree("flatrs+flat+dmt16") == 1
+    assert bench.dm_wgs("flatrs+flat+dm64") == 64 and bench.dm_tree("flatrs+flat+dm64") == 0
+    assert bench.dm_wgs("flatrs+flat+dmtx128") == 0 and bench.dm_tree("flatrs+flat+dmtx128") == 128
+    assert bench.dm_wgs("flatrs+flat+dmt16x256") == 16 and bench.dm_tree("flatrs+flat+dmt16x256") == 256
+    assert bench.dm_wgs("flatrs+flat") is None and bench.dm_tree("direct") == 0
     assert bench.transport_modes("off", 8) == ["direct"]
     assert bench.transport_modes("trees", 2) == ["direct"]
 
