@@ -91,3 +91,18 @@ def test_staged_host_buffers_4_ranks():
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=4: ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_fused_trees_vs_unfused_two_processes():
+    """the direct transport's fused trees (leaves read in place in the inbox
+    slots, deferred into the next exchange's launch) and the unfused form
+    (pull copies + k_reduce_tree) at C3 / C4 full size, 2 processes, 16 and
+    64 MiB chunks (64: leaves of 4 slots, the tree inside its own exchange);
+    every rank's output digest equals the oracle's in both forms
+    (tools/dm_tree_ab.py)"""
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_tree_ab.py"), "2", "16,64", "4"],
+                       env=env, capture_output=True, text=True, timeout=400)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
