@@ -173,6 +173,8 @@ struct DmMsg {
   int j;               // this launch's j-th message of this kind to / from `peer`: seq = base[peer] + j + 1
   int leaf = -1;       // k_dm_move_tree: >= 0 -- a pull whose slot is a leaf of the launch's tree (read in
                        // place, never copied); -1 -- copied by its own workgroups
+  int grp = -1;        // a push of the same bytes to several peers: index in m of the group's leader, whose
+                       // workgroups read the source once and store it into every member's slot; -1: alone
 };
 struct DmArgs {
   int nmsg = 0;
@@ -183,6 +185,8 @@ struct DmArgs {
   uint32_t *poison_host = nullptr; // mapped host word set together with the inbox's poison word
   uint64_t timeout_ticks = 0;      // wall_clock64 ticks
   DmMsg m[kMaxDm];
+  int ncopy = 0;                   // messages with workgroups of their own (standalone copies, group leaders):
+  int cidx[kMaxDm] = {};           // indices into m, in dispatch order
 };
 int launch_dm_move(const DmArgs &a, void *stream);
 
@@ -200,9 +204,7 @@ int launch_dm_move(const DmArgs &a, void *stream);
 struct DmTree {
   int nl = 0, pos = 0;
   unsigned swap = 0;
-  int twgs = 0;                 // tree workgroups (dispatched after the copy workgroups)
-  int ncopy = 0;                // copy messages, by index into DmArgs::m
-  int cidx[kMaxDm] = {};
+  int twgs = 0;                 // tree workgroups (dispatched after the copy workgroups, DmArgs::cidx)
   int leaf_msg[kMaxLeaves] = {};  // tree position -> DmArgs::m index (-1 at pos)
   const void *own_leaf = nullptr;
   void *out = nullptr;

@@ -165,6 +165,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
   if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
+  if (const char *e = getenv("BINE_DIRECT_MCAST")) mcast = atoi(e) != 0;
   tree_wgs_env = tree_wgs;
   if (slot < (1 << 20)) slot = 1 << 20;
   slot = slot / 4096 * 4096;
@@ -394,6 +395,16 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   // round's tree in place of copying them
   int tree_round = -1;
   const TreeSpec *ltree = tree;  // the tree of the launch being built
+  // the messages that get workgroups of their own: standalone copies and the
+  // leaders of push groups (members ride with their leader, leaves with the tree)
+  auto index_copies = [&]() {
+    a.ncopy = 0;
+    for (int i = 0; i < a.nmsg; i++) {
+      const DmMsg &m = a.m[i];
+      if (m.leaf >= 0 || (m.grp >= 0 && m.grp != i)) continue;
+      a.cidx[a.ncopy++] = i;
+    }
+  };
   auto flush = [&]() -> int {
     int rc;
     if (tree_round >= 0) {
@@ -407,14 +418,14 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       t.out = ltree->out + off;
       t.nvec = len / 16;
       for (int j = 0; j < kMaxLeaves; j++) t.leaf_msg[j] = -1;
-      for (int i = 0; i < a.nmsg; i++) {
+      for (int i = 0; i < a.nmsg; i++)
         if (a.m[i].leaf >= 0) t.leaf_msg[a.m[i].leaf] = i;
-        else t.cidx[t.ncopy++] = i;
-      }
+      index_copies();
       rc = launch_dm_move_tree(a, t, ltree->dtype, ltree->op, st);
       tree_round = -1;
       ltree = tree;
     } else {
+      index_copies();
       rc = launch_dm_move(a, st);
     }
     a.nmsg = 0;
@@ -436,6 +447,15 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.peer = x.peer;
       m.j = js[(size_t)x.peer]++;
       m.leaf = -1;
+      // the same bytes already pushed to another peer in this launch: one
+      // group, the source read once (BINE_DIRECT_MCAST=0: every push alone)
+      m.grp = -1;
+      if (mcast) {
+        const int me = a.nmsg - 1;
+        for (int q = 0; q < me && m.grp < 0; q++)
+          if (a.m[q].push && a.m[q].src == m.src && a.m[q].bytes == m.bytes) m.grp = a.m[q].grp;
+        if (m.grp < 0) m.grp = me;
+      }
       if (a.nmsg == kMaxDm)
         if (int rc = flush()) return rc;
     }
@@ -454,6 +474,7 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.push = 0;
       m.peer = x.peer;
       m.j = jr[(size_t)x.peer]++;
+      m.grp = -1;
       m.leaf = tree ? tree->leaf_of_recv[i] : -1;
       if (tree) tree_round = (int)k;
       if (a.nmsg == kMaxDm)
@@ -474,6 +495,7 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.push = 0;
       m.peer = x.peer;
       m.j = jr[(size_t)x.peer]++;
+      m.grp = -1;
       m.leaf = dtree->leaf_of_recv[i];
     }
     tree_round = 0;

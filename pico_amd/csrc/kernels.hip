@@ -936,6 +936,111 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi) {
   return true;
 }
 
+// one workgroup's share of a push GROUP led by message mi (the same bytes to
+// several peers, DmMsg::grp): each member's slot-reuse acknowledgement is
+// awaited, the source is read once and stored into every member's slot, and
+// every member is counted in and published exactly as a standalone push
+__device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi) {
+  using namespace dm;
+  uint8_t *own = a.own;
+  uint32_t *poison = reinterpret_cast<uint32_t *>(own + kPoisonOff);
+  __shared__ u32x4 *dv[kMaxDm];
+  __shared__ uint64_t dseq[kMaxDm];
+  __shared__ int dmem[kMaxDm];
+  __shared__ int nd, go;
+  if (threadIdx.x == 0) {
+    int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
+    int n = 0;
+    for (int j = 0; j < a.nmsg; j++) {
+      const DmMsg &m = a.m[j];
+      if (!m.push || m.grp != mi) continue;
+      const uint64_t seq = __hip_atomic_load(reinterpret_cast<const uint64_t *>(own + kBaseSendOff) + m.peer,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
+      const size_t k = (size_t)(seq % kSlots);
+      uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
+      dv[n] = reinterpret_cast<u32x4 *>(remote + kFlagsBytes + ((size_t)a.rank * kSlots + k) * a.slot);
+      dseq[n] = seq;
+      dmem[n] = j;
+      n++;
+      if (ok && seq > (uint64_t)kSlots) {
+        const uint64_t *w = reinterpret_cast<const uint64_t *>(own + kAckOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+        const long long t0 = wall_clock64();
+        while (ld_acq_sys(w) < seq - kSlots) {
+          if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
+            __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ok = 0;
+            break;
+          }
+          if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+            ok = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+    }
+    nd = n;
+    go = ok;
+  }
+  __syncthreads();
+  if (!go) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const DmMsg &L = a.m[mi];
+  const uint8_t *src = L.src;
+  const int n = nd;
+  // every slot is 16-B aligned (a multiple of 4 KiB from the inbox base):
+  // whole vectors from byte 0, the tail bytes by workgroup 0
+  const size_t nvec = L.bytes / 16;
+  if (wi == 0)
+    for (int d = 0; d < n; d++)
+      for (size_t i = nvec * 16 + threadIdx.x; i < L.bytes; i += kBlock)
+        reinterpret_cast<uint8_t *>(dv[d])[i] = src[i];
+  const u32x4 *vs = reinterpret_cast<const u32x4 *>(src);
+  constexpr int U = 4;
+  const size_t stride = (size_t)a.wgs * kBlock * U;
+  for (size_t b0 = (size_t)wi * kBlock * U + threadIdx.x; b0 < nvec; b0 += stride) {
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = b0 + (size_t)u * kBlock;
+      if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
+    }
+    for (int d = 0; d < n; d++) {
+      u32x4 *vd = dv[d];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const size_t i = b0 + (size_t)u * kBlock;
+        if (i < nvec) __builtin_nontemporal_store(x[u], vd + i);
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int d = 0; d < n; d++) {
+      const DmMsg &m = a.m[dmem[d]];
+      const size_t k = (size_t)(dseq[d] % kSlots);
+      uint32_t *cnt = reinterpret_cast<uint32_t *>(own + kCntPushOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+      const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (old + 1 == (uint32_t)a.wgs) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
+        uint64_t *sig = reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(sig, dseq[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  return true;
+}
+
+// a copy workgroup: its message alone, or the group it leads
+__device__ __forceinline__ bool dm_copy_wg(const DmArgs &a, int mi, int wi) {
+  return a.m[mi].push && a.m[mi].grp == mi ? dm_mcast_msg(a, mi, wi) : dm_copy_msg(a, mi, wi);
+}
+
 // thread 0, after its workgroup's share of the launch: the last workgroup of
 // the launch advances the sequence bases of every message (every workgroup has
 // read them; the next launch is stream-ordered after this one)
@@ -956,18 +1061,41 @@ __device__ __forceinline__ void dm_launch_done(const DmArgs &a) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
-  if (!dm_copy_msg(a, (int)(blockIdx.x / (unsigned)a.wgs), (int)(blockIdx.x % (unsigned)a.wgs))) return;
+  if (!dm_copy_wg(a, a.cidx[blockIdx.x / (unsigned)a.wgs], (int)(blockIdx.x % (unsigned)a.wgs))) return;
   dm_launch_done(a);
+}
+
+// every message: in range; copied by its own workgroups (cidx, each once),
+// carried by its group's leader (a push with the leader's bytes and source),
+// or -- tree launches -- a leaf; false otherwise
+static bool dm_args_ok(const DmArgs &a, bool leaves_ok) {
+  if (a.nmsg <= 0 || a.nmsg > kMaxDm || a.wgs < 1 || !a.own || !a.slot || a.ncopy < 0 || a.ncopy > a.nmsg)
+    return false;
+  uint64_t seen = 0;
+  for (int c = 0; c < a.ncopy; c++) {
+    const int i = a.cidx[c];
+    if (i < 0 || i >= a.nmsg || (seen >> i & 1) || a.m[i].leaf >= 0 || (a.m[i].grp >= 0 && a.m[i].grp != i))
+      return false;
+    seen |= 1ull << i;
+  }
+  for (int i = 0; i < a.nmsg; i++) {
+    const DmMsg &m = a.m[i];
+    if (m.peer < 0 || m.peer >= dm::kMaxPeers || m.j < 0 || m.j >= dm::kSlots || m.bytes > a.slot) return false;
+    if (m.grp >= 0) {
+      if (!m.push || m.grp >= a.nmsg || !(seen >> m.grp & 1) || a.m[m.grp].grp != m.grp ||
+          a.m[m.grp].src != m.src || a.m[m.grp].bytes != m.bytes)
+        return false;
+    } else if (!(seen >> i & 1) && !(leaves_ok && m.leaf >= 0)) {
+      return false;
+    }
+  }
+  return true;
 }
 
 int launch_dm_move(const DmArgs &a, void *stream) {
   if (a.nmsg <= 0) return BINE_SUCCESS;
-  if (a.nmsg > kMaxDm || a.wgs < 1 || !a.own || !a.slot) return BINE_ERR_ARG;
-  for (int i = 0; i < a.nmsg; i++)
-    if (a.m[i].peer < 0 || a.m[i].peer >= dm::kMaxPeers || a.m[i].j < 0 || a.m[i].j >= dm::kSlots ||
-        a.m[i].bytes > a.slot)
-      return BINE_ERR_ARG;
-  hipLaunchKernelGGL(k_dm_move, dim3((unsigned)(a.nmsg * a.wgs)), dim3(kBlock), 0, (hipStream_t)stream, a);
+  if (!dm_args_ok(a, false)) return BINE_ERR_ARG;
+  hipLaunchKernelGGL(k_dm_move, dim3((unsigned)(a.ncopy * a.wgs)), dim3(kBlock), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
@@ -977,9 +1105,9 @@ int launch_dm_move(const DmArgs &a, void *stream) {
 template <typename T, int OP, int NL>
 __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
   using namespace dm;
-  const unsigned ncw = (unsigned)t.ncopy * (unsigned)a.wgs;
+  const unsigned ncw = (unsigned)a.ncopy * (unsigned)a.wgs;
   if (blockIdx.x < ncw) {
-    if (!dm_copy_msg(a, t.cidx[blockIdx.x / (unsigned)a.wgs], (int)(blockIdx.x % (unsigned)a.wgs))) return;
+    if (!dm_copy_wg(a, a.cidx[blockIdx.x / (unsigned)a.wgs], (int)(blockIdx.x % (unsigned)a.wgs))) return;
     dm_launch_done(a);
     return;
   }
@@ -1067,7 +1195,7 @@ bool dm_tree_supported(int dtype, int op, int nl) {
 
 template <typename T, int OP>
 static hipError_t dmt_launch(const DmArgs &a, const DmTree &t, hipStream_t st) {
-  const dim3 g((unsigned)(t.ncopy * a.wgs + t.twgs));
+  const dim3 g((unsigned)(a.ncopy * a.wgs + t.twgs));
   switch (t.nl) {
     case 2: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 2>), g, dim3(kBlock), 0, st, a, t); break;
     case 4: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 4>), g, dim3(kBlock), 0, st, a, t); break;
@@ -1087,21 +1215,14 @@ static hipError_t dmt_t(const DmArgs &a, const DmTree &t, int op, hipStream_t st
 
 int launch_dm_move_tree(const DmArgs &a, const DmTree &t, int dtype, int op, void *stream) {
   if (!dm_tree_supported(dtype, op, t.nl)) return BINE_ERR_UNSUPPORTED;
-  if (a.nmsg <= 0 || a.nmsg > kMaxDm || a.wgs < 1 || !a.own || !a.slot || t.twgs < 1 || t.ncopy < 0 ||
-      t.ncopy + t.nl - 1 != a.nmsg || t.pos < 0 || t.pos >= t.nl || !t.nvec || t.nvec * 16 > a.slot || !t.out ||
-      !t.own_leaf || ((uintptr_t)t.out & 15) || ((uintptr_t)t.own_leaf & 15))
+  if (!dm_args_ok(a, true) || t.twgs < 1 || t.pos < 0 || t.pos >= t.nl || !t.nvec || t.nvec * 16 > a.slot ||
+      !t.out || !t.own_leaf || ((uintptr_t)t.out & 15) || ((uintptr_t)t.own_leaf & 15))
     return BINE_ERR_ARG;
-  for (int i = 0; i < a.nmsg; i++)
-    if (a.m[i].peer < 0 || a.m[i].peer >= dm::kMaxPeers || a.m[i].j < 0 || a.m[i].j >= dm::kSlots ||
-        a.m[i].bytes > a.slot)
-      return BINE_ERR_ARG;
-  // every copy message once, every leaf position but pos once, by a leaf pull of nvec vectors
+  // every leaf position but pos once, by a leaf pull of nvec vectors; no other leaves
   uint64_t seen = 0;
-  for (int c = 0; c < t.ncopy; c++) {
-    const int i = t.cidx[c];
-    if (i < 0 || i >= a.nmsg || a.m[i].leaf >= 0 || (seen >> i & 1)) return BINE_ERR_ARG;
-    seen |= 1ull << i;
-  }
+  int nleaf = 0;
+  for (int i = 0; i < a.nmsg; i++) nleaf += a.m[i].leaf >= 0;
+  if (nleaf != t.nl - 1) return BINE_ERR_ARG;
   for (int j = 0; j < t.nl; j++) {
     if (j == t.pos) continue;
     const int i = t.leaf_msg[j];

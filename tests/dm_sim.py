@@ -18,11 +18,11 @@ import pico_amd
 SLOTS = 4
 
 
-def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3, deferred=()):
+def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3, deferred=(), mcast=True):
     """DirectState::exchange for one exchange: list of launches, each a list
     of messages {kind, peer, seq}.  `deferred`: an earlier exchange's leaf
     receives (one slot each) pulled at the start of the first launch"""
-    maxb = max([b for _, b in sends] + [b for _, b in recvs] + [0])
+    maxb = max([x[1] for x in sends] + [b for _, b in recvs] + [0])
     rounds = (maxb + slot - 1) // slot
     out = []
     pre = []
@@ -30,18 +30,26 @@ def exchange_launches(rank, sends, recvs, seq_s, seq_r, slot, P, merge=3, deferr
         seq_r[p] += 1
         pre.append({"kind": "pull", "peer": p, "seq": seq_r[p]})
     ns, nr = [0] * P, [0] * P
-    for p, _ in sends:
+    for x in sends:
+        p = x[0]
         ns[p] += 1
         assert ns[p] <= SLOTS, "more messages to one peer than slots: refused by the library"
     for p, _ in recvs:
         nr[p] += 1
         assert nr[p] <= SLOTS
     def pushes(k):
+        # sends of the same source and size in one launch form a group (the
+        # library's multicast push: one set of workgroups waits for every
+        # member's acknowledgement, then writes all of them)
         out = []
-        for p, b in sends:
+        for x in sends:
+            p, b = x[0], x[1]
             if b > k * slot:
                 seq_s[p] += 1
-                out.append({"kind": "push", "peer": p, "seq": seq_s[p]})
+                m = {"kind": "push", "peer": p, "seq": seq_s[p]}
+                if len(x) > 2 and mcast:
+                    m["grp"] = (x[2], b, k)
+                out.append(m)
         return out
 
     def pulls(k):
@@ -180,7 +188,8 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                     # the tree runs inside exchange host[i]: K waits for it there
                     stream, deps = "K", [base + host[i]]
                 elif o["xchg"]:
-                    sends = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "SEND" and p["count"]]
+                    sends = [(p["peer"], p["count"] * esz, (p["src_buf"], p["src_off"])) for p in o["prims"]
+                             if p["type"] == "SEND" and p["count"]]
                     recvs = [(p["peer"], p["count"] * esz) for p in o["prims"] if p["type"] == "RECV" and p["count"]]
                     if i in defer:
                         held[i] = recvs
@@ -239,14 +248,22 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                     continue
                 # the current launch: its messages progress independently
                 launch = op["launches"][op["li"]]
+
+                def ack_ok(m):
+                    k = m["seq"] % SLOTS
+                    return m["seq"] <= SLOTS or ack[r][m["peer"]][k] >= m["seq"] - SLOTS
+
                 for m in launch:
                     if m.get("done"):
                         continue
                     p = m["peer"]
                     k = m["seq"] % SLOTS
                     if m["kind"] == "push":
-                        if m["seq"] > SLOTS and ack[r][p][k] < m["seq"] - SLOTS:
+                        if not ack_ok(m):
                             continue
+                        if "grp" in m and not all(ack_ok(x) for x in launch
+                                                  if x["kind"] == "push" and x.get("grp") == m["grp"]):
+                            continue   # a group writes only once every member's slot is free
                         assert ready[p][r][k] < m["seq"], "a ready flag would move backwards"
                         ready[p][r][k] = m["seq"]
                     else:
