@@ -186,7 +186,9 @@ struct DmArgs {
   uint64_t timeout_ticks = 0;      // wall_clock64 ticks
   DmMsg m[kMaxDm];
   int ncopy = 0;                   // messages with workgroups of their own (standalone copies, group leaders):
-  int cidx[kMaxDm] = {};           // indices into m, in dispatch order
+  int cidx[kMaxDm] = {};           // indices into m, in dispatch order,
+  int cwgs[kMaxDm] = {};           // and their workgroups (wgs; wgs x members for a group)
+  int ncw = 0;                     // sum of cwgs: the copy workgroups of the launch
 };
 int launch_dm_move(const DmArgs &a, void *stream);
 

@@ -399,10 +399,16 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   // leaders of push groups (members ride with their leader, leaves with the tree)
   auto index_copies = [&]() {
     a.ncopy = 0;
+    a.ncw = 0;
     for (int i = 0; i < a.nmsg; i++) {
       const DmMsg &m = a.m[i];
       if (m.leaf >= 0 || (m.grp >= 0 && m.grp != i)) continue;
-      a.cidx[a.ncopy++] = i;
+      int members = 1;
+      if (m.grp == i)
+        for (int q = i + 1; q < a.nmsg; q++) members += a.m[q].grp == i;
+      a.cidx[a.ncopy] = i;
+      a.cwgs[a.ncopy] = a.wgs * members;
+      a.ncw += a.cwgs[a.ncopy++];
     }
   };
   auto flush = [&]() -> int {

@@ -833,7 +833,7 @@ __device__ __forceinline__ uint64_t ld_acq_sys(const uint64_t *p) {
 // one workgroup's share of message mi (workgroup wi of a.wgs): wait, copy,
 // release, count in; the last workgroup of the message publishes.  false: the
 // transport is poisoned (the workgroup must leave the launch at once)
-__device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi) {
+__device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi, int nwg) {
   using namespace dm;
   const DmMsg &m = a.m[mi];
   uint8_t *own = a.own;
@@ -901,7 +901,7 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi) {
   const u32x4 *vs = reinterpret_cast<const u32x4 *>(src + head);
   u32x4 *vd = reinterpret_cast<u32x4 *>(dst + head);
   constexpr int U = 4;
-  const size_t stride = (size_t)a.wgs * kBlock * U;
+  const size_t stride = (size_t)nwg * kBlock * U;
   for (size_t b0 = (size_t)wi * kBlock * U + threadIdx.x; b0 < nvec; b0 += stride) {
     u32x4 x[U];
 #pragma unroll
@@ -921,7 +921,7 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t old = __hip_atomic_fetch_add(cnt_ptr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1 == (uint32_t)a.wgs) {
+    if (old + 1 == (uint32_t)nwg) {
       __hip_atomic_store(cnt_ptr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use: a later launch
       // system-scope release (buffer_wbl2 sc0 sc1), its write-back waited for
       // explicitly (the compiler may drop the wait after buffer_wbl2 when the
@@ -940,7 +940,7 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi) {
 // several peers, DmMsg::grp): each member's slot-reuse acknowledgement is
 // awaited, the source is read once and stored into every member's slot, and
 // every member is counted in and published exactly as a standalone push
-__device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi) {
+__device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi, int nwg) {
   using namespace dm;
   uint8_t *own = a.own;
   uint32_t *poison = reinterpret_cast<uint32_t *>(own + kPoisonOff);
@@ -998,7 +998,7 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi) {
         reinterpret_cast<uint8_t *>(dv[d])[i] = src[i];
   const u32x4 *vs = reinterpret_cast<const u32x4 *>(src);
   constexpr int U = 4;
-  const size_t stride = (size_t)a.wgs * kBlock * U;
+  const size_t stride = (size_t)nwg * kBlock * U;
   for (size_t b0 = (size_t)wi * kBlock * U + threadIdx.x; b0 < nvec; b0 += stride) {
     u32x4 x[U];
 #pragma unroll
@@ -1023,7 +1023,7 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi) {
       const size_t k = (size_t)(dseq[d] % kSlots);
       uint32_t *cnt = reinterpret_cast<uint32_t *>(own + kCntPushOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
       const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (old + 1 == (uint32_t)a.wgs) {
+      if (old + 1 == (uint32_t)nwg) {
         __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
         uint64_t *sig = reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
@@ -1036,9 +1036,16 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi) {
   return true;
 }
 
-// a copy workgroup: its message alone, or the group it leads
-__device__ __forceinline__ bool dm_copy_wg(const DmArgs &a, int mi, int wi) {
-  return a.m[mi].push && a.m[mi].grp == mi ? dm_mcast_msg(a, mi, wi) : dm_copy_msg(a, mi, wi);
+// copy workgroup b of the launch: the entry of DmArgs::cidx it belongs to
+// (entry c has cwgs[c] workgroups: wgs for a message alone, wgs x members for
+// a push group, so a group keeps the parallelism of its members), then its
+// message alone or the group it leads
+__device__ __forceinline__ bool dm_copy_wg(const DmArgs &a, unsigned b) {
+  int c = 0;
+  unsigned start = 0;
+  while (c + 1 < a.ncopy && b >= start + (unsigned)a.cwgs[c]) start += (unsigned)a.cwgs[c++];
+  const int mi = a.cidx[c], wi = (int)(b - start), nwg = a.cwgs[c];
+  return a.m[mi].push && a.m[mi].grp == mi ? dm_mcast_msg(a, mi, wi, nwg) : dm_copy_msg(a, mi, wi, nwg);
 }
 
 // thread 0, after its workgroup's share of the launch: the last workgroup of
@@ -1061,7 +1068,7 @@ __device__ __forceinline__ void dm_launch_done(const DmArgs &a) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_dm_move(DmArgs a) {
-  if (!dm_copy_wg(a, a.cidx[blockIdx.x / (unsigned)a.wgs], (int)(blockIdx.x % (unsigned)a.wgs))) return;
+  if (!dm_copy_wg(a, blockIdx.x)) return;
   dm_launch_done(a);
 }
 
@@ -1072,12 +1079,16 @@ static bool dm_args_ok(const DmArgs &a, bool leaves_ok) {
   if (a.nmsg <= 0 || a.nmsg > kMaxDm || a.wgs < 1 || !a.own || !a.slot || a.ncopy < 0 || a.ncopy > a.nmsg)
     return false;
   uint64_t seen = 0;
+  int ncw = 0;
   for (int c = 0; c < a.ncopy; c++) {
     const int i = a.cidx[c];
-    if (i < 0 || i >= a.nmsg || (seen >> i & 1) || a.m[i].leaf >= 0 || (a.m[i].grp >= 0 && a.m[i].grp != i))
+    if (i < 0 || i >= a.nmsg || (seen >> i & 1) || a.m[i].leaf >= 0 || (a.m[i].grp >= 0 && a.m[i].grp != i) ||
+        a.cwgs[c] < 1 || a.cwgs[c] > 1 << 16)
       return false;
     seen |= 1ull << i;
+    ncw += a.cwgs[c];
   }
+  if (ncw != a.ncw) return false;
   for (int i = 0; i < a.nmsg; i++) {
     const DmMsg &m = a.m[i];
     if (m.peer < 0 || m.peer >= dm::kMaxPeers || m.j < 0 || m.j >= dm::kSlots || m.bytes > a.slot) return false;
@@ -1095,7 +1106,7 @@ static bool dm_args_ok(const DmArgs &a, bool leaves_ok) {
 int launch_dm_move(const DmArgs &a, void *stream) {
   if (a.nmsg <= 0) return BINE_SUCCESS;
   if (!dm_args_ok(a, false)) return BINE_ERR_ARG;
-  hipLaunchKernelGGL(k_dm_move, dim3((unsigned)(a.ncopy * a.wgs)), dim3(kBlock), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(k_dm_move, dim3((unsigned)a.ncw), dim3(kBlock), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
@@ -1105,9 +1116,9 @@ int launch_dm_move(const DmArgs &a, void *stream) {
 template <typename T, int OP, int NL>
 __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
   using namespace dm;
-  const unsigned ncw = (unsigned)a.ncopy * (unsigned)a.wgs;
+  const unsigned ncw = (unsigned)a.ncw;
   if (blockIdx.x < ncw) {
-    if (!dm_copy_wg(a, a.cidx[blockIdx.x / (unsigned)a.wgs], (int)(blockIdx.x % (unsigned)a.wgs))) return;
+    if (!dm_copy_wg(a, blockIdx.x)) return;
     dm_launch_done(a);
     return;
   }
@@ -1195,7 +1206,7 @@ bool dm_tree_supported(int dtype, int op, int nl) {
 
 template <typename T, int OP>
 static hipError_t dmt_launch(const DmArgs &a, const DmTree &t, hipStream_t st) {
-  const dim3 g((unsigned)(a.ncopy * a.wgs + t.twgs));
+  const dim3 g((unsigned)(a.ncw + t.twgs));
   switch (t.nl) {
     case 2: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 2>), g, dim3(kBlock), 0, st, a, t); break;
     case 4: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 4>), g, dim3(kBlock), 0, st, a, t); break;
