@@ -454,7 +454,7 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       m.j = js[(size_t)x.peer]++;
       m.leaf = -1;
       // the same bytes already pushed to another peer in this launch: one
-      // group, the source read once (BINE_DIRECT_MCAST=0: every push alone)
+      // group, the source read once (BINE_DIRECT_MCAST=1; default: every push alone)
       m.grp = -1;
       if (mcast) {
         const int me = a.nmsg - 1;

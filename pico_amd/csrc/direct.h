@@ -64,7 +64,8 @@ struct DirectState {
                 const TreeSpec &dtree) const;
   int tree_wgs = 64;   // tree workgroups per launch (BINE_DIRECT_TREE_WGS; bine_comm_set_direct_tree)
   int tree_wgs_env = 64;  // the value init() settled on
-  bool mcast = true;      // pushes of the same bytes to several peers as one group (BINE_DIRECT_MCAST)
+  bool mcast = false;     // pushes of the same bytes to several peers as one group (BINE_DIRECT_MCAST=1;
+                          // off: no gain measured, profiles/r3_push_groups.txt)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }
   // stderr: this rank's flags and device-side sequence bases (after a timeout)
   void dump() const;
