@@ -94,14 +94,16 @@ def test_staged_host_buffers_4_ranks():
 
 
 @pytest.mark.gpu
-def test_fused_trees_vs_unfused_two_processes():
+@pytest.mark.parametrize("mcast", ["0", "1"])
+def test_fused_trees_vs_unfused_two_processes(mcast):
     """the direct transport's fused trees (leaves read in place in the inbox
     slots, deferred into the next exchange's launch) and the unfused form
     (pull copies + k_reduce_tree) at C3 / C4 full size, 2 processes, 16 and
     64 MiB chunks (64: leaves of 4 slots, the tree inside its own exchange);
     every rank's output digest equals the oracle's in both forms
-    (tools/dm_tree_ab.py)"""
-    env = dict(os.environ)
+    (tools/dm_tree_ab.py); mcast = 1: with the opt-in push groups
+    (BINE_DIRECT_MCAST)"""
+    env = dict(os.environ, BINE_DIRECT_MCAST=mcast)
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_tree_ab.py"), "2", "16,64", "4"],
                        env=env, capture_output=True, text=True, timeout=400)
     print(r.stdout[-3000:])
