@@ -526,6 +526,17 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
  * batch op waits for (-1 as UINT64_MAX: none).  `out` holds 3 (kinds 0, 1)
  * or 2 (kind 2) words per entry.  Returns the number of entries (may exceed
  * cap) or -status. */
+/* The direct transport's fused-tree decisions (bine_comm_set_direct_tree)
+ * for rank `rank`'s issue schedule, with the transport's shape rules at
+ * sub-message slot `slot` and launch structure `merge` (BINE_DIRECT_MERGE):
+ * host[i] = the exchange op whose launch evaluates tree op i (-1: not
+ * fused), defer[i] = 1 when exchange op i's receives are pulled by the next
+ * exchange (its tree deferred there).  Host only; `mode` as in
+ * bine_plan_schedule.  Returns the number of ops (may exceed cap) or
+ * -status. */
+int64_t bine_plan_dm_trees(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                           int in_place, size_t chunk_bytes, int mode, size_t slot, int merge, int dtype, int op,
+                           int32_t *host, int32_t *defer, int64_t cap);
 int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
                         size_t segsize, int in_place, size_t chunk_bytes, int mode, int kind, uint64_t *out,
                         int64_t cap);

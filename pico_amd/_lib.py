@@ -158,6 +158,8 @@ def lib():
         "bine_plan_schedule": ([i, i, i, sz, vp, i, sz, sz, i, sz, sz, i, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int64), vp], ctypes.c_int64),
         "bine_plan_stage": ([i, i, i, sz, vp, i, sz, sz, i, sz, i, i, vp, ctypes.c_int64], ctypes.c_int64),
+        "bine_plan_dm_trees": ([i, i, i, sz, vp, i, sz, i, sz, i, sz, i, i, i, vp, vp, ctypes.c_int64],
+                               ctypes.c_int64),
         "bine_allreduce_staged": ([vp, i, vp, vp, vp, vp, sz, i, i, sz, sz, vp, vp, vp], i),
         "bine_reduce_scatter_staged": ([vp, i, vp, vp, vp, vp, vp, i, i, sz, vp, vp, vp], i),
     }

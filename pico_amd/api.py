@@ -387,6 +387,26 @@ def schedule(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=No
     return ops, bool(cj.value), int(fw.value)
 
 
+def dm_tree_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, esz: int = 4,
+                 in_place: bool = False, chunk_bytes: int = 0, flat_ag=False, flat_rs: bool = False,
+                 slot: int = 16 << 20, merge: int = 3, dtype="float", op: str = "sum"):
+    """The direct transport's fused-tree decisions for rank `rank`'s issue
+    schedule (bine_plan_dm_trees, host only): (host, defer) per op -- host[i]
+    = the exchange whose launch evaluates tree op i (-1: not fused), defer[i]
+    = exchange i's receives are pulled by the next exchange."""
+    a = _algo(coll, algo)
+    rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
+    mode = (2 if flat_ag else 0) | (4 if flat_rs else 0) | (8 if flat_ag == 2 else 0)
+    args = (a, nranks, rank, count, rc, 0, esz, int(in_place), chunk_bytes, mode, slot, merge, _dtype(dtype),
+            OPS[op])
+    n = lib().bine_plan_dm_trees(*args, None, None, 0)
+    if n < 0:
+        raise BineError(int(-n), f"dm_tree_plan {coll}_{algo}")
+    host, defer = (ctypes.c_int32 * max(int(n), 1))(), (ctypes.c_int32 * max(int(n), 1))()
+    lib().bine_plan_dm_trees(*args, host, defer, n)
+    return list(host[:n]), list(defer[:n])
+
+
 def stage_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, esz: int = 4,
                segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0, flat_ag=False, flat_rs: bool = False):
     """The host staging of rank `rank`'s schedule (bine_plan_stage; host only):
@@ -539,4 +559,4 @@ __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "bcast", "loopback_bcast", "reduce_batch",
            "exchange", "vendor_allreduce", "reduce_tree", "allreduce_staged", "reduce_scatter_staged",
-           "stage_plan"] + list(ENTRY_POINTS)
+           "stage_plan", "dm_tree_plan"] + list(ENTRY_POINTS)

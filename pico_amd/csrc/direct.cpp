@@ -117,7 +117,7 @@ sockaddr_un addr_of(uint64_t key, int r, socklen_t *len) {
 }  // namespace
 
 DirectState::~DirectState() {
-  (void)hipDeviceSynchronize();
+  if (own || !peer.empty()) (void)hipDeviceSynchronize();  // nothing to wait for when nothing was set up
   for (size_t x = 0; x < peer.size(); x++) {
     if ((int)x == rank || !peer[x]) continue;
     (void)hipMemUnmap(peer[x], total);

@@ -803,7 +803,8 @@ struct Staging {
 // exchange, hosted[x] = the tree exchange x evaluates, tree_at[j] = i,
 // defer[i]: i's receives are pulled by the host; false: no fused tree at all.
 template <typename Ptr>
-static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, DmTreePlan &pl) {
+static bool plan_dm_trees(const Transport &tx, bool on, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op,
+                          DmTreePlan &pl) {
   const size_t n = sc.ops.size();
   pl.tree_at.assign(n, -1);
   pl.host.assign(n, -1);
@@ -811,7 +812,7 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
   pl.defer.assign(n, 0);
   pl.spec.resize(n);
   pl.leaves.resize(n);
-  if (!c->tx->stream_ordered() || !c->dm_tree || op < 0 || c->profile) return false;
+  if (!tx.stream_ordered() || !on || op < 0) return false;
   auto sends_of = [&](size_t x, std::vector<XSend> &s) {
     s.clear();
     for (const Prim &p : sc.ops[x].prims)
@@ -885,7 +886,7 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
       for (const XRecv &x : r2)
         dfr = dfr && !overlaps((const char *)x.ptr, x.bytes, ts.out, ts.leaf_bytes) &&
               !overlaps((const char *)x.ptr, x.bytes, ts.own_leaf, ts.leaf_bytes);
-      dfr = dfr && c->tx->defer_ok(s2, r2, r, ts);
+      dfr = dfr && tx.defer_ok(s2, r2, r, ts);
     }
     size_t hx = n;
     if (dfr) {
@@ -894,7 +895,7 @@ static bool plan_dm_trees(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz,
     } else if (pl.hosted[i] < 0) {
       bool own = true;  // in its own exchange: the output is written while the pushes still read
       for (const XSend &x : s) own = own && !overlaps((const char *)x.ptr, x.bytes, ts.out, ts.leaf_bytes);
-      if (own && c->tx->tree_ok(s, r, ts)) hx = i;
+      if (own && tx.tree_ok(s, r, ts)) hx = i;
     }
     if (hx == n) continue;
     pl.tree_at[j] = (int)i;
@@ -946,7 +947,8 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   int64_t h_waited[2] = {-1, -1};
   // trees evaluated inside an exchange launch (direct transport; plan_dm_trees)
   DmTreePlan &tp = c->tree_plan;
-  const bool dm_trees = !single && !stg && plan_dm_trees(c, sc, ptr, esz, dtype, op, tp);
+  const bool dm_trees = !single && !stg && plan_dm_trees(*c->tx, c->dm_tree && !c->profile, sc, ptr, esz, dtype,
+                                                         op, tp);
   std::vector<hipEvent_t> &tev = c->tree_ev;
   std::vector<char> &tpend = c->tree_pending;
   if (dm_trees) {
@@ -1756,6 +1758,55 @@ int64_t bine_plan_schedule(int algo, int nranks, int rank, size_t count, const i
   if (workspace) {
     for (int t = 0; t < 3; t++) workspace[t] = p.tmp_elems[t];
     workspace[3] = sc.stage_elems;
+  }
+  return n;
+}
+
+// plan_dm_trees' decisions for rank `rank`'s issue schedule, with the
+// direct transport's shape rules at `slot` / `merge` and distinct, aligned
+// stand-in addresses per buffer (the decisions depend on overlaps within a
+// buffer only): host[i] = the exchange whose launch evaluates tree op i (-1:
+// not fused), defer[i] = 1 if exchange i's receives are pulled by the next
+// exchange.  Returns the number of ops (may exceed cap) or -status.
+namespace {
+struct PlanOnlyTx final : Transport {
+  DirectState d;
+  int exchange(const std::vector<XSend> &, const std::vector<XRecv> &, hipStream_t) override {
+    return BINE_ERR_UNSUPPORTED;
+  }
+  bool stream_ordered() const override { return true; }
+  bool tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &t) const override {
+    return d.tree_ok(s, r, t);
+  }
+  bool defer_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const std::vector<XRecv> &dl,
+                const TreeSpec &t) const override {
+    return d.defer_ok(s, r, dl, t);
+  }
+};
+}  // namespace
+
+int64_t bine_plan_dm_trees(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                           int in_place, size_t chunk_bytes, int mode, size_t slot, int merge, int dtype, int op,
+                           int32_t *host, int32_t *defer, int64_t cap) {
+  if (!esz || !slot || merge < 0 || merge > 3) return -(int64_t)BINE_ERR_ARG;
+  PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, 0, in_place);
+  a.flat_ag = (mode & 2) != 0;
+  a.flat_rs = (mode & 4) != 0;
+  a.flat_ag_chunked = (mode & 8) != 0;
+  Plan p;
+  Schedule sc;
+  build(a, chunk_elems(chunk_bytes, esz), 0, (mode & 1) != 0, p, sc);
+  if (p.status != BINE_SUCCESS) return -(int64_t)p.status;
+  PlanOnlyTx tx;
+  tx.d.slot = slot;
+  tx.d.merge = merge;
+  auto ptr = [&](int buf, uint64_t off) { return (char *)((uintptr_t)(buf + 1) << 40) + off * esz; };
+  DmTreePlan pl;
+  plan_dm_trees(tx, true, sc, ptr, esz, dtype, op, pl);
+  const int64_t n = (int64_t)sc.ops.size();
+  for (int64_t i = 0; i < n && i < cap; i++) {
+    if (host) host[i] = pl.host[(size_t)i];
+    if (defer) defer[i] = pl.defer[(size_t)i];
   }
   return n;
 }

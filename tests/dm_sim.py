@@ -130,6 +130,9 @@ def dm_tree_plan(ops, esz, slot, kmax=32):
         while i2 < n and not ops[i2]["xchg"]:
             i2 += 1
         lb = t["count"] * esz
+        # the tree reads / writes whole 16-B vectors from 16-B aligned own leaf and output
+        if (t["aux_off"] * esz) % 16 or (t["dst_off"] * esz) % 16 or t["peer"] not in (2, 4, 8, 16):
+            continue
         dfr = (i2 < n and ((i2 == i + 1 and i2 < j) or i2 == j + 1) and i2 not in hosted and ops[i2]["wait"] != j
                and lb <= slot and lb % 16 == 0)
         if dfr:

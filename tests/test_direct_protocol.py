@@ -70,3 +70,36 @@ def test_fused_trees_multi_round(merge):
                      flat_rs=True, slot=256 << 10, merge=merge, dm_trees=True, stats=st)
     assert res is None, res["stuck"][:8]
     assert st["in_exchange"] > 0, st
+
+
+@pytest.mark.parametrize("case", [
+    ("allreduce", "bine_bdw_remap", 2, dict(count=2 << 20, chunk_bytes=1 << 20)),
+    ("allreduce", "bine_bdw_remap", 4, dict(count=4 << 20, chunk_bytes=1 << 20)),
+    ("allreduce", "bine_bdw_remap", 8, dict(count=8 << 20, chunk_bytes=1 << 20)),
+    ("allreduce", "bine_bdw_remap", 8, dict(count=8 << 20, chunk_bytes=4 << 20)),
+    ("allreduce", "bine_bdw_remap", 16, dict(count=16 << 20, chunk_bytes=1 << 20)),
+    ("allreduce", "bine_bdw_static", 8, dict(count=8 << 20, chunk_bytes=1 << 20)),
+    ("allreduce", "bine_bdw_remap", 8, dict(count=1_000_003, chunk_bytes=1 << 20)),
+    ("allreduce", "bine_bdw_remap", 4, dict(count=4 << 20, chunk_bytes=1 << 20, in_place=True)),
+    ("allreduce", "rabenseifner", 8, dict(count=8 << 20, chunk_bytes=1 << 20)),
+    ("reduce_scatter", "bine_permute_remap", 8, dict(rcounts=[1 << 20] * 8, chunk_bytes=1 << 20)),
+    ("reduce_scatter", "bine_send_remap", 4, dict(rcounts=[1 << 20] * 4, chunk_bytes=4 << 20)),
+    ("reduce_scatter", "bine_static", 8, dict(rcounts=[1 << 20] * 8, chunk_bytes=1 << 20)),
+], ids=lambda c: f"{c[0]}-{c[1]}-P{c[2]}-" + "-".join(f"{k}{v if not isinstance(v, list) else len(v)}"
+                                                         for k, v in c[3].items()))
+def test_simulator_restates_the_executors_tree_plan(case):
+    # the simulator's dm_tree_plan (what the deadlock check runs) makes the
+    # executor's plan_dm_trees decisions (bine_plan_dm_trees), rank by rank
+    import pico_amd
+    coll, algo, P, kw = case
+    slot = 1 << 20
+    n_fused = 0
+    for r in range(P):
+        sk = dict(kw)
+        ops, _, _ = pico_amd.schedule(coll, algo, P, r, esz=4, flat_ag=2, flat_rs=True, **sk)
+        host, defer = pico_amd.dm_tree_plan(coll, algo, P, r, esz=4, flat_ag=2, flat_rs=True, slot=slot, **sk)
+        h, _, d = dm_sim.dm_tree_plan(ops, 4, slot)
+        assert {j: x for j, x in enumerate(host) if x >= 0} == h, (r, host, h)
+        assert {i for i, x in enumerate(defer) if x} == d, (r, defer, d)
+        n_fused += len(h)
+    assert n_fused > 0
