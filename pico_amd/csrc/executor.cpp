@@ -797,7 +797,10 @@ struct Staging {
 //   * in its own exchange i otherwise (the last chunk's tree): the tree
 //     workgroups of round r beside the pushes of round r + 1 (merge 1), or of
 //     the one round; its output must overlap no block i sends;
-//   * not at all (the unfused form) when neither applies.
+//   * by itself otherwise (the last chunk's tree when its exchange already
+//     hosts the previous one): a launch of its own on the comm stream at the
+//     tree's place, pulling the leaves in place;
+//   * not at all (the unfused form) when none applies.
 // Always: the staging buffer is referenced by receives and trees only (no one
 // else reads what is no longer written there).  host[j] = the hosting
 // exchange, hosted[x] = the tree exchange x evaluates, tree_at[j] = i,
@@ -897,6 +900,13 @@ static bool plan_dm_trees(const Transport &tx, bool on, const Schedule &sc, Ptr 
       for (const XSend &x : s) own = own && !overlaps((const char *)x.ptr, x.bytes, ts.out, ts.leaf_bytes);
       if (own && tx.tree_ok(s, r, ts)) hx = i;
     }
+    if (hx == n && tx.defer_ok({}, {}, r, ts)) {
+      // no exchange can take it (i already hosts the previous chunk's tree,
+      // and nothing follows -- the last chunk): the tree op itself becomes a
+      // launch of its own on the comm stream that pulls i's leaves in place
+      hx = j;
+      pl.defer[i] = 1;
+    }
     if (hx == n) continue;
     pl.tree_at[j] = (int)i;
     pl.host[j] = (int)hx;
@@ -958,6 +968,16 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   for (size_t i = 0; i < sc.ops.size(); i++) {
     const SOp &o = sc.ops[i];
     hipStream_t st = o.xchg ? C : K;
+    if (dm_trees && tp.host[i] == (int)i) {
+      // a tree hosted by itself: its own launch on the comm stream pulls the
+      // leaves in place (after the exchange that was issued without them)
+      if (int rj = stream_join(c, C, K)) return rj;
+      static const std::vector<XSend> no_s;
+      static const std::vector<XRecv> no_r;
+      if (int rc = c->tx->exchange_tree(no_s, no_r, nullptr, &tp.leaves[i], &tp.spec[i], C)) return rc;
+      tev[i] = next_event(c);
+      HIP_TRY(hipEventRecord(tev[i], C));
+    }
     if (dm_trees && tp.host[i] >= 0) {
       // this tree runs inside exchange host[i]: K takes up its place in K's
       // order (later local ops follow it as they followed the tree) -- now,

@@ -144,11 +144,18 @@ def dm_tree_plan(ops, esz, slot, kmax=32):
             host[j] = i2
             hosted[i2] = j
             defer.add(i)
-        elif i not in hosted:
+            continue
+        if i not in hosted:
             s1 = ranges(ops[i], "SEND")
             if not any(ov(x, out) for x in s1) and len(s1) + len(recvs) <= kmax and lb % 16 == 0:
                 host[j] = i
                 hosted[i] = j
+                continue
+        if lb <= slot and lb % 16 == 0 and len(recvs) <= kmax:
+            # a launch of its own at the tree's place (the tree op hosts itself)
+            host[j] = j
+            hosted[j] = j
+            defer.add(i)
     return host, hosted, defer
 
 
@@ -180,16 +187,27 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
             stats["in_exchange"] += len(host) - len(defer)
         held = {}
         for _call in range(calls):
+            # entries of this call with symbolic deps, resolved once every op
+            # has its place (a tree may wait for a host issued after it)
+            ents, at = [], {}
             first_c = None
             for i, o in enumerate(ops):
                 stream = "C" if o["xchg"] else "K"
                 deps = []
                 if o["wait"] >= 0:
-                    deps.append(base + o["wait"])
+                    deps.append(("op", o["wait"]))
                 launches = []
-                if i in host:
+                if host.get(i) == i:
+                    # a tree hosting itself: its own launch on the comm stream
+                    # (after every K op issued before it), pulling its leaves
+                    srcs = [x for x in defer if x < i and dm_tree_src(ops, x) == i]
+                    launches = exchange_launches(r, [], [], seq_s[r], seq_r[r], slot, P, merge, held.pop(srcs[0]))
+                    ents.append({"stream": "C", "deps": [("Kb-ent", len(ents))], "launches": launches})
+                    # K takes up the tree's place: waits for that launch
+                    stream, deps, launches = "K", [("ent", len(ents) - 1)], []
+                elif i in host:
                     # the tree runs inside exchange host[i]: K waits for it there
-                    stream, deps = "K", [base + host[i]]
+                    stream, deps = "K", [("op", host[i])]
                 elif o["xchg"]:
                     sends = [(p["peer"], p["count"] * esz, (p["src_buf"], p["src_off"])) for p in o["prims"]
                              if p["type"] == "SEND" and p["count"]]
@@ -205,17 +223,32 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                         if srcs:
                             dl = held.pop(srcs[0])
                         # stream_join(C, K): the comm stream follows every K op issued so far
-                        deps.append(("K-before-host", base + i, base + j))
+                        deps.append(("Kb-host", i, j))
                     launches = exchange_launches(r, sends, recvs, seq_s[r], seq_r[r], slot, P, merge, dl)
                     if first_c is None and c_join:
-                        first_c = base + i
+                        first_c = i
                         # c_join: the comm stream waits for the caller's stream's prior work
-                        deps.append(("K-before", base + i))
-                seq.append({"stream": stream, "deps": deps, "launches": launches, "done": False, "li": 0,
-                            "started": False})
+                        deps.append(("Kb-op", i))
+                at[i] = len(ents)
+                ents.append({"stream": stream, "deps": deps, "launches": launches})
+
+            def res(d):
+                if d[0] == "op":
+                    return base + at[d[1]]
+                if d[0] == "ent":
+                    return base + d[1]
+                if d[0] == "Kb-ent":
+                    return ("K-before", base + d[1])
+                if d[0] == "Kb-op":
+                    return ("K-before", base + at[d[1]])
+                return ("K-before-host", base + at[d[1]], base + at[d[2]])
+
+            for e in ents:
+                seq.append({"stream": e["stream"], "deps": [res(d) for d in e["deps"]], "launches": e["launches"],
+                            "done": False, "li": 0, "started": False})
             if final_wait >= 0:
                 # the caller's stream waits for the comm stream's op final_wait before the next call
-                seq.append({"stream": "K", "deps": [base + final_wait], "launches": [], "done": False, "li": 0,
+                seq.append({"stream": "K", "deps": [base + at[final_wait]], "launches": [], "done": False, "li": 0,
                             "started": False})
             base = len(seq)
         ranks.append(seq)

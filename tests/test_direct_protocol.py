@@ -103,3 +103,46 @@ def test_simulator_restates_the_executors_tree_plan(case):
         assert {i for i, x in enumerate(defer) if x} == d, (r, defer, d)
         n_fused += len(h)
     assert n_fused > 0
+
+
+def _hbm_bytes_per_rank(coll, algo, P, rank, fused, esz=4, **kw):
+    """HBM bytes one rank moves in one call over the direct transport, from
+    the executed issue schedule: a push reads its source (its remote write is
+    the receiver's arrival), a receive is an arrival into this rank's inbox
+    plus -- unless a fused tree reads it in place -- a pull copy (read +
+    write), a tree reads its leaves and writes its output, a copy reads and
+    writes, a pairwise reduction reads two operands and writes one"""
+    import pico_amd
+    ops, _, _ = pico_amd.schedule(coll, algo, P, rank, esz=esz, flat_ag=2, flat_rs=True, **kw)
+    host, _ = pico_amd.dm_tree_plan(coll, algo, P, rank, esz=esz, flat_ag=2, flat_rs=True, slot=1 << 20, **kw)
+    leaf_ops = set()
+    for j, h in enumerate(host):
+        if fused and h >= 0:
+            i = j - 1
+            while not ops[i]["xchg"]:
+                i -= 1
+            leaf_ops.add(i)
+    b = 0
+    for i, o in enumerate(ops):
+        for p in o["prims"]:
+            n = p["count"] * esz
+            b += {"SEND": n, "RECV": n + (0 if i in leaf_ops else 2 * n), "REDUCE_TREE": (p["peer"] + 1) * n,
+                  "COPY": 2 * n, "REDUCE": 3 * n, "REDUCE3": 3 * n}[p["type"]]
+    return b
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_hbm_model_of_the_fused_trees(P):
+    # DESIGN.md §3 "Push groups" table: HBM bytes per rank per C3 call at P = 8,
+    # unfused 8.125 S vs fused trees 6.375 S (7.25 / 5.75 S at P = 4), and the
+    # reduce_scatter C4 (S = input): 4.625 / 2.875 S at P = 8
+    S = (P << 20) * 4
+    ar = {f: _hbm_bytes_per_rank("allreduce", "bine_bdw_remap", P, 0, f, count=P << 20, chunk_bytes=1 << 20) / S
+          for f in (False, True)}
+    want = {8: (8.125, 6.375), 4: (7.25, 5.75)}[P]
+    assert (ar[False], ar[True]) == want, ar
+    rs = {f: _hbm_bytes_per_rank("reduce_scatter", "bine_permute_remap", P, 0, f, rcounts=[1 << 20] * P,
+                                 chunk_bytes=1 << 20) / S for f in (False, True)}
+    if P == 8:
+        assert (rs[False], rs[True]) == (4.625, 2.875), rs
+    assert rs[True] < rs[False]
