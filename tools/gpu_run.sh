@@ -1,11 +1,11 @@
 # The GPU calls of a round, one step per line (tools/gpu_steps.sh: each step
-# under its own time limit, output in gpurun_out/<name>.log).  Edited per call;
-# this one: kernel trace and HBM counters of the fused-tree A/B at P = 2.  Run as
+# under its own time limit, output in gpurun_out/<name>.log).  Edited per call.
 #   /usr/local/graft/bin/gpurun --timeout 900 -- 'bash tools/gpu_run.sh'
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
- "abtrace:200:rocprofv3 --kernel-trace --output-format csv -d gpurun_out/abtrace -o ab_%pid% -- python3 -u tools/dm_tree_ab.py 2 16 4" \
- "abfetch:200:rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/abfetch -o ab_%pid% -- python3 -u tools/dm_tree_ab.py 2 16 4" \
- "abwrite:200:rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/abwrite -o ab_%pid% -- python3 -u tools/dm_tree_ab.py 2 16 4"
+ "large4:300:python -u tools/rccl_large.py 4" \
+ "rccl:400:python -u -m pytest tests/test_gpu_rccl.py -k 'matrix or orders or c1_four or fused_trees or staged' -x -v --timeout 300 --timeout-method thread -p no:cacheprovider" \
+ "ab4:200:python -u tools/dm_tree_ab.py 4 16,64 10" \
+ "full8:300:python -u tools/fullsize_multirank.py 8"
