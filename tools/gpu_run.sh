@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
- "large4:300:python -u tools/rccl_large.py 4" \
- "rccl:400:python -u -m pytest tests/test_gpu_rccl.py -k 'matrix or orders or c1_four or fused_trees or staged' -x -v --timeout 300 --timeout-method thread -p no:cacheprovider" \
+ "smoke:120:python -u -c 'import __graft_entry__ as g; g.smoke()'" \
+ "ab2:200:python -u tools/dm_tree_ab.py 2 16,64 10" \
  "ab4:200:python -u tools/dm_tree_ab.py 4 16,64 10" \
- "full8:300:python -u tools/fullsize_multirank.py 8"
+ "ab8q1:300:GPU_MAX_HW_QUEUES=1 python -u tools/dm_tree_ab.py 8 16,64 10"
