@@ -262,7 +262,11 @@ int bine_comm_set_flat_ag(bine_comm_t comm, int on);
  * reduction tree follow the whole count, whatever the chunking), while the
  * output completes chunk by chunk, so the two PCIe directions overlap each
  * other and the exchanges.  `chunk_bytes` = bytes one exchange round carries
- * over all blocks (0: 16 MiB).  Never graph-captured. */
+ * over all blocks (0: 16 MiB).  Never graph-captured.  A NULL `host_sbuf` /
+ * `host_rbuf` means that buffer is already on the device: `dev_sbuf` /
+ * `dev_rbuf` is the caller's own and nothing is copied for it (its stream
+ * argument may then be NULL).  The schedule is the same either way, so ranks
+ * with host buffers and ranks with device buffers can meet in one call. */
 int bine_allreduce_staged(bine_comm_t comm, int algo, const void *host_sbuf, void *host_rbuf, void *dev_sbuf,
                           void *dev_rbuf, size_t count, int dtype, int op, size_t segsize, size_t chunk_bytes,
                           void *h2d_stream, void *d2h_stream, void *stream);
@@ -354,6 +358,16 @@ int bine_comm_set_direct_wgs(bine_comm_t comm, int wgs);
  * cached graphs.  bench.py trials it on the node ("+dm" vs "+dmt"
  * transports, "+dmtxT" for T tree workgroups). */
 int bine_comm_set_direct_tree(bine_comm_t comm, int on);
+/* Diagnostics of the direct transport (BINE_DIRECT_STAMPS=<records> in the
+ * environment when the transport is set up): every workgroup of every
+ * exchange launch appends one record of 4 words -- tag = launch serial << 32
+ * | kind << 24 | message << 16 | workgroup (kind 0 push, 1 pull, 2 tree), and
+ * its wall_clock64 at entry, when its wait ended and when its copy or tree
+ * ended.  Copies up to `cap` records into `out` (4 words each) after
+ * synchronizing the device, sets *n to the number written so far (may exceed
+ * cap), and with reset != 0 starts over.  BINE_ERR_UNSUPPORTED when stamps are
+ * off. */
+int bine_comm_direct_stamps(bine_comm_t comm, uint64_t *out, size_t cap, size_t *n, int reset);
 
 /* Graph mode (RCCL communicators): the first collective call for a given
  * (algorithm, arguments, buffers, dtype, op, stream) captures the whole issue
@@ -365,6 +379,10 @@ int bine_comm_set_direct_tree(bine_comm_t comm, int on);
  * be the NULL stream (not capturable; such calls run eagerly), and buffers
  * must stay allocated while their graph is cached (up to 64 graphs; the cache
  * is dropped when the workspace grows and when graph mode is switched off).
+ * Schedules on two streams (graphs with parallel branches) are captured only
+ * on HIP runtimes >= 7.2; on older ones (torch's bundled 7.0) they run
+ * eagerly: that runtime's hipGraphLaunch crashes on such graphs when their
+ * streams share one hardware queue (tools/graph_fork_repro.cpp).
  * Off by default (BINE_GRAPHS=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_graphs(bine_comm_t comm, int on);
 

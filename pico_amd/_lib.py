@@ -151,6 +151,7 @@ def lib():
         "bine_comm_set_direct": ([vp, i], i),
         "bine_comm_set_direct_wgs": ([vp, i], i),
         "bine_comm_set_direct_tree": ([vp, i], i),
+        "bine_comm_direct_stamps": ([vp, vp, sz, ctypes.POINTER(sz), i], i),
         "bine_comm_set_profile": ([vp, i], i),
         "bine_comm_profile": ([vp, vp, ctypes.c_int64], ctypes.c_int64),
         "bine_exchange": ([vp, i, vp, vp, vp, i, vp, vp, vp, vp], i),

@@ -181,6 +181,19 @@ class Comm:
         alike; bit-identical"""
         check(lib().bine_comm_set_direct_tree(self.handle, int(on)), "bine_comm_set_direct_tree")
 
+    def direct_stamps(self, reset: bool = True):
+        """Direct-transport diagnostics (BINE_DIRECT_STAMPS=<records> at setup;
+        bine_comm_direct_stamps): numpy uint64 array (n, 4) of per-workgroup
+        records -- tag (serial << 32 | kind << 24 | msg << 16 | wg; kind 0 push,
+        1 pull, 2 tree), wall_clock64 at entry, wait done, copy done."""
+        import numpy as np
+        n = ctypes.c_size_t(0)
+        check(lib().bine_comm_direct_stamps(self.handle, None, 0, ctypes.byref(n), 0), "bine_comm_direct_stamps")
+        out = np.zeros((max(int(n.value), 1), 4), dtype=np.uint64)
+        check(lib().bine_comm_direct_stamps(self.handle, out.ctypes.data, int(n.value), ctypes.byref(n),
+                                            int(reset)), "bine_comm_direct_stamps")
+        return out[:min(int(n.value), out.shape[0])] if n.value else out[:0]
+
     def set_profile(self, on: bool) -> None:
         """Per-op device timing of the following collectives (bine_comm_set_profile)."""
         check(lib().bine_comm_set_profile(self.handle, int(on)), "bine_comm_set_profile")

@@ -189,7 +189,19 @@ struct DmArgs {
   int cidx[kMaxDm] = {};           // indices into m, in dispatch order,
   int cwgs[kMaxDm] = {};           // and their workgroups (wgs; wgs x members for a group)
   int ncw = 0;                     // sum of cwgs: the copy workgroups of the launch
+  // diagnostics (BINE_DIRECT_STAMPS): per-workgroup wall_clock64 stamps of
+  // entry / wait done / copy done, appended to `stamps` (dm::Stamp layout);
+  // null: off
+  uint64_t *stamps = nullptr;
+  uint32_t serial = 0;             // the launch's number (host-side count)
 };
+namespace dm {
+// stamps buffer: [0] records written (atomic), [1] capacity (records), then
+// records of 4 words: tag = serial << 32 | kind << 24 | msg << 16 | wg, and the
+// workgroup's wall_clock64 at entry, when its wait ended, when its copy (or
+// tree) ended.  kind: 0 push, 1 pull, 2 tree, 3 push group
+constexpr int kStampHdr = 8, kStampWords = 4;
+}  // namespace dm
 int launch_dm_move(const DmArgs &a, void *stream);
 
 // The flat reduce-scatter's tree evaluated INSIDE the exchange launch that

@@ -131,6 +131,7 @@ DirectState::~DirectState() {
   }
   if (own_fd >= 0) close(own_fd);
   if (hpoison) (void)hipHostFree(hpoison);
+  if (stamps) (void)hipFree(stamps);
 }
 
 static int map_handle(hipMemGenericAllocationHandle_t h, size_t size, int device, void **va, std::string &err) {
@@ -163,6 +164,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   }
   if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
+  if (const char *e = getenv("BINE_DIRECT_PULL_WGS")) pull_wgs = std::max(0, atoi(e));
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
   if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
   if (const char *e = getenv("BINE_DIRECT_MCAST")) mcast = atoi(e) != 0;
@@ -183,6 +185,18 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
     return BINE_ERR_NO_MEM;
   }
   *(volatile uint32_t *)hpoison = 0;
+  if (const char *e = getenv("BINE_DIRECT_STAMPS")) {
+    const uint64_t cap = strtoull(e, nullptr, 10);
+    if (cap) {
+      const size_t bytes = (dm::kStampHdr + cap * dm::kStampWords) * sizeof(uint64_t);
+      const uint64_t hdr[2] = {0, cap};
+      if (hipMalloc((void **)&stamps, bytes) != hipSuccess ||
+          hipMemcpy(stamps, hdr, sizeof hdr, hipMemcpyHostToDevice) != hipSuccess) {
+        err = "direct transport: no stamps buffer";
+        return BINE_ERR_NO_MEM;
+      }
+    }
+  }
   hipMemAllocationProp p{};
   p.type = hipMemAllocationTypePinned;
   p.location.type = hipMemLocationTypeDevice;
@@ -388,6 +402,7 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   a.own = (uint8_t *)own;
   a.poison_host = hpoison_dev;
   a.timeout_ticks = timeout_ticks;
+  a.stamps = stamps;
   // j = index of a message among this launch's messages of its kind to / from
   // its peer (the kernel adds it to the device-side base)
   std::vector<int> js((size_t)P, 0), jr((size_t)P, 0);
@@ -407,12 +422,13 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       if (m.grp == i)
         for (int q = i + 1; q < a.nmsg; q++) members += a.m[q].grp == i;
       a.cidx[a.ncopy] = i;
-      a.cwgs[a.ncopy] = a.wgs * members;
+      a.cwgs[a.ncopy] = (m.push || !pull_wgs ? a.wgs : pull_wgs) * members;
       a.ncw += a.cwgs[a.ncopy++];
     }
   };
   auto flush = [&]() -> int {
     int rc;
+    a.serial = serial++;
     if (tree_round >= 0) {
       DmTree t;
       t.nl = ltree->nl;
@@ -523,6 +539,9 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       if (int rc = pulls(k)) return rc;
       if (int rc = flush()) return rc;
     }
+    // a self-hosted tree (no messages of its own, rounds = 0): the launch
+    // that pulls the deferred leaves and evaluates the tree
+    if (rounds == 0 && a.nmsg) return flush();
     return BINE_SUCCESS;
   }
   for (size_t k = 0; k <= rounds; k++) {

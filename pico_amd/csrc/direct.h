@@ -29,6 +29,11 @@ struct DirectState {
   size_t slot = (size_t)16 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES)
   int wgs = 32;                    // workgroups per message (BINE_DIRECT_WGS; bine_comm_set_direct_wgs)
   int env_wgs = 32;                // the value init() settled on (the setter's 0)
+  int pull_wgs = 0;                // workgroups per copied pull (BINE_DIRECT_PULL_WGS; 0: wgs)
+  // diagnostics (BINE_DIRECT_STAMPS=<records>): per-workgroup stamps of every
+  // launch (DmArgs::stamps), read back with bine_comm_direct_stamps
+  uint64_t *stamps = nullptr;
+  uint32_t serial = 0;
   int merge = 3;                   // launch structure (BINE_DIRECT_MERGE): 2 = pushes + pulls of a round in one
                                    // launch, 1 = round k-1's pulls with round k's pushes, 0 = separate launches,
                                    // 3 = 2 for one-round exchanges, else 1

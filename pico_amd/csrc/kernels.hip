@@ -830,6 +830,20 @@ __device__ __forceinline__ uint64_t ld_acq_sys(const uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// diagnostics (BINE_DIRECT_STAMPS, DmArgs::stamps): thread 0 of a workgroup
+// appends its (entry, wait done, copy done) wall_clock64 stamps
+__device__ __forceinline__ void dm_stamp(uint64_t *st, uint32_t serial, int kind, int msg, int wg, uint64_t t0,
+                                         uint64_t t1, uint64_t t2) {
+  if (!st) return;
+  const uint64_t i = __hip_atomic_fetch_add(st, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (i >= st[1]) return;
+  uint64_t *r = st + dm::kStampHdr + i * dm::kStampWords;
+  r[0] = (uint64_t)serial << 32 | (uint64_t)kind << 24 | (uint64_t)(msg & 255) << 16 | (uint64_t)(wg & 0xffff);
+  r[1] = t0;
+  r[2] = t1;
+  r[3] = t2;
+}
+
 // one workgroup's share of message mi (workgroup wi of a.wgs): wait, copy,
 // release, count in; the last workgroup of the message publishes.  false: the
 // transport is poisoned (the workgroup must leave the launch at once)
@@ -866,7 +880,9 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi, int
     cnt_ptr = reinterpret_cast<uint32_t *>(own + kCntPullOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
   }
   __shared__ int go;
+  uint64_t t0 = 0, t1 = 0;
   if (threadIdx.x == 0) {
+    if (a.stamps) t0 = wall_clock64();
     int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
     if (ok && wait_ptr) {
       const long long t0 = wall_clock64();
@@ -885,6 +901,7 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi, int
       }
     }
     go = ok;
+    if (a.stamps) t1 = wall_clock64();
   }
   __syncthreads();
   if (!go) return false;  // poisoned: the transport is dead, counters and bases no longer matter
@@ -920,6 +937,7 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi, int
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (a.stamps) dm_stamp(a.stamps, a.serial, m.push ? 0 : 1, mi, wi, t0, t1, wall_clock64());
     const uint32_t old = __hip_atomic_fetch_add(cnt_ptr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
     if (old + 1 == (uint32_t)nwg) {
       __hip_atomic_store(cnt_ptr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use: a later launch
@@ -1127,7 +1145,11 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
   // every leaf: its slot in our inbox, the sender's ready mark to wait for
   const u32x4 *lp[NL];
   __shared__ int go;
-  if (threadIdx.x == 0) go = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
+  uint64_t t0 = 0, t1 = 0;
+  if (threadIdx.x == 0) {
+    if (a.stamps) t0 = wall_clock64();
+    go = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
+  }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < NL; j++) {
@@ -1158,6 +1180,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
       }
     }
   }
+  if (threadIdx.x == 0 && a.stamps) t1 = wall_clock64();
   __syncthreads();
   if (!go) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the senders released before their marks
@@ -1178,6 +1201,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (a.stamps) dm_stamp(a.stamps, a.serial, 2, 255, tw, t0, t1, wall_clock64());
 #pragma unroll
     for (int j = 0; j < NL; j++) {
       if (j == t.pos) continue;

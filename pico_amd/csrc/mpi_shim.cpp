@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -44,37 +45,80 @@ struct Entry {
   size_t ev_next = 0;
 };
 
-// Host buffers the shim has page-locked (hipHostRegister), so that the
-// staging copies are DMA straight from / to the caller's memory and run
-// asynchronously on the copy streams.  pico_core keeps its buffers for the
-// whole run (pico_core_allreduce_utils.c:13-25); each is registered once, on
-// first use, and released at MPI_Finalize (MPI_COMM_SELF's delete callback).
-// BINE_HOST_REGISTER=0 turns it off (pageable copies).
-std::vector<std::pair<uintptr_t, uintptr_t>> g_pinned;  // [lo, hi), page-rounded
-constexpr size_t kPinMinBytes = 1 << 20;
-
-bool pin_host(const void *p, size_t n) {
+// Host buffers page-locked for ONE call.  A permanent
+// registration cache is unsafe in a general MPI library: a buffer freed and
+// allocated again at the same address keeps the old registration, whose pages
+// the kernel driver invalidated at munmap -- the next copy through it faulted
+// the GPU (profiles/r4_host_pin_probe.txt).  So the call's host buffers are
+// registered at its start and unregistered before it returns, once every
+// stream that copies them has drained (bounded, below).  Measured cost of the
+// per-call registration against round 3's permanent one: 10.085 vs 10.066 ms
+// for a 256 MiB host round trip (profiles/r4_host_stage_probe.txt).  Memory
+// the caller page-locked itself is used as it is.  BINE_HOST_REGISTER=0 keeps
+// the buffers pageable (HIP's own staging copies).
+bool register_on() {
   static const bool on = !getenv("BINE_HOST_REGISTER") || atoi(getenv("BINE_HOST_REGISTER")) != 0;
-  if (!on || n < kPinMinBytes) return false;
-  const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
-  const uintptr_t lo = (uintptr_t)p & ~(pg - 1), hi = ((uintptr_t)p + n + pg - 1) & ~(pg - 1);
-  for (const auto &r : g_pinned) {
-    if (lo >= r.first && hi <= r.second) return true;
-    if (lo < r.second && r.first < hi) return false;  // overlaps another registration: stay pageable
-  }
-  if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterMapped) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  g_pinned.emplace_back(lo, hi);
-  return true;
+  return on;
 }
 
-void unpin_all() {
-  for (const auto &r : g_pinned) (void)hipHostUnregister((void *)r.first);
-  (void)hipGetLastError();
-  g_pinned.clear();
+// Host waits of the shim are bounded: a stream that does
+// not drain within BINE_SYNC_TIMEOUT_S (default 120 s) makes the call return
+// MPI_ERR_OTHER naming the stream, instead of hanging the caller.
+double sync_timeout_s() {
+  static const double v = getenv("BINE_SYNC_TIMEOUT_S") ? atof(getenv("BINE_SYNC_TIMEOUT_S")) : 120.0;
+  return v;
 }
+
+int drain(hipStream_t s, const char *what, int rank) {
+  const double t0 = MPI_Wtime();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return MPI_SUCCESS;
+    if (q != hipErrorNotReady) {
+      fprintf(stderr, "libbine(amd) rank %d: %s stream: %s\n", rank, what, hipGetErrorString(q));
+      return MPI_ERR_OTHER;
+    }
+    const double el = MPI_Wtime() - t0;
+    if (el > sync_timeout_s()) {
+      fprintf(stderr, "libbine(amd) rank %d: the %s stream did not drain within %.0f s (BINE_SYNC_TIMEOUT_S); "
+                      "returning MPI_ERR_OTHER\n", rank, what, sync_timeout_s());
+      return MPI_ERR_OTHER;
+    }
+    if (el > 2e-3) usleep(50);  // spin first: short calls
+  }
+}
+
+struct CallPins {
+  std::vector<std::pair<uintptr_t, uintptr_t>> want, regs;  // [lo, hi), page-rounded
+  bool drained = true;  // false: a copy may still read / write the pages (never unregister then)
+  void add(const void *p, size_t n) {
+    if (!register_on() || !p || p == MPI_IN_PLACE || !n) return;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost) return;  // caller's own
+    (void)hipGetLastError();
+    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    want.emplace_back((uintptr_t)p & ~(pg - 1), ((uintptr_t)p + n + pg - 1) & ~(pg - 1));
+  }
+  // register the union of the wanted ranges (two buffers may share a page)
+  void commit() {
+    std::sort(want.begin(), want.end());
+    for (size_t i = 0; i < want.size();) {
+      uintptr_t lo = want[i].first, hi = want[i].second;
+      for (i++; i < want.size() && want[i].first <= hi; i++) hi = std::max(hi, want[i].second);
+      if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterDefault) == hipSuccess) regs.emplace_back(lo, hi);
+      else (void)hipGetLastError();  // stays pageable: HIP stages those copies itself
+    }
+  }
+  ~CallPins() {
+    if (!drained) {
+      if (!regs.empty()) fprintf(stderr, "libbine(amd): a stream did not drain; %zu host registrations kept\n",
+                                 regs.size());
+      return;
+    }
+    for (const auto &r : regs) (void)hipHostUnregister((void *)r.first);
+    (void)hipGetLastError();
+  }
+};
 
 int g_keyval = MPI_KEYVAL_INVALID;
 int g_self_keyval = MPI_KEYVAL_INVALID;
@@ -104,7 +148,6 @@ int comm_delete(MPI_Comm, int, void *val, void *) {
 int self_delete(MPI_Comm, int, void *, void *) {
   for (auto *e : g_entries) release(e);
   g_entries.clear();
-  unpin_all();
   return MPI_SUCCESS;
 }
 
@@ -263,15 +306,6 @@ int follow(Entry *e, hipStream_t dst, hipStream_t src) {
   return MPI_SUCCESS;
 }
 
-// device->host copies of the pipelined path: "dma" (hipMemcpyAsync, the
-// copy engines) or "kernel" (k_copy storing straight into the page-locked,
-// device-mapped host buffer, so host->device DMA and device->host stores run
-// on different engines); BINE_STAGE_D2H, default dma
-bool d2h_kernel() {
-  static const bool v = getenv("BINE_STAGE_D2H") && !strcmp(getenv("BINE_STAGE_D2H"), "kernel");
-  return v;
-}
-
 // staging chunk of the pipelined path (BINE_STAGE_CHUNK_BYTES, default 16 MiB)
 size_t stage_chunk_bytes() {
   static const size_t v = [] {
@@ -282,16 +316,35 @@ size_t stage_chunk_bytes() {
   return v;
 }
 
+// the end of a call: every stream that touched the caller's buffers (or the
+// communicator's) drained within the bound, then the communicator's own
+int finish(Entry *e, CallPins &pins, std::initializer_list<std::pair<hipStream_t, const char *>> streams) {
+  for (const auto &x : streams)
+    if (int rc = drain(x.first, x.second, e->rank)) {
+      pins.drained = false;
+      return rc;
+    }
+  const hipStream_t cs = (hipStream_t)bine_comm_stream(e->comm);
+  if (int rc = drain(cs, "communicator", e->rank)) {
+    pins.drained = false;
+    return rc;
+  }
+  return to_mpi(bine_comm_synchronize(e->comm));
+}
+
 // Run `body(dev_sbuf, dev_rbuf, first_elem, elems, stream)` with host buffers
 // staged through the device.  Host->device copies run on the h2d stream,
 // device->host copies on the d2h stream, the collective on the communicator's
 // stream, chained by events.  `esz` > 0 declares the collective separable by
-// element (element i of the result depends only on element i of the inputs,
-// through a reduction whose result bits do not depend on how the buffer is
-// cut -- see do_allreduce): then the buffer is cut into chunks and chunk k's
-// host->device copy, collective and device->host copy are pipelined, so the
-// two PCIe directions and the device work overlap.  Otherwise one collective
-// over the whole buffer, between the two staged copies.
+// element (element i of the result depends only on element i of the inputs --
+// P = 1, where every algorithm is the copy, see do_allreduce): then the buffer
+// is cut into chunks and chunk k's host->device copy, collective and
+// device->host copy are pipelined, so the two PCIe directions and the device
+// work overlap.  Otherwise one collective over the whole buffer, between the
+// two staged copies.  Every rank calls `body` the same number of times with
+// the same counts whatever its buffers are (device buffers: the same chunks,
+// uncopied), so ranks with host and with device buffers meet in one
+// schedule.
 template <typename F>
 int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t rbytes, bool read_rbuf, size_t esz,
                  size_t count, F body) {
@@ -303,84 +356,82 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
   bool stage_s = !in_place && sbuf && sbytes && !on_device(sbuf);
   bool stage_r = rbuf && rbytes && !on_device(rbuf);
   int rc;
-  if (!stage_s && !stage_r) {  // device buffers: the collective as it is (the CUDA_AWARE-style path)
-    int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st);
-    if (bst != BINE_SUCCESS) return to_mpi(bst);
-    if (hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
-    return to_mpi(bine_comm_synchronize(e->comm));
-  }
   if ((rc = copy_streams(e))) return rc;
+  CallPins pins;
   if (stage_s) {
     void *d;
     if ((rc = stage(e, 0, sbytes, &d))) return rc;
     ds = d;
-    pin_host(sbuf, sbytes);
+    pins.add(sbuf, sbytes);
   }
-  void *rbuf_dev = nullptr;  // rbuf as the device addresses it (page-locked and mapped), for d2h_kernel()
   if (stage_r) {
     void *d;
     if ((rc = stage(e, 1, rbytes, &d))) return rc;
     dr = d;
-    if (pin_host(rbuf, rbytes) && d2h_kernel() && hipHostGetDevicePointer(&rbuf_dev, rbuf, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      rbuf_dev = nullptr;
-    }
+    pins.add(rbuf, rbytes);
   }
+  pins.commit();
   const bool fill_r = stage_r && (in_place || read_rbuf);  // (every earlier call has drained all three streams)
   const size_t ch = esz ? stage_chunk_bytes() / esz * esz : 0;
   const size_t total = count * esz;
-  if (ch && total >= 2 * ch && (!stage_s || sbytes == total) && (!stage_r || rbytes == total)) {
-    for (size_t off = 0; off < total; off += ch) {
-      const size_t len = std::min(ch, total - off);
-      if (stage_s && hipMemcpyAsync((char *)ds + off, (const char *)sbuf + off, len, hipMemcpyHostToDevice,
-                                    e->h2d) != hipSuccess)
-        return MPI_ERR_OTHER;
-      if (fill_r && hipMemcpyAsync((char *)dr + off, (char *)rbuf + off, len, hipMemcpyHostToDevice, e->h2d) !=
-                        hipSuccess)
-        return MPI_ERR_OTHER;
-      if ((rc = follow(e, st, e->h2d))) return rc;
-      const void *cs = in_place ? BINE_IN_PLACE : (const void *)((const char *)ds + off);
-      int bst = body(cs, (char *)dr + off, off / esz, len / esz, (void *)st);
-      if (bst != BINE_SUCCESS) return to_mpi(bst);
-      if (stage_r) {
-        if ((rc = follow(e, e->d2h, st))) return rc;
-        if (rbuf_dev) {
-          if (bine_copy((char *)rbuf_dev + off, (char *)dr + off, len, (void *)e->d2h) != BINE_SUCCESS)
-            return MPI_ERR_OTHER;
-        } else if (hipMemcpyAsync((char *)rbuf + off, (char *)dr + off, len, hipMemcpyDeviceToHost, e->d2h) !=
-                   hipSuccess) {
+  auto issue = [&]() -> int {
+    if (ch && total >= 2 * ch && (stage_s || stage_r) && (!stage_s || sbytes == total) &&
+        (!stage_r || rbytes == total)) {
+      for (size_t off = 0; off < total; off += ch) {
+        const size_t len = std::min(ch, total - off);
+        if (stage_s && hipMemcpyAsync((char *)ds + off, (const char *)sbuf + off, len, hipMemcpyHostToDevice,
+                                      e->h2d) != hipSuccess)
           return MPI_ERR_OTHER;
+        if (fill_r && hipMemcpyAsync((char *)dr + off, (char *)rbuf + off, len, hipMemcpyHostToDevice, e->h2d) !=
+                          hipSuccess)
+          return MPI_ERR_OTHER;
+        if (int r2 = follow(e, st, e->h2d)) return r2;
+        const void *cs = in_place ? BINE_IN_PLACE : (const void *)((const char *)ds + off);
+        if (int bst = body(cs, (char *)dr + off, off / esz, len / esz, (void *)st)) return to_mpi(bst);
+        if (stage_r) {
+          if (int r2 = follow(e, e->d2h, st)) return r2;
+          if (hipMemcpyAsync((char *)rbuf + off, (char *)dr + off, len, hipMemcpyDeviceToHost, e->d2h) != hipSuccess)
+            return MPI_ERR_OTHER;
         }
       }
+      return MPI_SUCCESS;
     }
-  } else {
     if (stage_s && hipMemcpyAsync((void *)ds, sbuf, sbytes, hipMemcpyHostToDevice, e->h2d) != hipSuccess)
       return MPI_ERR_OTHER;
     if (fill_r && hipMemcpyAsync(dr, rbuf, rbytes, hipMemcpyHostToDevice, e->h2d) != hipSuccess)
       return MPI_ERR_OTHER;
-    if ((rc = follow(e, st, e->h2d))) return rc;
-    int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st);
-    if (bst != BINE_SUCCESS) return to_mpi(bst);
+    if (int r2 = follow(e, st, e->h2d)) return r2;
+    if (int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st)) return to_mpi(bst);
     if (stage_r) {
-      if ((rc = follow(e, e->d2h, st))) return rc;
+      if (int r2 = follow(e, e->d2h, st)) return r2;
       if (hipMemcpyAsync(rbuf, dr, rbytes, hipMemcpyDeviceToHost, e->d2h) != hipSuccess) return MPI_ERR_OTHER;
     }
-  }
-  if (hipStreamSynchronize(e->d2h) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
-  return to_mpi(bine_comm_synchronize(e->comm));
+    return MPI_SUCCESS;
+  };
+  rc = issue();
+  // drain whatever was issued (also after an error: the registrations must
+  // outlive every copy that uses them)
+  const int rc2 = finish(e, pins, {{e->h2d, "host-to-device"}, {e->d2h, "device-to-host"}, {st, "collective"}});
+  return rc ? rc : rc2;
 }
 
 // The staging pipelined into the collective itself (bine_*_staged): for
-// collectives whose result bits follow the whole count's block ownership
-// (floating point at P > 1), so they cannot be cut into independent calls.
-// The core copies each input piece in just before the first operation that
-// touches it and each output piece back right after its last writer, with the
-// flat forms on (bit-identical) so the output completes chunk by chunk.  Used
-// when both buffers are on the host and the input spans at least two staging
-// chunks; BINE_STAGE_PIPELINE=0 keeps the serial H2D -> collective -> D2H.
+// collectives whose result bits follow the whole count's block ownership, so
+// they cannot be cut into independent calls.  The core copies each input piece
+// in just before the first operation that touches it and each output piece
+// back right after its last writer, with the flat forms on (bit-identical) so
+// the output completes chunk by chunk.  Chosen from (P, bytes) only -- the
+// same on every rank -- and run whatever the buffers are: a device buffer is
+// passed as is (NULL host pointer, nothing copied), so every rank issues the
+// same schedule.  BINE_STAGE_PIPELINE=0 keeps the serial H2D -> collective ->
+// D2H.
 bool staged_pipeline_on() {
   static const bool v = !getenv("BINE_STAGE_PIPELINE") || atoi(getenv("BINE_STAGE_PIPELINE")) != 0;
   return v;
+}
+
+bool use_staged(const Entry *e, size_t bytes) {
+  return e->size > 1 && staged_pipeline_on() && bytes >= 2 * stage_chunk_bytes();
 }
 
 template <typename G>
@@ -390,24 +441,22 @@ int with_staged(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t rb
   const bool in_place = sbuf == MPI_IN_PLACE;
   int rc;
   if ((rc = copy_streams(e))) return rc;
-  void *ds = nullptr, *dr = nullptr;
-  if (!in_place) {
+  const bool host_s = !in_place && sbuf && !on_device(sbuf), host_r = rbuf && !on_device(rbuf);
+  void *ds = in_place ? nullptr : (void *)sbuf, *dr = rbuf;
+  CallPins pins;
+  if (host_s) {
     if ((rc = stage(e, 0, sbytes, &ds))) return rc;
-    pin_host(sbuf, sbytes);
+    pins.add(sbuf, sbytes);
   }
-  if ((rc = stage(e, 1, rbytes, &dr))) return rc;
-  pin_host(rbuf, rbytes);
-  const int bst = body(in_place ? BINE_IN_PLACE : sbuf, rbuf, ds, dr, (void *)e->h2d, (void *)e->d2h, (void *)st);
-  if (bst != BINE_SUCCESS) return to_mpi(bst);
-  if (hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
-  return to_mpi(bine_comm_synchronize(e->comm));
-}
-
-// both buffers on the host and large enough for the pipeline to pay
-bool use_staged(const void *sbuf, size_t sbytes, const void *rbuf, size_t rbytes) {
-  if (!staged_pipeline_on() || !rbuf || !rbytes || on_device(rbuf)) return false;
-  if (sbuf != MPI_IN_PLACE && (!sbuf || on_device(sbuf))) return false;
-  return std::max(sbytes, rbytes) >= 2 * stage_chunk_bytes();
+  if (host_r) {
+    if ((rc = stage(e, 1, rbytes, &dr))) return rc;
+    pins.add(rbuf, rbytes);
+  }
+  pins.commit();
+  const void *hs = in_place ? BINE_IN_PLACE : host_s ? sbuf : nullptr;
+  const int bst = body(hs, host_r ? rbuf : nullptr, ds, dr, (void *)e->h2d, (void *)e->d2h, (void *)st);
+  const int rc2 = finish(e, pins, {{e->h2d, "host-to-device"}, {e->d2h, "device-to-host"}, {st, "collective"}});
+  return bst != BINE_SUCCESS ? to_mpi(bst) : rc2;
 }
 
 int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datatype dtype, MPI_Op op,
@@ -422,22 +471,21 @@ int do_allreduce(int algo, const void *sbuf, void *rbuf, size_t count, MPI_Datat
   const size_t esz = bine_dtype_size(dt);
   const size_t bytes = count * esz;
   const size_t seg = bine_allreduce_segsize;
-  // separable by element, so the staged path may pipeline it chunk by chunk:
-  // at P = 1 every algorithm is the copy sbuf -> rbuf (libbine_allreduce.c:
-  // 849-852); on the plain integer types every MPI_Op is associative and
-  // commutative in the element type, so the result bits do not depend on the
-  // reduction tree, i.e. on how the buffer is cut.  Floating-point results
-  // depend on the tree (block ownership follows the count): one collective.
-  const bool integer = dt <= BINE_UINT64;
-  const bool separable = e->size == 1 || integer;
-  if (!separable && use_staged(sbuf, bytes, rbuf, bytes))
+  // Every choice below depends on (P, count, type) only -- never on where a
+  // rank's buffers live -- so all ranks issue the same collectives (ADVICE
+  // r3).  P = 1: every algorithm is the copy sbuf -> rbuf
+  // (libbine_allreduce.c:849-852), separable by element, so the staged path
+  // pipelines it as independent chunks.  P > 1: the result bits follow the
+  // whole count's block ownership (floating point) -- one collective, with the
+  // staging pipelined into it when the buffer is large enough.
+  if (use_staged(e, bytes))
     return with_staged(e, sbuf, bytes, rbuf, bytes,
                        [&](const void *hs, void *hr, void *ds, void *dr, void *h2d, void *d2h, void *st) {
                          return bine_allreduce_staged(e->comm, algo, hs, hr, ds, dr, count, dt, o,
                                                       algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? seg : 0,
                                                       stage_chunk_bytes(), h2d, d2h, st);
                        });
-  return with_buffers(e, sbuf, bytes, rbuf, bytes, false, separable ? esz : 0, count,
+  return with_buffers(e, sbuf, bytes, rbuf, bytes, false, e->size == 1 ? esz : 0, count,
                       [&](const void *s, void *r, size_t, size_t n, void *st) {
                         return bine_allreduce(e->comm, algo, s, r, n, dt, o,
                                               algo == BINE_AR_BINE_BDW_REMAP_SEGMENTED ? seg : 0, st);
@@ -458,7 +506,7 @@ int do_reduce_scatter(int algo, const void *sbuf, void *rbuf, const int rcounts[
   const bool in_place = sbuf == MPI_IN_PLACE;
   // MPI_IN_PLACE: the input is the whole rbuf
   const size_t rbytes = (in_place ? total : (size_t)rcounts[e->rank]) * esz;
-  if (e->size > 1 && use_staged(sbuf, total * esz, rbuf, rbytes))
+  if (use_staged(e, total * esz))  // (P, counts, type): the same on every rank
     return with_staged(e, sbuf, total * esz, rbuf, rbytes,
                        [&](const void *hs, void *hr, void *ds, void *dr, void *h2d, void *d2h, void *st) {
                          return bine_reduce_scatter_staged(e->comm, algo, hs, hr, ds, dr, rcounts, dt, o,

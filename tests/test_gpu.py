@@ -730,6 +730,28 @@ def test_mpi_typed_entry_points_match_mpich(dev, np_, flat):
     assert p.returncode == 0 and "OPCHECK ok" in p.stdout, (p.stdout[-1500:], p.stderr[-1500:])
 
 
+CHURN = os.path.join(ROOT, "integration", "_build", "buffer_churn")
+
+
+@pytest.mark.skipif(not os.path.exists(CHURN), reason="integration/buffer_churn not built (integration/Makefile)")
+@pytest.mark.parametrize("np_", [1, 2])
+def test_libbine_host_buffers_freed_and_reallocated(dev, np_):
+    """integration/buffer_churn: libbine.so's
+    allreduce_bine_bdw_remap on 64 MiB malloc buffers, the buffers freed and
+    malloc'd again at the same addresses, new data, a second call -- both vs
+    PMPI_Allreduce, in and out of place, float and int64, and no caller buffer
+    left page-locked after a call; at P = 2 also rank 0's buffers on the
+    device and rank 1's on the host in one call (allreduce and
+    reduce_scatter, below and above the staging pipeline's threshold)"""
+    import subprocess
+    env = dict(os.environ, BINE_FAKE_HOSTS="1", BINE_SYNC_TIMEOUT_S="60")
+    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_), "buffer_churn"],
+                       env=env, capture_output=True, text=True, timeout=150)
+    print(p.stdout[-3000:])
+    assert p.returncode == 0 and "CHURN ok" in p.stdout, (p.stdout[-2000:], p.stderr[-1500:])
+    assert "same addresses: yes" in p.stdout  # glibc mmap reuse: the hazard's shape was exercised
+
+
 @pytest.mark.parametrize("relay", [0, 64, "flat"], ids=["direct", "relay", "flat"])
 @pytest.mark.parametrize("P", [2, 4, 6, 8])
 def test_allgather_family_matches_oracle(dev, P, relay):

@@ -85,12 +85,14 @@ def test_staged_host_buffers_4_ranks():
     (bine_allreduce_staged / bine_reduce_scatter_staged): 4 processes, RCCL and
     the direct transport, 13 cases (allreduce / reduce_scatter algorithms x
     dtypes x in place x chunk) bit-exact vs the oracle with the device input
-    NaN-poisoned, plus C3's 256 MiB per rank vs the committed digest
-    (tools/staged_check.py)"""
-    # one HW queue per process: the 4 ranks' kernels then run side by side on
-    # the shared device instead of time-sliced behind the test process's own
-    # queues (profiles/r3_multiproc_hw_queues.txt); no graph replay here
-    env = dict(os.environ, PYTHONPATH=ROOT, GPU_MAX_HW_QUEUES="1")
+    NaN-poisoned, again with rank 0's buffers on the device and the others'
+    staged (one schedule for both), plus C3's 256 MiB per rank vs the
+    committed digest (tools/staged_check.py)"""
+    # default HW queues (round 3 ran this with one queue per process after a
+    # 180 s silence in the suite; every host wait of the staged path is now
+    # bounded -- bine_comm_synchronize, libbine.so's drains -- and each case
+    # prints a start line, so a stall names its case and stream)
+    env = dict(os.environ, PYTHONPATH=ROOT, BINE_SYNC_TIMEOUT_S="60")
     r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "staged_check.py"), "4", "1"], env=env,
                  timeout=170)
     tail = "\n".join(r.stdout.splitlines()[-16:])

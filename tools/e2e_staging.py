@@ -6,7 +6,7 @@ bine_bdw_remap_over, 256 MiB per rank, host (malloc) buffers -- per
 configuration the median of pico_core's own per-iteration times (its CSV,
 max over ranks, first 20 % dropped), every iteration checked by pico_core
 against PMPI_Allreduce.  Configurations: the staging pipeline's chunk
-(BINE_STAGE_CHUNK_BYTES) and page-locking on / off (BINE_HOST_REGISTER).
+(BINE_STAGE_CHUNK_BYTES) and per-call page-locking on / off (BINE_HOST_REGISTER).
 Configuration set "pipeline" (5th argument; floating point at P > 1): the
 serial path (BINE_STAGE_PIPELINE=0: H2D, then the collective, then D2H)
 against the staging pipelined into the collective (bine_allreduce_staged)
@@ -47,15 +47,14 @@ if __name__ == "__main__":
     esz = {"float": 4, "double": 8, "int64": 8, "int32": 4}[dtype]
     S = count * esz
     out = {"np": np_, "dtype": dtype, "count": count, "bytes_per_rank": S}
-    cfgs = [("pageable, one collective (round-2 path)", {"BINE_HOST_REGISTER": "0", "BINE_STAGE_CHUNK_BYTES": str(1 << 40)}),
-            ("page-locked, one collective", {"BINE_STAGE_CHUNK_BYTES": str(1 << 40)}),
-            ("page-locked, 4 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(4 << 20)}),
-            ("page-locked, 8 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(8 << 20)}),
-            ("page-locked, 16 MiB chunks (default)", {}),
-            ("page-locked, 32 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(32 << 20)}),
-            ("page-locked, 16 MiB chunks, device->host by kernel stores", {"BINE_STAGE_D2H": "kernel"}),
-            ("page-locked, 8 MiB chunks, device->host by kernel stores",
-             {"BINE_STAGE_D2H": "kernel", "BINE_STAGE_CHUNK_BYTES": str(8 << 20)})]
+    # host buffers page-locked per call (registered at the start of each call,
+    # unregistered before it returns; round 4) or pageable (HIP's own staging)
+    cfgs = [("pageable, one collective", {"BINE_HOST_REGISTER": "0", "BINE_STAGE_CHUNK_BYTES": str(1 << 40)}),
+            ("page-locked per call, one collective", {"BINE_STAGE_CHUNK_BYTES": str(1 << 40)}),
+            ("pageable, 16 MiB chunks", {"BINE_HOST_REGISTER": "0"}),
+            ("page-locked per call, 8 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(8 << 20)}),
+            ("page-locked per call, 16 MiB chunks (default)", {}),
+            ("page-locked per call, 32 MiB chunks", {"BINE_STAGE_CHUNK_BYTES": str(32 << 20)})]
     if len(sys.argv) > 5 and sys.argv[5] == "pipeline":
         cfgs = [("serial: H2D, collective, D2H (BINE_STAGE_PIPELINE=0)", {"BINE_STAGE_PIPELINE": "0"}),
                 ("pipelined into the collective, 16 MiB rounds (default)", {}),

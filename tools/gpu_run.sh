@@ -4,8 +4,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
 bash tools/gpu_steps.sh \
- "smoke:120:python -u -c 'import __graft_entry__ as g; g.smoke()'" \
- "ab2:200:python -u tools/dm_tree_ab.py 2 16,64 10" \
- "ab4:200:python -u tools/dm_tree_ab.py 4 16,64 10" \
- "ab8q1:300:GPU_MAX_HW_QUEUES=1 python -u tools/dm_tree_ab.py 8 16,64 10"
+ "churn:200:$T tests/test_gpu.py -k 'freed_and_reallocated or match_mpich or pico_core_dropin or pico_core_c1'" \
+ "staged:230:$T tests/test_gpu_rccl.py -k staged" \
+ "e2e1:300:python -u tools/e2e_staging.py 1 float 67108864 20" \
+ "rsg_q1:150:GPU_MAX_HW_QUEUES=1 BINE_SEGV_TRACE=1 BINE_SEGV_TRACE_DIR=\$PWD/gpurun_out python -u tools/rs_graph_probe.py 4 flatrs+flat+dm16 64 1"

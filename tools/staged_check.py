@@ -2,7 +2,8 @@
 """Host-buffer collectives with the staging pipelined into the collective
 (bine_allreduce_staged / bine_reduce_scatter_staged) in P real processes
 sharing the box's one GPU (distinct NCCL_HOSTIDs), over RCCL and over the
-direct peer-memory transport.  Host buffers are page-locked (as libbine.so
+direct peer-memory transport, and ("mixed") with rank 0's buffers already on
+the device (NULL host pointers) while the others' are staged.  Host buffers are page-locked (as libbine.so
 registers pico_core's); the device input is NaN-poisoned before every call,
 so a piece the pipeline failed to copy in shows.  Every rank's host output
 is compared bit for bit with the oracle (small cases: element by element;
@@ -63,12 +64,17 @@ def worker(rank, P, port, want, big, q):
     st, h2d, d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     tdt = {"float": torch.float32, "double": torch.float64, "int64": torch.int64}
     bad = []
-    for transport in ("rccl", "direct"):
+    for transport in ("rccl", "direct", "mixed"):
         if transport == "direct":
             comm.set_direct(True)
         for (coll, algo, dt, n, op, chunk, in_place), w in zip(CASES, want):
             if w is None:
                 continue
+            # mixed: rank 0's buffers already on the device (NULL host
+            # pointers: nothing copied for it), the others' on the host -- the
+            # same schedule on every rank
+            on_dev = transport == "mixed" and rank == 0
+            print(f"rank {rank} {transport} {coll} {algo} {dt} n={n} ... start", flush=True)
             total = n if coll == "allreduce" else n * P
             inp = O.inputs(dt, total, P)[rank]
             hs = torch.from_numpy(inp.copy()).pin_memory()
@@ -83,23 +89,28 @@ def worker(rank, P, port, want, big, q):
             poison = float("nan") if dt != "int64" else -1
             ds.fill_(poison)
             dr.fill_(poison)
+            if on_dev:  # the input where the collective reads it: ds, or dr in place
+                (dr[:outn] if in_place else ds).copy_(hs[:outn] if in_place else hs)
             torch.cuda.synchronize()
-            hsrc = pico_amd.IN_PLACE if in_place else hs
+            hsrc = pico_amd.IN_PLACE if in_place else (None if on_dev else hs)
+            hdst = None if on_dev else hr
             if coll == "allreduce":
-                pico_amd.allreduce_staged(algo, hsrc, hr, ds, dr, n, dt, op, comm, h2d, d2h, chunk_bytes=chunk,
+                pico_amd.allreduce_staged(algo, hsrc, hdst, ds, dr, n, dt, op, comm, h2d, d2h, chunk_bytes=chunk,
                                           stream=st)
             else:
-                pico_amd.reduce_scatter_staged(algo, hsrc, hr, ds, dr, [n] * P, dt, op, comm, h2d, d2h,
+                pico_amd.reduce_scatter_staged(algo, hsrc, hdst, ds, dr, [n] * P, dt, op, comm, h2d, d2h,
                                                chunk_bytes=chunk, stream=st)
             st.synchronize()
             comm.synchronize()
+            if on_dev:
+                hr.copy_(dr)
             got = hr.numpy()[:n] if coll == "reduce_scatter" else hr.numpy()
             ok = np.array_equal(got, w[rank])
             if not ok:
                 bad.append(f"{transport} {coll} {algo} {dt} n={n} chunk={chunk} in_place={in_place}")
             print(f"rank {rank} {transport} {coll} {algo} {dt} n={n} chunk={chunk >> 10}KiB in_place={in_place}: "
                   f"{'ok' if ok else 'MISMATCH'}", flush=True)
-        if big:  # C3's shape through the staged path, vs the committed oracle digest
+        if big and transport != "mixed":  # C3's shape through the staged path, vs the committed oracle digest
             with open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")) as f:
                 gold = json.load(f)["digests"]
             key = f"C3/allreduce/bine_bdw_remap/float/N{C3_N}/P{P}"
