@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import platform
 import statistics
@@ -654,14 +655,13 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
         except pico_amd.BineError as e:   # symmetric: setup is agreed over RCCL
             out["C1_direct_fused"] = {"error": str(e)}
     del sb, rb
-    # C4 / C5 are bandwidth-bound (1 GiB / 256 MiB per rank): issued eagerly on
-    # the chosen transport and chunk, whatever graph replay did for C3 -- a
-    # replay saves host issue time only, and a fault in a replay of a shape
-    # no test replays must not cost the headline line (one-GPU rehearsal with
-    # GPU_MAX_HW_QUEUES=1: hipGraphLaunch of the captured C4 reduce_scatter
-    # segfaulted inside HIP 7.0; eager, and with the default queues, it runs
-    # bit-exactly -- profiles/r3_rs_graph_probe.txt)
-    apply_transport(comm, mode, chunk, False)
+    # C4 / C5 on the chosen transport, chunk and graph setting.  (Round 3 issued
+    # them eagerly after a replay of the C4 reduce_scatter segfaulted inside
+    # torch's HIP 7.0 under GPU_MAX_HW_QUEUES=1; the cause is that runtime's
+    # Graph::UpdateStreams on graphs with parallel branches, and the library
+    # now captures two-stream schedules only on HIP >= 7.2 --
+    # profiles/r4_graph_fork_repro.txt.)
+    apply_transport(comm, mode, chunk, graphs)
     trees = mode == "trees"
     # C4: reduce_scatter_bine_permute_remap fp32, 1 GiB input per rank
     n = C4_ELEMS
@@ -675,9 +675,11 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
     ok, _ = check_digest(pico_amd, rb, n // world, "float",
                          gkey("C4", "reduce_scatter", "bine_permute_remap", "float", n, world, trees), rank)
     S = n * 4
+    nm = node_model("C4", world, mode, chunk)
     out["C4_reduce_scatter_bine_permute_remap_f32_1GiB"] = {
         "ms": round(st["median_ms"], 4), "busbw_per_rank_GBs": round((world - 1) / world * S / (st["median_ms"] * 1e-3) / 1e9, 2),
-        "graph_replay": False, "parity_ok": all_ok(torch, dist, ok)}
+        "graph_replay": graphs, "parity_ok": all_ok(torch, dist, ok), "model_ms": nm.get("model_ms"),
+        "frac_of_model": round(nm["model_ms"] / st["median_ms"], 4) if nm.get("model_ms") else None}
     del sb, rb
     # C5: allreduce_bine_bdw_remap fp64 / int64 SUM, 256 MiB per rank
     n = C5_ELEMS
@@ -691,10 +693,12 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
         ok, _ = check_digest(pico_amd, rb, n, dt, gkey("C5", "allreduce", "bine_bdw_remap", dt, n, world, trees), rank)
         S = n * 8
         ms = st["median_ms"]
+        nm = node_model("C5", world, mode, chunk)
         out[f"C5_allreduce_bine_bdw_remap_{dt}_256MiB"] = {
             "ms": round(ms, 4), "algbw_per_rank_GBs": round(S / (ms * 1e-3) / 1e9, 2),
             "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2),
-            "graph_replay": False, "parity_ok": all_ok(torch, dist, ok)}
+            "graph_replay": graphs, "parity_ok": all_ok(torch, dist, ok), "model_ms": nm.get("model_ms"),
+            "frac_of_model": round(nm["model_ms"] / ms, 4) if nm.get("model_ms") else None}
         del sb, rb
     torch.cuda.empty_cache()
     return out
@@ -755,6 +759,23 @@ MODES = {"off": ["direct"],
          # launches (bine_comm_set_direct_tree: no pull copies of the leaves)
          "auto": ["direct", "flat", "relay", "relay+flat", "flatrs+flat", "flatrs+flat+ag", "trees",
                   "direct+dm", "flatrs+flat+dm", "flatrs+flat+dmt", "relay+flat+dm"]}
+
+
+def node_model(cfg, world, mode, chunk):
+    """pico_amd.model's expected time of BASELINE config `cfg` on this node for
+    transport `mode` (its workgroup suffixes dropped) at pipelining chunk
+    `chunk`: max(link time, HBM time) + launches x boundary; with
+    BINE_FAKE_HOSTS (several ranks on one GPU) the one-GPU form (every rank's
+    bytes through one HBM, no link)"""
+    try:
+        from pico_amd import model as NM
+        t = re.sub(r"(\+dmt?)\d*(x\d+)?", r"\1", mode)
+        m = NM.config_model(cfg, world, t, chunk, one_gpu=os.environ.get("BINE_FAKE_HOSTS") == "1")
+        m.update(link_GBs=NM.LINK_GBS, hbm_rate_GBs=NM.HBM_RATE_GBS, boundary_us=NM.T_BOUNDARY_US,
+                 one_gpu=os.environ.get("BINE_FAKE_HOSTS") == "1")
+        return m
+    except Exception as e:  # the model is a report, never a reason to lose the line
+        return {"error": str(e)}
 
 
 def transport_modes(relay: str, world: int):
@@ -1095,6 +1116,7 @@ def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, 
     # schedule, up to 7 x 153 when every step loads all links)
     link_peak = round(XGMI_LINK_GBS * egress / L, 2) if L else XGMI_LINK_GBS
     achieved = egress / (ms * 1e-3) / 1e9   # the headline statistic (median), as value and ms_per_step
+    nm = node_model("C3", world, chosen, chunk) if nelem == C3_ELEMS and algo == "bine_bdw_remap" else {}
     out = {
         "metric": METRIC, "value": round(algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -1136,6 +1158,11 @@ def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, 
                      "traffic": None,
                      "egress_bytes": egress,
                      "link_time_bytes": L,
+                     # what the node model (pico_amd/model.py) expects for this
+                     # transport and chunk; frac_of_model = model / measured
+                     "model_ms": nm.get("model_ms"),
+                     "frac_of_model": round(nm["model_ms"] / ms, 4) if nm.get("model_ms") else None,
+                     "model": nm,
                      "note": "achieved = this rank's xGMI egress bytes (executed schedule) / ms_per_step "
                              "(the median that also gives value); peak = 153 GB/s per link x egress / link_time_bytes (sum over exchange ops "
                              "of the busiest link's bytes): 153 for the literal one-peer-per-step schedule, up "

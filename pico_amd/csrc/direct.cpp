@@ -170,6 +170,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (const char *e = getenv("BINE_DIRECT_MCAST")) mcast = atoi(e) != 0;
   tree_wgs_env = tree_wgs;
   if (slot < (1 << 20)) slot = 1 << 20;
+  if (slot > ((size_t)1 << 30)) slot = (size_t)1 << 30;  // write-through stores address a slot by 32-bit offsets
   slot = slot / 4096 * 4096;
   if (wgs < 1) wgs = 1;
   env_wgs = wgs;

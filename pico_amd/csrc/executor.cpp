@@ -1014,6 +1014,14 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     int rc = stream_join(c, C, K);
     if (rc) return rc;
   }
+  // fused trees: the comm stream follows K again only when K has work of its
+  // own since it last did (k_dirty), and K takes up a tree's place lazily --
+  // it waits for the newest hosting launch (k_pending) just before its next
+  // own op.  With every tree hosted on the comm stream K stays idle, and its
+  // joins -- a barrier packet on each stream per chunk -- would only add gaps
+  // between the exchange launches
+  bool k_dirty = !(joined || ((sc.c_join || ordered) && !single));
+  hipEvent_t k_pending = nullptr;
   std::vector<hipEvent_t> &evs = c->op_ev;
   evs.resize(sc.ops.size());
   const bool prof = c->profile;
@@ -1045,7 +1053,10 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     if (dm_trees && tp.host[i] == (int)i) {
       // a tree hosted by itself: its own launch on the comm stream pulls the
       // leaves in place (after the exchange that was issued without them)
-      if (int rj = stream_join(c, C, K)) return rj;
+      if (k_dirty) {
+        if (int rj = stream_join(c, C, K)) return rj;
+        k_dirty = false;
+      }
       static const std::vector<XSend> no_s;
       static const std::vector<XRecv> no_r;
       if (int rc = c->tx->exchange_tree(no_s, no_r, nullptr, &tp.leaves[i], &tp.spec[i], C)) return rc;
@@ -1057,13 +1068,18 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       // order (later local ops follow it as they followed the tree) -- now,
       // or right after the host is issued when that comes next
       if (tev[i]) {
-        HIP_TRY(hipStreamWaitEvent(K, tev[i], 0));
+        k_pending = tev[i];
         if (sc.signals[i]) evs[i] = tev[i];
       } else {
         tpend[i] = 1;
       }
       continue;
     }
+    if (!o.xchg && k_pending) {  // K's next own op: after every tree hosted so far
+      HIP_TRY(hipStreamWaitEvent(K, k_pending, 0));
+      k_pending = nullptr;
+    }
+    if (!o.xchg) k_dirty = true;
     if (trace_on())
       fprintf(stderr, "bine[%d] op %zu/%zu %s wait %lld prims %zu\n", c->rank, i, sc.ops.size(),
               o.xchg ? "xchg" : "local", (long long)o.wait, o.prims.size());
@@ -1116,8 +1132,12 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       if (dm_trees && tp.defer[i]) recvs.clear();  // pulled by the next exchange, for its tree
       if (hj >= 0) {
         // the tree reads the own leaf and writes its output where K's earlier
-        // ops may still be writing / reading: C follows K first
-        if (int rj = stream_join(c, C, K)) return rj;
+        // ops may still be writing / reading: C follows K first (if K has
+        // had any since C last did)
+        if (k_dirty) {
+          if (int rj = stream_join(c, C, K)) return rj;
+          k_dirty = false;
+        }
         const bool own = tp.tree_at[(size_t)hj] == (int)i;
         rc = own ? c->tx->exchange_tree(sends, recvs, &tp.spec[(size_t)hj], nullptr, nullptr, C)
                  : c->tx->exchange_tree(sends, recvs, nullptr, &tp.leaves[(size_t)hj], &tp.spec[(size_t)hj], C);
@@ -1126,7 +1146,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
         HIP_TRY(hipEventRecord(e, C));
         tev[(size_t)hj] = e;
         if (tpend[(size_t)hj]) {  // the tree's place in K's order came first
-          HIP_TRY(hipStreamWaitEvent(K, e, 0));
+          k_pending = e;
           if (sc.signals[(size_t)hj]) evs[(size_t)hj] = e;
         }
       } else {
@@ -1156,6 +1176,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   if (stg && stg->out_host) {  // the caller's stream ends after the last copy back
     if (int rc = stream_join(c, K, stg->d2h)) return rc;
   }
+  if (k_pending && !ordered) HIP_TRY(hipStreamWaitEvent(K, k_pending, 0));  // (ordered: the join below covers it)
   if (sc.final_wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
   if (ordered) return stream_join(c, K, C);
   return BINE_SUCCESS;

@@ -595,6 +595,26 @@ int BINE_FN(launch_reduce_batch)(int n, const void *const *a, const void *const 
   return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
+// system-coherent 16-B accesses of the direct transport (protocol notes at
+// k_dm_move below); here because the tree body uses them too
+// A 16-B store written through to memory (system coherent: sc0 sc1, and
+// non-temporal) -- the stores into a peer's inbox slot.  Through a buffer
+// resource (the compiler schedules it and tracks its counters; raw stride-0
+// addressing, 2 GiB range, gfx9 untyped dword3 0x00020000) with the cache
+// policy sc0 | sc1 | nt = 1 | 16 | 2; `base` is wave-uniform.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(void *base) {
+  // the base is the same in every lane; readfirstlane says so to the compiler
+  // (otherwise it wraps each store in a waterfall loop)
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  const uint64_t u = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32 |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)u, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, uint64_t vec, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(vec * 16), 0, 19);
+}
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ----------------------------------------------------------------------------
 // tree reduction: the owner's side of the flat reduce-scatter phase.  One
 // launch evaluates the reference's whole reduction tree of a block from its P
@@ -818,16 +838,53 @@ int BINE_FN(launch_reduce_tree)(int nl, const void *const *leaf, void *out, size
 // else follows from (seq, peer): the slot in the receiver's inbox, the flag to
 // wait on -- push: the receiver's ack of the slot's previous use (seq -
 // kSlots); pull: the sender's ready mark for seq -- and the flag to publish.
-// Thread 0 of each workgroup polls the wait flag (system-scope acquire) with a
-// time limit; the workgroup copies its grid-strided share; every workgroup
-// releases its stores and counts itself in; the last one of the message
-// resets the counter for the slot's next use and publishes seq in the peer's
-// inbox (system-scope release).  A wait that times out marks the transport
-// poisoned; every later launch then exits at once, so no wait outlives the
-// time limit.  No host-side state: launches can be captured and replayed.
+// Thread 0 of each workgroup polls the wait flag with a time limit; the
+// workgroup copies its grid-strided share; every workgroup counts itself in;
+// the last one of the message resets the counter for the slot's next use and
+// publishes seq in the peer's inbox.  A wait that times out marks the
+// transport poisoned; every later launch then exits at once, so no wait
+// outlives the time limit.  No host-side state: launches can be captured and
+// replayed.
+//
+// Memory protocol (round 4).  Bytes stored into a peer's inbox slot are
+// written THROUGH to memory (global_store_dwordx4 ... sc0 sc1 nt: system
+// coherent, so no L2 keeps them dirty); a workgroup waits for its stores'
+// acknowledgements (vmcnt 0) before it counts itself in with a RELAXED
+// system-scope atomic, and the last arriver publishes the flag with a relaxed
+// system-scope store -- the flag is issued after every byte of the message
+// was acknowledged.  No L2 write-back anywhere: round 3 released every
+// workgroup's stores with buffer_wbl2 sc0 sc1, and those write-backs
+// serialise -- a 16 MiB message by 512 workgroups took 47 us with them and
+// 9.4 us written through (5.9 us with no protocol at all;
+// profiles/r4_fence_probe.txt).  A reader polls with relaxed system-scope
+// loads; once the flag is seen, its thread 0 invalidates once (the acquire
+// fence: buffer_inv sc0 sc1, waited for) before the workgroup barrier -- the
+// invalidation is of the CU's L1 and the XCD's L2, shared by every wave of
+// the workgroup -- and the waves then read the slot with ordinary
+// non-temporal loads.
 
-__device__ __forceinline__ uint64_t ld_acq_sys(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint64_t ld_rlx_sys(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// thread 0 of a reader, after it saw the flag: one system-scope acquire
+// (invalidation), completed before the workgroup barrier that follows
+__device__ __forceinline__ void acquire_once() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  vm_wait();
+}
+// the end of a workgroup's share of a message: its stores acknowledged, then
+// counted in (relaxed); true on the message's last arriver (thread 0 only)
+__device__ __forceinline__ bool count_in(uint32_t *cnt, uint32_t nwg) {
+  vm_wait();
+  __syncthreads();
+  if (threadIdx.x != 0) return false;
+  const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (old + 1 != nwg) return false;
+  __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use: a later launch
+  return true;
+}
+__device__ __forceinline__ void publish(uint64_t *flag, uint64_t seq) {
+  __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // diagnostics (BINE_DIRECT_STAMPS, DmArgs::stamps): thread 0 of a workgroup
@@ -885,9 +942,9 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi, int
     if (a.stamps) t0 = wall_clock64();
     int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
     if (ok && wait_ptr) {
-      const long long t0 = wall_clock64();
-      while (ld_acq_sys(wait_ptr) < wait_val) {
-        if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
+      const long long w0 = wall_clock64();
+      while (ld_rlx_sys(wait_ptr) < wait_val) {
+        if (wall_clock64() - w0 > (long long)a.timeout_ticks) {
           __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           ok = 0;
@@ -900,57 +957,69 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi, int
         __builtin_amdgcn_s_sleep(2);
       }
     }
+    // a pull reads what the peer wrote into our slot: one acquire; a push
+    // only writes the slot the peer acknowledged (its reads were complete
+    // before it counted in), nothing to acquire
+    if (ok && !m.push) acquire_once();
     go = ok;
     if (a.stamps) t1 = wall_clock64();
   }
   __syncthreads();
   if (!go) return false;  // poisoned: the transport is dead, counters and bases no longer matter
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the peer released before its mark
   // grid-strided 16-B vectors (src / dst co-aligned mod 16: slots and plan
   // offsets are), bytes before the first boundary and after the last vector
   // by workgroup 0
   const size_t head = std::min<uint64_t>((16 - ((uintptr_t)dst & 15)) & 15, m.bytes);
   const size_t nvec = (m.bytes - head) / 16;
   if (wi == 0) {
-    for (size_t i = threadIdx.x; i < head; i += kBlock) dst[i] = src[i];
-    for (size_t i = head + nvec * 16 + threadIdx.x; i < m.bytes; i += kBlock) dst[i] = src[i];
+    // a push's bytes into the slot written through too (system-scope byte
+    // stores); a pull reads them after the acquire above
+    auto put = [&](size_t i) {
+      if (m.push) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else dst[i] = src[i];
+    };
+    for (size_t i = threadIdx.x; i < head; i += kBlock) put(i);
+    for (size_t i = head + nvec * 16 + threadIdx.x; i < m.bytes; i += kBlock) put(i);
   }
   const u32x4 *vs = reinterpret_cast<const u32x4 *>(src + head);
   u32x4 *vd = reinterpret_cast<u32x4 *>(dst + head);
   constexpr int U = 4;
   const size_t stride = (size_t)nwg * kBlock * U;
-  for (size_t b0 = (size_t)wi * kBlock * U + threadIdx.x; b0 < nvec; b0 += stride) {
-    u32x4 x[U];
+  if (m.push) {
+    const __amdgpu_buffer_rsrc_t r = wt_rsrc(vd);  // (a push's head is empty: vd is the slot)
+    for (size_t b0 = (size_t)wi * kBlock * U + threadIdx.x; b0 < nvec; b0 += stride) {
+      u32x4 x[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const size_t i = b0 + (size_t)u * kBlock;
-      if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
+      for (int u = 0; u < U; u++) {
+        const size_t i = b0 + (size_t)u * kBlock;
+        if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const size_t i = b0 + (size_t)u * kBlock;
+        if (i < nvec) st_wt(r, i, x[u]);
+      }
     }
+  } else {
+    for (size_t b0 = (size_t)wi * kBlock * U + threadIdx.x; b0 < nvec; b0 += stride) {
+      u32x4 x[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const size_t i = b0 + (size_t)u * kBlock;
-      if (i < nvec) __builtin_nontemporal_store(x[u], vd + i);
+      for (int u = 0; u < U; u++) {
+        const size_t i = b0 + (size_t)u * kBlock;
+        if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const size_t i = b0 + (size_t)u * kBlock;
+        if (i < nvec) __builtin_nontemporal_store(x[u], vd + i);
+      }
     }
   }
-  // release this workgroup's stores, count it in; the last one of the message
-  // publishes
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (a.stamps) dm_stamp(a.stamps, a.serial, m.push ? 0 : 1, mi, wi, t0, t1, wall_clock64());
-    const uint32_t old = __hip_atomic_fetch_add(cnt_ptr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1 == (uint32_t)nwg) {
-      __hip_atomic_store(cnt_ptr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use: a later launch
-      // system-scope release (buffer_wbl2 sc0 sc1), its write-back waited for
-      // explicitly (the compiler may drop the wait after buffer_wbl2 when the
-      // vmcnt scoreboard is provably empty, MI355X_MICROARCH.md "Compiler
-      // hazard"), then a relaxed system-scope flag store (sc0 sc1): the
-      // flag cannot overtake the data (ISA: profiles/r3_dm_move_isa.txt)
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(sig_ptr, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  // stores acknowledged (written through) / slot reads complete, count in; the
+  // last one of the message publishes
+  const bool last = count_in(cnt_ptr, (uint32_t)nwg);
+  if (threadIdx.x == 0 && a.stamps) dm_stamp(a.stamps, a.serial, m.push ? 0 : 1, mi, wi, t0, t1, wall_clock64());
+  if (last) publish(sig_ptr, seq);
   return true;
 }
 
@@ -983,7 +1052,7 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi, in
       if (ok && seq > (uint64_t)kSlots) {
         const uint64_t *w = reinterpret_cast<const uint64_t *>(own + kAckOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
         const long long t0 = wall_clock64();
-        while (ld_acq_sys(w) < seq - kSlots) {
+        while (ld_rlx_sys(w) < seq - kSlots) {
           if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
             __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1002,8 +1071,7 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi, in
     go = ok;
   }
   __syncthreads();
-  if (!go) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (!go) return false;  // (writes only into acknowledged slots: nothing to acquire)
   const DmMsg &L = a.m[mi];
   const uint8_t *src = L.src;
   const int n = nd;
@@ -1013,7 +1081,8 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi, in
   if (wi == 0)
     for (int d = 0; d < n; d++)
       for (size_t i = nvec * 16 + threadIdx.x; i < L.bytes; i += kBlock)
-        reinterpret_cast<uint8_t *>(dv[d])[i] = src[i];
+        __hip_atomic_store(reinterpret_cast<uint8_t *>(dv[d]) + i, src[i], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
   const u32x4 *vs = reinterpret_cast<const u32x4 *>(src);
   constexpr int U = 4;
   const size_t stride = (size_t)nwg * kBlock * U;
@@ -1025,29 +1094,27 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi, in
       if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
     }
     for (int d = 0; d < n; d++) {
-      u32x4 *vd = dv[d];
+      const __amdgpu_buffer_rsrc_t r = wt_rsrc(dv[d]);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const size_t i = b0 + (size_t)u * kBlock;
-        if (i < nvec) __builtin_nontemporal_store(x[u], vd + i);
+        if (i < nvec) st_wt(r, i, x[u]);
       }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  vm_wait();  // every member's bytes acknowledged (written through)
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int d = 0; d < n; d++) {
       const DmMsg &m = a.m[dmem[d]];
       const size_t k = (size_t)(dseq[d] % kSlots);
       uint32_t *cnt = reinterpret_cast<uint32_t *>(own + kCntPushOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
-      const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (old + 1 == (uint32_t)nwg) {
         __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
-        uint64_t *sig = reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(sig, dseq[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        publish(reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride),
+                dseq[d]);
       }
     }
   }
@@ -1074,7 +1141,9 @@ __device__ __forceinline__ void dm_launch_done(const DmArgs &a) {
   if (threadIdx.x != 0) return;
   uint8_t *own = a.own;
   uint32_t *lc = reinterpret_cast<uint32_t *>(own + kLaunchCntOff);
-  const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  // relaxed: every workgroup read its bases before it got here (the values
+  // fed its addresses), and the next launch follows in stream order
+  const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (ol + 1 == gridDim.x) {
     __hip_atomic_store(lc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int i = 0; i < a.nmsg; i++) {
@@ -1165,7 +1234,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
     if (threadIdx.x == 0 && go) {
       const uint64_t *w = reinterpret_cast<const uint64_t *>(own + kReadyOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
       const long long t0 = wall_clock64();
-      while (ld_acq_sys(w) < seq) {
+      while (ld_rlx_sys(w) < seq) {
         if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
           __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1180,10 +1249,12 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
       }
     }
   }
-  if (threadIdx.x == 0 && a.stamps) t1 = wall_clock64();
+  if (threadIdx.x == 0) {
+    if (go) acquire_once();  // every leaf's mark seen: what the senders wrote before it
+    if (a.stamps) t1 = wall_clock64();
+  }
   __syncthreads();
   if (!go) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the senders released before their marks
   // the tree over this workgroup's tiles (k_reduce_tree's tile body).  Fewer
   // vectors in flight per lane than k_reduce_tree: the copy workgroups of the
   // launch get this kernel's register allocation too
@@ -1196,9 +1267,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
     if ((ti + 1) * tile <= t.nvec) tree_tile<T, OP, NL, U, false>(lp, vo, b, t.nvec, t.swap);
     else tree_tile<T, OP, NL, U, true>(lp, vo, b, t.nvec, t.swap);
   }
-  // every leaf slice read: count in per leaf; the last tree workgroup of a
-  // leaf acknowledges its slot to the sender (as a pull's last workgroup does)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // every leaf slice read (loads complete): count in per leaf; the last tree
+  // workgroup of a leaf acknowledges its slot to the sender (as a pull's last
+  // workgroup does)
+  vm_wait();
   __syncthreads();
   if (threadIdx.x == 0) {
     if (a.stamps) dm_stamp(a.stamps, a.serial, 2, 255, tw, t0, t1, wall_clock64());
@@ -1210,14 +1282,11 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
       const size_t k = (size_t)(seq % kSlots);
       uint32_t *cnt = reinterpret_cast<uint32_t *>(own + kCntPullOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
-      const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (old + 1 == (uint32_t)t.twgs) {
         __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
-        uint64_t *sig = reinterpret_cast<uint64_t *>(remote + kAckOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(sig, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        publish(reinterpret_cast<uint64_t *>(remote + kAckOff + ((size_t)a.rank * kSlots + k) * kFlagStride), seq);
       }
     }
   }
@@ -1325,16 +1394,17 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
   return r;
 }
 
-// the whole workgroup: thread 0 polls (system-scope acquire loads, bounded),
-// everyone then acquires.  false: the transport is poisoned (now or earlier)
-__device__ __forceinline__ bool wait_flag(const DmFusedArgs &a, const uint64_t *p, uint64_t v) {
+// the whole workgroup: thread 0 polls (relaxed system-scope loads, bounded)
+// and, for a ready mark (acq: the slot is read next), acquires once.  false:
+// the transport is poisoned (now or earlier)
+__device__ __forceinline__ bool wait_flag(const DmFusedArgs &a, const uint64_t *p, uint64_t v, bool acq) {
   __shared__ int go;
   uint32_t *poison = reinterpret_cast<uint32_t *>(a.own + kPoisonOff);
   if (threadIdx.x == 0) {
     int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
     if (ok && p) {
       const long long t0 = wall_clock64();
-      while (ld_acq_sys(p) < v) {
+      while (ld_rlx_sys(p) < v) {
         if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
           __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1348,29 +1418,20 @@ __device__ __forceinline__ bool wait_flag(const DmFusedArgs &a, const uint64_t *
         __builtin_amdgcn_s_sleep(2);
       }
     }
+    if (ok && acq) acquire_once();
     go = ok;
   }
   __syncthreads();
   const bool ok = go != 0;
   __syncthreads();  // `go` is reused by the next wait
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   return ok;
 }
 
-// the whole workgroup, after its share of message m: release, count in; the
-// last workgroup of the message publishes seq (k_dm_move's protocol)
+// the whole workgroup, after its share of message m: stores acknowledged /
+// reads complete, count in; the last workgroup of the message publishes seq
+// (k_dm_move's protocol)
 __device__ __forceinline__ void arrive(const DmFusedArgs &a, const Msg &m) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(m.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1 == (uint32_t)a.wgs) {
-      __hip_atomic_store(m.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(m.sig, m.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (count_in(m.cnt, (uint32_t)a.wgs)) publish(m.sig, m.seq);
 }
 
 // this workgroup's slice of a message of n vectors
@@ -1379,10 +1440,18 @@ __device__ __forceinline__ void slice(uint64_t n, int wgs, uint64_t *lo, uint64_
   *hi = n * (blockIdx.x + 1) / (uint64_t)wgs;
 }
 
-__device__ __forceinline__ void copy_slice(const Msg &m, int wgs) {
+// a push writes the peer's slot through; a pull reads its own slot after
+// the acquire of wait_flag
+__device__ __forceinline__ void copy_slice(const Msg &m, int wgs, bool push) {
   uint64_t lo, hi;
   slice(m.nvec, wgs, &lo, &hi);
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) __builtin_nontemporal_store(__builtin_nontemporal_load(m.src + i), m.dst + i);
+  if (push) {
+    const __amdgpu_buffer_rsrc_t r = wt_rsrc(m.dst);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) st_wt(r, i, __builtin_nontemporal_load(m.src + i));
+  } else {
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock)
+      __builtin_nontemporal_store(__builtin_nontemporal_load(m.src + i), m.dst + i);
+  }
 }
 }  // namespace dmf
 
@@ -1393,8 +1462,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   // phase A: our blocks into the peers' inboxes
   for (int i = 0; i < a.na; i++) {
     const Msg m = resolve(a, a.m[i]);
-    if (!wait_flag(a, m.wait, m.wait_val)) return;
-    copy_slice(m, a.wgs);
+    if (!wait_flag(a, m.wait, m.wait_val, false)) return;
+    copy_slice(m, a.wgs, true);
     arrive(a, m);
   }
   // phase B: the peers' blocks, read in place in our inbox as the tree's
@@ -1403,7 +1472,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   // whose previous use must have been acknowledged first
   for (int i = 0; i < a.nb + a.nc; i++) {
     const Msg m = resolve(a, a.m[a.na + i]);
-    if (!wait_flag(a, m.wait, m.wait_val)) return;
+    if (!wait_flag(a, m.wait, m.wait_val, i < a.nb)) return;
   }
   const u32x4 *lp[kMaxLeaves];
 #pragma unroll
@@ -1411,9 +1480,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
     lp[j] = j >= a.nl ? nullptr
             : j == a.pos ? reinterpret_cast<const u32x4 *>(a.own_leaf)
                          : resolve(a, a.m[a.leaf[j]]).src;
-  u32x4 *cp[kMaxFusedPeers];
+  __amdgpu_buffer_rsrc_t cp[kMaxFusedPeers];
 #pragma unroll
-  for (int i = 0; i < kMaxFusedPeers; i++) cp[i] = i < a.nc ? resolve(a, a.m[a.na + a.nb + i]).dst : nullptr;
+  for (int i = 0; i < kMaxFusedPeers; i++)
+    if (i < a.nc) cp[i] = wt_rsrc(resolve(a, a.m[a.na + a.nb + i]).dst);
   {
     u32x4 *out = reinterpret_cast<u32x4 *>(a.out);
     uint64_t lo, hi;
@@ -1432,7 +1502,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
       out[i] = v[0];
 #pragma unroll
       for (int c = 0; c < kMaxFusedPeers; c++)
-        if (c < a.nc) __builtin_nontemporal_store(v[0], cp[c] + i);
+        if (c < a.nc) st_wt(cp[c], i, v[0]);
     }
   }
   // every leaf slice is read (the senders may reuse their slots) and every
@@ -1441,15 +1511,15 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   // phase C: the peers' results out of our inbox
   for (int i = 0; i < a.nd; i++) {
     const Msg m = resolve(a, a.m[a.na + a.nb + a.nc + i]);
-    if (!wait_flag(a, m.wait, m.wait_val)) return;
-    copy_slice(m, a.wgs);
+    if (!wait_flag(a, m.wait, m.wait_val, true)) return;
+    copy_slice(m, a.wgs, false);
     arrive(a, m);
   }
   // the launch's last workgroup advances the sequence bases (every workgroup
   // has read them: each resolve() happened before its launch-counter add)
   if (threadIdx.x == 0) {
     uint32_t *lc = reinterpret_cast<uint32_t *>(a.own + dm::kLaunchCntOff);
-    const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ol = __hip_atomic_fetch_add(lc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ol + 1 == gridDim.x) {
       __hip_atomic_store(lc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int i = 0; i < nm; i++) {

@@ -1,0 +1,166 @@
+"""Node model of the reduce-family collectives: what a
+C3 / C4 / C5 call should take at P ranks on one node for each transport,
+derived from the executed issue schedule, so the driver's first multi-GPU
+line can be judged on arrival (bench.py puts `model_ms` and `frac_of_model`
+in its N > 1 roofline).  Host only.
+
+    t_model = max(t_link, t_hbm) + launches x t_boundary
+
+* t_link: exchange ops run one after another, the links of one op in
+  parallel; per op its busiest directed link's bytes at LINK_GBS (153 GB/s,
+  the task's per-link figure; bench.py's link roofline uses the same sum).
+* t_hbm: the HBM bytes one rank's call moves (`hbm_bytes`) at the transport
+  kernels' rate.  A send reads its source (its write lands in the receiver's
+  HBM and is counted there, as the receiver's arrival); a receive is that
+  arrival plus -- unless a fused tree reads it in place in the inbox slot --
+  the copy out of the slot / RCCL's FIFO (read + write); a tree reads its
+  leaves and writes its output; a copy reads and writes; a pairwise reduction
+  reads two operands and writes one.  RCCL P2P moves bytes the way the
+  unfused direct transport does (FIFO in the receiver, copied out by the
+  receiving kernel).
+* launches: kernel launches per call (an exchange of r slot rounds: r
+  launches when r = 1, else r + 1; a local op one; a fused tree none, or one
+  when it is hosted by itself) x the measured launch-to-launch gap.
+
+On one GPU (P processes sharing it, the only multi-rank setting this pool
+offers) every rank's bytes go through the one HBM and no link is involved:
+t = P x hbm_bytes / rate + launches x t_boundary.
+"""
+from __future__ import annotations
+
+LINK_GBS = 153.0          # one xGMI link, one direction (task statement); 7 per GPU
+HBM_RATE_GBS = 5000.0     # the direct transport's kernels on one MI355X ("Direct transport, measured")
+T_BOUNDARY_US = 4.0       # launch-to-launch gap on the comm stream (tools/dm_stamps.py "gap_us_med")
+SLOT_BYTES = 16 << 20     # the direct transport's sub-message slot (BINE_DIRECT_SLOT_BYTES)
+
+TRANSPORTS = {
+    # the transports bench.py trials (their names; "+dm16", "+dmt64x128" ...
+    # are the same transports with other workgroup counts)
+    "direct": "the literal Bine schedule over RCCL P2P",
+    "flat": "the flat allgather phase over RCCL P2P",
+    "relay": "permutation steps relayed over all links, RCCL P2P",
+    "relay+flat": "relay + the flat allgather phase, RCCL P2P",
+    "flatrs+flat": "flat reduce-scatter + flat allgather phases over RCCL P2P",
+    "trees": "P - 1 relabelled instances on edge-disjoint pairings, RCCL P2P",
+    "flatrs+flat+dm": "flat phases over the direct transport, pull copies + tree launches",
+    "flatrs+flat+dmt": "flat phases over the direct transport, fused trees",
+}
+RELAY_MIN_BYTES = 256 << 10   # bench.py's relay setting
+
+
+def _flags(transport):
+    """(flat_ag, flat_rs, relay, trees, direct, fused) of a transport name"""
+    t = transport
+    return ("flat" in t, "flatrs" in t, "relay" in t, t.startswith("trees"), "+dm" in t, "+dmt" in t)
+
+
+def _schedule(coll, algo, P, rank, esz, transport, chunk_bytes, count=0, rcounts=None):
+    import pico_amd
+    flat_ag, flat_rs, relay, trees, _, _ = _flags(transport)
+    kw = dict(esz=esz, chunk_bytes=chunk_bytes, flat_ag=flat_ag, flat_rs=flat_rs)
+    if coll == "allreduce":
+        kw["count"] = count
+    else:
+        kw["rcounts"] = rcounts
+    ops = pico_amd.schedule(coll, algo, P, rank, relay_min_bytes=RELAY_MIN_BYTES if relay and P >= 3 else 0,
+                            trees=trees, **kw)[0]
+    return ops, kw
+
+
+def _fused(coll, algo, P, rank, kw, slot):
+    """exchange ops whose receives a fused tree reads in place, the tree ops
+    hosted by an exchange launch and those hosted by themselves (executor.cpp
+    plan_dm_trees, via bine_plan_dm_trees)"""
+    import pico_amd
+    ops = pico_amd.schedule(coll, algo, P, rank, **kw)[0]
+    host, _ = pico_amd.dm_tree_plan(coll, algo, P, rank, slot=slot, **kw)
+    leaf_ops, self_hosted, hosted = set(), set(), set()
+    for j, h in enumerate(host):
+        if h < 0:
+            continue
+        hosted.add(j)
+        if h == j:
+            self_hosted.add(j)
+        i = j - 1
+        while not ops[i]["xchg"]:
+            i -= 1
+        leaf_ops.add(i)
+    return leaf_ops, hosted, self_hosted
+
+
+def hbm_bytes(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0,
+              rcounts=None, slot=SLOT_BYTES):
+    """HBM bytes (reads + writes) one rank moves in one call (module doc)"""
+    ops, kw = _schedule(coll, algo, P, rank, esz, transport, chunk_bytes, count, rcounts)
+    leaf_ops = _fused(coll, algo, P, rank, kw, slot)[0] if _flags(transport)[5] else set()
+    b = 0
+    for i, o in enumerate(ops):
+        for p in o["prims"]:
+            n = p["count"] * esz
+            b += {"SEND": n, "RECV": n + (0 if i in leaf_ops else 2 * n), "REDUCE_TREE": (p["peer"] + 1) * n,
+                  "COPY": 2 * n, "REDUCE": 3 * n, "REDUCE3": 3 * n}[p["type"]]
+    return b
+
+
+def link_bytes(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0,
+               rcounts=None):
+    """sum over exchange ops of the busiest directed link's bytes"""
+    ops, _ = _schedule(coll, algo, P, rank, esz, transport, chunk_bytes, count, rcounts)
+    L = 0
+    for o in ops:
+        if o["xchg"]:
+            lk = {}
+            for p in o["prims"]:
+                lk[(p["type"], p["peer"])] = lk.get((p["type"], p["peer"]), 0) + esz * p["count"]
+            L += max(lk.values())
+    return L
+
+
+def launches(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0,
+             rcounts=None, slot=SLOT_BYTES):
+    """kernel launches per call (module doc)"""
+    ops, kw = _schedule(coll, algo, P, rank, esz, transport, chunk_bytes, count, rcounts)
+    direct, fused = _flags(transport)[4:]
+    hosted, self_hosted = (_fused(coll, algo, P, rank, kw, slot)[1:] if fused else (set(), set()))
+    n = 0
+    for j, o in enumerate(ops):
+        if o["xchg"]:
+            if direct:
+                r = max(1, -(-max(p["count"] * esz for p in o["prims"]) // slot))
+                n += r if r == 1 else r + 1
+            else:
+                n += 1
+        elif j in self_hosted or j not in hosted:
+            n += 1
+    return n
+
+
+def model_ms(coll, algo, P, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0, rcounts=None,
+             one_gpu=False, hbm_rate_gbs=HBM_RATE_GBS, link_gbs=LINK_GBS, t_boundary_us=T_BOUNDARY_US,
+             slot=SLOT_BYTES):
+    """expected ms of one call (module doc): {"model_ms", "t_link_ms", "t_hbm_ms", "launches", "hbm_bytes",
+    "link_bytes"} (rank 0's schedule; the collectives are symmetric)"""
+    kw = dict(esz=esz, transport=transport, chunk_bytes=chunk_bytes, count=count, rcounts=rcounts)
+    hb = hbm_bytes(coll, algo, P, slot=slot, **kw)
+    lb = link_bytes(coll, algo, P, **kw) if P > 1 else 0
+    nl = launches(coll, algo, P, slot=slot, **kw)
+    t_hbm = (P if one_gpu else 1) * hb / (hbm_rate_gbs * 1e9) * 1e3
+    t_link = 0.0 if one_gpu else lb / (link_gbs * 1e9) * 1e3
+    return {"model_ms": round(max(t_link, t_hbm) + nl * t_boundary_us * 1e-3, 4), "t_link_ms": round(t_link, 4),
+            "t_hbm_ms": round(t_hbm, 4), "launches": nl, "hbm_bytes": hb, "link_bytes": lb}
+
+
+CONFIGS = {
+    # BASELINE configs at full size: (collective, algorithm, element size, count or per-rank block)
+    "C3": ("allreduce", "bine_bdw_remap", 4, 67_108_864),
+    "C4": ("reduce_scatter", "bine_permute_remap", 4, 268_435_456),
+    "C5": ("allreduce", "bine_bdw_remap", 8, 33_554_432),
+}
+
+
+def config_model(cfg, P, transport, chunk_bytes=16 << 20, **kw):
+    coll, algo, esz, n = CONFIGS[cfg]
+    if coll == "allreduce":
+        return model_ms(coll, algo, P, esz=esz, transport=transport, chunk_bytes=chunk_bytes, count=n, **kw)
+    return model_ms(coll, algo, P, esz=esz, transport=transport, chunk_bytes=chunk_bytes, rcounts=[n // P] * P,
+                    **kw)

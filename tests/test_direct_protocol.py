@@ -107,28 +107,15 @@ def test_simulator_restates_the_executors_tree_plan(case):
 
 def _hbm_bytes_per_rank(coll, algo, P, rank, fused, esz=4, **kw):
     """HBM bytes one rank moves in one call over the direct transport, from
-    the executed issue schedule: a push reads its source (its remote write is
-    the receiver's arrival), a receive is an arrival into this rank's inbox
-    plus -- unless a fused tree reads it in place -- a pull copy (read +
-    write), a tree reads its leaves and writes its output, a copy reads and
-    writes, a pairwise reduction reads two operands and writes one"""
-    import pico_amd
-    ops, _, _ = pico_amd.schedule(coll, algo, P, rank, esz=esz, flat_ag=2, flat_rs=True, **kw)
-    host, _ = pico_amd.dm_tree_plan(coll, algo, P, rank, esz=esz, flat_ag=2, flat_rs=True, slot=1 << 20, **kw)
-    leaf_ops = set()
-    for j, h in enumerate(host):
-        if fused and h >= 0:
-            i = j - 1
-            while not ops[i]["xchg"]:
-                i -= 1
-            leaf_ops.add(i)
-    b = 0
-    for i, o in enumerate(ops):
-        for p in o["prims"]:
-            n = p["count"] * esz
-            b += {"SEND": n, "RECV": n + (0 if i in leaf_ops else 2 * n), "REDUCE_TREE": (p["peer"] + 1) * n,
-                  "COPY": 2 * n, "REDUCE": 3 * n, "REDUCE3": 3 * n}[p["type"]]
-    return b
+    the executed issue schedule (pico_amd.model.hbm_bytes -- the node model
+    bench.py prints beside its multi-GPU line): a push reads its source (its
+    remote write is the receiver's arrival), a receive is an arrival into this
+    rank's inbox plus -- unless a fused tree reads it in place -- a pull copy
+    (read + write), a tree reads its leaves and writes its output, a copy
+    reads and writes, a pairwise reduction reads two operands and writes one"""
+    from pico_amd import model
+    return model.hbm_bytes(coll, algo, P, rank, esz=esz, transport="flatrs+flat+dmt" if fused else "flatrs+flat+dm",
+                           slot=1 << 20, **kw)
 
 
 @pytest.mark.parametrize("P", [4, 8])

@@ -59,9 +59,23 @@ def summarize(st, calls):
                      "work_us_med": round(float(np.median(c)), 2), "work_us_p90": round(float(np.percentile(c, 90)), 2),
                      "busy_us_per_call": round(union(t1[m], t2[m]) * TICK_US / calls, 1),
                      "span_us_per_call": round(union(t0[m], t2[m]) * TICK_US / calls, 1)}
+    # launches: [first workgroup's entry, last workgroup's end]; the gap from
+    # one launch's end to the next one's start (launch boundaries, stream
+    # waits) and how much of each launch its workgroups spend working
+    serial = st[:, 0] >> 32
+    spans = {}
+    for s_, a_, b_ in zip(serial.tolist(), t0.tolist(), t2.tolist()):
+        lo, hi = spans.get(s_, (a_, b_))
+        spans[s_] = (min(lo, a_), max(hi, b_))
+    seq = sorted(spans.values())
+    gaps = [max(0, seq[k + 1][0] - seq[k][1]) * TICK_US for k in range(len(seq) - 1)]
+    lens = [(b_ - a_) * TICK_US for a_, b_ in seq]
     out["all"] = {"busy_us_per_call": round(union(t1, t2) * TICK_US / calls, 1),
                   "span_us_per_call": round(union(t0, t2) * TICK_US / calls, 1),
-                  "launches_per_call": round(len(set((st[:, 0] >> 32).tolist())) / calls, 1)}
+                  "launches_per_call": round(len(spans) / calls, 1),
+                  "launch_us_med": round(float(np.median(lens)), 2) if lens else None,
+                  "gap_us_med": round(float(np.median(gaps)), 2) if gaps else None,
+                  "gap_us_p90": round(float(np.percentile(gaps, 90)), 2) if gaps else None}
     return out
 
 

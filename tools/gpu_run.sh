@@ -4,9 +4,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
+T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 bash tools/gpu_steps.sh \
- "churn:200:$T tests/test_gpu.py -k 'freed_and_reallocated or match_mpich or pico_core_dropin or pico_core_c1'" \
- "staged:230:$T tests/test_gpu_rccl.py -k staged" \
- "e2e1:300:python -u tools/e2e_staging.py 1 float 67108864 20" \
- "rsg_q1:150:GPU_MAX_HW_QUEUES=1 BINE_SEGV_TRACE=1 BINE_SEGV_TRACE_DIR=\$PWD/gpurun_out python -u tools/rs_graph_probe.py 4 flatrs+flat+dm16 64 1"
+ "ab2:150:python -u tools/dm_tree_ab.py 2 16,64 4" \
+ "stamps2:600:python -u tools/dm_stamps.py 2 8 base: w64t128:BINE_DIRECT_WGS=64,BINE_DIRECT_TREE_WGS=128 w64t64:BINE_DIRECT_WGS=64,BINE_DIRECT_TREE_WGS=64 w96t128:BINE_DIRECT_WGS=96,BINE_DIRECT_TREE_WGS=128 w64t128p128:BINE_DIRECT_WGS=64,BINE_DIRECT_TREE_WGS=128,BINE_DIRECT_PULL_WGS=128 w64t128c64:BINE_DIRECT_WGS=64,BINE_DIRECT_TREE_WGS=128,BINE_CHUNK_BYTES=67108864 w128t256c64:BINE_DIRECT_WGS=128,BINE_DIRECT_TREE_WGS=256,BINE_CHUNK_BYTES=67108864" \
+ "rccl:600:$T tests/test_gpu_rccl.py"

@@ -16,4 +16,10 @@ for spec in "$@"; do
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
     echo "stopping after $name (rc=$rc)"; exit $rc
   fi
+  # a GPU fault inside a step that still exits 1 (a failed test, a rank that
+  # caught it): nothing more runs on the GPU in this call
+  if grep -q -E "illegal memory access|MEMORY_APERTURE|Memory access fault|HSA_STATUS_ERROR|page fault" \
+       "gpurun_out/$name.log"; then
+    echo "stopping after $name: GPU fault in its output"; exit 86
+  fi
 done
