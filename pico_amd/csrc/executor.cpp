@@ -364,6 +364,8 @@ struct DmTreePlan {
   std::vector<char> defer;
   std::vector<TreeSpec> spec;                // by tree op j
   std::vector<std::vector<XRecv>> leaves;    // by tree op j: exchange i's receives
+  bool any = false;   // some tree is fused
+  bool solo = false;  // every local op is a fused tree: the whole call on one stream (execute)
 };
 
 }  // namespace bine
@@ -414,7 +416,9 @@ struct bine_comm {
   // scratch of execute(): trees evaluated inside their exchange (plan_dm_trees)
   bool dm_tree = false;  // bine_comm_set_direct_tree
   int dm_tree_wgs = 0;   // its tree workgroups per launch (0: the transport's default)
-  bine::DmTreePlan tree_plan;
+  // fused-tree plans (plan_dm_trees) per (plan, buffers, dtype, op, settings):
+  // a pure function of those, cached so a call's issue path does not redo it
+  std::map<std::string, bine::DmTreePlan> tree_cache;
   std::vector<hipEvent_t> tree_ev;
   std::vector<char> tree_pending;
   // per-op device timing of the latest collective (bine_comm_set_profile)
@@ -983,11 +987,20 @@ static bool plan_dm_trees(const Transport &tx, bool on, const Schedule &sc, Ptr 
     pl.spec[j] = std::move(ts);
     any = true;
   }
+  pl.any = any;
+  pl.solo = any;
+  for (size_t j = 0; j < n && pl.solo; j++)
+    if (!sc.ops[j].xchg && pl.host[j] < 0) pl.solo = false;
   return any;
 }
 
+// tp: the call's fused-tree plan (tree_plan_for; null: none).  With tp->solo
+// every local op is a tree hosted by an exchange launch, so nothing is left to
+// overlap on a second stream: the whole call goes to K -- no cross-stream
+// events at all, and graph mode captures it as one branch (§4.3 of DESIGN.md)
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
-                   hipStream_t K, bool single = false, bool joined = false, const Staging *stg = nullptr) {
+                   hipStream_t K, bool single = false, bool joined = false, const Staging *stg = nullptr,
+                   const DmTreePlan *tpl = nullptr) {
   char *base[6];
   base[BINE_BUF_SBUF] = (char *)sbuf;
   base[BINE_BUF_RBUF] = (char *)rbuf;
@@ -998,7 +1011,8 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     const int rc = try_fused(c, sc, ptr, esz, dtype, op, K);
     if (rc >= 0) return rc;
   }
-  hipStream_t C = single ? K : c->cstream;
+  const bool solo = tpl && tpl->solo && !single && !stg;
+  hipStream_t C = single || solo ? K : c->cstream;
   // host staging: the host -> device copies overwrite the device input (and,
   // in place, the output) that the previous call's ops may still read or
   // write: the h2d stream follows K first (K follows the previous call's comm
@@ -1009,8 +1023,8 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   // every exchange of this call after every exchange of the previous one,
   // whichever stream that one used: the comm stream follows K at the start
   // and K follows the comm stream at the end
-  const bool ordered = c->tx->stream_ordered() && !single;
-  if ((sc.c_join || ordered) && !single && !joined) {  // joined: the comm stream already follows K (graph capture)
+  const bool ordered = c->tx->stream_ordered() && !single && !solo;
+  if ((sc.c_join || ordered) && !single && !solo && !joined) {  // joined: the comm stream already follows K (graph capture)
     int rc = stream_join(c, C, K);
     if (rc) return rc;
   }
@@ -1020,7 +1034,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   // own op.  With every tree hosted on the comm stream K stays idle, and its
   // joins -- a barrier packet on each stream per chunk -- would only add gaps
   // between the exchange launches
-  bool k_dirty = !(joined || ((sc.c_join || ordered) && !single));
+  bool k_dirty = C != K && !(joined || ((sc.c_join || ordered) && !single));
   hipEvent_t k_pending = nullptr;
   std::vector<hipEvent_t> &evs = c->op_ev;
   evs.resize(sc.ops.size());
@@ -1038,9 +1052,9 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
   if (stg) hev.assign(sc.ops.size(), nullptr);
   int64_t h_waited[2] = {-1, -1};
   // trees evaluated inside an exchange launch (direct transport; plan_dm_trees)
-  DmTreePlan &tp = c->tree_plan;
-  const bool dm_trees = !single && !stg && plan_dm_trees(*c->tx, c->dm_tree && !c->profile, sc, ptr, esz, dtype,
-                                                         op, tp);
+  static const DmTreePlan no_trees;
+  const DmTreePlan &tp = tpl ? *tpl : no_trees;
+  const bool dm_trees = !single && !stg && tpl && tpl->any;
   std::vector<hipEvent_t> &tev = c->tree_ev;
   std::vector<char> &tpend = c->tree_pending;
   if (dm_trees) {
@@ -1053,7 +1067,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     if (dm_trees && tp.host[i] == (int)i) {
       // a tree hosted by itself: its own launch on the comm stream pulls the
       // leaves in place (after the exchange that was issued without them)
-      if (k_dirty) {
+      if (k_dirty && C != K) {
         if (int rj = stream_join(c, C, K)) return rj;
         k_dirty = false;
       }
@@ -1061,14 +1075,14 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       static const std::vector<XRecv> no_r;
       if (int rc = c->tx->exchange_tree(no_s, no_r, nullptr, &tp.leaves[i], &tp.spec[i], C)) return rc;
       tev[i] = next_event(c);
-      HIP_TRY(hipEventRecord(tev[i], C));
+      if (C != K) HIP_TRY(hipEventRecord(tev[i], C));  // (one stream: nothing waits for it)
     }
     if (dm_trees && tp.host[i] >= 0) {
       // this tree runs inside exchange host[i]: K takes up its place in K's
       // order (later local ops follow it as they followed the tree) -- now,
       // or right after the host is issued when that comes next
       if (tev[i]) {
-        k_pending = tev[i];
+        if (C != K) k_pending = tev[i];
         if (sc.signals[i]) evs[i] = tev[i];
       } else {
         tpend[i] = 1;
@@ -1099,7 +1113,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
         hw = w;
       }
     }
-    if (o.wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
+    if (o.wait >= 0 && !single && !solo) HIP_TRY(hipStreamWaitEvent(st, evs[(size_t)o.wait], 0));
     if (roctx_on()) {
       char lbl[64];
       snprintf(lbl, sizeof lbl, "bine op %zu %s (%zu prims)", i, o.xchg ? "exchange" : "local", o.prims.size());
@@ -1134,7 +1148,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
         // the tree reads the own leaf and writes its output where K's earlier
         // ops may still be writing / reading: C follows K first (if K has
         // had any since C last did)
-        if (k_dirty) {
+        if (k_dirty && C != K) {
           if (int rj = stream_join(c, C, K)) return rj;
           k_dirty = false;
         }
@@ -1143,10 +1157,10 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
                  : c->tx->exchange_tree(sends, recvs, nullptr, &tp.leaves[(size_t)hj], &tp.spec[(size_t)hj], C);
         if (rc) return rc;
         hipEvent_t e = next_event(c);
-        HIP_TRY(hipEventRecord(e, C));
+        if (C != K) HIP_TRY(hipEventRecord(e, C));
         tev[(size_t)hj] = e;
         if (tpend[(size_t)hj]) {  // the tree's place in K's order came first
-          k_pending = e;
+          if (C != K) k_pending = e;
           if (sc.signals[(size_t)hj]) evs[(size_t)hj] = e;
         }
       } else {
@@ -1162,7 +1176,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     // an event of the pool may be re-recorded by a later op once the pool
     // wraps: any later record only delays a waiter, never lets it run early.
     // Ops nothing waits for record no event (host cost per op).
-    if (sc.signals[i] && !single) {
+    if (sc.signals[i] && !single && !solo) {
       evs[i] = next_event(c);
       HIP_TRY(hipEventRecord(evs[i], st));
     }
@@ -1177,7 +1191,7 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     if (int rc = stream_join(c, K, stg->d2h)) return rc;
   }
   if (k_pending && !ordered) HIP_TRY(hipStreamWaitEvent(K, k_pending, 0));  // (ordered: the join below covers it)
-  if (sc.final_wait >= 0 && !single) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
+  if (sc.final_wait >= 0 && !single && !solo) HIP_TRY(hipStreamWaitEvent(K, evs[(size_t)sc.final_wait], 0));
   if (ordered) return stream_join(c, K, C);
   return BINE_SUCCESS;
 }
@@ -1224,6 +1238,33 @@ static void build(const PlanArgs &args, size_t ch, size_t relay_min_bytes, bool 
   }
 }
 
+// The call's fused-tree plan (plan_dm_trees), cached per (plan, the buffers'
+// addresses, dtype, op, the direct transport's settings): null when the call
+// has none (no direct transport, trees off, single-stream or staged calls)
+static const DmTreePlan *tree_plan_for(bine_comm *c, const std::string &plan_key_s, const Schedule &sc,
+                                       const void *sbuf, void *rbuf, size_t esz, int dtype, int op) {
+  auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
+  if (!rt || !rt->dm_on || !rt->dm || !c->dm_tree || c->profile || op < 0) return nullptr;
+  char buf[256];
+  snprintf(buf, sizeof buf, "|%p|%p|%p|%p|%p|%p|%d|%d|%zu|%d|%zu|%d", sbuf, rbuf, c->tmp[0], c->tmp[1], c->tmp[2],
+           c->tmp[3], dtype, op, esz, rt->dm->merge, rt->dm->slot, rt->dm->tree_wgs);
+  const std::string key = plan_key_s + buf;
+  auto it = c->tree_cache.find(key);
+  if (it == c->tree_cache.end()) {
+    if (c->tree_cache.size() >= 256) c->tree_cache.clear();
+    char *base[6];
+    base[BINE_BUF_SBUF] = (char *)sbuf;
+    base[BINE_BUF_RBUF] = (char *)rbuf;
+    for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
+    base[BINE_BUF_STAGE] = (char *)c->tmp[3];
+    auto ptr = [&](int b, uint64_t off) { return base[b] + off * esz; };
+    DmTreePlan pl;
+    plan_dm_trees(*c->tx, true, sc, ptr, esz, dtype, op, pl);
+    it = c->tree_cache.emplace(key, std::move(pl)).first;
+  }
+  return it->second.any ? &it->second : nullptr;
+}
+
 // Graph mode: the first call for a (plan, buffers, dtype, op, stream,
 // transport options) key runs eagerly -- RCCL connects to new peers lazily and
 // the allgather option sizes its staging area, neither of which may happen
@@ -1234,7 +1275,8 @@ static void build(const PlanArgs &args, size_t ch, size_t relay_min_bytes, bool 
 // that key replays the graph with one hipGraphLaunch.  Work and ordering are
 // the eager schedule's, so results are bit-identical (GPU tests).
 static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule &sc, const void *sbuf, void *rbuf,
-                     size_t esz, int dtype, int op, hipStream_t K, bool single) {
+                     size_t esz, int dtype, int op, hipStream_t K, bool single, const DmTreePlan *tpl) {
+  const bool one = single || (tpl && tpl->solo);  // the whole call on K: a one-branch graph
   const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
   char buf[192];
   snprintf(buf, sizeof buf, "|%p|%p|%d|%d|%p|%d|%d|%d|%d", sbuf, rbuf, dtype, op, (void *)K, (int)single,
@@ -1246,7 +1288,7 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
     HIP_TRY(hipGraphLaunch(it->second.x, K));
     return BINE_SUCCESS;
   }
-  int rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single);  // this call, eagerly
+  int rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, false, nullptr, tpl);  // this call, eagerly
   if (rc) return rc;
   if (rt && rt->stage_gen != c->graph_stage_gen) {
     // the allgather option's staging area moved (freed after a synchronize of
@@ -1268,11 +1310,11 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
   // comm stream forked in, hipStreamEndCapture segfaulted (RCCL 2.26.6 / HIP
   // 7.0, both capture modes; tools/graph_probe.py, profiles/r2_graph_capture.txt).
   bine_comm::GraphEntry e;
-  const hipStream_t O = single ? K : c->cstream;
+  const hipStream_t O = one ? K : c->cstream;
   HIP_TRY(hipStreamBeginCapture(O, hipStreamCaptureModeThreadLocal));
-  if (!single) rc = stream_join(c, K, O);
-  if (!rc) rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, true);
-  if (!rc && !single) rc = stream_join(c, O, K);
+  if (!one) rc = stream_join(c, K, O);
+  if (!rc) rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, true, nullptr, tpl);
+  if (!rc && !one) rc = stream_join(c, O, K);
   const hipError_t ee = hipStreamEndCapture(O, &e.g);
   if (rc || ee != hipSuccess) {
     if (e.g) (void)hipGraphDestroy(e.g);
@@ -1371,13 +1413,15 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     }
     stg->rg = &sit->second;
   }
+  const void *src = a.in_place ? rbuf : sbuf;
+  const DmTreePlan *tpl = single || stg ? nullptr : tree_plan_for(c, key, sc, src, rbuf, a.esz, dtype, op);
   rc = order_begin(c, K);
   if (rc) {
   } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && !stg &&
-             (single || multi_branch_graphs_ok()))
-    rc = run_graph(c, key, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single);
+             (single || (tpl && tpl->solo) || multi_branch_graphs_ok()))
+    rc = run_graph(c, key, sc, src, rbuf, a.esz, dtype, op, K, single, tpl);
   else
-    rc = execute(c, sc, a.in_place ? rbuf : sbuf, rbuf, a.esz, dtype, op, K, single, false, stg);
+    rc = execute(c, sc, src, rbuf, a.esz, dtype, op, K, single, false, stg, tpl);
   if (!rc) rc = order_end(c, K);
   if (roctx_on()) roctxRangePop();
   return rc;

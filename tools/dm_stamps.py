@@ -8,7 +8,8 @@ workgroup (push, pull, tree) the time spent waiting for the peer's flag and
 the time spent copying / reducing, plus the call's timing (bench.timed: max
 over ranks, median after dropping 20 %) and its digest check.  Knobs via the
 environment (BINE_DIRECT_WGS = push workgroups per message, _PULL_WGS,
-_TREE_WGS, BINE_CHUNK_BYTES ...); several settings in one run:
+_TREE_WGS, BINE_CHUNK_BYTES ...; DM_STAMPS_GRAPHS=1: graph replay); several
+settings in one run:
 usage: python tools/dm_stamps.py P ITERS SETTING [SETTING ...]
        SETTING = name:VAR=val,VAR=val   (e.g. w128:BINE_DIRECT_WGS=128)
 One JSON line per setting.
@@ -103,7 +104,7 @@ def worker(rank, P, iters, env, port, q):
         nout = n if coll == "allreduce" else n // P
         rb = torch.empty(nout, dtype=torch.float32, device="cuda:0")
         pico_amd.fill_pico(sb, n, "float", 1234 + rank)
-        bench.apply_transport(comm, "flatrs+flat+dmt", chunk)
+        bench.apply_transport(comm, "flatrs+flat+dmt", chunk, os.environ.get("DM_STAMPS_GRAPHS") == "1")
         rb.fill_(float("nan"))
         if coll == "allreduce":
             fn = lambda: pico_amd.allreduce("bine_bdw_remap", sb, rb, n, "float", "sum", comm, stream=stream)
@@ -118,8 +119,8 @@ def worker(rank, P, iters, env, port, q):
         t = bench.timed(torch, stream, fn, iters, 0, dist, (comm.synchronize,))
         stamps = comm.direct_stamps(reset=True)
         ok, _ = bench.check_digest(pico_amd, rb, nout, "float", key, rank, stream)
-        res[cfg] = {"ms": round(t["median_ms"], 4), "parity_ok": bench.all_ok(torch, dist, ok),
-                    "stamps": summarize(stamps, iters)}
+        res[cfg] = {"ms": round(t["median_ms"], 4), "host_issue_ms": round(t["issue_ms"], 4),
+                    "parity_ok": bench.all_ok(torch, dist, ok), "stamps": summarize(stamps, iters)}
         del sb, rb
         torch.cuda.empty_cache()
     comm.destroy()

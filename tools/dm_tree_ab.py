@@ -55,7 +55,8 @@ def worker(rank, P, tree, chunks, iters, wgs, port, q):
                 key = bench.gkey("C4", "reduce_scatter", "bine_permute_remap", "float", n, P)
             st = bench.timed(torch, stream, fn, iters, 3, dist, (comm.synchronize,))
             ok, _ = bench.check_digest(pico_amd, rb, nout, "float", key, rank, stream)
-            res[f"{cfg}/{ch}MiB"] = {"ms": round(st["median_ms"], 4), "parity_ok": bench.all_ok(torch, dist, ok)}
+            res[f"{cfg}/{ch}MiB"] = {"ms": round(st["median_ms"], 4), "min_ms": round(st["min_ms"], 4),
+                                    "max_ms": round(st["max_ms"], 4), "parity_ok": bench.all_ok(torch, dist, ok)}
         del sb, rb
         torch.cuda.empty_cache()
     comm.destroy()
