@@ -101,16 +101,18 @@ def test_staged_host_buffers_4_ranks():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mcast", ["0", "1"])
-def test_fused_trees_vs_unfused_two_processes(mcast):
+@pytest.mark.parametrize("mcast,merge", [("0", "3"), ("1", "3"), ("0", "2")])
+def test_fused_trees_vs_unfused_two_processes(mcast, merge):
     """the direct transport's fused trees (leaves read in place in the inbox
     slots, deferred into the next exchange's launch) and the unfused form
     (pull copies + k_reduce_tree) at C3 / C4 full size, 2 processes, 16 and
     64 MiB chunks (64: leaves of 4 slots, the tree inside its own exchange);
     every rank's output digest equals the oracle's in both forms
     (tools/dm_tree_ab.py); mcast = 1: with the opt-in push groups
-    (BINE_DIRECT_MCAST)"""
-    env = dict(os.environ, BINE_DIRECT_MCAST=mcast)
+    (BINE_DIRECT_MCAST); merge = 2: one launch per slot round (BINE_DIRECT_MERGE)
+    -- the last chunk's tree then hosted by a launch of its own with no
+    messages of its own (that launch was never issued)"""
+    env = dict(os.environ, BINE_DIRECT_MCAST=mcast, BINE_DIRECT_MERGE=merge)
     r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_tree_ab.py"), "2", "16,64", "4"],
                  env=env, timeout=170)
     print(r.stdout[-3000:])
