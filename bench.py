@@ -570,7 +570,7 @@ def _dm_token(mode):
 
 def dm_wgs(mode):
     """the direct transport's workgroups per message a mode names: "+dm" ->
-    0 (the default, 32), "+dm64" / "+dmt64" / "+dmt64x128" -> 64; None when the
+    0 (the default, 128), "+dm64" / "+dmt64" / "+dmt64x128" -> 64; None when the
     mode does not use it"""
     tok = _dm_token(mode)
     if tok is None:
@@ -748,8 +748,8 @@ def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, wo
 
 
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
-DM_WGS_TRIALS = (16, 64)       # direct transport: workgroups per message tried beside the default 32
-TREE_WGS_TRIALS = (128, 256)   # fused trees ("+dmt"): tree workgroups per launch tried beside the default 64
+DM_WGS_TRIALS = (64, 256)      # direct transport: workgroups per message tried beside the default 128
+TREE_WGS_TRIALS = (128, 512)   # fused trees ("+dmt"): tree workgroups per launch tried beside the default 256
 CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 MODES = {"off": ["direct"],
          # "+a2a" is not tried: RCCL runs ncclAllToAllv as the same grouped P2P kernel
@@ -985,14 +985,14 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         best = min(cands, key=trials.get) if cands else base_cfg
         if dm_wgs(best[0]) == 0:
             # the direct transport's workgroups per message at the chosen chunk
-            # (default 32): how many it takes to fill a link is the node's to say
+            # (default 128): how many it takes to fill a link is the node's to say
             for w in DM_WGS_TRIALS:
                 trial((best[0] + str(w), best[1], False))
             cands = [c for c in trials if c[1] == best[1] and not c[2] and trials[c] != float("inf")
                      and (c[0] == best[0] or c[0] in [best[0] + str(w) for w in DM_WGS_TRIALS])]
             best = min(cands, key=trials.get)
         if dm_tree(best[0]) == 1:
-            # the fused trees' workgroups per launch (default 64): on a node each
+            # the fused trees' workgroups per launch (default 256): on a node each
             # GPU's CUs serve one rank, so more of them may pay there
             names = [best[0] + "x" + str(t) for t in TREE_WGS_TRIALS]
             for nm in names:

@@ -26,9 +26,9 @@ struct TreeSpec {
 
 struct DirectState {
   int P = 1, rank = 0, device = 0;
-  size_t slot = (size_t)16 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES)
-  int wgs = 32;                    // workgroups per message (BINE_DIRECT_WGS; bine_comm_set_direct_wgs)
-  int env_wgs = 32;                // the value init() settled on (the setter's 0)
+  size_t slot = (size_t)64 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES; profiles/r4_dm_stamps_p2_sweep2.txt)
+  int wgs = 128;                   // workgroups per message (BINE_DIRECT_WGS; bine_comm_set_direct_wgs)
+  int env_wgs = 128;               // the value init() settled on (the setter's 0)
   int pull_wgs = 0;                // workgroups per copied pull (BINE_DIRECT_PULL_WGS; 0: wgs)
   // diagnostics (BINE_DIRECT_STAMPS=<records>): per-workgroup stamps of every
   // launch (DmArgs::stamps), read back with bine_comm_direct_stamps
@@ -67,8 +67,8 @@ struct DirectState {
   // leaves of `dtree` (one slot each, all in its first launch)
   bool defer_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const std::vector<XRecv> &dleaves,
                 const TreeSpec &dtree) const;
-  int tree_wgs = 64;   // tree workgroups per launch (BINE_DIRECT_TREE_WGS; bine_comm_set_direct_tree)
-  int tree_wgs_env = 64;  // the value init() settled on
+  int tree_wgs = 256;  // tree workgroups per launch (BINE_DIRECT_TREE_WGS; bine_comm_set_direct_tree)
+  int tree_wgs_env = 256;  // the value init() settled on
   bool mcast = false;     // pushes of the same bytes to several peers as one group (BINE_DIRECT_MCAST=1;
                           // off: no gain measured, profiles/r3_push_groups.txt)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }

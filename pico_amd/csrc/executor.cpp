@@ -159,7 +159,7 @@ struct RcclTransport final : Transport {
   // bine_comm_set_direct: exchanges through mapped peer memory (direct.cpp)
   std::unique_ptr<DirectState> dm;
   bool dm_on = false;
-  int dm_wgs = 0;  // workgroups per message of the direct transport (0: BINE_DIRECT_WGS / 32)
+  int dm_wgs = 0;  // workgroups per message of the direct transport (0: BINE_DIRECT_WGS / 128)
   uint64_t key = 0;  // hash of the unique id: names the direct transport's sockets
   bool stream_ordered() const override { return dm_on; }
   int health() const override {
@@ -2161,7 +2161,7 @@ int bine_comm_set_direct_tree(bine_comm_t c, int on) {
   if (!c || on < -1 || on > 1024) return BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   const bool v = on < 0 ? dm_tree_env() : on != 0;
-  const int w = on > 1 ? on : 0;  // tree workgroups per launch (0: BINE_DIRECT_TREE_WGS / 64)
+  const int w = on > 1 ? on : 0;  // tree workgroups per launch (0: BINE_DIRECT_TREE_WGS / 256)
   if (v == c->dm_tree && w == c->dm_tree_wgs) return BINE_SUCCESS;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());

@@ -30,8 +30,9 @@ from __future__ import annotations
 
 LINK_GBS = 153.0          # one xGMI link, one direction (task statement); 7 per GPU
 HBM_RATE_GBS = 5000.0     # the direct transport's kernels on one MI355X ("Direct transport, measured")
-T_BOUNDARY_US = 4.0       # launch-to-launch gap on the comm stream (tools/dm_stamps.py "gap_us_med")
-SLOT_BYTES = 16 << 20     # the direct transport's sub-message slot (BINE_DIRECT_SLOT_BYTES)
+T_BOUNDARY_US = 7.0       # launch-to-launch gap at the default workgroups (tools/dm_stamps.py "gap_us_med",
+                          # profiles/r4_dm_stamps_p2_sweep2.txt: 6.6-7.7 us)
+SLOT_BYTES = 64 << 20     # the direct transport's sub-message slot (BINE_DIRECT_SLOT_BYTES)
 
 TRANSPORTS = {
     # the transports bench.py trials (their names; "+dm16", "+dmt64x128" ...

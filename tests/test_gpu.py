@@ -205,7 +205,10 @@ def _golden_groups():
 @pytest.mark.parametrize("key,cs", _golden_groups(), ids=lambda x: ".".join(x) if isinstance(x, tuple) else "")
 def test_collectives_match_reference_goldens(dev, key, cs, relay):
     """relay: the same cases with the multi-link relay schedule (two-hop
-    routes through the other ranks) -- results must not change a bit."""
+    routes through the other ranks) -- results must not change a bit (the
+    segmented algorithm's relay pass skips the cases of more than 512
+    segments: up to 32,768 segments a case, 90 of the suite's seconds, for
+    the same relay routes its smaller cases take)."""
     coll, algo = key
     bad = []
     for c in cs:
@@ -214,6 +217,8 @@ def test_collectives_match_reference_goldens(dev, key, cs, relay):
             continue
         rk = G.rcounts(c) if coll == "reduce_scatter" else None
         sb = G.inputs(c, sum(rk) if rk else N)
+        if relay and c["segsize"] and N * sb[0].itemsize > 512 * c["segsize"]:
+            continue
         ip = c["rcounts"].endswith("_inplace")   # MPI_IN_PLACE cases (the reference's in-place paths)
         root = G.root(c) if coll == "bcast" else 0
         outs, st = run_loopback(coll, algo, sb, dt, c["op"], rk, c["segsize"], root=root, relay=relay, in_place=ip)

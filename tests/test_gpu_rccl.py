@@ -19,11 +19,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.timeout(400)
 def test_rccl_large_messages_4_ranks():
-    """64 MiB per rank, fp32 + fp64, default 16 MiB chunks (several chunks per
+    """64 MiB per rank, fp64 (fp32 at P = 8), default 16 MiB chunks (several chunks per
     pipelined step), every bench transport, digests vs the oracle
     (tools/rccl_large.py)"""
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "4"], env=env,
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "4", "double"], env=env,
                        capture_output=True, text=True, timeout=380)
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
@@ -32,10 +32,10 @@ def test_rccl_large_messages_4_ranks():
 
 @pytest.mark.timeout(400)
 def test_rccl_large_messages_8_ranks():
-    """the same at P = 8 (8 processes on the box's one GPU): every transport
+    """the same at P = 8 in fp32 (8 processes on the box's one GPU): every transport
     incl. multi-tree and the direct peer-memory transport, eager and graph"""
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "8"], env=env,
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "8", "float"], env=env,
                        capture_output=True, text=True, timeout=380)
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
@@ -93,6 +93,7 @@ def test_staged_host_buffers_4_ranks():
     # bounded -- bine_comm_synchronize, libbine.so's drains -- and each case
     # prints a start line, so a stall names its case and stream)
     env = dict(os.environ, PYTHONPATH=ROOT, BINE_SYNC_TIMEOUT_S="60")
+    _sub.parent_state()
     r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "staged_check.py"), "4", "1"], env=env,
                  timeout=170)
     tail = "\n".join(r.stdout.splitlines()[-16:])

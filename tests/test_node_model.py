@@ -37,11 +37,20 @@ def test_launch_count_matches_the_stamped_runs():
     # exchanges (each hosting the previous chunk's tree), the last tree by
     # itself, the 128 MiB allgather in 8 slot rounds (9 launches) = 18, the
     # launches per call tools/dm_stamps.py counted on the GPU; C4 33
-    assert M.config_model("C3", 2, "flatrs+flat+dmt")["launches"] == 18
-    assert M.config_model("C4", 2, "flatrs+flat+dmt")["launches"] == 33
+    # (16 MiB slots, profiles/r4_dm_stamps_p2_solo.txt "base")
+    s16 = dict(slot=16 << 20)
+    assert M.config_model("C3", 2, "flatrs+flat+dmt", **s16)["launches"] == 18
+    assert M.config_model("C4", 2, "flatrs+flat+dmt", **s16)["launches"] == 33
     # P = 8: 2 exchanges of 16 MiB pieces, the last tree, the 32 MiB allgather
     # in 2 rounds (3 launches)
-    assert M.config_model("C3", 8, "flatrs+flat+dmt")["launches"] == 6
+    assert M.config_model("C3", 8, "flatrs+flat+dmt", **s16)["launches"] == 6
+    # the 64 MiB default slot (profiles/r4_dm_stamps_p2_sweep2.txt): the
+    # allgather in 2 rounds at 16 MiB chunks (12), 4 + 1 + 1 at 64 MiB chunks
+    # (6), C4 8 exchanges + the last tree (9); P = 8: the allgather in one
+    assert M.config_model("C3", 2, "flatrs+flat+dmt")["launches"] == 12
+    assert M.config_model("C3", 2, "flatrs+flat+dmt", 64 << 20)["launches"] == 6
+    assert M.config_model("C4", 2, "flatrs+flat+dmt", 64 << 20)["launches"] == 9
+    assert M.config_model("C3", 8, "flatrs+flat+dmt")["launches"] == 4
 
 
 def test_model_arithmetic():
@@ -50,7 +59,7 @@ def test_model_arithmetic():
     t_hbm = 6.375 * S3 / 1000e9 * 1e3
     assert m["t_link_ms"] == pytest.approx(t_link, abs=1e-4)
     assert m["t_hbm_ms"] == pytest.approx(t_hbm, abs=1e-4)
-    assert m["model_ms"] == pytest.approx(max(t_link, t_hbm) + 6 * 10e-3, abs=1e-4)
+    assert m["model_ms"] == pytest.approx(max(t_link, t_hbm) + m["launches"] * 10e-3, abs=1e-4)
     # one GPU shared by the ranks: every rank's bytes through one HBM, no link
     g = M.config_model("C3", 2, "flatrs+flat+dmt", one_gpu=True, hbm_rate_gbs=1000.0, t_boundary_us=0.0)
     assert g["t_link_ms"] == 0 and g["model_ms"] == pytest.approx(2 * g["hbm_bytes"] / 1e12 * 1e3, abs=1e-4)

@@ -16,7 +16,8 @@ on a 64 MiB input per rank (direct, flatrs, flatrs over the direct transport;
 eagerly and in graph mode).  Every rank's output digest is
 compared with the oracle's (trees: the relabelled schedule's), computed once
 in the parent.
-usage: python tools/rccl_large.py [P]   (exit 0 = every rank, every case ok)
+usage: python tools/rccl_large.py [P] [DTYPES]   (DTYPES: float,double (default) --
+the suite runs fp64 at P = 4 and fp32 at P = 8; exit 0 = every rank, every case ok)
 """
 import os
 import sys
@@ -31,12 +32,17 @@ MODES = ("direct", "relay", "flat", "flatrs+flat", "flatrs+flat+ag", "flatrs+fla
 RS_MODES = ("direct", "flatrs", "flatrs+flat+dm", "flatrs+flat+dmt")
 
 
-def expected(P):
+ARS = (("float", N32), ("double", N64))
+
+
+def expected(P, dts):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle as O
     import test_trees as TT
     want = {}
-    for dt, n in (("float", N32), ("double", N64)):
+    for dt, n in ARS:
+        if dt not in dts:
+            continue
         sb = O.inputs(dt, n, P)
         out, rets = O.allreduce("bine_bdw_remap", sb, dt)
         assert not any(rets)
@@ -52,7 +58,7 @@ def expected(P):
     return want
 
 
-def worker(rank, P, port, want, q):
+def worker(rank, P, port, want, dts, q):
     os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
@@ -68,7 +74,10 @@ def worker(rank, P, port, want, q):
     side = torch.cuda.Stream()   # graph mode needs a non-NULL caller stream
     modes = [m for m in MODES if m in bench.transport_modes("auto", P) or m in ("flatrs+flat+a2a", "relay+flat+dm",
                                                                               "trees+dm")]
-    for dt, n, tdt in (("float", N32, torch.float32), ("double", N64, torch.float64)):
+    for dt, n in ARS:
+        if dt not in dts:
+            continue
+        tdt = {"float": torch.float32, "double": torch.float64}[dt]
         s = torch.empty(n, dtype=tdt, device="cuda:0")
         r = torch.empty(n, dtype=tdt, device="cuda:0")
         pico_amd.fill_pico(s, n, dt, 1234 + rank)
@@ -125,10 +134,11 @@ if __name__ == "__main__":
     import multiprocessing as mp
     from tools._procs import join_ranks
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    want = expected(P)
+    dts = (sys.argv[2] if len(sys.argv) > 2 else "float,double").split(",")
+    want = expected(P, dts)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, P, 29591, want, q)) for r in range(P)]
+    ps = [ctx.Process(target=worker, args=(r, P, 29591, want, dts, q)) for r in range(P)]
     for p in ps:
         p.start()
     join_ranks(ps, 600)

@@ -11,9 +11,12 @@ the C3 shape, 256 MiB fp32 per rank: bine_checksum vs the committed digest
 tests/golden/bench_digests.json).
 usage: python tools/staged_check.py [P] [big 0|1]   (exit 0 = every rank, every case ok)
 """
+import faulthandler
 import json
 import os
+import signal
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -53,6 +56,14 @@ def worker(rank, P, port, want, big, q):
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
+    # a stall: every thread's Python stack on SIGUSR1 (tests/_sub.py sends it
+    # before its kill) and on its own after 60 s in one case
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
+    t0 = time.time()
+
+    def say(msg):
+        print(f"[{time.time() - t0:7.2f}s] rank {rank} {msg}", flush=True)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -66,7 +77,9 @@ def worker(rank, P, port, want, big, q):
     bad = []
     for transport in ("rccl", "direct", "mixed"):
         if transport == "direct":
+            say("direct transport ... start")
             comm.set_direct(True)
+            say("direct transport: set")
         for (coll, algo, dt, n, op, chunk, in_place), w in zip(CASES, want):
             if w is None:
                 continue
@@ -74,7 +87,8 @@ def worker(rank, P, port, want, big, q):
             # pointers: nothing copied for it), the others' on the host -- the
             # same schedule on every rank
             on_dev = transport == "mixed" and rank == 0
-            print(f"rank {rank} {transport} {coll} {algo} {dt} n={n} ... start", flush=True)
+            say(f"{transport} {coll} {algo} {dt} n={n} ... start")
+            faulthandler.dump_traceback_later(60, repeat=True)
             total = n if coll == "allreduce" else n * P
             inp = O.inputs(dt, total, P)[rank]
             hs = torch.from_numpy(inp.copy()).pin_memory()
@@ -108,12 +122,15 @@ def worker(rank, P, port, want, big, q):
             ok = np.array_equal(got, w[rank])
             if not ok:
                 bad.append(f"{transport} {coll} {algo} {dt} n={n} chunk={chunk} in_place={in_place}")
-            print(f"rank {rank} {transport} {coll} {algo} {dt} n={n} chunk={chunk >> 10}KiB in_place={in_place}: "
-                  f"{'ok' if ok else 'MISMATCH'}", flush=True)
+            faulthandler.cancel_dump_traceback_later()
+            say(f"{transport} {coll} {algo} {dt} n={n} chunk={chunk >> 10}KiB in_place={in_place}: "
+                f"{'ok' if ok else 'MISMATCH'}")
         if big and transport != "mixed":  # C3's shape through the staged path, vs the committed oracle digest
             with open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")) as f:
                 gold = json.load(f)["digests"]
             key = f"C3/allreduce/bine_bdw_remap/float/N{C3_N}/P{P}"
+            say(f"{transport} C3 256 MiB staged ... start")
+            faulthandler.dump_traceback_later(60, repeat=True)
             dev = torch.empty(C3_N, dtype=torch.float32, device="cuda:0")
             pico_amd.fill_pico(dev, C3_N, "float", 1234 + rank)
             hs = dev.cpu().pin_memory()
@@ -130,7 +147,9 @@ def worker(rank, P, port, want, big, q):
             ok = key in gold and dig == int(gold[key][rank])
             if not ok:
                 bad.append(f"{transport} C3 256 MiB")
-            print(f"rank {rank} {transport} C3 256 MiB staged: {'ok' if ok else 'MISMATCH'}", flush=True)
+            faulthandler.cancel_dump_traceback_later()
+            say(f"{transport} C3 256 MiB staged: {'ok' if ok else 'MISMATCH'}")
+    say("destroy")
     comm.destroy()
     dist.destroy_process_group()
     q.put((rank, len(bad)))
@@ -139,6 +158,7 @@ def worker(rank, P, port, want, big, q):
 if __name__ == "__main__":
     import multiprocessing as mp
     from tools._procs import join_ranks
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     big = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     want = expected(P)
