@@ -14,6 +14,7 @@ import os
 import numpy as np
 import pytest
 
+import _sub
 import golden_util as G
 from oracle import oracle as O
 
@@ -636,12 +637,11 @@ def test_pico_amd_core_writes_pico_core_csv(dev, tmp_path, coll, algo, dtype):
     """pico_amd_core: pico_core's CLI / env / ground-truth check / CSV layout,
     buffers in HBM, calls through libbine.so's libbine.h symbols.  One rank
     (the Bine allgathers return MPI_ERR_ARG at P = 1, like the reference)."""
-    import subprocess
     exe = os.path.join(ROOT, "pico_amd", "lib", "pico_amd_core")
     env = dict(os.environ, COLLECTIVE_TYPE=coll, OUTPUT_DIR=str(tmp_path), DATA_DIR=str(tmp_path),
                OUTPUT_LEVEL="all", LOCATION="local", SEGMENTED="no", PICO_SEED="1234",
                PATH="/opt/conda/bin:" + os.environ.get("PATH", ""))
-    p = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "1", exe, "1048576", "5", algo, dtype], env=env,
+    p = _sub.run_kw(["/opt/conda/bin/mpiexec", "-n", "1", exe, "1048576", "5", algo, dtype], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
     csv = tmp_path / f"1048576_{algo}_{dtype}.csv"
@@ -681,13 +681,12 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat,
     every result against MPICH's own PMPI_* collective (pico_core_utils.c:
     553-610), aborting on a mismatch; 2 ranks share the GPU through RCCL's
     socket transport (distinct NCCL_HOSTIDs), optionally with the flat phases"""
-    import subprocess
     env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
     if flat == "dm":
         env.update(BINE_DIRECT="1")
     elif flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
-    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, count,
+    p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, count,
                         "5", algo, dtype], env=env, capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
     assert "Last Iter Time" in p.stdout
@@ -703,11 +702,10 @@ def test_reference_pico_core_c1(dev, tmp_path, algo, flat):
     checked by pico_core against MPICH's PMPI_Allreduce (pico_core_utils.c:
     553-610, 960-992); the 4 ranks share the GPU through RCCL's socket
     transport (distinct NCCL_HOSTIDs); host buffers, staged by libbine.so"""
-    import subprocess
     env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
     if flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
-    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), "4", "ALLREDUCE", "262144",
+    p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), "4", "ALLREDUCE", "262144",
                         "20", algo, "float"], env=env, capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
     assert "Last Iter Time" in p.stdout
@@ -726,11 +724,10 @@ def test_mpi_typed_entry_points_match_mpich(dev, np_, flat):
     reduce_scatter, reduce; host buffers) equal MPICH's own PMPI_* collectives
     for every order-independent (type, op) pair, and return MPI_ERR_OP where
     MPICH rejects the pair; 2 ranks share the GPU as above"""
-    import subprocess
     env = dict(os.environ, BINE_FAKE_HOSTS="1")
     if flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
-    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_)], env=env,
+    p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_)], env=env,
                        capture_output=True, text=True, timeout=150)
     assert p.returncode == 0 and "OPCHECK ok" in p.stdout, (p.stdout[-1500:], p.stderr[-1500:])
 
@@ -748,9 +745,8 @@ def test_libbine_host_buffers_freed_and_reallocated(dev, np_):
     left page-locked after a call; at P = 2 also rank 0's buffers on the
     device and rank 1's on the host in one call (allreduce and
     reduce_scatter, below and above the staging pipeline's threshold)"""
-    import subprocess
     env = dict(os.environ, BINE_FAKE_HOSTS="1", BINE_SYNC_TIMEOUT_S="60")
-    p = subprocess.run(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_), "buffer_churn"],
+    p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_), "buffer_churn"],
                        env=env, capture_output=True, text=True, timeout=150)
     print(p.stdout[-3000:])
     assert p.returncode == 0 and "CHURN ok" in p.stdout, (p.stdout[-2000:], p.stderr[-1500:])

@@ -27,6 +27,8 @@ import os
 import numpy as np
 import pytest
 
+import _sub
+
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -287,10 +289,9 @@ def test_full_size_configs_eight_processes():
     the direct peer-memory transport, the flat phases over RCCL P2P) -- every
     rank's output digest equal to the committed oracle digest of pico_core's
     inputs (tools/fullsize_multirank.py)"""
-    import subprocess
     import sys
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "fullsize_multirank.py"), "8"], env=env,
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "fullsize_multirank.py"), "8"], env=env,
                        capture_output=True, text=True, timeout=680)
     tail = "\n".join(r.stdout.splitlines()[-20:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]

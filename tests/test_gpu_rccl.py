@@ -5,7 +5,6 @@ GPU of the test box (distinct NCCL_HOSTIDs, RCCL's socket transport), checked
 bit for bit against the oracle on every rank (tools/rccl_matrix.py).  The
 8-rank run of the same matrix is in profiles/r1_rccl_matrix_1gpu.txt."""
 import os
-import subprocess
 import sys
 
 import pytest
@@ -23,7 +22,7 @@ def test_rccl_large_messages_4_ranks():
     pipelined step), every bench transport, digests vs the oracle
     (tools/rccl_large.py)"""
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "4", "double"], env=env,
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "4", "double"], env=env,
                        capture_output=True, text=True, timeout=380)
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
@@ -35,7 +34,7 @@ def test_rccl_large_messages_8_ranks():
     """the same at P = 8 in fp32 (8 processes on the box's one GPU): every transport
     incl. multi-tree and the direct peer-memory transport, eager and graph"""
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "8", "float"], env=env,
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "8", "float"], env=env,
                        capture_output=True, text=True, timeout=380)
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
@@ -44,7 +43,7 @@ def test_rccl_large_messages_8_ranks():
 
 def test_rccl_matrix_4_ranks():
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_matrix.py"), "4"], env=env,
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_matrix.py"), "4"], env=env,
                        capture_output=True, text=True, timeout=150)
     tail = "\n".join(r.stdout.splitlines()[-12:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
@@ -59,7 +58,7 @@ def test_direct_transport_orders_calls_across_streams():
     digest (tools/dm_order.py) -- the sequence bases the calls share are
     reached in call order (executor.cpp order_begin / order_end)"""
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_order.py"), "2", "8"], env=env,
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_order.py"), "2", "8"], env=env,
                        capture_output=True, text=True, timeout=280)
     tail = "\n".join(r.stdout.splitlines()[-8:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
@@ -73,7 +72,7 @@ def test_c1_four_processes_every_transport():
     over the direct transport (literal, and flat = ONE k_dm_fused launch per
     call), every output vs the committed oracle digests (tools/c1_probe.py)"""
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "c1_probe.py"), "4", "30"], env=env,
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "c1_probe.py"), "4", "30"], env=env,
                        capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + "\n" + r.stderr[-2000:]
     assert '"exitcodes": [0, 0, 0, 0]' in r.stdout
@@ -93,9 +92,12 @@ def test_staged_host_buffers_4_ranks():
     # bounded -- bine_comm_synchronize, libbine.so's drains -- and each case
     # prints a start line, so a stall names its case and stream)
     env = dict(os.environ, PYTHONPATH=ROOT, BINE_SYNC_TIMEOUT_S="60")
+    if os.environ.get("STAGED_NCCL_LOG_DIR"):   # RCCL's own log per rank (diagnostics)
+        env.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,NET,P2P,PROXY",
+                   NCCL_DEBUG_FILE=os.path.join(os.environ["STAGED_NCCL_LOG_DIR"], "nccl.%h.%p.log"))
     _sub.parent_state()
     r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "staged_check.py"), "4", "1"], env=env,
-                 timeout=170)
+                 timeout=int(os.environ.get("STAGED_TIMEOUT_S", "170")))
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=4: ok" in r.stdout
