@@ -98,13 +98,32 @@ def cpu_delta(a, b, secs):
     return out
 
 
-def run_kw(cmd, env=None, capture_output=True, text=True, timeout=None, cwd=None):
+# HW queues per rank when several ranks share the test box's one GPU: 8 in all
+# for the ranks.  The test process itself holds up to 4 more; past the GPU's
+# hardware queue slots the scheduler time-slices the queues, and a rank whose
+# queue is off the GPU stalls peers whose kernels spin waiting for it -- idle
+# queues of another process are enough (tools/contention_probe.py,
+# profiles/r4_queue_oversubscription.txt).  On a node every
+# rank has a GPU of its own and HIP's default (4) applies.
+RANK_QUEUES_TOTAL = 8
+
+
+def queues_per_rank(ranks):
+    return max(1, RANK_QUEUES_TOTAL // max(1, ranks))
+
+
+def run_kw(cmd, env=None, capture_output=True, text=True, timeout=None, cwd=None, ranks=1):
     """subprocess.run's keyword form of run() (its output always captured)"""
     assert capture_output and text
-    return run(cmd, env, timeout, cwd=cwd)
+    return run(cmd, env, timeout, cwd=cwd, ranks=ranks)
 
 
-def run(cmd, env, timeout, cwd=None):
+def run(cmd, env, timeout, cwd=None, ranks=1):
+    """ranks > 1: the command starts that many GPU processes on the one GPU;
+    unless the caller chose GPU_MAX_HW_QUEUES, each gets queues_per_rank()"""
+    if ranks > 1:
+        env = dict(os.environ if env is None else env)
+        env.setdefault("GPU_MAX_HW_QUEUES", str(queues_per_rank(ranks)))
     c0, w0 = _self_cpu(), time.time()
     s0 = _cpu_state()
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,

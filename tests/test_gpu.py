@@ -687,7 +687,7 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat,
     elif flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
     p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, count,
-                        "5", algo, dtype], env=env, capture_output=True, text=True, timeout=150)
+                        "5", algo, dtype], env=env, capture_output=True, text=True, timeout=150, ranks=np_)
     assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
     assert "Last Iter Time" in p.stdout
 
@@ -706,7 +706,7 @@ def test_reference_pico_core_c1(dev, tmp_path, algo, flat):
     if flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
     p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), "4", "ALLREDUCE", "262144",
-                        "20", algo, "float"], env=env, capture_output=True, text=True, timeout=150)
+                        "20", algo, "float"], env=env, capture_output=True, text=True, timeout=150, ranks=4)
     assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
     assert "Last Iter Time" in p.stdout
     csv = tmp_path / "data" / f"262144_{algo}_float.csv"
@@ -728,7 +728,7 @@ def test_mpi_typed_entry_points_match_mpich(dev, np_, flat):
     if flat:
         env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
     p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_)], env=env,
-                       capture_output=True, text=True, timeout=150)
+                       capture_output=True, text=True, timeout=150, ranks=np_)
     assert p.returncode == 0 and "OPCHECK ok" in p.stdout, (p.stdout[-1500:], p.stderr[-1500:])
 
 
@@ -747,7 +747,7 @@ def test_libbine_host_buffers_freed_and_reallocated(dev, np_):
     reduce_scatter, below and above the staging pipeline's threshold)"""
     env = dict(os.environ, BINE_FAKE_HOSTS="1", BINE_SYNC_TIMEOUT_S="60")
     p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_), "buffer_churn"],
-                       env=env, capture_output=True, text=True, timeout=150)
+                       env=env, capture_output=True, text=True, timeout=150, ranks=np_)
     print(p.stdout[-3000:])
     assert p.returncode == 0 and "CHURN ok" in p.stdout, (p.stdout[-2000:], p.stderr[-1500:])
     assert "same addresses: yes" in p.stdout  # glibc mmap reuse: the hazard's shape was exercised

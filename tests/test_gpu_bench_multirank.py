@@ -32,7 +32,7 @@ def test_bench_two_ranks_one_gpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "5", "--warmup", "1"]
-    r = _sub.run_kw(cmd, env=env, capture_output=True, text=True, timeout=380, cwd=ROOT)
+    r = _sub.run_kw(cmd, env=env, capture_output=True, text=True, timeout=380, cwd=ROOT, ranks=2)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]

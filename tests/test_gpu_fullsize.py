@@ -292,7 +292,7 @@ def test_full_size_configs_eight_processes():
     import sys
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "fullsize_multirank.py"), "8"], env=env,
-                       capture_output=True, text=True, timeout=680)
+                       capture_output=True, text=True, timeout=680, ranks=8)
     tail = "\n".join(r.stdout.splitlines()[-20:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=8: ok" in r.stdout

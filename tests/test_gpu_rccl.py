@@ -23,7 +23,7 @@ def test_rccl_large_messages_4_ranks():
     (tools/rccl_large.py)"""
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "4", "double"], env=env,
-                       capture_output=True, text=True, timeout=380)
+                       capture_output=True, text=True, timeout=380, ranks=4)
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=4" in r.stdout
@@ -35,7 +35,7 @@ def test_rccl_large_messages_8_ranks():
     incl. multi-tree and the direct peer-memory transport, eager and graph"""
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "8", "float"], env=env,
-                       capture_output=True, text=True, timeout=380)
+                       capture_output=True, text=True, timeout=380, ranks=8)
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=8" in r.stdout
@@ -44,7 +44,7 @@ def test_rccl_large_messages_8_ranks():
 def test_rccl_matrix_4_ranks():
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_matrix.py"), "4"], env=env,
-                       capture_output=True, text=True, timeout=150)
+                       capture_output=True, text=True, timeout=150, ranks=4)
     tail = "\n".join(r.stdout.splitlines()[-12:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=4" in r.stdout
@@ -59,7 +59,7 @@ def test_direct_transport_orders_calls_across_streams():
     reached in call order (executor.cpp order_begin / order_end)"""
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_order.py"), "2", "8"], env=env,
-                       capture_output=True, text=True, timeout=280)
+                       capture_output=True, text=True, timeout=280, ranks=2)
     tail = "\n".join(r.stdout.splitlines()[-8:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=2" in r.stdout
@@ -73,7 +73,7 @@ def test_c1_four_processes_every_transport():
     call), every output vs the committed oracle digests (tools/c1_probe.py)"""
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "c1_probe.py"), "4", "30"], env=env,
-                       capture_output=True, text=True, timeout=280)
+                       capture_output=True, text=True, timeout=280, ranks=4)
     assert r.returncode == 0, r.stdout[-3000:] + "\n" + r.stderr[-2000:]
     assert '"exitcodes": [0, 0, 0, 0]' in r.stdout
 
@@ -87,17 +87,21 @@ def test_staged_host_buffers_4_ranks():
     NaN-poisoned, again with rank 0's buffers on the device and the others'
     staged (one schedule for both), plus C3's 256 MiB per rank vs the
     committed digest (tools/staged_check.py)"""
-    # default HW queues (round 3 ran this with one queue per process after a
-    # 180 s silence in the suite; every host wait of the staged path is now
-    # bounded -- bine_comm_synchronize, libbine.so's drains -- and each case
-    # prints a start line, so a stall names its case and stream)
+    # The round-3 / round-4 silences in the suite were not a host wait: one
+    # rank's own fill kernel went unscheduled for > 60 s while its peers'
+    # kernels spun waiting for it -- more HW queues on the shared GPU than it
+    # has slots (the suite's process holds 4 more); idle queues of another
+    # process reproduce it standalone (tools/contention_probe.py, DESIGN.md
+    # §4.6).  So the ranks run with 2 queues each (_sub.queues_per_rank), every
+    # host wait of the staged path is bounded, each case prints a start line,
+    # and a time-out dumps every rank's stack and thread states.
     env = dict(os.environ, PYTHONPATH=ROOT, BINE_SYNC_TIMEOUT_S="60")
     if os.environ.get("STAGED_NCCL_LOG_DIR"):   # RCCL's own log per rank (diagnostics)
         env.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,NET,P2P,PROXY",
                    NCCL_DEBUG_FILE=os.path.join(os.environ["STAGED_NCCL_LOG_DIR"], "nccl.%h.%p.log"))
     _sub.parent_state()
     r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "staged_check.py"), "4", "1"], env=env,
-                 timeout=int(os.environ.get("STAGED_TIMEOUT_S", "170")))
+                 timeout=int(os.environ.get("STAGED_TIMEOUT_S", "170")), ranks=4)
     tail = "\n".join(r.stdout.splitlines()[-16:])
     assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
     assert "RESULT P=4: ok" in r.stdout
@@ -117,6 +121,6 @@ def test_fused_trees_vs_unfused_two_processes(mcast, merge):
     messages of its own (that launch was never issued)"""
     env = dict(os.environ, BINE_DIRECT_MCAST=mcast, BINE_DIRECT_MERGE=merge)
     r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_tree_ab.py"), "2", "16,64", "4"],
-                 env=env, timeout=170)
+                 env=env, timeout=170, ranks=2)
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

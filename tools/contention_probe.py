@@ -10,6 +10,10 @@ process may hold, one holder at a time:
   dev:G     G GiB of device memory (torch caching allocator)
   pin:G     G GiB of page-locked host memory (torch's host caching allocator)
   reg:G     G GiB of malloc'd host memory registered with hipHostRegister
+  q:N       N streams that have each run a kernel (HW queues created; the
+            holder runs with GPU_MAX_HW_QUEUES=N)
+A holder spec may end in /VAR=val,VAR=val: environment of the check's ranks
+(e.g. none/GPU_MAX_HW_QUEUES=8).
 usage: python tools/contention_probe.py HOLDER [HOLDER ...]   (one JSON line each)
 """
 import json
@@ -35,6 +39,12 @@ elif kind == "dev":
     for _ in range(max(1, n // step)):
         keep.append(torch.empty(step, dtype=torch.uint8, device="cuda"))
     torch.cuda.synchronize()
+elif kind == "q":
+    keep = [torch.cuda.Stream() for _ in range(int(g))]
+    for s in keep:
+        with torch.cuda.stream(s):
+            torch.ones(1024, device="cuda").sum()
+    torch.cuda.synchronize()
 elif kind == "pin":
     step = 256 << 20
     for _ in range(max(1, n // step)):
@@ -56,23 +66,28 @@ time.sleep(600)
 
 
 def probe(spec):
-    kind, _, g = spec.partition(":")
+    hspec, _, renv = spec.partition("/")
+    kind, _, g = hspec.partition(":")
     holder = None
     line = ""
     if kind != "none":
+        henv = dict(os.environ, GPU_MAX_HW_QUEUES=g) if kind == "q" else None
         holder = subprocess.Popen([sys.executable, "-c", HOLD, kind, g or "0"], stdout=subprocess.PIPE, text=True,
-                                  start_new_session=True)
+                                  start_new_session=True, env=henv)
         line = holder.stdout.readline().strip()
     t0 = time.time()
     env = dict(os.environ, PYTHONPATH=ROOT, BINE_SYNC_TIMEOUT_S="60")
+    env.update(dict(x.split("=", 1) for x in renv.split(",") if x))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _sub
     try:
         r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "staged_check.py"), "4", "1"], env=env,
-                     timeout=150)
+                     timeout=90)
         rc, tail = r.returncode, r.stdout.splitlines()[-1:]
     except AssertionError as e:
-        rc, tail = "timeout", str(e).splitlines()[-30:]
+        txt = str(e)
+        rc, tail = "timeout", [ln for ln in txt.splitlines() if "start" in ln or "ok" in ln][-8:] + \
+            txt[txt.find("threads of the group"):].splitlines()[:60]
     dt = time.time() - t0
     if holder:
         os.killpg(holder.pid, 9)
