@@ -466,7 +466,7 @@ def bench_n1(steps: int, warmup: int, want_cpu: bool, cpu_budget: float):
                      "us_per_launch": round(st_k["region_ms"] * 1e3, 3),
                      "note": "achieved = 2 S (read sbuf + write rbuf) / the average launch duration: K calls "
                              "(one k_copy launch each) back to back between one HIP event pair on the launch "
-                             "stream (agrees with the kernel-trace average, profiles/r2_bench_kernel_stats.csv); "
+                             "stream (agrees with the kernel-trace average, profiles/r4_bench_kernel_stats.csv); "
                              "traffic = PMC FETCH_SIZE x 2 (gfx950) + WRITE_SIZE per launch "
                              "(profiles/latest_pmc.json)"},
         "wall_s": round(st["wall_s"], 4),

@@ -136,7 +136,7 @@ def run(cmd, env, timeout, cwd=None, ranks=1):
                                 capture_output=True, text=True, timeout=20).stdout
         except Exception as e:  # noqa: BLE001 -- diagnostics only
             ps = f"(ps failed: {e})"
-        threads = _group_threads(p.pid)
+        threads = _group_threads(p.pid) + "\n" + kfd_queues()
         sockets = _sockets()
         try:
             os.killpg(p.pid, signal.SIGUSR1)
@@ -157,11 +157,21 @@ def run(cmd, env, timeout, cwd=None, ranks=1):
     return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
+def kfd_queues():
+    sys_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools")
+    import sys
+    if sys_path not in sys.path:
+        sys.path.insert(0, sys_path)
+    import kfd_queues as K
+    return K.summary()
+
+
 def parent_state():
     """what this (pytest) process holds on the GPU and in page-locked host
     memory, printed before a multi-process check (shown with its failure)"""
     import sys
     print("parent: " + _sockets().replace("\n", "; "), flush=True)
+    print("parent: " + kfd_queues(), flush=True)
     torch = sys.modules.get("torch")
     if torch is None or not torch.cuda.is_initialized():
         print("parent: no GPU context", flush=True)
