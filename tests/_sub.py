@@ -98,14 +98,18 @@ def cpu_delta(a, b, secs):
     return out
 
 
-# HW queues per rank when several ranks share the test box's one GPU: 8 in all
-# for the ranks.  The test process itself holds up to 4 more; past the GPU's
-# hardware queue slots the scheduler time-slices the queues, and a rank whose
-# queue is off the GPU stalls peers whose kernels spin waiting for it -- idle
-# queues of another process are enough (tools/contention_probe.py,
-# profiles/r4_queue_oversubscription.txt).  On a node every
-# rank has a GPU of its own and HIP's default (4) applies.
-RANK_QUEUES_TOTAL = 8
+# HW queues per rank when several ranks share the test box's one GPU: 4 per
+# stream priority in all for the ranks (HIP keeps a pool of GPU_MAX_HW_QUEUES
+# queues per priority, plus one: tools/kfd_queues.py).  The test process holds
+# its own (tests/conftest.py: 2 per priority); past the GPU's hardware queue
+# slots the scheduler time-slices the queues, and a rank whose queue is off
+# the GPU stalls peers whose kernels spin waiting for it -- idle queues of
+# another process are enough (tools/contention_probe.py,
+# profiles/r4_queue_oversubscription.txt).  The box exports
+# GPU_MAX_HW_QUEUES=4, so the rank value is set, not defaulted
+# (BINE_TEST_RANK_QUEUES overrides).  On a node every rank has a GPU of its
+# own and HIP's default applies.
+RANK_QUEUES_TOTAL = 4
 
 
 def queues_per_rank(ranks):
@@ -120,10 +124,10 @@ def run_kw(cmd, env=None, capture_output=True, text=True, timeout=None, cwd=None
 
 def run(cmd, env, timeout, cwd=None, ranks=1):
     """ranks > 1: the command starts that many GPU processes on the one GPU;
-    unless the caller chose GPU_MAX_HW_QUEUES, each gets queues_per_rank()"""
+    each gets queues_per_rank() HW queues per priority"""
     if ranks > 1:
         env = dict(os.environ if env is None else env)
-        env.setdefault("GPU_MAX_HW_QUEUES", str(queues_per_rank(ranks)))
+        env["GPU_MAX_HW_QUEUES"] = os.environ.get("BINE_TEST_RANK_QUEUES", str(queues_per_rank(ranks)))
     c0, w0 = _self_cpu(), time.time()
     s0 = _cpu_state()
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
