@@ -337,21 +337,21 @@ int bine_comm_set_flat_rs(bine_comm_t comm, int on);
  * communicator, at the same point).  Sequence numbers live in device memory,
  * so graph mode captures and replays these collectives too.  At most 4
  * messages to one peer per exchange group
- * (BINE_ERR_UNSUPPORTED beyond).  Knobs: BINE_DIRECT_SLOT_BYTES (16 MiB),
- * BINE_DIRECT_WGS (workgroups per message, 32), BINE_DIRECT_MERGE (launch
+ * (BINE_ERR_UNSUPPORTED beyond).  Knobs: BINE_DIRECT_SLOT_BYTES (64 MiB),
+ * BINE_DIRECT_WGS (workgroups per message, 128), BINE_DIRECT_MERGE (launch
  * structure: 3 = the mix above, 2 = one launch per round, 1 = pipelined, 0 =
  * separate push and pull launches).  At most 64 ranks.  Loopback:
  * UNSUPPORTED. */
 int bine_comm_set_direct(bine_comm_t comm, int on);
 /* Workgroups per message of the direct transport's copy launches (0: the
- * default, BINE_DIRECT_WGS or 32).  Local, not collective; drops cached graphs
+ * default, BINE_DIRECT_WGS or 128).  Local, not collective; drops cached graphs
  * (their launches carry the old grid).  bench.py trials it on the node. */
 int bine_comm_set_direct_wgs(bine_comm_t comm, int wgs);
 /* Direct transport: the flat reduce-scatter's trees evaluated inside the
  * exchange launches (on >= 1: the leaves read in place in the inbox slots,
  * each tree in the first launch of the exchange after the one that receives
  * its leaves, or in its own -- the default; on >= 2 also sets the tree
- * workgroups per launch (1: BINE_DIRECT_TREE_WGS, 64); 0: pull copies into
+ * workgroups per launch (1: BINE_DIRECT_TREE_WGS, 256); 0: pull copies into
  * the staging area + a separate tree launch; -1: BINE_DIRECT_TREE, default
  * on).  Bit-identical either way.  Collective: every rank must use the same
  * setting (it decides in which launch a leaf is pulled).  Local call; drops
@@ -382,7 +382,9 @@ int bine_comm_direct_stamps(bine_comm_t comm, uint64_t *out, size_t cap, size_t 
  * Schedules on two streams (graphs with parallel branches) are captured only
  * on HIP runtimes >= 7.2; on older ones (torch's bundled 7.0) they run
  * eagerly: that runtime's hipGraphLaunch crashes on such graphs when their
- * streams share one hardware queue (tools/graph_fork_repro.cpp).
+ * streams share one hardware queue (tools/graph_fork_repro.cpp); with
+ * GPU_MAX_HW_QUEUES=1 on such a runtime nothing is captured (RCCL forks
+ * streams of its own inside a capture).
  * Off by default (BINE_GRAPHS=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_graphs(bine_comm_t comm, int on);
 

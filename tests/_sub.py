@@ -98,22 +98,24 @@ def cpu_delta(a, b, secs):
     return out
 
 
-# HW queues per rank when several ranks share the test box's one GPU: 4 per
-# stream priority in all for the ranks (HIP keeps a pool of GPU_MAX_HW_QUEUES
-# queues per priority, plus one: tools/kfd_queues.py).  The test process holds
-# its own (tests/conftest.py: 2 per priority); past the GPU's hardware queue
+# HW queues per stream priority for each rank when several ranks share the
+# test box's one GPU (HIP keeps a pool of GPU_MAX_HW_QUEUES queues per
+# priority, plus one: tools/kfd_queues.py).  Past the GPU's hardware queue
 # slots the scheduler time-slices the queues, and a rank whose queue is off
 # the GPU stalls peers whose kernels spin waiting for it -- idle queues of
 # another process are enough (tools/contention_probe.py,
-# profiles/r4_queue_oversubscription.txt).  The box exports
-# GPU_MAX_HW_QUEUES=4, so the rank value is set, not defaulted
-# (BINE_TEST_RANK_QUEUES overrides).  On a node every rank has a GPU of its
-# own and HIP's default applies.
-RANK_QUEUES_TOTAL = 4
+# profiles/r4_queue_oversubscription.txt).  Measured in the
+# suite (the test process at 2, tests/conftest.py): 4 ranks at HIP's 4 ran
+# 3-10x slow and stalled the staged check, at 1 they run as fast as alone;
+# 8 ranks at 1 took 4-7x longer than at 4 (one queue serialises each rank's
+# RCCL, copy and reduction launches).  The box exports GPU_MAX_HW_QUEUES=4,
+# so the value is set, not defaulted (BINE_TEST_RANK_QUEUES overrides).  On a
+# node every rank has a GPU of its own and HIP's default applies.
+RANK_QUEUES = {2: 4, 3: 1, 4: 1}
 
 
 def queues_per_rank(ranks):
-    return max(1, RANK_QUEUES_TOTAL // max(1, ranks))
+    return RANK_QUEUES.get(ranks, 4)
 
 
 def run_kw(cmd, env=None, capture_output=True, text=True, timeout=None, cwd=None, ranks=1):
