@@ -9,7 +9,7 @@ the committed oracle digests.  Meant to run under
   rocprofv3 --kernel-trace --marker-trace --stats -- python3 tools/c1_probe.py 4
 with BINE_ROCTX=1, so the trace shows each step's kernel time and the host's
 issue ranges (profiles/r2_c1_*).
-usage: python tools/c1_probe.py [P] [iters]
+usage: python tools/c1_probe.py [P] [iters] [MODE,MODE...]   (default: direct,flatrs+flat,direct+dm,flatrs+flat+dm)
 """
 import json
 import os
@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(rank, P, iters, port, q):
+def worker(rank, P, iters, port, q, modes=("direct", "flatrs+flat", "direct+dm", "flatrs+flat+dm")):
     os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
@@ -40,7 +40,7 @@ def worker(rank, P, iters, port, q):
     res = {}
     # +dm: the direct peer-memory transport; with the flat phases a C1 call is
     # then ONE k_dm_fused launch (BINE_DIRECT_FUSED=0: the primitives one by one)
-    for mode in ("direct", "flatrs+flat", "direct+dm", "flatrs+flat+dm"):
+    for mode in modes:
         bench.apply_transport(comm, mode, 0)
         for algo in ("bine_bdw_remap", "bine_lat"):
             st = bench.timed(torch, stream,
@@ -62,7 +62,8 @@ if __name__ == "__main__":
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, P, iters, 29601, q)) for r in range(P)]
+    modes = tuple(sys.argv[3].split(",")) if len(sys.argv) > 3 else ("direct", "flatrs+flat", "direct+dm", "flatrs+flat+dm")
+    ps = [ctx.Process(target=worker, args=(r, P, iters, 29601, q, modes)) for r in range(P)]
     for p in ps:
         p.start()
     for p in ps:
