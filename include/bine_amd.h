@@ -382,9 +382,10 @@ int bine_comm_direct_stamps(bine_comm_t comm, uint64_t *out, size_t cap, size_t 
  * Schedules on two streams (graphs with parallel branches) are captured only
  * on HIP runtimes >= 7.2; on older ones (torch's bundled 7.0) they run
  * eagerly: that runtime's hipGraphLaunch crashes on such graphs when their
- * streams share one hardware queue (tools/graph_fork_repro.cpp); with
- * GPU_MAX_HW_QUEUES=1 on such a runtime nothing is captured (RCCL forks
- * streams of its own inside a capture).
+ * streams share one hardware queue (tools/graph_fork_repro.cpp).  RCCL forks
+ * streams of its own inside a capture, so on such a runtime only
+ * single-stream calls over the direct transport are captured (and none
+ * under GPU_MAX_HW_QUEUES=1).
  * Off by default (BINE_GRAPHS=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_graphs(bine_comm_t comm, int on);
 

@@ -1339,18 +1339,25 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
 // libbine-free repro tools/graph_fork_repro.{cpp,py}, symbolised stack and
 // disassembly in profiles/r4_graph_fork_repro.txt.  /opt/rocm's 7.2 runtime
 // (libbine.so under pico_core) replays the same graph.  On 7.0 a multi-stream
-// schedule therefore runs eagerly in graph mode; single-stream schedules (the
-// small, launch-bound collectives a replay is for) are captured -- except
-// under GPU_MAX_HW_QUEUES=1, where even they may branch: RCCL forks its own
-// streams inside a capture (the 4-process RCCL matrix's graph pass crashed so
-// on 7.0 with one queue per process), so on 7.0 with one queue nothing is
-// captured.
+// schedule therefore runs eagerly in graph mode, and so does every schedule
+// with RCCL calls in it: RCCL forks streams of its own inside a capture, so
+// even a single-stream schedule becomes a graph with parallel branches (the
+// 4-process RCCL matrix's graph pass crashed on 7.0 with 1 and with 2 HW
+// queues per process).  What 7.0 captures: single-stream schedules over the
+// direct transport (our kernels only, one branch), not under
+// GPU_MAX_HW_QUEUES=1.
 static bool multi_branch_graphs_ok() {
   static const bool v = [] {
     int rt = 0;
     return hipRuntimeGetVersion(&rt) == hipSuccess && rt >= 70200000;
   }();
   return v;
+}
+// the call makes no RCCL calls: one rank (no exchanges), or its exchanges go
+// to the direct transport (not poisoned)
+static bool rccl_free(const bine_comm *c) {
+  const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
+  return c->size == 1 || (rt && rt->dm_on && rt->dm && !rt->dm->poisoned());
 }
 static bool one_hw_queue() {
   static const bool v = getenv("GPU_MAX_HW_QUEUES") && atoi(getenv("GPU_MAX_HW_QUEUES")) == 1;
@@ -1426,7 +1433,7 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   rc = order_begin(c, K);
   if (rc) {
   } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && !stg &&
-             (multi_branch_graphs_ok() || ((single || (tpl && tpl->solo)) && !one_hw_queue())))
+             (multi_branch_graphs_ok() || ((single || (tpl && tpl->solo)) && rccl_free(c) && !one_hw_queue())))
     rc = run_graph(c, key, sc, src, rbuf, a.esz, dtype, op, K, single, tpl);
   else
     rc = execute(c, sc, src, rbuf, a.esz, dtype, op, K, single, false, stg, tpl);
