@@ -106,17 +106,17 @@ def cpu_delta(a, b, secs):
 # another process are enough (tools/contention_probe.py,
 # profiles/r4_queue_oversubscription.txt).  Measured in the
 # suite (the test process at 2, tests/conftest.py): 4 ranks at HIP's 4 ran
-# 3-10x slow and stalled the staged check, at 1 they run as fast as alone;
-# 8 ranks: 59 s / 25 s (the two 8-rank checks) at 4, 117 s / 74 s at 1 (one
-# queue serialises each rank's RCCL, copy and reduction launches), 18 s / 8 s
-# at 2.  The box exports GPU_MAX_HW_QUEUES=4,
-# so the value is set, not defaulted (BINE_TEST_RANK_QUEUES overrides).  On a
-# node every rank has a GPU of its own and HIP's default applies.
-RANK_QUEUES = {2: 4, 3: 1, 4: 1}
+# 3-10x slow and stalled the staged check; every rank count at 2 runs as fast
+# as alone (the whole suite in 286 s, profiles/r4_gpu_suite.txt); 8 ranks at
+# 1 took 4-7x longer (one queue serialises each rank's RCCL, copy and
+# reduction launches).  The box exports GPU_MAX_HW_QUEUES=4, so the value is
+# set, not defaulted (BINE_TEST_RANK_QUEUES overrides).  On a node every rank
+# has a GPU of its own and HIP's default applies.
+RANK_QUEUES = 2
 
 
 def queues_per_rank(ranks):
-    return RANK_QUEUES.get(ranks, 2)
+    return RANK_QUEUES
 
 
 def run_kw(cmd, env=None, capture_output=True, text=True, timeout=None, cwd=None, ranks=1):

@@ -92,7 +92,7 @@ def test_staged_host_buffers_4_ranks():
     # kernels spun waiting for it -- more HW queues on the shared GPU than it
     # has slots (the suite's process holds 4 more); idle queues of another
     # process reproduce it standalone (tools/contention_probe.py, DESIGN.md
-    # §4.6).  So the ranks run with one queue each (_sub.queues_per_rank), every
+    # §4.6).  So the ranks run with 2 queues each (_sub.queues_per_rank), every
     # host wait of the staged path is bounded, each case prints a start line,
     # and a time-out dumps every rank's stack and thread states.
     env = dict(os.environ, PYTHONPATH=ROOT, BINE_SYNC_TIMEOUT_S="60")
