@@ -383,9 +383,9 @@ int bine_comm_direct_stamps(bine_comm_t comm, uint64_t *out, size_t cap, size_t 
  * on HIP runtimes >= 7.2; on older ones (torch's bundled 7.0) they run
  * eagerly: that runtime's hipGraphLaunch crashes on such graphs when their
  * streams share one hardware queue (tools/graph_fork_repro.cpp).  RCCL forks
- * streams of its own inside a capture, so on such a runtime only
- * single-stream calls over the direct transport are captured (and none
- * under GPU_MAX_HW_QUEUES=1).
+ * streams of its own inside a capture, so on such a runtime single-stream
+ * calls are captured over the direct transport with GPU_MAX_HW_QUEUES >= 2
+ * and over RCCL with >= 4 (HIP's default); the rest runs eagerly.
  * Off by default (BINE_GRAPHS=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_graphs(bine_comm_t comm, int on);
 

@@ -1343,9 +1343,10 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
 // with RCCL calls in it: RCCL forks streams of its own inside a capture, so
 // even a single-stream schedule becomes a graph with parallel branches (the
 // 4-process RCCL matrix's graph pass crashed on 7.0 with 1 and with 2 HW
-// queues per process).  What 7.0 captures: single-stream schedules over the
-// direct transport (our kernels only, one branch), not under
-// GPU_MAX_HW_QUEUES=1.
+// queues per process; it replays with HIP's default 4, where some parallel
+// stream lands on another queue).  What 7.0 captures: single-stream
+// schedules over the direct transport (our kernels only, one branch) with at
+// least 2 HW queues, and single-stream RCCL schedules with at least 4.
 static bool multi_branch_graphs_ok() {
   static const bool v = [] {
     int rt = 0;
@@ -1359,8 +1360,9 @@ static bool rccl_free(const bine_comm *c) {
   const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
   return c->size == 1 || (rt && rt->dm_on && rt->dm && !rt->dm->poisoned());
 }
-static bool one_hw_queue() {
-  static const bool v = getenv("GPU_MAX_HW_QUEUES") && atoi(getenv("GPU_MAX_HW_QUEUES")) == 1;
+// HIP's hardware queues per stream priority (GPU_MAX_HW_QUEUES, default 4)
+static int hw_queues() {
+  static const int v = getenv("GPU_MAX_HW_QUEUES") ? atoi(getenv("GPU_MAX_HW_QUEUES")) : 4;
   return v;
 }
 
@@ -1433,7 +1435,8 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   rc = order_begin(c, K);
   if (rc) {
   } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && !stg &&
-             (multi_branch_graphs_ok() || ((single || (tpl && tpl->solo)) && rccl_free(c) && !one_hw_queue())))
+             (multi_branch_graphs_ok() ||
+              ((single || (tpl && tpl->solo)) && hw_queues() >= (rccl_free(c) ? 2 : 4))))
     rc = run_graph(c, key, sc, src, rbuf, a.esz, dtype, op, K, single, tpl);
   else
     rc = execute(c, sc, src, rbuf, a.esz, dtype, op, K, single, false, stg, tpl);

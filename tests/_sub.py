@@ -119,18 +119,19 @@ def queues_per_rank(ranks):
     return RANK_QUEUES
 
 
-def run_kw(cmd, env=None, capture_output=True, text=True, timeout=None, cwd=None, ranks=1):
+def run_kw(cmd, env=None, capture_output=True, text=True, timeout=None, cwd=None, ranks=1, queues=None):
     """subprocess.run's keyword form of run() (its output always captured)"""
     assert capture_output and text
-    return run(cmd, env, timeout, cwd=cwd, ranks=ranks)
+    return run(cmd, env, timeout, cwd=cwd, ranks=ranks, queues=queues)
 
 
-def run(cmd, env, timeout, cwd=None, ranks=1):
+def run(cmd, env, timeout, cwd=None, ranks=1, queues=None):
     """ranks > 1: the command starts that many GPU processes on the one GPU;
-    each gets queues_per_rank() HW queues per priority"""
+    each gets `queues` (default queues_per_rank()) HW queues per priority"""
     if ranks > 1:
         env = dict(os.environ if env is None else env)
-        env["GPU_MAX_HW_QUEUES"] = os.environ.get("BINE_TEST_RANK_QUEUES", str(queues_per_rank(ranks)))
+        env["GPU_MAX_HW_QUEUES"] = str(queues) if queues else os.environ.get("BINE_TEST_RANK_QUEUES",
+                                                                              str(queues_per_rank(ranks)))
     c0, w0 = _self_cpu(), time.time()
     s0 = _cpu_state()
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,

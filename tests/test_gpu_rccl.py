@@ -29,6 +29,21 @@ def test_rccl_large_messages_4_ranks():
     assert "RESULT P=4" in r.stdout
 
 
+@pytest.mark.timeout(300)
+def test_rccl_graph_replay_hip_default_queues():
+    """graph mode over RCCL with HIP's default 4 HW queues per process (a
+    node's setting): on torch's HIP 7.0 single-stream RCCL schedules are
+    captured only there (executor.cpp multi_branch_graphs_ok / hw_queues);
+    2 processes, 64 MiB fp32, every transport eager and graph
+    (tools/rccl_large.py)"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_large.py"), "2", "float"], env=env,
+                    capture_output=True, text=True, timeout=280, ranks=2, queues=4)
+    tail = "\n".join(r.stdout.splitlines()[-16:])
+    assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
+    assert "RESULT P=2" in r.stdout
+
+
 @pytest.mark.timeout(400)
 def test_rccl_large_messages_8_ranks():
     """the same at P = 8 in fp32 (8 processes on the box's one GPU): every transport
