@@ -72,8 +72,9 @@ def worker(rank, P, port, want, dts, q):
     comm = pico_amd.Comm.from_torch_distributed(0)
     bad, n_ok = [], 0
     side = torch.cuda.Stream()   # graph mode needs a non-NULL caller stream
-    modes = [m for m in MODES if m in bench.transport_modes("auto", P) or m in ("flatrs+flat+a2a", "relay+flat+dm",
-                                                                              "trees+dm")]
+    modes = [m for m in MODES if (m in bench.transport_modes("auto", P) or m in ("flatrs+flat+a2a", "relay+flat+dm",
+                                                                               "trees+dm"))
+             and (P in (4, 8) or not m.startswith("trees"))]   # multi-tree: P = 4, 8 only
     for dt, n in ARS:
         if dt not in dts:
             continue
