@@ -11,7 +11,11 @@ Configuration set "pipeline" (5th argument; floating point at P > 1): the
 serial path (BINE_STAGE_PIPELINE=0: H2D, then the collective, then D2H)
 against the staging pipelined into the collective (bine_allreduce_staged)
 at several chunks.
-usage: python tools/e2e_staging.py [NP] [DTYPE] [COUNT] [ITERS] [chunks|pipeline]"""
+Configuration set "c1" (BASELINE config C1: 262,144 fp32 per rank at P = 4,
+the reference's own CPU-runnable case): the transports libbine.so offers --
+RCCL, RCCL with the flat phases, the direct transport, the direct transport
+with the flat phases (one k_dm_fused launch per call).
+usage: python tools/e2e_staging.py [NP] [DTYPE] [COUNT] [ITERS] [chunks|pipeline|c1]"""
 import json
 import os
 import statistics
@@ -33,9 +37,9 @@ def run(np_, dtype, count, iters, env_extra):
         if p.returncode != 0:
             return {"error": (p.stdout[-400:] + p.stderr[-400:])}
         rows = open(os.path.join(tmp, "data", f"{count}_bine_bdw_remap_over_{dtype}.csv")).read().splitlines()[1:]
-        hi = [int(r.split(",")[0]) * 1e-6 for r in rows]   # ns -> ms
+        hi = [float(r.split(",")[0]) * 1e-6 for r in rows]   # ns -> ms
         kept = hi[int(len(hi) * 0.2):]
-        return {"ms_median": round(statistics.median(kept), 3), "ms_min": round(min(kept), 3), "iters": len(hi),
+        return {"ms_median": round(statistics.median(kept), 4), "ms_min": round(min(kept), 4), "iters": len(hi),
                 "pico_core_check": "passed"}
 
 
@@ -63,6 +67,12 @@ if __name__ == "__main__":
                 ("pipelined, 32 MiB rounds", {"BINE_STAGE_CHUNK_BYTES": str(32 << 20)}),
                 ("pipelined, 64 MiB rounds", {"BINE_STAGE_CHUNK_BYTES": str(64 << 20)})]
         out["transport"] = "direct peer memory (BINE_DIRECT=1)" if os.environ.get("BINE_DIRECT") == "1" else "RCCL"
+    if len(sys.argv) > 5 and sys.argv[5] == "c1":
+        flat = {"BINE_FLAT_RS": "1", "BINE_FLAT_AG": "1"}
+        cfgs = [("RCCL", {}), ("RCCL, flat phases", flat), ("direct transport", {"BINE_DIRECT": "1"}),
+                ("direct transport, flat phases (one k_dm_fused launch)", dict(flat, BINE_DIRECT="1")),
+                ("RCCL, flat phases, pageable (BINE_HOST_REGISTER=0)", dict(flat, BINE_HOST_REGISTER="0")),
+                ("direct transport, flat phases, pageable", dict(flat, BINE_DIRECT="1", BINE_HOST_REGISTER="0"))]
     for name, env in cfgs:
         r = run(np_, dtype, count, iters, env)
         if "ms_median" in r:
