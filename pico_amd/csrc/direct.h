@@ -69,6 +69,13 @@ struct DirectState {
                 const TreeSpec &dtree) const;
   int tree_wgs = 256;  // tree workgroups per launch (BINE_DIRECT_TREE_WGS; bine_comm_set_direct_tree)
   int tree_wgs_env = 256;  // the value init() settled on
+  bool wgs_set = false, tree_wgs_set = false;  // given by the environment (not scaled below)
+  // `share` ranks of this transport on this rank's GPU (only where several
+  // processes share one device): above 2, the default workgroup counts are
+  // cut by share / 2 -- every co-located rank's exchange launch competes for
+  // the same chip's workgroup slots, and waiting workgroups hold slots the
+  // pushes they wait for need.  On a node share is 1.
+  void scale_for_shared_gpu(int share);
   bool mcast = false;     // pushes of the same bytes to several peers as one group (BINE_DIRECT_MCAST=1;
                           // off: no gain measured, profiles/r3_push_groups.txt)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }

@@ -156,6 +156,31 @@ struct RcclTransport final : Transport {
     *all = v;
     return BINE_SUCCESS;
   }
+  // how many ranks of this communicator run on this rank's GPU (same host
+  // name and PCI bus id): more than one only when processes share a device
+  int ranks_on_my_gpu(int device, int *same) {
+    char bus[64] = {0}, host[256] = {0};
+    (void)hipDeviceGetPCIBusId(bus, sizeof bus, device);
+    (void)hipGetLastError();
+    gethostname(host, sizeof host - 1);
+    uint64_t h = 1469598103934665603ull;  // FNV-1a of "host/bus"
+    for (const char *s : {(const char *)host, "/", (const char *)bus})
+      for (; *s; s++) h = (h ^ (uint8_t)*s) * 1099511628211ull;
+    uint64_t *d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)size * sizeof(uint64_t)));
+    hipError_t e = hipMemcpy(d + rank, &h, sizeof h, hipMemcpyHostToDevice);
+    ncclResult_t nr = ncclSuccess;
+    if (e == hipSuccess) nr = ncclAllGather(d + rank, d, 1, ncclUint64, comm, nullptr);
+    if (e == hipSuccess && nr == ncclSuccess) e = hipStreamSynchronize(nullptr);
+    std::vector<uint64_t> all((size_t)size);
+    if (e == hipSuccess && nr == ncclSuccess) e = hipMemcpy(all.data(), d, all.size() * sizeof(uint64_t),
+                                                            hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    NCCL_TRY(nr);
+    HIP_TRY(e);
+    *same = (int)std::count(all.begin(), all.end(), h);
+    return BINE_SUCCESS;
+  }
   // bine_comm_set_direct: exchanges through mapped peer memory (direct.cpp)
   std::unique_ptr<DirectState> dm;
   bool dm_on = false;
@@ -2128,6 +2153,9 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
       set_err("direct transport unavailable on some rank: %s", err.empty() ? "(a peer failed)" : err.c_str());
       return BINE_ERR_UNSUPPORTED;
     }
+    int same = 1;
+    if (int rc3 = r->ranks_on_my_gpu(c->device, &same)) return rc3;
+    d->scale_for_shared_gpu(same);
     if (r->dm_wgs) d->wgs = r->dm_wgs;
     if (c->dm_tree_wgs) d->tree_wgs = c->dm_tree_wgs;
     r->dm = std::move(d);
