@@ -1007,6 +1007,14 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         trial((best[0], best[1], True))
         if trials[(best[0], best[1], True)] < trials.get(best, float("inf")):
             best = (best[0], best[1], True)
+    if dm_dead and dm_wgs(best[0]) is not None:
+        # a direct transport that timed out in a later trial cannot be set
+        # again on this communicator (it stays poisoned): the pick falls back
+        # to the fastest checked setting without it
+        ok_c = [c for c, v in trials.items() if v != float("inf") and dm_wgs(c[0]) is None]
+        best = min(ok_c, key=trials.get) if ok_c else base_cfg
+        if rank == 0:
+            print(f"bench: the direct transport failed in trial {dm_dead[0]}; picking {tname(best)}", file=sys.stderr)
     run1 = None
     if best != base_cfg:
         apply_transport(comm, *best)
@@ -1054,7 +1062,13 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
                                                            chosen, chunk, graphs, not dm_dead)) if extras else {}
-    apply_transport(comm, chosen, chunk, graphs)
+    try:
+        apply_transport(comm, chosen, chunk, graphs)
+    except pico_amd.BineError as e:   # the direct transport timed out in a side measurement: RCCL from here on
+        if rank == 0:
+            print(f"bench: {tname(best)} unavailable after the side measurements ({e}); RCCL P2P for the rest",
+                  file=sys.stderr)
+        apply_transport(comm, "direct", chunk, False)
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}
     vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
