@@ -163,10 +163,10 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
     return BINE_ERR_UNSUPPORTED;
   }
   if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
-  if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e), wgs_set = true;
+  if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
   if (const char *e = getenv("BINE_DIRECT_PULL_WGS")) pull_wgs = std::max(0, atoi(e));
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
-  if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e)), tree_wgs_set = true;
+  if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
   if (const char *e = getenv("BINE_DIRECT_MCAST")) mcast = atoi(e) != 0;
   tree_wgs_env = tree_wgs;
   if (slot < (1 << 20)) slot = 1 << 20;
@@ -226,10 +226,10 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   return BINE_SUCCESS;
 }
 
-void DirectState::scale_for_shared_gpu(int share) {
-  if (share <= 2) return;
-  if (!wgs_set) env_wgs = wgs = std::max(16, wgs * 2 / share);
-  if (!tree_wgs_set) tree_wgs_env = tree_wgs = std::max(32, tree_wgs * 2 / share);
+void DirectState::scale_for_shared_gpu(int s) {
+  share = s;
+  env_wgs = wgs = scaled(wgs, 16);
+  tree_wgs_env = tree_wgs = scaled(tree_wgs, 32);
 }
 
 // Phase 2 (after every rank's phase 1 succeeded -- the caller agrees on that

@@ -2156,8 +2156,8 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
     int same = 1;
     if (int rc3 = r->ranks_on_my_gpu(c->device, &same)) return rc3;
     d->scale_for_shared_gpu(same);
-    if (r->dm_wgs) d->wgs = r->dm_wgs;
-    if (c->dm_tree_wgs) d->tree_wgs = c->dm_tree_wgs;
+    if (r->dm_wgs) d->wgs = d->scaled(r->dm_wgs, 16);
+    if (c->dm_tree_wgs) d->tree_wgs = d->scaled(c->dm_tree_wgs, 32);
     r->dm = std::move(d);
   }
   if (on && r->dm->poisoned()) {
@@ -2199,7 +2199,7 @@ int bine_comm_set_direct_wgs(bine_comm_t c, int wgs) {
   HIP_TRY(hipDeviceSynchronize());  // no launch of the old shape may still run
   c->drop_graphs();                 // captured direct launches carry the old grid
   r->dm_wgs = wgs;
-  if (r->dm) r->dm->wgs = wgs ? wgs : r->dm->env_wgs;
+  if (r->dm) r->dm->wgs = wgs ? r->dm->scaled(wgs, 16) : r->dm->env_wgs;
   return BINE_SUCCESS;
 }
 
@@ -2215,7 +2215,7 @@ int bine_comm_set_direct_tree(bine_comm_t c, int on) {
   c->dm_tree = v;
   c->dm_tree_wgs = w;
   if (auto *r = dynamic_cast<RcclTransport *>(c->tx.get()))
-    if (r->dm) r->dm->tree_wgs = w ? w : r->dm->tree_wgs_env;
+    if (r->dm) r->dm->tree_wgs = w ? r->dm->scaled(w, 32) : r->dm->tree_wgs_env;
   return BINE_SUCCESS;
 }
 
