@@ -1068,6 +1068,28 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
     if (c->prof.size() < sc.ops.size()) c->prof.resize(sc.ops.size());
     c->prof_n = sc.ops.size();
   }
+  // profile events of op i on stream s (begin: its fields and start event)
+  auto prof_begin = [&](size_t i, hipStream_t s) -> int {
+    const SOp &o = sc.ops[i];
+    auto &pt = c->prof[i];
+    if (!pt.a) HIP_TRY(hipEventCreate(&pt.a));
+    if (!pt.b) HIP_TRY(hipEventCreate(&pt.b));
+    pt.xchg = o.xchg ? 1 : 0;
+    pt.nprims = (int)o.prims.size();
+    pt.bytes = 0;
+    for (const Prim &x : o.prims) {  // exchanges: bytes sent; local ops: algorithmic HBM bytes
+      if (x.type == BINE_PRIM_SEND) pt.bytes += x.count * esz;
+      else if (x.type == BINE_PRIM_REDUCE || x.type == BINE_PRIM_REDUCE3) pt.bytes += 3 * x.count * esz;
+      else if (x.type == BINE_PRIM_REDUCE_TREE) pt.bytes += (uint64_t)(x.peer + 1) * x.count * esz;
+      else if (x.type == BINE_PRIM_COPY) pt.bytes += 2 * x.count * esz;
+    }
+    HIP_TRY(hipEventRecord(pt.a, s));
+    return BINE_SUCCESS;
+  };
+  auto prof_end = [&](size_t i, hipStream_t s) -> int {
+    HIP_TRY(hipEventRecord(c->prof[i].b, s));
+    return BINE_SUCCESS;
+  };
   std::vector<XSend> &sends = c->xs;
   std::vector<XRecv> &recvs = c->xr;
   // staging: the input buffer's device copy (SBUF, or RBUF in place) and the
@@ -1098,11 +1120,21 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       }
       static const std::vector<XSend> no_s;
       static const std::vector<XRecv> no_r;
+      if (prof)
+        if (int rp = prof_begin(i, C)) return rp;
       if (int rc = c->tx->exchange_tree(no_s, no_r, nullptr, &tp.leaves[i], &tp.spec[i], C)) return rc;
+      if (prof)
+        if (int rp = prof_end(i, C)) return rp;
       tev[i] = next_event(c);
       if (C != K) HIP_TRY(hipEventRecord(tev[i], C));  // (one stream: nothing waits for it)
     }
     if (dm_trees && tp.host[i] >= 0) {
+      // profile: a tree inside another exchange's launch has no launch of its
+      // own -- a zero-length entry; its time is inside the hosting exchange's
+      if (prof && tp.host[i] != (int)i) {
+        if (int rp = prof_begin(i, C)) return rp;
+        if (int rp = prof_end(i, C)) return rp;
+      }
       // this tree runs inside exchange host[i]: K takes up its place in K's
       // order (later local ops follow it as they followed the tree) -- now,
       // or right after the host is issued when that comes next
@@ -1144,21 +1176,8 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       snprintf(lbl, sizeof lbl, "bine op %zu %s (%zu prims)", i, o.xchg ? "exchange" : "local", o.prims.size());
       roctxRangePushA(lbl);
     }
-    if (prof) {
-      auto &pt = c->prof[i];
-      if (!pt.a) HIP_TRY(hipEventCreate(&pt.a));
-      if (!pt.b) HIP_TRY(hipEventCreate(&pt.b));
-      pt.xchg = o.xchg ? 1 : 0;
-      pt.nprims = (int)o.prims.size();
-      pt.bytes = 0;
-      for (const Prim &x : o.prims) {  // exchanges: bytes sent; local ops: algorithmic HBM bytes
-        if (x.type == BINE_PRIM_SEND) pt.bytes += x.count * esz;
-        else if (x.type == BINE_PRIM_REDUCE || x.type == BINE_PRIM_REDUCE3) pt.bytes += 3 * x.count * esz;
-        else if (x.type == BINE_PRIM_REDUCE_TREE) pt.bytes += (uint64_t)(x.peer + 1) * x.count * esz;
-        else if (x.type == BINE_PRIM_COPY) pt.bytes += 2 * x.count * esz;
-      }
-      HIP_TRY(hipEventRecord(pt.a, st));
-    }
+    if (prof)
+      if (int rp = prof_begin(i, st)) return rp;
     int rc = BINE_SUCCESS;
     if (o.xchg) {
       sends.clear();
@@ -1196,7 +1215,8 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       rc = run_local(o.prims, ptr, dtype, op, esz, K);
       if (rc) { set_err("local primitive failed (%s)", bine_status_string(rc)); return rc; }
     }
-    if (prof) HIP_TRY(hipEventRecord(c->prof[i].b, st));
+    if (prof)
+      if (int rp = prof_end(i, st)) return rp;
     if (roctx_on()) roctxRangePop();
     // an event of the pool may be re-recorded by a later op once the pool
     // wraps: any later record only delays a waiter, never lets it run early.
@@ -1269,7 +1289,7 @@ static void build(const PlanArgs &args, size_t ch, size_t relay_min_bytes, bool 
 static const DmTreePlan *tree_plan_for(bine_comm *c, const std::string &plan_key_s, const Schedule &sc,
                                        const void *sbuf, void *rbuf, size_t esz, int dtype, int op) {
   auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
-  if (!rt || !rt->dm_on || !rt->dm || !c->dm_tree || c->profile || op < 0) return nullptr;
+  if (!rt || !rt->dm_on || !rt->dm || !c->dm_tree || op < 0) return nullptr;
   char buf[256];
   snprintf(buf, sizeof buf, "|%p|%p|%p|%p|%p|%p|%d|%d|%zu|%d|%zu|%d", sbuf, rbuf, c->tmp[0], c->tmp[1], c->tmp[2],
            c->tmp[3], dtype, op, esz, rt->dm->merge, rt->dm->slot, rt->dm->tree_wgs);
