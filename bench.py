@@ -551,15 +551,17 @@ def step_profile(torch, comm, call):
     span = max(o["start_ms"] + o["ms"] for o in ops)
     xs = [o for o in ops if o["xchg"]]
     ls = [o for o in ops if not o["xchg"]]
-    xb, lb = sum(o["ms"] for o in xs), sum(o["ms"] for o in ls)
-    ov = overlap_frac([(o["start_ms"], o["ms"]) for o in xs], [(o["start_ms"], o["ms"]) for o in ls])
+    lb_ops = [o for o in ls if o["nprims"]]   # nprims 0: a tree inside an exchange launch (no launch of its own)
+    xb, lb = sum(o["ms"] for o in xs), sum(o["ms"] for o in lb_ops)
+    ov = overlap_frac([(o["start_ms"], o["ms"]) for o in xs], [(o["start_ms"], o["ms"]) for o in lb_ops])
     return {"ops": len(ops), "span_ms": round(span, 4), "exchange_busy_ms": round(xb, 4),
             "local_busy_ms": round(lb, 4), "overlap_frac": None if ov is None else round(ov, 4),
             "exchanges": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4), "peers": o["nprims"],
                            "egress_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 2) if o["ms"] > 0 else None}
                           for o in xs[:24]],
             "local": [{"start_ms": round(o["start_ms"], 4), "ms": round(o["ms"], 4),
-                       "hbm_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 1) if o["ms"] > 0 else None}
+                       "hbm_GBs": round(o["bytes"] / (o["ms"] * 1e-3) / 1e9, 1) if o["ms"] > 0 and o["nprims"] else None}
+                      | ({"inside_exchange": True} if not o["nprims"] else {})
                       for o in ls[:24]]}
 
 

@@ -397,8 +397,10 @@ int bine_comm_set_graphs(bine_comm_t comm, int on);
  * bine_comm_profile() waits for the latest collective's events and fills one
  * entry per op: kind, primitives, bytes (exchange: bytes this rank sends;
  * local: algorithmic HBM bytes), start relative to the first op's start and
- * duration.  Returns the number of ops (may exceed cap) or -status.  Off by
- * default (the events cost host time per op).  BINE_ROCTX=1 additionally
+ * duration.  An op evaluated inside another exchange's launch (the direct
+ * transport's fused trees) reports nprims = 0, bytes = 0 and ~0 ms: its time
+ * is the hosting exchange's.  Returns the number of ops (may exceed cap) or
+ * -status.  Off by default (the events cost host time per op).  BINE_ROCTX=1 additionally
  * brackets every collective and every issued op with a roctx range. */
 typedef struct {
   int32_t xchg;

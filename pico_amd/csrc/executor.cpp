@@ -1134,6 +1134,8 @@ static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbu
       if (prof && tp.host[i] != (int)i) {
         if (int rp = prof_begin(i, C)) return rp;
         if (int rp = prof_end(i, C)) return rp;
+        c->prof[i].nprims = 0;  // nothing launched for it (bine_comm_profile)
+        c->prof[i].bytes = 0;
       }
       // this tree runs inside exchange host[i]: K takes up its place in K's
       // order (later local ops follow it as they followed the tree) -- now,

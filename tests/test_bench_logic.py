@@ -31,3 +31,31 @@ def test_dm_wgs_mode_suffix():
     assert bench.dm_wgs("flatrs+flat") is None and bench.dm_wgs("trees") is None
     assert bench.dm_wgs("flatrs+flat+dm") == 0 and bench.dm_wgs("direct+dm") == 0
     assert bench.dm_wgs("flatrs+flat+dm64") == 64 and bench.dm_wgs("relay+flat+dm16") == 16
+
+
+def test_step_profile_counts_trees_inside_exchanges_as_no_local_time():
+    # bine_comm_profile: a fused tree evaluated inside an exchange launch
+    # reports nprims 0 / bytes 0 (include/bine_amd.h); it is neither local
+    # busy time nor an HBM rate
+    class Comm:
+        def set_profile(self, on):
+            pass
+
+        def synchronize(self):
+            pass
+
+        def profile(self):
+            return [{"xchg": 1, "nprims": 14, "bytes": 1 << 20, "start_ms": 0.0, "ms": 0.5},
+                    {"xchg": 0, "nprims": 0, "bytes": 0, "start_ms": 0.1, "ms": 0.006},
+                    {"xchg": 0, "nprims": 1, "bytes": 3 << 20, "start_ms": 0.6, "ms": 0.2}]
+
+    class Torch:
+        class cuda:
+            @staticmethod
+            def synchronize():
+                pass
+
+    p = bench.step_profile(Torch, Comm(), lambda: None)
+    assert p["local_busy_ms"] == 0.2 and p["ops"] == 3
+    assert p["local"][0]["inside_exchange"] and p["local"][0]["hbm_GBs"] is None
+    assert "inside_exchange" not in p["local"][1] and p["local"][1]["hbm_GBs"] > 0
