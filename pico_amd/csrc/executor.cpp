@@ -160,8 +160,18 @@ struct RcclTransport final : Transport {
   // name and PCI bus id): more than one only when processes share a device
   int ranks_on_my_gpu(int device, int *same) {
     char bus[64] = {0}, host[256] = {0};
-    (void)hipDeviceGetPCIBusId(bus, sizeof bus, device);
-    (void)hipGetLastError();
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess || !bus[0]) {
+      // no bus id: the device UUID, else this rank alone (never a false match)
+      (void)hipGetLastError();
+      hipUUID u{};
+      if (hipDeviceGetUuid(&u, device) == hipSuccess) {
+        for (int k = 0; k < 16 && 2 * k + 2 < (int)sizeof bus; k++)
+          snprintf(bus + 2 * k, 3, "%02x", (unsigned char)u.bytes[k]);
+      } else {
+        (void)hipGetLastError();
+        snprintf(bus, sizeof bus, "rank-%d", rank);
+      }
+    }
     gethostname(host, sizeof host - 1);
     uint64_t h = 1469598103934665603ull;  // FNV-1a of "host/bus"
     for (const char *s : {(const char *)host, "/", (const char *)bus})
