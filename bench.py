@@ -635,7 +635,8 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
             out[f"C1_allreduce_{algo}_f32_1MiB" + ("_graph" if g else "")] = {
                 "us": round(st["median_ms"] * 1e3, 2),
                 "algbw_per_rank_GBs": round(n1 * 4 / (st["median_ms"] * 1e-3) / 1e9, 2),
-                "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok)}
+                "host_issue_us": round(st["issue_ms"] * 1e3, 2), "parity_ok": all_ok(torch, dist, ok),
+                **({"captured": comm.graphs_cached() > 0} if g else {})}
     comm.set_graphs(False)
     if dm_ok and "+dm" not in mode and world > 1:
         # C1 also over the direct peer-memory transport with the flat phases:
@@ -922,12 +923,19 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         try:
             # inside: enabling the direct transport fails on every rank alike
             # when peer memory cannot be mapped (BINE_ERR_UNSUPPORTED)
+            if cfg[2]:
+                comm.set_graphs(False)   # an empty graph cache: graphs_cached() then says whether this one captured
             apply_transport(comm, *cfg)
             rbuf.fill_(float("nan"))   # a transport that writes nothing cannot pass on the last one's output
             st = timed(torch, stream, run, 3, 2, dist, (comm.synchronize,))
             ok, _ = parity(cfg[0])
             verdicts[cfg] = ok
             trials[cfg] = st["median_ms"] if ok is not False else float("inf")
+            if cfg[2] and comm.graphs_cached() == 0:
+                # the library kept every call eager (its HIP-runtime gate,
+                # include/bine_amd.h): not a graph replay, so not picked as one
+                verdicts[cfg] = "eager (not captured)"
+                trials[cfg] = float("inf")
             if ok is False and rank == 0:
                 print(f"bench: transport {tname(cfg)} EXCLUDED: output digest differs from the oracle's",
                       file=sys.stderr)

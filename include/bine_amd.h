@@ -388,6 +388,10 @@ int bine_comm_direct_stamps(bine_comm_t comm, uint64_t *out, size_t cap, size_t 
  * and over RCCL with >= 4 (HIP's default); the rest runs eagerly.
  * Off by default (BINE_GRAPHS=1 turns it on); loopback: BINE_ERR_UNSUPPORTED. */
 int bine_comm_set_graphs(bine_comm_t comm, int on);
+/* Number of graphs graph mode holds (captured and replayable) -- 0 while
+ * every call ran eagerly (graph mode off, NULL stream, or a schedule the
+ * runtime gate above keeps eager); -status on error. */
+int64_t bine_comm_graphs_cached(bine_comm_t comm);
 
 /* Per-op device timing ("hipEvents per step"): with profiling on, every op
  * of a collective's issue schedule -- an exchange group on the comm stream or

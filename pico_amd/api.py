@@ -165,6 +165,13 @@ class Comm:
         stream must not be the NULL stream."""
         check(lib().bine_comm_set_graphs(self.handle, int(on)), "bine_comm_set_graphs")
 
+    def graphs_cached(self) -> int:
+        """graphs graph mode holds (0: every call so far ran eagerly)"""
+        n = lib().bine_comm_graphs_cached(self.handle)
+        if n < 0:
+            check(int(-n), "bine_comm_graphs_cached")
+        return int(n)
+
     def set_direct(self, on: bool) -> None:
         """RCCL communicators on one node: exchanges through mapped peer memory
         (bine_comm_set_direct); bit-identical; the first enable is collective."""

@@ -2160,6 +2160,12 @@ int bine_comm_set_graphs(bine_comm_t c, int on) {
   return BINE_SUCCESS;
 }
 
+int64_t bine_comm_graphs_cached(bine_comm_t c) {
+  if (!c) return -(int64_t)BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return (int64_t)c->graph_cache.size();
+}
+
 int bine_comm_set_direct(bine_comm_t c, int on) {
   if (!c) return BINE_ERR_ARG;
   auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
