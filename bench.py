@@ -681,12 +681,16 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
     nm = node_model("C4", world, mode, chunk)
     out["C4_reduce_scatter_bine_permute_remap_f32_1GiB"] = {
         "ms": round(st["median_ms"], 4), "busbw_per_rank_GBs": round((world - 1) / world * S / (st["median_ms"] * 1e-3) / 1e9, 2),
-        "graph_replay": graphs, "parity_ok": all_ok(torch, dist, ok), "model_ms": nm.get("model_ms"),
+        "graph_replay": graphs and comm.graphs_cached() > 0, "parity_ok": all_ok(torch, dist, ok),
+        "model_ms": nm.get("model_ms"),
         "frac_of_model": round(nm["model_ms"] / st["median_ms"], 4) if nm.get("model_ms") else None}
     del sb, rb
     # C5: allreduce_bine_bdw_remap fp64 / int64 SUM, 256 MiB per rank
     n = C5_ELEMS
     for dt, tdt in (("double", torch.float64), ("int64", torch.int64)):
+        if graphs:   # an empty graph cache: graphs_cached() below is this configuration's
+            comm.set_graphs(False)
+            comm.set_graphs(True)
         sb = torch.empty(n, dtype=tdt, device=dev)
         rb = torch.empty(n, dtype=tdt, device=dev)
         pico_amd.fill_pico(sb, n, dt, 1234 + rank)
@@ -700,8 +704,8 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
         out[f"C5_allreduce_bine_bdw_remap_{dt}_256MiB"] = {
             "ms": round(ms, 4), "algbw_per_rank_GBs": round(S / (ms * 1e-3) / 1e9, 2),
             "busbw_per_rank_GBs": round(2 * (world - 1) / world * S / (ms * 1e-3) / 1e9, 2),
-            "graph_replay": graphs, "parity_ok": all_ok(torch, dist, ok), "model_ms": nm.get("model_ms"),
-            "frac_of_model": round(nm["model_ms"] / ms, 4) if nm.get("model_ms") else None}
+            "graph_replay": graphs and comm.graphs_cached() > 0, "parity_ok": all_ok(torch, dist, ok),
+            "model_ms": nm.get("model_ms"), "frac_of_model": round(nm["model_ms"] / ms, 4) if nm.get("model_ms") else None}
         del sb, rb
     torch.cuda.empty_cache()
     return out
