@@ -129,11 +129,15 @@ def test_graph_mode_size1_comm(dev):
                 pico_amd.allreduce("bine_bdw_remap", s, r, n, "float", "sum", comm)
             torch.cuda.synchronize()
             assert torch.equal(r, s), i
+        # one rank, no RCCL calls: captured on every runtime (executor.cpp
+        # rccl_free; the suite's process runs with 2 HW queues, conftest.py)
+        assert comm.graphs_cached() == 1
         r.zero_()
         pico_amd.allreduce("bine_bdw_remap", s, r, n, "float", "sum", comm, stream=0)   # NULL stream: eager
         torch.cuda.synchronize()
         assert torch.equal(r, s)
         comm.set_graphs(False)
+        assert comm.graphs_cached() == 0
     finally:
         comm.destroy()
 
