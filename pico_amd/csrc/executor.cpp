@@ -1477,7 +1477,8 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     snprintf(lbl, sizeof lbl, "bine %s P=%d count=%zu", bine_algo_name(a.algo), a.P, a.count);
     roctxRangePushA(lbl);
   }
-  const bool single = bytes <= c->single_stream_bytes;
+  // one rank: local ops only, so one stream (and a one-branch graph)
+  const bool single = bytes <= c->single_stream_bytes || c->size == 1;
   if (stg) {
     auto sit = c->stage_cache.find(key);
     if (sit == c->stage_cache.end()) {
