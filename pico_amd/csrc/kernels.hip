@@ -1394,44 +1394,63 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
   return r;
 }
 
-// the whole workgroup: thread 0 polls (relaxed system-scope loads, bounded)
-// and, for a ready mark (acq: the slot is read next), acquires once.  false:
-// the transport is poisoned (now or earlier)
-__device__ __forceinline__ bool wait_flag(const DmFusedArgs &a, const uint64_t *p, uint64_t v, bool acq) {
-  __shared__ int go;
+// The waits and arrivals of a phase's messages run side by side, one thread
+// per message: one flag round trip per phase instead of one per message
+// (a small collective is a chain of such round trips).
+//
+// wait_all: thread t < n polls message first + t's flag (relaxed
+// system-scope loads, bounded); after the barrier, when any of them is a
+// ready mark (acq: its slot is read next), thread 0 acquires once -- every
+// poll has completed before the barrier -- and a second barrier orders the
+// workgroup's reads after it.  false: the transport is poisoned (now or
+// earlier).
+__device__ __forceinline__ bool wait_all(const DmFusedArgs &a, int first, int n, bool acq) {
+  __shared__ int bad;
   uint32_t *poison = reinterpret_cast<uint32_t *>(a.own + kPoisonOff);
-  if (threadIdx.x == 0) {
-    int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
-    if (ok && p) {
+  if (threadIdx.x == 0) bad = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  __syncthreads();
+  if ((int)threadIdx.x < n && !bad) {
+    const Msg m = resolve(a, a.m[first + threadIdx.x]);
+    if (m.wait) {
       const long long t0 = wall_clock64();
-      while (ld_rlx_sys(p) < v) {
+      while (ld_rlx_sys(m.wait) < m.wait_val) {
         if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
           __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          ok = 0;
+          bad = 1;
           break;
         }
         if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-          ok = 0;
+          bad = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
     }
-    if (ok && acq) acquire_once();
-    go = ok;
   }
   __syncthreads();
-  const bool ok = go != 0;
-  __syncthreads();  // `go` is reused by the next wait
+  const bool ok = !bad;
+  if (threadIdx.x == 0 && ok && acq && n) acquire_once();
+  __syncthreads();  // the reads after the acquire; `bad` is reused by the next wait
   return ok;
 }
 
-// the whole workgroup, after its share of message m: stores acknowledged /
-// reads complete, count in; the last workgroup of the message publishes seq
-// (k_dm_move's protocol)
-__device__ __forceinline__ void arrive(const DmFusedArgs &a, const Msg &m) {
-  if (count_in(m.cnt, (uint32_t)a.wgs)) publish(m.sig, m.seq);
+// arrive_all: the workgroup's shares of messages first .. first + n - 1 are
+// done (stores acknowledged, reads complete); thread t counts in for message
+// t, and the last workgroup of a message publishes its seq (k_dm_move's
+// protocol)
+__device__ __forceinline__ void arrive_all(const DmFusedArgs &a, int first, int n) {
+  vm_wait();
+  __syncthreads();
+  if ((int)threadIdx.x < n) {
+    const Msg m = resolve(a, a.m[first + threadIdx.x]);
+    const uint32_t old = __hip_atomic_fetch_add(m.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == (uint32_t)a.wgs) {
+      __hip_atomic_store(m.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use
+      publish(m.sig, m.seq);
+    }
+  }
+  __syncthreads();  // every thread's resolve() before thread 0's launch-counter add (the kernel's end)
 }
 
 // this workgroup's slice of a message of n vectors
@@ -1441,7 +1460,7 @@ __device__ __forceinline__ void slice(uint64_t n, int wgs, uint64_t *lo, uint64_
 }
 
 // a push writes the peer's slot through; a pull reads its own slot after
-// the acquire of wait_flag
+// the acquire of wait_all
 __device__ __forceinline__ void copy_slice(const Msg &m, int wgs, bool push) {
   uint64_t lo, hi;
   slice(m.nvec, wgs, &lo, &hi);
@@ -1459,21 +1478,16 @@ template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   using namespace dmf;
   const int nm = a.na + a.nb + a.nc + a.nd;
-  // phase A: our blocks into the peers' inboxes
-  for (int i = 0; i < a.na; i++) {
-    const Msg m = resolve(a, a.m[i]);
-    if (!wait_flag(a, m.wait, m.wait_val, false)) return;
-    copy_slice(m, a.wgs, true);
-    arrive(a, m);
-  }
+  // phase A: our blocks into the peers' inboxes (each slot's previous use
+  // acknowledged first)
+  if (!wait_all(a, 0, a.na, false)) return;
+  for (int i = 0; i < a.na; i++) copy_slice(resolve(a, a.m[i]), a.wgs, true);
+  arrive_all(a, 0, a.na);
   // phase B: the peers' blocks, read in place in our inbox as the tree's
   // leaves; each result vector goes to `out` and, for the flat allgather
   // (phase C's pushes), straight from registers into every peer's slot --
   // whose previous use must have been acknowledged first
-  for (int i = 0; i < a.nb + a.nc; i++) {
-    const Msg m = resolve(a, a.m[a.na + i]);
-    if (!wait_flag(a, m.wait, m.wait_val, i < a.nb)) return;
-  }
+  if (!wait_all(a, a.na, a.nb + a.nc, a.nb > 0)) return;
   const u32x4 *lp[kMaxLeaves];
 #pragma unroll
   for (int j = 0; j < kMaxLeaves; j++)
@@ -1507,14 +1521,12 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   }
   // every leaf slice is read (the senders may reuse their slots) and every
   // result slice is in the peers' inboxes
-  for (int i = 0; i < a.nb + a.nc; i++) arrive(a, resolve(a, a.m[a.na + i]));
+  arrive_all(a, a.na, a.nb + a.nc);
   // phase C: the peers' results out of our inbox
-  for (int i = 0; i < a.nd; i++) {
-    const Msg m = resolve(a, a.m[a.na + a.nb + a.nc + i]);
-    if (!wait_flag(a, m.wait, m.wait_val, true)) return;
-    copy_slice(m, a.wgs, false);
-    arrive(a, m);
-  }
+  const int d0 = a.na + a.nb + a.nc;
+  if (!wait_all(a, d0, a.nd, true)) return;
+  for (int i = 0; i < a.nd; i++) copy_slice(resolve(a, a.m[d0 + i]), a.wgs, false);
+  arrive_all(a, d0, a.nd);
   // the launch's last workgroup advances the sequence bases (every workgroup
   // has read them: each resolve() happened before its launch-counter add)
   if (threadIdx.x == 0) {
