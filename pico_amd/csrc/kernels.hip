@@ -1212,7 +1212,11 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
   uint8_t *own = a.own;
   uint32_t *poison = reinterpret_cast<uint32_t *>(own + kPoisonOff);
   // every leaf: its slot in our inbox, the sender's ready mark to wait for
+  // -- polled side by side, lane j for leaf j in one loop (one flag round
+  // trip, not one per leaf)
   const u32x4 *lp[NL];
+  const uint64_t *wp = nullptr;
+  uint64_t wseq = 0;
   __shared__ int go;
   uint64_t t0 = 0, t1 = 0;
   if (threadIdx.x == 0) {
@@ -1231,24 +1235,28 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
     const size_t k = (size_t)(seq % kSlots);
     lp[j] = reinterpret_cast<const u32x4 *>(own + kFlagsBytes + ((size_t)m.peer * kSlots + k) * a.slot);
-    if (threadIdx.x == 0 && go) {
-      const uint64_t *w = reinterpret_cast<const uint64_t *>(own + kReadyOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
-      const long long t0 = wall_clock64();
-      while (ld_rlx_sys(w) < seq) {
-        if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
-          __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          go = 0;
-          break;
-        }
-        if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-          go = 0;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
+    if ((int)threadIdx.x == j) {
+      wp = reinterpret_cast<const uint64_t *>(own + kReadyOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+      wseq = seq;
     }
   }
+  if (wp && go) {
+    const long long tw = wall_clock64();
+    while (ld_rlx_sys(wp) < wseq) {
+      if (wall_clock64() - tw > (long long)a.timeout_ticks) {
+        __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        go = 0;
+        break;
+      }
+      if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+        go = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();  // every leaf's poll has completed
   if (threadIdx.x == 0) {
     if (go) acquire_once();  // every leaf's mark seen: what the senders wrote before it
     if (a.stamps) t1 = wall_clock64();
