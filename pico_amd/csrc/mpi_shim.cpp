@@ -396,16 +396,15 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
       }
       return MPI_SUCCESS;
     }
-    if (stage_s && hipMemcpyAsync((void *)ds, sbuf, sbytes, hipMemcpyHostToDevice, e->h2d) != hipSuccess)
+    // unpipelined: copy in, collective, copy out depend on each other in
+    // turn, so they share the collective's stream -- no cross-stream event
+    // hops (a small call's latency is mostly such hops: C1 end to end)
+    if (stage_s && hipMemcpyAsync((void *)ds, sbuf, sbytes, hipMemcpyHostToDevice, st) != hipSuccess)
       return MPI_ERR_OTHER;
-    if (fill_r && hipMemcpyAsync(dr, rbuf, rbytes, hipMemcpyHostToDevice, e->h2d) != hipSuccess)
+    if (fill_r && hipMemcpyAsync(dr, rbuf, rbytes, hipMemcpyHostToDevice, st) != hipSuccess)
       return MPI_ERR_OTHER;
-    if (int r2 = follow(e, st, e->h2d)) return r2;
     if (int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st)) return to_mpi(bst);
-    if (stage_r) {
-      if (int r2 = follow(e, e->d2h, st)) return r2;
-      if (hipMemcpyAsync(rbuf, dr, rbytes, hipMemcpyDeviceToHost, e->d2h) != hipSuccess) return MPI_ERR_OTHER;
-    }
+    if (stage_r && hipMemcpyAsync(rbuf, dr, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess) return MPI_ERR_OTHER;
     return MPI_SUCCESS;
   };
   rc = issue();
