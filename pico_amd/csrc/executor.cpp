@@ -419,7 +419,7 @@ struct bine_comm {
   size_t tmp_bytes[4] = {0, 0, 0, 0};
   size_t relay_min_bytes = 0;  // relay mode: smallest relayed part (0: off)
   bool trees = false;          // multi-tree mode (allreduce, P = 4 / 8)
-  size_t chunk_bytes = 0;      // pipelining chunk (0: default_chunk_bytes())
+  size_t chunk_bytes = 0;      // pipelining chunk (0: default_chunk_bytes(direct transport on))
   size_t single_stream_bytes = 1 << 20;  // collectives up to this size run on the caller's stream only
   int flat_ag = 0;             // allreduce: one-step all-peers allgather phase (2: cut with the flat RS chunks)
   bool flat_rs = false;        // one-step all-peers reduce-scatter phase + tree kernel
@@ -680,12 +680,14 @@ static int ensure_workspace(bine_comm *c, const uint64_t *elems, size_t esz, hip
   return BINE_SUCCESS;
 }
 
-static size_t default_chunk_bytes() {
-  static size_t v = [] {
-    const char *e = getenv("BINE_CHUNK_BYTES");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)16 << 20;
-  }();
-  return v;
+// BINE_CHUNK_BYTES, else 16 MiB -- 64 MiB over the direct transport, whose
+// exchange launches take whole 64 MiB slots (C3 at P = 2 on one GPU: 0.50 ms
+// at 64 MiB vs 0.66 at 16, profiles/r4_dm_stamps_p2_sweep2.txt; the node
+// model: 0.45 vs 0.47 ms at P = 8).  Bit-identical either way.
+static size_t default_chunk_bytes(bool direct) {
+  static const char *e = getenv("BINE_CHUNK_BYTES");
+  if (e) return (size_t)strtoull(e, nullptr, 10);
+  return (size_t)(direct ? 64 : 16) << 20;
 }
 
 // ---------------------------------------------------------------------------
@@ -1442,7 +1444,10 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     if (!bine_op_valid(dtype, op)) return BINE_ERR_ARG;
   }
   std::lock_guard<std::mutex> g(c->mu);
-  if (chunk_bytes == kCommChunk) chunk_bytes = c->chunk_bytes ? c->chunk_bytes : default_chunk_bytes();
+  if (chunk_bytes == kCommChunk) {
+    const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
+    chunk_bytes = c->chunk_bytes ? c->chunk_bytes : default_chunk_bytes(rt && rt->dm_on);
+  }
   HIP_TRY(hipSetDevice(c->device));
   a.P = c->size;
   a.rank = c->rank;
