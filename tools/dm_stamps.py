@@ -97,7 +97,7 @@ def worker(rank, P, iters, env, port, q):
         comm = pico_amd.Comm.from_torch_distributed(0)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    chunk = int(os.environ.get("BINE_CHUNK_BYTES", 16 << 20))
+    chunk = 0   # the library's default (BINE_CHUNK_BYTES, else 64 MiB over the direct transport)
     res = {}
     for cfg, n, coll in (("C3", bench.C3_ELEMS, "allreduce"), ("C4", bench.C4_ELEMS, "reduce_scatter")):
         sb = torch.empty(n, dtype=torch.float32, device="cuda:0")
