@@ -333,8 +333,10 @@ int bine_comm_set_flat_rs(bine_comm_t comm, int on);
  * system scope.  Same bytes in the same places: results bit-identical.  Every
  * wait has a time limit (BINE_DIRECT_TIMEOUT_S, default 10 s); a timeout
  * disables the transport (BINE_ERR_INTERNAL from then on) instead of
- * hanging.  The first call with on = 1 is collective (every rank of the
- * communicator, at the same point).  Sequence numbers live in device memory,
+ * hanging.  Every call with on = 1 is collective (every rank of the
+ * communicator, at the same point): the first sets the transport up, later
+ * ones rebuild it on every rank when it was disabled by a timeout on any
+ * rank.  Sequence numbers live in device memory,
  * so graph mode captures and replays these collectives too.  At most 4
  * messages to one peer per exchange group
  * (BINE_ERR_UNSUPPORTED beyond).  Knobs: BINE_DIRECT_SLOT_BYTES (64 MiB),

@@ -2179,6 +2179,22 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());
+  if (on && r->dm) {
+    // collective as well once the transport exists: a transport poisoned on
+    // any rank (a wait timed out) is rebuilt on every rank -- fresh inboxes,
+    // flags and sequence bases.  Every rank's kernels have ended (each waited
+    // for its device above, and a timed-out wait ends its launch) before the
+    // agreement, so nothing touches the old inboxes when they go.
+    int all = 0;
+    if (int rc2 = r->agree(!r->dm->poisoned(), &all)) return rc2;
+    if (!all) {
+      if (trace_on()) fprintf(stderr, "[bine dm r%d] poisoned on some rank: rebuilding\n", c->rank);
+      r->dm_on = false;
+      c->drop_graphs();  // captured launches carry the old inboxes
+      c->tree_cache.clear();
+      r->dm.reset();
+    }
+  }
   if (on && !r->dm) {  // collective: every rank maps every peer's inbox
     auto d = std::make_unique<DirectState>();
     std::string err;

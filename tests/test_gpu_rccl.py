@@ -139,3 +139,15 @@ def test_fused_trees_vs_unfused_two_processes(mcast, merge):
                  env=env, timeout=170, ranks=2)
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+@pytest.mark.timeout(300)
+def test_direct_transport_rebuilt_after_a_timeout():
+    """a wait that times out disables the direct transport on its rank; the
+    next bine_comm_set_direct(1) rebuilds it on every rank and C3 matches the
+    oracle's digest again (tools/dm_rebuild_check.py, 2 processes)"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_rebuild_check.py"), "2"], env=env,
+                 timeout=280, ranks=2)
+    assert r.returncode == 0, r.stdout[-3000:] + "\n" + r.stderr[-2000:]
+    assert "RESULT P=2: ok" in r.stdout

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""A direct transport disabled by a timed-out wait is rebuilt by the next
+bine_comm_set_direct(1) on every rank (executor.cpp): P processes on the one
+GPU; the wait limit is first set absurdly low (BINE_DIRECT_TIMEOUT_S=1e-7, so
+the first exchange times out and poisons the transport), the next call must
+report BINE_ERR_INTERNAL, then with the limit back at 10 s set_direct(1)
+rebuilds it and C3 allreduces (256 MiB fp32 per rank) match the committed
+oracle digest again.
+usage: python tools/dm_rebuild_check.py [P]   (exit 0 = every rank ok)"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def worker(rank, P, port, q):
+    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
+    os.environ["BINE_DIRECT_TIMEOUT_S"] = "1e-7"
+    import torch
+    import torch.distributed as dist
+    import pico_amd
+    import bench
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    with bench.quiet_stdout():
+        comm = pico_amd.Comm.from_torch_distributed(0)
+    stream = torch.cuda.Stream()
+    n = bench.C3_ELEMS
+    sb = torch.empty(n, dtype=torch.float32, device="cuda:0")
+    rb = torch.empty(n, dtype=torch.float32, device="cuda:0")
+    pico_amd.fill_pico(sb, n, "float", 1234 + rank)
+    key = bench.gkey("C3", "allreduce", "bine_bdw_remap", "float", n, P)
+    out = {}
+
+    def call():
+        pico_amd.allreduce("bine_bdw_remap", sb, rb, n, "float", "sum", comm, stream=stream)
+        stream.synchronize()
+
+    bench.apply_transport(comm, "flatrs+flat+dmt", 16 << 20)
+    poisoned = False
+    for _ in range(3):   # the first exchange times out; a later call reports it
+        try:
+            call()
+        except pico_amd.BineError as e:
+            poisoned = "timed out" in str(e) or "poisoned" in str(e)
+            break
+    out["poisoned"] = poisoned
+    torch.cuda.synchronize()
+    os.environ["BINE_DIRECT_TIMEOUT_S"] = "10"
+    try:
+        bench.apply_transport(comm, "flatrs+flat+dmt", 16 << 20)   # rebuilds (collective)
+        ok = True
+        for _ in range(3):
+            rb.fill_(float("nan"))
+            call()
+            o, _ = bench.check_digest(pico_amd, rb, n, "float", key, rank, stream)
+            ok = ok and bool(o)
+        out["rebuilt_ok"] = ok
+    except pico_amd.BineError as e:
+        out["rebuilt_ok"] = False
+        out["error"] = str(e)
+    comm.destroy()
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+if __name__ == "__main__":
+    import multiprocessing as mp
+    import socket
+    from tools._procs import join_ranks
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=worker, args=(r, P, port, q)) for r in range(P)]
+    for p in ps:
+        p.start()
+    join_ranks(ps, 240)
+    res = {}
+    while not q.empty():
+        r, o = q.get()
+        res[r] = o
+    ok = len(res) == P and all(o["poisoned"] and o["rebuilt_ok"] for o in res.values())
+    print(f"RESULT P={P}: {'ok' if ok else 'FAILED'} {res} exitcodes {[p.exitcode for p in ps]}", flush=True)
+    sys.exit(0 if ok else 1)
