@@ -914,7 +914,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     # correct one; the fastest pair is kept
     trials, verdicts = {}, {}
 
-    dm_dead = []   # the direct transport failed once (setup or a timed-out wait): not tried again
+    dm_dead = []   # the direct transport could not be set up: not tried again (a timed-out wait is not
+    #                this: the next bine_comm_set_direct(1) rebuilds the transport on every rank)
 
     def trial(cfg):
         # a setting the planner rejects fails identically on every rank before
@@ -950,9 +951,9 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             comm.synchronize()
             trials[cfg] = float("inf")
             verdicts[cfg] = "error"
-            if dm_wgs(cfg[0]) is not None:
-                # symmetric: setup is agreed over RCCL and a poisoned transport
-                # reports on every rank, so every rank stops trying together
+            if dm_wgs(cfg[0]) is not None and e.status == 6:   # BINE_ERR_UNSUPPORTED: setup failed
+                # symmetric: setup is agreed over RCCL, so every rank stops
+                # trying together
                 dm_dead.append(tname(cfg))
 
     mid = 16 << 20 if 16 << 20 in chunks else chunks[0]
@@ -1022,9 +1023,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         if trials[(best[0], best[1], True)] < trials.get(best, float("inf")):
             best = (best[0], best[1], True)
     if dm_dead and dm_wgs(best[0]) is not None:
-        # a direct transport that timed out in a later trial cannot be set
-        # again on this communicator (it stays poisoned): the pick falls back
-        # to the fastest checked setting without it
+        # a direct transport that could not be set up in a later trial: the
+        # pick falls back to the fastest checked setting without it
         ok_c = [c for c, v in trials.items() if v != float("inf") and dm_wgs(c[0]) is None]
         best = min(ok_c, key=trials.get) if ok_c else base_cfg
         if rank == 0:
