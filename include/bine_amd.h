@@ -183,9 +183,16 @@ int bine_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void 
 int bine_get_unique_id(void *id /* BINE_UNIQUE_ID_BYTES */);
 /* RCCL version codes (NCCL_VERSION encoding, e.g. 22606 = 2.26.6): the library
  * the process maps (ncclGetVersion) and the headers this library was compiled
- * against.  bine_comm_init_rccl refuses a runtime of another major version or
- * older than 2.26.0 (BINE_ERR_RCCL, reason in bine_last_error). */
+ * against, both written even on failure.  Returns BINE_ERR_RCCL (reason in
+ * bine_last_error) for a skewed pair: either code outside the window whose ABI
+ * for every RCCL type this library passes was checked (bine_rccl_abi_check);
+ * bine_comm_init_rccl refuses such a runtime, and also one whose results in
+ * the creation-time ABI probe (every type / op this library passes, run
+ * through the runtime) differ. */
 int bine_rccl_version(int *runtime, int *compiled);
+/* The pure check behind bine_rccl_version: BINE_SUCCESS iff both version codes
+ * lie in the checked ABI window (2.26.0 ... 2.27.99). */
+int bine_rccl_abi_check(int runtime, int compiled);
 /* One process per GPU, RCCL P2P over xGMI.  `id` from rank 0's
  * bine_get_unique_id(), broadcast by the caller (MPI, torch.distributed...). */
 int bine_comm_init_rccl(bine_comm_t *comm, int nranks, int rank, const void *id, int device);
@@ -569,6 +576,21 @@ int64_t bine_plan_dm_trees(int algo, int nranks, int rank, size_t count, const i
 int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
                         size_t segsize, int in_place, size_t chunk_bytes, int mode, int kind, uint64_t *out,
                         int64_t cap);
+
+/* The direct transport's residency cut (host only): every launch's
+ * workgroups -- `cw[0..n)` per copied message, *tw for a fused tree (NULL:
+ * none) -- are scaled proportionally, each >= 1, to sum to at most `cap` =
+ * CUs x resident blocks per CU of the launched kernel / ranks sharing the GPU,
+ * so that every waiting workgroup of every co-located rank's current launch
+ * is resident at once and no waiter can hold the slot its producer needs.
+ * Returns 0 (unchanged: fits, or cap <= 0), 1 (scaled) or -1 (the parts alone
+ * exceed cap; unchanged). */
+int bine_dm_fit_residency(int *cw, int n, int *tw, int cap);
+/* That cap on the current device (needs a GPU): kind 0 = k_dm_move, 1 =
+ * k_dm_move_tree for (dtype, op, nl leaves), 2 = k_dm_fused for (dtype, op);
+ * CUs x resident blocks per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor)
+ * / share.  -1: no such kernel; 0: the device could not be queried. */
+int bine_dm_launch_cap(int kind, int dtype, int op, int nl, int share);
 
 #ifdef __cplusplus
 }

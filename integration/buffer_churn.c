@@ -130,6 +130,29 @@ static void check_reduce_scatter(const char *tag, MPI_Datatype dt, size_t block,
   free(rc);
 }
 
+/* ragged counts with a rank that receives nothing and passes no rbuf (ADVICE
+ * r4): the staged path is chosen from the total on every rank, so that rank
+ * must still issue the schedule its peers issue instead of refusing the call */
+static void check_reduce_scatter_zero(const char *tag, MPI_Datatype dt, size_t block, unsigned seed) {
+  const size_t esz = dt == MPI_FLOAT ? 4 : 8;
+  int *rc = malloc(sizeof(int) * (size_t)size);
+  size_t total = 0;
+  for (int i = 0; i < size; i++) total += (size_t)(rc[i] = i == size - 1 ? 0 : (int)block);
+  const size_t mine = (size_t)rc[rank];
+  void *hs = malloc(total * esz), *want = malloc(block * esz), *got = malloc(block * esz);
+  fill(hs, dt, total, seed + 7927u * (unsigned)rank);
+  PMPI_Reduce_scatter(hs, want, rc, dt, MPI_SUM, MPI_COMM_WORLD);
+  void *r = mine ? malloc(mine * esz) : NULL;
+  const int e = reduce_scatter_bine_send_remap(hs, r, rc, dt, MPI_SUM, MPI_COMM_WORLD);
+  if (mine) memcpy(got, r, mine * esz);
+  report(tag, e == MPI_SUCCESS && (!mine || memcmp(got, want, mine * esz) == 0));
+  free(r);
+  free(hs);
+  free(want);
+  free(got);
+  free(rc);
+}
+
 int main(int argc, char **argv) {
   MPI_Init(&argc, &argv);
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
@@ -172,6 +195,15 @@ int main(int argc, char **argv) {
         snprintf(tag, sizeof tag, "mixed placement reduce_scatter %s block=%zu", dn[d], block);
         check_reduce_scatter(tag, dts[d], block, rank == 0, 47u + (unsigned)k);
       }
+  }
+  if (size > 1) {
+    /* above the staged threshold (2 x 16 MiB in total) and below it */
+    const size_t blocks[2] = {((size_t)48 << 20) / 4 / (size_t)(size - 1) + 3, 1001};
+    for (int k = 0; k < 2; k++) {
+      snprintf(tag, sizeof tag, "reduce_scatter send_remap float block=%zu, last rank 0 elements and no rbuf",
+               blocks[k]);
+      check_reduce_scatter_zero(tag, MPI_FLOAT, blocks[k], 53u + (unsigned)k);
+    }
   }
   if (rank == 0) printf(fails ? "CHURN FAILED %d of %d\n" : "CHURN ok %d\n", fails ? fails : cases, cases);
   MPI_Finalize();

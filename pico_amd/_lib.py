@@ -116,6 +116,9 @@ def lib():
         "bine_fill_pico": ([vp, sz, i, u32, vp], i),
         "bine_copy": ([vp, vp, sz, vp], i),
         "bine_rccl_version": ([ctypes.POINTER(i), ctypes.POINTER(i)], i),
+        "bine_rccl_abi_check": ([i, i], i),
+        "bine_dm_fit_residency": ([ctypes.POINTER(i), i, ctypes.POINTER(i), i], i),
+        "bine_dm_launch_cap": ([i, i, i, i, i], i),
         "bine_checksum": ([vp, sz, i, ctypes.POINTER(u64), vp], i),
         "bine_get_unique_id": ([vp], i),
         "bine_comm_init_rccl": ([ctypes.POINTER(vp), i, i, vp, i], i),

@@ -176,10 +176,27 @@ struct DmMsg {
   int grp = -1;        // a push of the same bytes to several peers: index in m of the group's leader, whose
                        // workgroups read the source once and store it into every member's slot; -1: alone
 };
+// Residency: every workgroup of a direct-transport launch
+// may wait on a flag that a workgroup of a peer's launch sets.  A launch whose
+// workgroups cannot all be resident at once -- together with the launches of
+// the other `share` ranks on the same GPU -- can fill the chip with waiters
+// whose producers never get a slot: a residency stall (the hardware
+// scheduler's time slicing resolves it slowly, or a wait times out).  So every
+// launch is cut to fit: its workgroups (each copy entry's cwgs, the tree's
+// twgs, the fused kernel's wgs) are scaled so that they sum to at most
+// cap = CUs x resident blocks per CU of the kernel (hipOccupancy...) / share.
+// dm_fit_residency: scale `cw[0..n)` and *tw (null: none) proportionally,
+// each >= 1, to sum <= cap.  0: unchanged (already fits or cap <= 0),
+// 1: scaled, -1: n parts (+ the tree) alone exceed cap (left unchanged).
+int dm_fit_residency(int *cw, int n, int *tw, int cap);
+// the cap itself on the current device: kind 0 k_dm_move, 1 k_dm_move_tree for
+// (dtype, op, nl), 2 k_dm_fused for (dtype, op); -1: no such kernel, 0: unknown
+int dm_launch_cap(int kind, int dtype, int op, int nl, int share);
 struct DmArgs {
   int nmsg = 0;
   int wgs = 1;
   int rank = 0;
+  int share = 1;                   // ranks of this transport on this GPU (the residency cap's divisor)
   uint64_t slot = 0;               // bytes per slot
   uint8_t *own = nullptr;          // this rank's inbox (flags, counters, sequence bases, peer table)
   uint32_t *poison_host = nullptr; // mapped host word set together with the inbox's poison word
@@ -244,6 +261,7 @@ bool dm_tree_supported(int dtype, int op, int nl);
 constexpr int kMaxFusedPeers = 15;  // P <= 16
 struct DmFusedArgs {
   int wgs = 1, rank = 0;
+  int share = 1;                       // as DmArgs::share (wgs is cut to the residency cap)
   uint64_t slot = 0;
   uint8_t *own = nullptr;
   uint32_t *poison_host = nullptr;

@@ -226,11 +226,31 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   return BINE_SUCCESS;
 }
 
-void DirectState::scale_for_shared_gpu(int s) {
-  share = s;
-  env_wgs = wgs = scaled(wgs, 16);
-  tree_wgs_env = tree_wgs = scaled(tree_wgs, 32);
+int dm_fit_residency(int *cw, int n, int *tw, int cap) {
+  long tot = tw ? *tw : 0;
+  for (int i = 0; i < n; i++) tot += cw[i];
+  const int parts = n + (tw && *tw > 0 ? 1 : 0);
+  if (cap <= 0 || tot <= cap) return 0;
+  if (parts > cap) return -1;
+  long sum = 0;
+  auto cut = [&](int &v) {
+    v = (int)std::max<long>(1, (long)v * cap / tot);
+    sum += v;
+  };
+  for (int i = 0; i < n; i++) cut(cw[i]);
+  if (tw && *tw > 0) cut(*tw);
+  // the floors of the proportional shares sum to <= cap; the minimum of one
+  // per part can push it over: take the excess from the largest parts
+  while (sum > cap) {
+    int *big = tw && *tw > 0 ? tw : &cw[0];
+    for (int i = 0; i < n; i++)
+      if (cw[i] > *big) big = &cw[i];
+    (*big)--;
+    sum--;
+  }
+  return 1;
 }
+
 
 // Phase 2 (after every rank's phase 1 succeeded -- the caller agrees on that
 // over RCCL first, so no rank waits here for a peer that gave up): hand our
@@ -405,6 +425,7 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   DmArgs a;
   a.wgs = wgs;
   a.rank = rank;
+  a.share = share;
   a.slot = slot;
   a.own = (uint8_t *)own;
   a.poison_host = hpoison_dev;

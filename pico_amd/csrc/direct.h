@@ -71,14 +71,11 @@ struct DirectState {
   int tree_wgs = 256;  // tree workgroups per launch (BINE_DIRECT_TREE_WGS; bine_comm_set_direct_tree)
   int tree_wgs_env = 256;  // the value init() settled on
   // `share` ranks of this transport on this rank's GPU (more than one only
-  // where several processes share a device): above 2 every workgroup count
-  // (default, environment, setter) is cut by share / 2 -- every co-located
-  // rank's exchange launch competes for the same chip's workgroup slots, and
-  // waiting workgroups hold slots the pushes they wait for need (DESIGN.md
-  // §4.4).  On a node share is 1 and nothing changes.
+  // where several processes share a device; 1 on a node): the divisor of
+  // every launch's residency cap (bine_internal.h dm_fit_residency), so the
+  // co-located ranks' current launches are resident together.  Round 4's
+  // share / 2 cut of the workgroup counts is subsumed by the cap.
   int share = 1;
-  int scaled(int v, int floor) const { return share > 2 ? std::max(floor, v * 2 / share) : v; }
-  void scale_for_shared_gpu(int share);
   bool mcast = false;     // pushes of the same bytes to several peers as one group (BINE_DIRECT_MCAST=1;
                           // off: no gain measured, profiles/r3_push_groups.txt)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }

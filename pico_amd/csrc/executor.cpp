@@ -156,6 +156,71 @@ struct RcclTransport final : Transport {
     *all = v;
     return BINE_SUCCESS;
   }
+  // The RCCL ABI probe at communicator creation (see bine_rccl_abi_check): the
+  // enum values this library passes, run through the loaded runtime in one
+  // group and checked on the host -- int32 MIN, uint32 MAX, int64 SUM, float
+  // SUM, double PROD (ops on data whose result depends on reading the type
+  // right), and a uint8 allgather (the exchanges' byte type: a misread element
+  // size would move the wrong number of bytes)
+  int abi_probe() {
+    constexpr int kG = 8;  // bytes each rank contributes to the allgather
+    struct Probe {
+      int32_t i32[2];
+      uint32_t u32;
+      int32_t pad;
+      int64_t i64;
+      float f32;
+      int32_t pad2;
+      double f64;
+      uint8_t g[64 * kG];
+    };
+    if (size > 64) return BINE_SUCCESS;  // the probe's gather area: up to 64 ranks
+    Probe h{};
+    h.i32[0] = rank + 1;
+    h.i32[1] = -(rank + 1);
+    h.u32 = 0x10000u * (uint32_t)rank + 7u;
+    h.i64 = ((int64_t)1 << 40) + rank;
+    h.f32 = 0.5f + (float)rank;
+    h.f64 = rank == 0 ? 3.0 : 1.0;
+    uint8_t mine[kG];
+    for (int k = 0; k < kG; k++) mine[k] = (uint8_t)(rank * 37 + k * 11 + 1);
+    Probe *d = nullptr;
+    uint8_t *gs = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(Probe)));
+    hipError_t e = hipMalloc(&gs, kG);
+    if (e == hipSuccess) e = hipMemcpy(d, &h, sizeof h, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(gs, mine, kG, hipMemcpyHostToDevice);
+    ncclResult_t nr = ncclSuccess;
+    if (e == hipSuccess) {
+      nr = ncclGroupStart();
+      if (nr == ncclSuccess) nr = ncclAllReduce(d->i32, d->i32, 2, ncclInt32, ncclMin, comm, nullptr);
+      if (nr == ncclSuccess) nr = ncclAllReduce(&d->u32, &d->u32, 1, ncclUint32, ncclMax, comm, nullptr);
+      if (nr == ncclSuccess) nr = ncclAllReduce(&d->i64, &d->i64, 1, ncclInt64, ncclSum, comm, nullptr);
+      if (nr == ncclSuccess) nr = ncclAllReduce(&d->f32, &d->f32, 1, ncclFloat32, ncclSum, comm, nullptr);
+      if (nr == ncclSuccess) nr = ncclAllReduce(&d->f64, &d->f64, 1, ncclFloat64, ncclProd, comm, nullptr);
+      if (nr == ncclSuccess) nr = ncclAllGather(gs, d->g, kG, ncclUint8, comm, nullptr);
+      const ncclResult_t ne = ncclGroupEnd();
+      if (nr == ncclSuccess) nr = ne;
+    }
+    if (e == hipSuccess && nr == ncclSuccess) e = hipStreamSynchronize(nullptr);
+    Probe o{};
+    if (e == hipSuccess && nr == ncclSuccess) e = hipMemcpy(&o, d, sizeof o, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (gs) (void)hipFree(gs);
+    NCCL_TRY(nr);
+    HIP_TRY(e);
+    const int64_t P = size;
+    bool ok = o.i32[0] == 1 && o.i32[1] == -(int32_t)P && o.u32 == 0x10000u * (uint32_t)(P - 1) + 7u &&
+              o.i64 == P * ((int64_t)1 << 40) + P * (P - 1) / 2 && o.f32 == 0.5f * (float)P + (float)(P * (P - 1) / 2) &&
+              o.f64 == 3.0;
+    for (int x = 0; ok && x < size; x++)
+      for (int k = 0; k < kG; k++) ok = ok && o.g[x * kG + k] == (uint8_t)(x * 37 + k * 11 + 1);
+    if (!ok) {
+      set_err("RCCL ABI probe failed on rank %d: the runtime reads this library's types / ops differently", rank);
+      return BINE_ERR_RCCL;
+    }
+    return BINE_SUCCESS;
+  }
   // how many ranks of this communicator run on this rank's GPU (same host
   // name and PCI bus id): more than one only when processes share a device
   int ranks_on_my_gpu(int device, int *same) {
@@ -802,6 +867,7 @@ static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int 
   if (t.peer < 2 || t.peer > kMaxLeaves || t.pos < 0 || t.pos >= t.peer || tbytes % 16 || !tbytes) return -1;
   DmFusedArgs a;
   a.wgs = d.wgs;
+  a.share = d.share;
   a.rank = c->rank;
   a.slot = d.slot;
   a.own = (uint8_t *)d.own;
@@ -1680,34 +1746,57 @@ int bine_get_unique_id(void *id) {
   return BINE_SUCCESS;
 }
 
-// RCCL the process actually maps vs the headers this library was compiled
-// against.  In a torch process the loader resolves librccl.so.1 to torch's
-// bundled RCCL (2.26.x in this image) although the headers are ROCm's (2.27.x):
-// the calls used here (group P2P, AllGather, AllToAllv, AllReduce, CommInitRank,
-// 128-byte unique ids) have one ABI across that range, so a different minor
-// version is accepted and reported (bench.py records both); a different major
-// version, or a runtime older than the oldest one the RCCL matrix was run on,
-// is refused at communicator creation.
-constexpr int kMinRcclVersion = 22600;  // 2.26.0
+// RCCL ABI pin.  In a torch process the loader resolves
+// librccl.so.1 to torch's bundled RCCL (2.26.6 in this image) although the
+// library is compiled against ROCm's headers (2.27.7).  What crosses that
+// boundary is exactly: the 128-byte ncclUniqueId, the opaque ncclComm_t, the
+// ncclResult_t / ncclDataType_t / ncclRedOp_t values below, and the argument
+// lists of ncclCommInitRank, ncclSend / ncclRecv, ncclGroupStart / End,
+// ncclAllGather, ncclAllToAllv, ncclAllReduce, ncclGetVersion,
+// ncclGetErrorString, ncclCommDestroy.  (1) Build time: the static_asserts pin
+// the compiled headers to those values -- a header that renumbers any of them
+// does not compile.  (2) Version window: both the compiled headers and the
+// runtime must lie in the window whose ABI for these items was checked
+// (header text: 2.27.3 -- rocprofiler-sdk's copy -- and 2.27.7; runtime 2.26.6
+// behaviourally, by the GPU suite's every-type RCCL matrix and the probe
+// below); anything outside it is refused (bine_rccl_abi_check, a pure function
+// with a CPU test).  (3) At communicator creation one grouped probe (abi_probe)
+// runs the types and ops the library passes through the RUNTIME and checks
+// the results on the host: a runtime that reads any of them differently fails
+// the probe instead of corrupting data later.
+static_assert(sizeof(ncclUniqueId) == 128 && NCCL_UNIQUE_ID_BYTES == 128, "ncclUniqueId layout");
+static_assert(sizeof(ncclComm_t) == sizeof(void *), "ncclComm_t is an opaque pointer");
+static_assert(sizeof(ncclResult_t) == 4 && sizeof(ncclDataType_t) == 4 && sizeof(ncclRedOp_t) == 4,
+              "enum sizes");
+static_assert(ncclSuccess == 0, "ncclResult_t");
+static_assert(ncclInt8 == 0 && ncclUint8 == 1 && ncclInt32 == 2 && ncclUint32 == 3 && ncclInt64 == 4 &&
+                  ncclUint64 == 5 && ncclFloat32 == 7 && ncclFloat64 == 8,
+              "ncclDataType_t numbering");
+static_assert(ncclSum == 0 && ncclProd == 1 && ncclMax == 2 && ncclMin == 3, "ncclRedOp_t numbering");
+constexpr int kRcclAbiLo = 22600, kRcclAbiHi = 22799;  // 2.26.0 ... 2.27.99
+static_assert(NCCL_VERSION_CODE >= kRcclAbiLo && NCCL_VERSION_CODE <= kRcclAbiHi,
+              "compiled against RCCL headers outside the checked ABI window");
+
+int bine_rccl_abi_check(int runtime, int compiled) {
+  const bool rt_ok = runtime >= kRcclAbiLo && runtime <= kRcclAbiHi;
+  const bool ct_ok = compiled >= kRcclAbiLo && compiled <= kRcclAbiHi;
+  if (rt_ok && ct_ok) return BINE_SUCCESS;
+  set_err("RCCL ABI skew: runtime %d, headers %d; both must lie in the checked window %d..%d", runtime, compiled,
+          kRcclAbiLo, kRcclAbiHi);
+  return BINE_ERR_RCCL;
+}
 
 int bine_rccl_version(int *runtime, int *compiled) {
   int v = 0;
   NCCL_TRY(ncclGetVersion(&v));
   if (runtime) *runtime = v;
   if (compiled) *compiled = NCCL_VERSION_CODE;
-  return BINE_SUCCESS;
+  return bine_rccl_abi_check(v, NCCL_VERSION_CODE);
 }
 
 int bine_comm_init_rccl(bine_comm_t *out, int nranks, int rank, const void *id, int device) {
   if (!out || nranks < 1 || rank < 0 || rank >= nranks || !id) return BINE_ERR_ARG;
-  int rv = 0;
-  int rc0 = bine_rccl_version(&rv, nullptr);
-  if (rc0) return rc0;
-  if (rv / 10000 != NCCL_VERSION_CODE / 10000 || rv < kMinRcclVersion) {
-    set_err("RCCL runtime %d is not ABI-compatible with the headers this library was built with (%d; need major "
-            "%d, >= %d)", rv, NCCL_VERSION_CODE, NCCL_VERSION_CODE / 10000, kMinRcclVersion);
-    return BINE_ERR_RCCL;
-  }
+  if (int rc0 = bine_rccl_version(nullptr, nullptr)) return rc0;  // the version window (refuses a skewed pair)
   auto c = std::make_unique<bine_comm>();
   c->rank = rank;
   c->size = nranks;
@@ -1724,6 +1813,7 @@ int bine_comm_init_rccl(bine_comm_t *out, int nranks, int rank, const void *id, 
   for (size_t i = 0; i < sizeof u; i++) h = (h ^ ((const unsigned char *)id)[i]) * 1099511628211ull;
   tx->key = h;
   NCCL_TRY(ncclCommInitRank(&tx->comm, nranks, u, rank));
+  if (int rc2 = tx->abi_probe()) return rc2;
   c->tx = std::move(tx);
   *out = c.release();
   return BINE_SUCCESS;
@@ -2215,9 +2305,9 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
     }
     int same = 1;
     if (int rc3 = r->ranks_on_my_gpu(c->device, &same)) return rc3;
-    d->scale_for_shared_gpu(same);
-    if (r->dm_wgs) d->wgs = d->scaled(r->dm_wgs, 16);
-    if (c->dm_tree_wgs) d->tree_wgs = d->scaled(c->dm_tree_wgs, 32);
+    d->share = same;
+    if (r->dm_wgs) d->wgs = r->dm_wgs;
+    if (c->dm_tree_wgs) d->tree_wgs = c->dm_tree_wgs;
     r->dm = std::move(d);
   }
   if (on && r->dm->poisoned()) {
@@ -2259,7 +2349,7 @@ int bine_comm_set_direct_wgs(bine_comm_t c, int wgs) {
   HIP_TRY(hipDeviceSynchronize());  // no launch of the old shape may still run
   c->drop_graphs();                 // captured direct launches carry the old grid
   r->dm_wgs = wgs;
-  if (r->dm) r->dm->wgs = wgs ? r->dm->scaled(wgs, 16) : r->dm->env_wgs;
+  if (r->dm) r->dm->wgs = wgs ? wgs : r->dm->env_wgs;
   return BINE_SUCCESS;
 }
 
@@ -2275,7 +2365,7 @@ int bine_comm_set_direct_tree(bine_comm_t c, int on) {
   c->dm_tree = v;
   c->dm_tree_wgs = w;
   if (auto *r = dynamic_cast<RcclTransport *>(c->tx.get()))
-    if (r->dm) r->dm->tree_wgs = w ? r->dm->scaled(w, 32) : r->dm->tree_wgs_env;
+    if (r->dm) r->dm->tree_wgs = w ? w : r->dm->tree_wgs_env;
   return BINE_SUCCESS;
 }
 
@@ -2333,5 +2423,14 @@ int bine_comm_set_relay(bine_comm_t c, size_t min_part_bytes) {
 }
 
 int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);
+
+int bine_dm_launch_cap(int kind, int dtype, int op, int nl, int share) {
+  return dm_launch_cap(kind, dtype, op, nl, share);
+}
+
+int bine_dm_fit_residency(int *cw, int n, int *tw, int cap) {
+  if ((n > 0 && !cw) || n < 0 || n > kMaxDm) return -1;
+  return dm_fit_residency(cw, n, tw, cap);
+}
 
 }  // extern "C"

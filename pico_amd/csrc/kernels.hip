@@ -26,6 +26,8 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -468,6 +470,7 @@ int launch_copy(void *dst, const void *src, size_t bytes, void *stream) {
                      bytes);
   return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
+
 
 #endif  // BINE_OPSET == 0
 
@@ -1190,9 +1193,40 @@ static bool dm_args_ok(const DmArgs &a, bool leaves_ok) {
   return true;
 }
 
-int launch_dm_move(const DmArgs &a, void *stream) {
-  if (a.nmsg <= 0) return BINE_SUCCESS;
-  if (!dm_args_ok(a, false)) return BINE_ERR_ARG;
+// Workgroup slots one direct-transport launch may take on the current device
+// (bine_internal.h dm_fit_residency): CUs x resident blocks per CU of kernel
+// `k` (the occupancy API: registers, LDS, wave slots) / share; 0 if unknown.
+// Both factors are queried once per kernel and device.
+static int dm_cap(const void *k, int share) {
+  static std::mutex mu;
+  static std::map<std::pair<const void *, int>, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find({k, dev});
+  if (it == cache.end()) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, kBlock, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      cus = per = 0;
+    }
+    it = cache.emplace(std::make_pair(k, dev), cus * per).first;
+  }
+  return it->second / std::max(1, share);
+}
+
+int launch_dm_move(const DmArgs &a0, void *stream) {
+  if (a0.nmsg <= 0) return BINE_SUCCESS;
+  if (!dm_args_ok(a0, false)) return BINE_ERR_ARG;
+  DmArgs a = a0;
+  if (dm_fit_residency(a.cwgs, a.ncopy, nullptr, dm_cap((const void *)k_dm_move, a.share)) > 0) {
+    a.ncw = 0;
+    for (int c = 0; c < a.ncopy; c++) a.ncw += a.cwgs[c];
+  }
   hipLaunchKernelGGL(k_dm_move, dim3((unsigned)a.ncw), dim3(kBlock), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
@@ -1306,7 +1340,25 @@ bool dm_tree_supported(int dtype, int op, int nl) {
 }
 
 template <typename T, int OP>
-static hipError_t dmt_launch(const DmArgs &a, const DmTree &t, hipStream_t st) {
+static const void *dmt_kernel(int nl) {
+  switch (nl) {
+    case 2: return (const void *)k_dm_move_tree<T, OP, 2>;
+    case 4: return (const void *)k_dm_move_tree<T, OP, 4>;
+    case 8: return (const void *)k_dm_move_tree<T, OP, 8>;
+    case 16: return (const void *)k_dm_move_tree<T, OP, 16>;
+    default: return nullptr;
+  }
+}
+
+template <typename T, int OP>
+static hipError_t dmt_launch(const DmArgs &a0, const DmTree &t0, hipStream_t st) {
+  DmArgs a = a0;
+  DmTree t = t0;
+  if (const void *k = dmt_kernel<T, OP>(t.nl))
+    if (dm_fit_residency(a.cwgs, a.ncopy, &t.twgs, dm_cap(k, a.share)) > 0) {
+      a.ncw = 0;
+      for (int c = 0; c < a.ncopy; c++) a.ncw += a.cwgs[c];
+    }
   const dim3 g((unsigned)(a.ncw + t.twgs));
   switch (t.nl) {
     case 2: hipLaunchKernelGGL((k_dm_move_tree<T, OP, 2>), g, dim3(kBlock), 0, st, a, t); break;
@@ -1553,7 +1605,11 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
 }
 
 template <typename T, int OP>
-static hipError_t fused_launch(const DmFusedArgs &a, hipStream_t st) {
+static hipError_t fused_launch(const DmFusedArgs &a0, hipStream_t st) {
+  DmFusedArgs a = a0;
+  int w = a.wgs;
+  dm_fit_residency(&w, 1, nullptr, dm_cap((const void *)k_dm_fused<T, OP>, a.share));
+  a.wgs = w;
   hipLaunchKernelGGL((k_dm_fused<T, OP>), dim3((unsigned)a.wgs), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
@@ -1736,6 +1792,42 @@ int launch_checksum(const void *buf, size_t n, int dtype, uint64_t *host_out, vo
   (void)hipFree(d);
   if (rc == BINE_SUCCESS) *host_out = h;
   return rc;
+}
+
+// workgroup slots of the current device for one direct-transport kernel
+// (bine_dm_launch_cap): kind 0 k_dm_move, 1 k_dm_move_tree<T, OP, nl>,
+// 2 k_dm_fused<T, OP>; T / OP from (dtype, op) as the launchers pick them
+template <typename T>
+static const void *dm_kernel_t(int kind, int op, int nl) {
+  auto pick = [&](auto opc) -> const void * {
+    constexpr int OP = decltype(opc)::value;
+    return kind == 1 ? dmt_kernel<T, OP>(nl) : (const void *)k_dm_fused<T, OP>;
+  };
+  switch (op) {
+    case BINE_SUM: return pick(std::integral_constant<int, BINE_SUM>{});
+    case BINE_PROD: return pick(std::integral_constant<int, BINE_PROD>{});
+    case BINE_MAX: return pick(std::integral_constant<int, BINE_MAX>{});
+    case BINE_MIN: return pick(std::integral_constant<int, BINE_MIN>{});
+    default: return nullptr;
+  }
+}
+
+int dm_launch_cap(int kind, int dtype, int op, int nl, int share) {
+  const void *k = nullptr;
+  if (kind == 0) {
+    k = (const void *)k_dm_move;
+  } else if (kind == 1 || kind == 2) {
+    switch (dtype) {
+      case BINE_FLOAT: k = dm_kernel_t<float>(kind, op, nl); break;
+      case BINE_DOUBLE: k = dm_kernel_t<double>(kind, op, nl); break;
+      case BINE_INT32: k = dm_kernel_t<int32_t>(kind, op, nl); break;
+      case BINE_INT64: k = dm_kernel_t<int64_t>(kind, op, nl); break;
+      case BINE_UINT32: k = dm_kernel_t<uint32_t>(kind, op, nl); break;
+      case BINE_UINT64: k = dm_kernel_t<uint64_t>(kind, op, nl); break;
+      default: break;
+    }
+  }
+  return k ? dm_cap(k, share) : -1;
 }
 
 }  // namespace bine

@@ -276,6 +276,7 @@ bool on_device(const void *p) {
 }
 
 int stage(Entry *e, int slot, size_t bytes, void **dev) {
+  bytes = std::max<size_t>(bytes, 256);  // a zero-byte buffer still gets an address
   if (e->dev_bytes[slot] < bytes) {
     if (e->dev[slot]) (void)hipFree(e->dev[slot]);
     e->dev[slot] = nullptr;
@@ -450,6 +451,11 @@ int with_staged(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t rb
   if (host_r) {
     if ((rc = stage(e, 1, rbytes, &dr))) return rc;
     pins.add(rbuf, rbytes);
+  } else if (!dr) {
+    // a rank that receives nothing may pass no rbuf (reduce_scatter with
+    // rcounts[rank] == 0): it still issues the schedule its peers issue, so it
+    // gets a device placeholder instead of refusing the call on its own
+    if ((rc = stage(e, 1, 0, &dr))) return rc;
   }
   pins.commit();
   const void *hs = in_place ? BINE_IN_PLACE : host_s ? sbuf : nullptr;

@@ -160,11 +160,27 @@ def dm_tree_plan(ops, esz, slot, kmax=32):
 
 
 def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay_min_bytes=0, trees=False,
-        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20, merge=3, dm_trees=False, stats=None):
+        flat_ag=False, flat_rs=False, calls=3, slot=16 << 20, merge=3, dm_trees=False, stats=None,
+        residency=None):
     """simulate `calls` consecutive collectives on all ranks; returns None if
     every one completes, else a description of the deadlock.  dm_trees: the
     flat reduce-scatter's trees fused into exchange launches as the executor
-    does over the direct transport (deferred leaf pulls; `stats` counts them)"""
+    does over the direct transport (deferred leaf pulls; `stats` counts them).
+
+    residency (None: every workgroup of a started launch is resident, i.e. the
+    protocol alone): {"gpu_of": [gpu of rank r], "slots": workgroup slots per
+    GPU, "wgs": workgroups per message, "cap": True to apply the library's
+    residency cut (dm_fit_residency: a launch's workgroups scaled to
+    slots / ranks on its GPU), "policy": "rr" (the GPU's dispatcher takes one
+    workgroup from each rank's launch in turn), "seq" (one rank's whole
+    launch first) or "adv" (adversarial: a workgroup that will wait whenever
+    some rank's next one does -- the dispatcher may pick any queue)}.  Each message is then `wgs`
+    workgroups dispatched in the launch's message order (the kernel's
+    blockIdx order); a dispatched workgroup holds its slot until its wait is
+    satisfied; the message's flag moves when its last workgroup is done.  A
+    residency stall is reported like a protocol deadlock, with
+    "residency": True.  `stats` (if given) gets "max_launch_wgs" and
+    "max_gpu_wgs" (the most workgroups of concurrent launches on one GPU)."""
     seq_s = [[0] * P for _ in range(P)]
     seq_r = [[0] * P for _ in range(P)]
     # ready[owner][from][slot], ack[owner][from][slot]: plain stores, as the
@@ -267,9 +283,96 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                 return j
         return None
 
+    res_on = residency is not None
+    if res_on:
+        gpu_of = residency["gpu_of"]
+        ngpu = max(gpu_of) + 1
+        free = [residency["slots"]] * ngpu
+        share = [gpu_of.count(g) for g in range(ngpu)]
+        policy = residency.get("policy", "rr")
+        turn = [0] * ngpu
+
+        def launch_wgs(r, launch):
+            """the workgroups of each message of a launch (the library's cut applied if asked)"""
+            if "wg" not in launch[0]:
+                cw = [residency["wgs"]] * len(launch)
+                if residency.get("cap"):
+                    fit(cw, None, residency["slots"] // share[gpu_of[r]])
+                for m, w in zip(launch, cw):
+                    m["wg"], m["disp"], m["fin"] = w, 0, 0
+                if stats is not None:
+                    stats["max_launch_wgs"] = max(stats.get("max_launch_wgs", 0), sum(cw))
+            return launch
+
+    def cond(r, launch, m):
+        """the flag condition of message m of rank r's current launch"""
+        p, k = m["peer"], m["seq"] % SLOTS
+
+        def ack_ok(x):
+            return x["seq"] <= SLOTS or ack[r][x["peer"]][x["seq"] % SLOTS] >= x["seq"] - SLOTS
+
+        if m["kind"] == "push":
+            # a group writes only once every member's slot is free
+            return ack_ok(m) and ("grp" not in m or all(ack_ok(x) for x in launch
+                                                       if x["kind"] == "push" and x.get("grp") == m["grp"]))
+        return ready[r][p][k] >= m["seq"]
+
+    def complete(r, m):
+        p, k = m["peer"], m["seq"] % SLOTS
+        if m["kind"] == "push":
+            assert ready[p][r][k] < m["seq"], "a ready flag would move backwards"
+            ready[p][r][k] = m["seq"]
+        else:
+            assert ack[p][r][k] < m["seq"], "an ack flag would move backwards"
+            ack[p][r][k] = m["seq"]
+        m["done"] = True
+
+    def current(r):
+        """rank r's runnable comm-stream launch (deps met), or None"""
+        j = head(r, "C")
+        if j is None:
+            return None
+        op = ranks[r][j]
+        if not all(dep_done(r, d) for d in op["deps"]) or op["li"] >= len(op["launches"]):
+            return None
+        return op["launches"][op["li"]]
+
     progress = True
     while progress:
         progress = False
+        if res_on:
+            # dispatch: each GPU fills its free slots from its ranks' current launches
+            for g in range(ngpu):
+                mine = [r for r in range(P) if gpu_of[r] == g]
+                while free[g] > 0:
+                    cands = []
+                    for r in mine:
+                        L = current(r)
+                        if L is not None and any(m["disp"] < m["wg"] for m in launch_wgs(r, L)):
+                            cands.append(r)
+                    if not cands:
+                        break
+                    if policy == "seq":
+                        r = cands[0]
+                    elif policy == "adv":
+                        # adversarial: a workgroup that will wait, if any rank's next one does
+                        def nxt(x):
+                            L = current(x)
+                            return L, next(m for m in L if m["disp"] < m["wg"])
+                        waiting = [x for x in cands if not cond(x, *nxt(x))]
+                        r = (waiting or cands)[turn[g] % len(waiting or cands)]
+                        turn[g] += 1
+                    else:
+                        r = cands[turn[g] % len(cands)]
+                        turn[g] += 1
+                    L = current(r)
+                    m = next(x for x in L if x["disp"] < x["wg"])
+                    m["disp"] += 1
+                    free[g] -= 1
+                    progress = True
+                if stats is not None:
+                    held = sum(m["disp"] - m["fin"] for r in mine for L in [current(r)] if L for m in L)
+                    stats["max_gpu_wgs"] = max(stats.get("max_gpu_wgs", 0), held)
         for r in range(P):
             for stream in ("C", "K"):
                 j = head(r, stream)
@@ -284,30 +387,22 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                     continue
                 # the current launch: its messages progress independently
                 launch = op["launches"][op["li"]]
-
-                def ack_ok(m):
-                    k = m["seq"] % SLOTS
-                    return m["seq"] <= SLOTS or ack[r][m["peer"]][k] >= m["seq"] - SLOTS
-
                 for m in launch:
                     if m.get("done"):
                         continue
-                    p = m["peer"]
-                    k = m["seq"] % SLOTS
-                    if m["kind"] == "push":
-                        if not ack_ok(m):
-                            continue
-                        if "grp" in m and not all(ack_ok(x) for x in launch
-                                                  if x["kind"] == "push" and x.get("grp") == m["grp"]):
-                            continue   # a group writes only once every member's slot is free
-                        assert ready[p][r][k] < m["seq"], "a ready flag would move backwards"
-                        ready[p][r][k] = m["seq"]
-                    else:
-                        if ready[r][p][k] < m["seq"]:
-                            continue
-                        assert ack[p][r][k] < m["seq"], "an ack flag would move backwards"
-                        ack[p][r][k] = m["seq"]
-                    m["done"] = True
+                    if res_on:
+                        # dispatched workgroups whose wait is over finish and free their slots
+                        w = m["disp"] - m["fin"]
+                        if w and cond(r, launch, m):
+                            m["fin"] += w
+                            free[gpu_of[r]] += w
+                            progress = True
+                            if m["fin"] == m["wg"]:
+                                complete(r, m)
+                        continue
+                    if not cond(r, launch, m):
+                        continue
+                    complete(r, m)
                     progress = True
                 if all(m.get("done") for m in launch):
                     op["li"] += 1
@@ -324,4 +419,34 @@ def run(coll, algo, P, count=0, rcounts=None, esz=4, chunk_bytes=16 << 20, relay
                 stuck.append((r, stream, j, op["deps"], pend))
     if not stuck:
         return None
-    return {"stuck": stuck, "ready": ready, "ack": ack}
+    out = {"stuck": stuck, "ready": ready, "ack": ack}
+    if res_on:
+        out["residency"] = True
+        out["free_slots"] = list(free)
+    return out
+
+
+def fit(cw, tw, cap):
+    """restatement of dm_fit_residency (bine_internal.h; the library's own is
+    tested against it through bine_dm_fit_residency): scale the parts
+    proportionally, each >= 1, to sum <= cap; 0 unchanged, 1 scaled, -1 the
+    parts alone exceed cap"""
+    tot = sum(cw) + (tw[0] if tw else 0)
+    parts = len(cw) + (1 if tw and tw[0] > 0 else 0)
+    if cap <= 0 or tot <= cap:
+        return 0
+    if parts > cap:
+        return -1
+    for i in range(len(cw)):
+        cw[i] = max(1, cw[i] * cap // tot)
+    if tw and tw[0] > 0:
+        tw[0] = max(1, tw[0] * cap // tot)
+    s = sum(cw) + (tw[0] if tw else 0)
+    while s > cap:
+        if tw and tw[0] > 0 and tw[0] >= max(cw + [0]):
+            tw[0] -= 1
+        else:
+            i = max(range(len(cw)), key=lambda x: (cw[x], -x))
+            cw[i] -= 1
+        s -= 1
+    return 1

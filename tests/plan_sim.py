@@ -45,6 +45,8 @@ def poison(a):
     """a recognisable non-value for the device copies the staging must fill"""
     if a.dtype.kind == "f":
         a[:] = np.nan
+    elif a.dtype.kind == "O":   # symbolic runs: an unwritten element is None
+        a[:] = None
     else:
         a.view(np.uint8)[:] = 0xA5
     return a
@@ -79,14 +81,14 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         if coll == "allgather":
             # in place: rbufs[r] already holds the rank's block where the
             # algorithm expects it (P * count elements)
-            rb = np.array(rbufs[r]).copy() if in_place else np.zeros(P * count, O.NP_DTYPES[dtype])
+            rb = np.array(rbufs[r]).copy() if in_place else poison(np.empty(P * count, O.NP_DTYPES[dtype]))
             sb = np.zeros(0, O.NP_DTYPES[dtype]) if in_place else sbufs[r].copy()
         elif rbufs is not None:
             rb = rbufs[r]
-        elif coll == "reduce_scatter":
-            rb = np.zeros(max(rcounts[r], 1), O.NP_DTYPES[dtype])
+        elif coll == "reduce_scatter":   # output buffers start poisoned too (the GPU tests' NaN fill)
+            rb = poison(np.empty(max(rcounts[r], 1), O.NP_DTYPES[dtype]))
         else:
-            rb = np.zeros(max(count, 1), O.NP_DTYPES[dtype])
+            rb = poison(np.empty(max(count, 1), O.NP_DTYPES[dtype]))
         if coll != "allgather":
             sb = sbufs[r].copy()
         if in_place and coll != "allgather":
@@ -97,9 +99,11 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             sb = rb
         if chunk_bytes is not None:
             tmp = info["tmp_elems"]  # the schedule's own plan (multi-tree plans differ)
-        tbufs = [np.zeros(max(int(t), 1) + 16, O.NP_DTYPES[dtype]) for t in tmp]
+        # workspaces start poisoned: the device's persist across calls, so a plan that
+        # reads a temporary before writing it would see a previous call's bytes
+        tbufs = [poison(np.empty(max(int(t), 1) + 16, O.NP_DTYPES[dtype])) for t in tmp]
         # relay staging (BINE_BUF_STAGE), exactly as large as the executor allocates
-        tbufs.append(np.zeros(info["stage_elems"] if chunk_bytes is not None else 0, O.NP_DTYPES[dtype]))
+        tbufs.append(poison(np.empty(info["stage_elems"] if chunk_bytes is not None else 0, O.NP_DTYPES[dtype])))
         bufs.append([sb, rb] + tbufs)
         if stage:
             dev_in = rb if in_place else sb

@@ -72,3 +72,25 @@ def test_op_valid_matches_mpich_table():
                 want = o in ("sum", "prod")   # C99 complex: SUM / PROD only
             assert bool(lib.bine_op_valid(dv, ov)) == want, (d, o)
     assert not lib.bine_op_valid(17, 0) and not lib.bine_op_valid(0, 12)
+
+
+def test_rccl_abi_window_refuses_a_skewed_pair():
+    """the RCCL pair the library is built against / runs on
+    must lie in the window whose ABI for every type it passes was checked
+    (executor.cpp: static_asserts on the header values, bine_rccl_abi_check,
+    the creation-time probe); outside it bine_rccl_version refuses."""
+    L = pico_amd.lib()
+    assert L.bine_rccl_abi_check(22606, 22707) == 0     # torch's runtime, ROCm 7.2's headers
+    assert L.bine_rccl_abi_check(22703, 22703) == 0
+    err = 5   # BINE_ERR_RCCL (include/bine_amd.h)
+    for rt, ct in ((22509, 22707), (22800, 22707), (22606, 22800), (32000, 22707), (22606, 21900)):
+        rc = L.bine_rccl_abi_check(rt, ct)
+        assert rc != 0, (rt, ct)
+        if err is not None:
+            assert rc == err
+        assert b"skew" in L.bine_last_error()
+    # this process's own pair (loading librccl needs no GPU): inside the window
+    import ctypes
+    rt, ct = ctypes.c_int(), ctypes.c_int()
+    assert L.bine_rccl_version(ctypes.byref(rt), ctypes.byref(ct)) == 0, L.bine_last_error()
+    assert 22600 <= rt.value <= 22799 and 22600 <= ct.value <= 22799

@@ -133,3 +133,86 @@ def test_hbm_model_of_the_fused_trees(P):
     if P == 8:
         assert (rs[False], rs[True]) == (4.625, 2.875), rs
     assert rs[True] < rs[False]
+
+
+# ---- residency -------------------------------------------------
+# The trial that timed out in two of six 8-rank rehearsals on one GPU (DESIGN.md
+# section 4.4): relay+flat+dm, C3 (67,108,864 fp32 per rank), 16 MiB chunks, 64 MiB
+# slots, RELAY_MIN_BYTES 256 KiB, the default 128 workgroups per message cut by
+# share / 2 = 4 to 32.  k_dm_move holds 32 VGPRs (8 waves per SIMD: 8 workgroups
+# of 256 threads per CU), so one MI355X has 256 x 8 = 2048 workgroup slots.
+TRIAL = dict(count=67_108_864, esz=4, chunk_bytes=16 << 20, relay_min_bytes=256 << 10, flat_ag=True,
+             slot=64 << 20, merge=3)
+SLOTS_MI355X = 256 * 8
+
+
+def test_relay_flat_dm_trial_protocol_is_deadlock_free():
+    """the exact trial configuration with every workgroup resident: the
+    protocol itself completes -- the recorded timeout was not a protocol
+    deadlock"""
+    assert dm_sim.run("allreduce", "bine_bdw_remap", 8, calls=2, **TRIAL) is None
+
+
+def test_shared_gpu_residency_stall_and_the_cut():
+    """8 ranks on one GPU: without the library's residency cut a dispatcher
+    order exists in which the chip fills with waiting workgroups whose
+    producers have no slot (a residency stall -- what the hardware scheduler
+    resolves by time slicing, slowly, or not within the 10 s wait); with
+    the cut (dm_fit_residency: each launch <= slots / ranks on the GPU) every
+    co-located rank's current launch is resident at once and no dispatcher
+    order stalls"""
+    kw = dict(TRIAL, count=8 << 20)
+    gpu = {"gpu_of": [0] * 8, "slots": SLOTS_MI355X}
+    st = {}
+    res = dm_sim.run("allreduce", "bine_bdw_remap", 8, calls=2, stats=st,
+                     residency=dict(gpu, wgs=128, cap=False, policy="seq"), **kw)
+    assert res is not None and res["residency"] and res["free_slots"] == [0]
+    assert st["max_launch_wgs"] == 14 * 128   # 7 pushes + 7 pulls of 128 workgroups
+    for pol in ("seq", "rr", "adv"):
+        for wgs in (32, 128):
+            st = {}
+            res = dm_sim.run("allreduce", "bine_bdw_remap", 8, calls=2, stats=st,
+                             residency=dict(gpu, wgs=wgs, cap=True, policy=pol), **kw)
+            assert res is None, (pol, wgs, res and res["stuck"][:4])
+            assert st["max_launch_wgs"] <= SLOTS_MI355X // 8 and st["max_gpu_wgs"] <= SLOTS_MI355X
+
+
+def test_node_residency_one_rank_per_gpu():
+    """one rank per GPU (the node): launches larger than the chip complete
+    without the cut too (dispatch is in order within a launch and nothing a
+    workgroup waits for sits behind it on its own GPU); the cut makes every
+    launch one wave of residency"""
+    kw = dict(TRIAL, count=16 << 20)
+    for cap in (False, True):
+        st = {}
+        res = dm_sim.run("allreduce", "bine_bdw_remap", 8, calls=2, stats=st,
+                         residency={"gpu_of": list(range(8)), "slots": SLOTS_MI355X, "wgs": 256, "cap": cap,
+                                    "policy": "seq"}, **kw)
+        assert res is None
+        assert (st["max_launch_wgs"] <= SLOTS_MI355X) == cap
+
+
+def test_fit_residency_library_matches_restatement():
+    """bine_dm_fit_residency (the library's cut) == dm_sim.fit on random
+    launches: sum <= cap, every part >= 1, unchanged when it fits"""
+    import ctypes
+    import random
+    import pico_amd
+    L = pico_amd.lib()
+    rng = random.Random(5)
+    for _ in range(2000):
+        n = rng.randint(0, 32)
+        cw = [rng.choice([1, 16, 32, 64, 128, 256, 512]) * rng.randint(1, 3) for _ in range(n)]
+        tw = rng.choice([None, 0, 32, 256, 512])
+        cap = rng.choice([0, 1, 8, 64, 160, 256, 1280, 2048, 4096])
+        a = (ctypes.c_int * max(n, 1))(*cw)
+        t = ctypes.c_int(tw or 0)
+        rc = L.bine_dm_fit_residency(a, n, ctypes.byref(t) if tw is not None else None, cap)
+        pc, pt = list(cw), ([tw] if tw is not None else None)
+        want = dm_sim.fit(pc, pt, cap)
+        assert rc == want, (cw, tw, cap)
+        assert list(a)[:n] == pc and (tw is None or t.value == pt[0])
+        if rc == 1:
+            assert sum(pc) + (pt[0] if pt else 0) <= cap and min(pc + [1]) >= 1
+        if rc == 0:
+            assert pc == cw

@@ -924,3 +924,22 @@ def test_vendor_allreduce_needs_rccl():
     with pytest.raises(pico_amd.BineError) as e:
         pico_amd.vendor_allreduce(x, x, 16, "float", "sum", c)
     assert e.value.status == 6  # BINE_ERR_UNSUPPORTED
+
+
+def test_direct_transport_launch_caps(dev):
+    """the residency cap of every direct-transport kernel on this device
+    (bine_dm_launch_cap: CUs x resident blocks per CU / share): k_dm_move's
+    32 VGPRs hold 8 workgroups per CU, k_dm_move_tree<float, SUM, 8>'s 96
+    hold 5 -- 2048 and 1280 slots on MI355X's 256 CUs; every launch is cut to
+    its cap / ranks on the GPU (tests/test_direct_protocol.py)"""
+    L = pico_amd.lib()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    mv = L.bine_dm_launch_cap(0, 0, 0, 0, 1)
+    tr8 = L.bine_dm_launch_cap(1, pico_amd.DTYPES["float"], pico_amd.OPS["sum"], 8, 1)
+    fu = L.bine_dm_launch_cap(2, pico_amd.DTYPES["float"], pico_amd.OPS["sum"], 0, 1)
+    print(f"CUs {cus}: k_dm_move {mv}, k_dm_move_tree<f,SUM,8> {tr8}, k_dm_fused<f,SUM> {fu}")
+    assert mv > 0 and tr8 > 0 and fu > 0
+    assert mv % cus == 0 and tr8 % cus == 0 and fu % cus == 0
+    assert mv >= tr8                     # the tree's registers cost residency
+    assert L.bine_dm_launch_cap(0, 0, 0, 0, 8) == mv // 8
+    assert L.bine_dm_launch_cap(1, pico_amd.DTYPES["float"], pico_amd.OPS["sum"], 3, 1) == -1

@@ -55,6 +55,35 @@ def small():
     return d
 
 
+R64_F, R64_D = 16_777_216, 8_388_608   # tools/rccl_large.py: 64 MiB per rank in fp32 / fp64
+
+
+def rccl_large():
+    """tools/rccl_large.py's cases (64 MiB per rank, P = 2, 4, 8): the inputs'
+    own digests (so a rank can tell a corrupted input from a wrong result),
+    allreduce_bine_bdw_remap fp32 / fp64 (+ multi-tree at P = 4, 8) and
+    reduce_scatter_bine_permute_remap fp32"""
+    import test_trees as TT
+    d = {}
+    for dt, n in (("float", R64_F), ("double", R64_D)):
+        d[key("L64", "input", "fill_pico", dt, n, 8)] = [O.digest(O.fill(dt, n, 1234 + r)) for r in range(8)]
+    for P in (2, 4, 8):
+        for dt, n in (("float", R64_F), ("double", R64_D)):
+            sb = O.inputs(dt, n, P)
+            want, rets = O.allreduce("bine_bdw_remap", sb, dt)
+            assert not any(rets)
+            d[key("L64", "allreduce", "bine_bdw_remap", dt, n, P)] = [O.digest(w) for w in want]
+            if P in (4, 8):
+                want = TT.relabelled_oracle("bine_bdw_remap", sb, dt)
+                d[key("L64", "allreduce", "bine_bdw_remap", dt, n, P, True)] = [O.digest(w) for w in want]
+        sb = O.inputs("float", R64_F, P)
+        want, rets = O.reduce_scatter("bine_permute_remap", sb, [R64_F // P] * P, "float")
+        assert not any(rets)
+        d[key("L64", "reduce_scatter", "bine_permute_remap", "float", R64_F, P)] = [O.digest(w) for w in want]
+        print(f"L64 P={P}", flush=True)
+    return d
+
+
 def big():
     import test_trees as TT
     d = {}
@@ -105,6 +134,7 @@ def main():
         with open(OUT) as f:
             d = json.load(f).get("digests", {})
     d.update(small())
+    d.update(rccl_large())
     if not quick:
         d.update(big())
     doc = {"generator": "tools/make_bench_digests.py (oracle/bine_oracle.c, pinned by tests/golden/index.json.gz)",
