@@ -401,6 +401,12 @@ int bine_comm_set_graphs(bine_comm_t comm, int on);
  * every call ran eagerly (graph mode off, NULL stream, or a schedule the
  * runtime gate above keeps eager); -status on error. */
 int64_t bine_comm_graphs_cached(bine_comm_t comm);
+/* Large collectives this communicator issued as ONE k_dm_fused launch over
+ * the direct transport (every exchange and tree of the call in one kernel:
+ * bine_comm_set_direct + bine_comm_set_direct_tree on, flat phases, at most
+ * 4 slot-sized chunks; BINE_DIRECT_FUSED_LARGE=0 turns the form off);
+ * eager issues only (graph replays are not counted). */
+int64_t bine_comm_fused_calls(bine_comm_t comm);
 
 /* Per-op device timing ("hipEvents per step"): with profiling on, every op
  * of a collective's issue schedule -- an exchange group on the comm stream or

@@ -152,6 +152,7 @@ def lib():
         "bine_comm_set_flat_rs": ([vp, i], i),
         "bine_comm_set_graphs": ([vp, i], i),
         "bine_comm_graphs_cached": ([vp], ctypes.c_int64),
+        "bine_comm_fused_calls": ([vp], ctypes.c_int64),
         "bine_comm_set_direct": ([vp, i], i),
         "bine_comm_set_direct_wgs": ([vp, i], i),
         "bine_comm_set_direct_tree": ([vp, i], i),

@@ -165,6 +165,13 @@ class Comm:
         stream must not be the NULL stream."""
         check(lib().bine_comm_set_graphs(self.handle, int(on)), "bine_comm_set_graphs")
 
+    def fused_calls(self) -> int:
+        """large collectives issued as one k_dm_fused launch (bine_comm_fused_calls)"""
+        n = lib().bine_comm_fused_calls(self.handle)
+        if n < 0:
+            check(int(-n), "bine_comm_fused_calls")
+        return int(n)
+
     def graphs_cached(self) -> int:
         """graphs graph mode holds (0: every call so far ran eagerly)"""
         n = lib().bine_comm_graphs_cached(self.handle)

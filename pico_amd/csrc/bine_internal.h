@@ -246,19 +246,33 @@ struct DmTree {
 int launch_dm_move_tree(const DmArgs &a, const DmTree &t, int dtype, int op, void *stream);
 bool dm_tree_supported(int dtype, int op, int nl);
 
-// The whole flat-form small collective in ONE launch over the direct
-// transport (k_dm_fused): phase A pushes this rank's blocks into the peers'
-// inboxes; phase B waits for the peers' blocks and evaluates the reference's
-// reduction tree (the REDUCE_TREE primitive: own leaf at `pos`, the received
-// blocks read straight out of the inbox slots, `swap` per level) into `out`;
-// phase C pushes `out` to the peers and copies theirs out of the inbox (the
-// flat allgather; absent for the one-shot latency form).  Workgroup w handles
+// A whole flat-form collective in ONE launch over the direct transport
+// (k_dm_fused): phase A pushes this rank's blocks (every chunk) into the
+// peers' inboxes; then for each chunk c, phase B_c waits for the peers' blocks
+// of that chunk and evaluates the reference's reduction tree (the
+// REDUCE_TREE primitive: own leaf at `pos`, the received blocks read straight
+// out of the inbox slots, `swap` per level) into its `out`, pushing each
+// result vector from registers into the peers' slots (the flat allgather's
+// piece c); phase D copies the peers' results out of the inbox (absent for
+// the one-shot latency form and for reduce-scatters).  Workgroup w handles
 // the same 1/wgs slice of every message in every phase, so a workgroup only
-// ever reads back what it wrote itself: no grid-wide barrier.  Messages use
-// the same slots, flags, counters and device-side sequence bases as
-// k_dm_move (j = the message's index among this launch's messages of its kind
-// to / from its peer).
+// ever reads back what it wrote itself: no grid-wide barrier.  Every wait
+// is for a flag that a peer sets in an EARLIER phase, and every workgroup of
+// every rank's launch is resident (the residency cut), so the phases
+// complete in order.  Messages use the same slots, flags, counters and
+// device-side sequence bases as k_dm_move (j = the message's index among
+// this launch's messages of its kind to / from its peer, < kSlots: no slot
+// is used twice in one launch).
 constexpr int kMaxFusedPeers = 15;  // P <= 16
+constexpr int kMaxFusedTrees = 4;   // chunks of the tree phase
+constexpr int kMaxFusedMsgs = 4 * kMaxFusedPeers;
+struct DmFusedTree {
+  const void *own_leaf = nullptr;
+  void *out = nullptr;
+  uint64_t nvec = 0;                   // 16-B vectors per leaf / of out
+  int b0 = 0, nb = 0, nc = 0;          // leaves m[b0, b0 + nb), then the pushes of out m[b0 + nb, b0 + nb + nc)
+  int8_t leaf[kMaxLeaves] = {};        // leaf j != pos: index in m of the pull carrying it
+};
 struct DmFusedArgs {
   int wgs = 1, rank = 0;
   int share = 1;                       // as DmArgs::share (wgs is cut to the residency cap)
@@ -266,18 +280,16 @@ struct DmFusedArgs {
   uint8_t *own = nullptr;
   uint32_t *poison_host = nullptr;
   uint64_t timeout_ticks = 0;
-  int na = 0, nb = 0, nc = 0, nd = 0;  // phase A pushes, A pulls (tree leaves), C pushes, C pulls
-  DmMsg m[4 * kMaxFusedPeers];         // in that order
+  int na = 0, nt = 0, d0 = 0, nd = 0;  // phase A pushes m[0, na); trees t[0, nt); phase D pulls m[d0, d0 + nd)
+  DmMsg m[kMaxFusedMsgs];
   int nl = 0, pos = 0;
   unsigned swap = 0;
-  int leaf[kMaxLeaves];                // leaf j != pos: index in m of the A pull carrying it
-  const void *own_leaf = nullptr;
-  void *out = nullptr;
-  uint64_t nvec = 0;                   // 16-B vectors per leaf / of out
+  DmFusedTree t[kMaxFusedTrees];
 };
 // BINE_ERR_UNSUPPORTED: (dtype, op) has no fused instantiation (the caller
 // issues the primitives one by one)
 int launch_dm_fused(const DmFusedArgs &a, int dtype, int op, void *stream);
+int dm_fused_check(const DmFusedArgs &a, int dtype, int op);  // launch_dm_fused's argument check alone
 bool dm_fused_supported(int dtype, int op);
 int launch_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void *stream);
 

@@ -168,6 +168,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
   if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
   if (const char *e = getenv("BINE_DIRECT_MCAST")) mcast = atoi(e) != 0;
+  if (const char *e = getenv("BINE_DIRECT_FUSED_WGS")) fused_wgs = std::max(1, atoi(e));
   tree_wgs_env = tree_wgs;
   if (slot < (1 << 20)) slot = 1 << 20;
   if (slot > ((size_t)1 << 30)) slot = (size_t)1 << 30;  // write-through stores address a slot by 32-bit offsets

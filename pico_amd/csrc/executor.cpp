@@ -519,6 +519,8 @@ struct bine_comm {
   // fused-tree plans (plan_dm_trees) per (plan, buffers, dtype, op, settings):
   // a pure function of those, cached so a call's issue path does not redo it
   std::map<std::string, bine::DmTreePlan> tree_cache;
+  std::map<std::string, bool> fused_cache;  // fused_for
+  int64_t fused_calls = 0;                  // bine_comm_fused_calls
   std::vector<hipEvent_t> tree_ev;
   std::vector<char> tree_pending;
   // per-op device timing of the latest collective (bine_comm_set_profile)
@@ -839,109 +841,183 @@ static bool fused_on() {
   return on;
 }
 
-// The flat form of a small collective over the direct transport as ONE
-// launch (k_dm_fused, bine_internal.h DmFusedArgs) when its schedule is
-//   [exchange A][REDUCE_TREE over A's received blocks + the own leaf][exchange C]?
-// with exchange C (optional) sending the tree's output block and receiving
-// into the caller's buffer -- allreduce_bine_bdw_remap / _static / segmented
-// / rabenseifner ... with the flat phases, and the one-shot bine_lat.  The
-// kernel's workgroups each own the same slice of every message, so it is
-// correct only when no workgroup writes bytes another one may still read:
-// the tree's output overlaps no block exchange A sends, and every block
-// exchange C receives is disjoint from A's sends or exactly one of them (the
-// same slice then belongs to the same workgroup in both phases).  Returns -1
-// when the schedule or the arguments do not qualify (the caller then issues
-// the primitives).
+// BINE_DIRECT_FUSED_LARGE=0: large direct-transport collectives keep their
+// per-exchange launches (k_dm_move / k_dm_move_tree) instead of k_dm_fused
+static bool fused_large_on() {
+  static const bool on = !getenv("BINE_DIRECT_FUSED_LARGE") || atoi(getenv("BINE_DIRECT_FUSED_LARGE")) != 0;
+  return on;
+}
+
+// The flat form of a collective over the direct transport as ONE launch
+// (k_dm_fused, bine_internal.h DmFusedArgs) when its schedule is
+//   ([exchange X_c][REDUCE_TREE over X_c's received blocks + the own leaf])
+//   for chunks c = 0 .. C-1, then optionally [exchange AG]
+// with exchange AG (the flat allgather) sending the concatenated tree outputs
+// to every peer and receiving into the caller's buffer --
+// allreduce_bine_bdw_remap / _static / segmented / rabenseifner ... with the
+// flat phases, the one-shot bine_lat, and the flat reduce-scatters.  AG's
+// sends become the trees' result pushes (piece c = tree c's output, pushed
+// from registers, one slot each but the last), its receives are cut into
+// slot-sized pieces -- exactly the messages the per-exchange launches move,
+// so ranks may choose either form independently.  The kernel's workgroups each own the same slice of
+// every message, so it is correct only when no workgroup writes bytes another
+// one may still read: the trees' outputs overlap no block the X exchanges
+// send, and every piece AG receives is disjoint from the X sends or exactly
+// one of them (the same slice then belongs to the same workgroup in both
+// phases).  A message of more than one slot, more than kSlots messages to or
+// from one peer, more than kMaxFusedTrees chunks or kMaxFusedMsgs messages:
+// not this form.  Returns false when the schedule or the arguments do not
+// qualify (the caller then issues the primitives).
 template <typename Ptr>
-static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, hipStream_t K) {
+static bool build_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
+                        DmFusedArgs &a) {
   auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
   if (!rt || !rt->dm_on || !rt->dm || c->profile || !fused_on() || op < 0 || !dm_fused_supported(dtype, op))
-    return -1;
+    return false;
+  if (!single && !fused_large_on()) return false;
   const auto &ops = sc.ops;
-  if (ops.size() < 2 || ops.size() > 3 || !ops[0].xchg || ops[1].xchg || ops[1].prims.size() != 1 ||
-      ops[1].prims[0].type != BINE_PRIM_REDUCE_TREE || (ops.size() == 3 && !ops[2].xchg))
-    return -1;
+  const size_t nops = ops.size();
+  size_t C = 0, i = 0;
+  while (i + 1 < nops && ops[i].xchg && !ops[i + 1].xchg) {
+    if (ops[i + 1].prims.size() != 1 || ops[i + 1].prims[0].type != BINE_PRIM_REDUCE_TREE) return false;
+    C++;
+    i += 2;
+  }
+  const bool ag = i < nops;
+  if (C == 0 || C > (size_t)kMaxFusedTrees || (ag && (i + 1 != nops || !ops[i].xchg))) return false;
   const DirectState &d = *rt->dm;
-  const Prim &t = ops[1].prims[0];
-  const uint64_t tbytes = t.count * esz;
-  if (t.peer < 2 || t.peer > kMaxLeaves || t.pos < 0 || t.pos >= t.peer || tbytes % 16 || !tbytes) return -1;
-  DmFusedArgs a;
-  a.wgs = d.wgs;
+  const Prim &t0 = ops[1].prims[0];
+  if (t0.peer < 2 || t0.peer > kMaxLeaves || t0.pos < 0 || t0.pos >= t0.peer) return false;
+  a = DmFusedArgs{};
+  a.wgs = single ? d.wgs : d.fused_wgs;
   a.share = d.share;
   a.rank = c->rank;
   a.slot = d.slot;
   a.own = (uint8_t *)d.own;
   a.poison_host = d.hpoison_dev;
   a.timeout_ticks = d.timeout_ticks;
-  a.nl = t.peer;
-  a.pos = t.pos;
-  a.swap = (unsigned)t.flags >> 8;
-  a.own_leaf = ptr(t.aux_buf, t.aux_off);
-  a.out = ptr(t.dst_buf, t.dst_off);
-  a.nvec = tbytes / 16;
-  for (int j = 0; j < kMaxLeaves; j++) a.leaf[j] = -1;
-  std::vector<int> js((size_t)c->size, 0), jr((size_t)c->size, 0);
+  a.nl = t0.peer;
+  a.pos = t0.pos;
+  a.swap = (unsigned)t0.flags >> 8;
+  a.nt = (int)C;
   struct Range { const char *lo, *hi; };
-  std::vector<Range> a_src;
   auto overlap = [](Range x, Range y) { return x.lo < y.hi && y.lo < x.hi; };
-  const Range out_r{(const char *)a.out, (const char *)a.out + tbytes};
+  std::vector<Range> outs, owns, a_src;
+  for (size_t k = 0; k < C; k++) {
+    const Prim &t = ops[2 * k + 1].prims[0];
+    const uint64_t tb = t.count * esz;
+    if (t.peer != a.nl || t.pos != a.pos || ((unsigned)t.flags >> 8) != a.swap || !tb || tb % 16 || tb > d.slot)
+      return false;
+    DmFusedTree &ft = a.t[k];
+    ft.own_leaf = ptr(t.aux_buf, t.aux_off);
+    ft.out = ptr(t.dst_buf, t.dst_off);
+    ft.nvec = tb / 16;
+    outs.push_back({(const char *)ft.out, (const char *)ft.out + tb});
+    owns.push_back({(const char *)ft.own_leaf, (const char *)ft.own_leaf + tb});
+    for (int j = 0; j < kMaxLeaves; j++) ft.leaf[j] = -1;
+  }
+  std::vector<int> js((size_t)c->size, 0), jr((size_t)c->size, 0);
   int n = 0;
-  auto add = [&](const Prim &x, bool push, const void *src, void *dst) -> bool {
-    if (n >= 4 * kMaxFusedPeers || x.peer < 0 || x.peer >= c->size || x.count * esz > d.slot) return false;
-    int &j = push ? js[(size_t)x.peer] : jr[(size_t)x.peer];
+  auto add = [&](int peer, uint64_t bytes, bool push, const void *src, void *dst) -> bool {
+    if (n >= kMaxFusedMsgs || peer < 0 || peer >= c->size || peer == c->rank || bytes > d.slot || !bytes)
+      return false;
+    int &j = push ? js[(size_t)peer] : jr[(size_t)peer];
     if (j >= dm::kSlots) return false;
     DmMsg &m = a.m[n++];
     m.src = (const uint8_t *)src;
     m.dst = (uint8_t *)dst;
-    m.bytes = x.count * esz;
+    m.bytes = bytes;
     m.push = push ? 1 : 0;
-    m.peer = x.peer;
+    m.peer = peer;
     m.j = j++;
     return true;
   };
-  // exchange A: sends (any source but the tree's output), receives = the
-  // tree's non-own leaves (leaf k of the staging area: k-th leaf != pos)
-  for (const Prim &x : ops[0].prims)
-    if (x.type == BINE_PRIM_SEND) {
-      const char *p = ptr(x.src_buf, x.src_off);
-      const Range r{p, p + x.count * esz};
-      if (overlap(r, out_r) || !add(x, true, p, nullptr)) return -1;
-      a_src.push_back(r);
-      a.na++;
-    }
-  for (const Prim &x : ops[0].prims)
-    if (x.type == BINE_PRIM_RECV) {
-      if (x.dst_buf != t.src_buf || x.count != t.count || x.dst_off < t.src_off ||
-          (x.dst_off - t.src_off) % t.count)
-        return -1;
-      const uint64_t k = (x.dst_off - t.src_off) / t.count;
-      if (k >= (uint64_t)t.peer - 1) return -1;
-      const int leaf = (int)k < t.pos ? (int)k : (int)k + 1;
-      if (a.leaf[leaf] >= 0) return -1;
-      a.leaf[leaf] = n;
-      if (!add(x, false, nullptr, ptr(x.dst_buf, x.dst_off))) return -1;
-      a.nb++;
-    }
-  if (a.nb != t.peer - 1) return -1;
-  if (ops.size() == 3) {
-    for (const Prim &x : ops[2].prims)
-      if (x.type == BINE_PRIM_SEND) {  // the tree's output, re-read by the workgroup that wrote it
-        if (ptr(x.src_buf, x.src_off) != a.out || x.count != t.count || !add(x, true, a.out, nullptr)) return -1;
-        a.nc++;
-      }
-    for (const Prim &x : ops[2].prims)
-      if (x.type == BINE_PRIM_RECV) {
-        char *p = ptr(x.dst_buf, x.dst_off);
+  // phase A: every X exchange's sends (any source but a tree's output)
+  for (size_t k = 0; k < C; k++)
+    for (const Prim &x : ops[2 * k].prims)
+      if (x.type == BINE_PRIM_SEND) {
+        const char *p = ptr(x.src_buf, x.src_off);
         const Range r{p, p + x.count * esz};
-        if (overlap(r, out_r) || overlap(r, Range{(const char *)a.own_leaf, (const char *)a.own_leaf + tbytes}))
-          return -1;
-        for (const Range &y : a_src)
-          if (overlap(r, y) && (r.lo != y.lo || r.hi != y.hi)) return -1;
-        if (!add(x, false, nullptr, p)) return -1;
-        a.nd++;
+        for (const Range &o : outs)
+          if (overlap(r, o)) return false;
+        if (!add(x.peer, x.count * esz, true, p, nullptr)) return false;
+        a_src.push_back(r);
+        a.na++;
+      }
+  // the allgather's sends: the trees' outputs, concatenated, to every peer
+  std::vector<int> ag_peers;
+  if (ag) {
+    for (size_t k = 1; k < C; k++)
+      if (outs[k].lo != outs[k - 1].hi) return false;
+    for (const Prim &x : ops[nops - 1].prims)
+      if (x.type == BINE_PRIM_SEND) {
+        if (ptr(x.src_buf, x.src_off) != outs[0].lo || ptr(x.src_buf, x.src_off) + x.count * esz != outs[C - 1].hi)
+          return false;
+        ag_peers.push_back(x.peer);
       }
   }
+  // phases B_c: X_c's receives are tree c's non-own leaves (leaf k of the
+  // staging area: the k-th leaf != pos), then the result pushes of piece c
+  for (size_t k = 0; k < C; k++) {
+    const Prim &t = ops[2 * k + 1].prims[0];
+    DmFusedTree &ft = a.t[k];
+    ft.b0 = n;
+    for (const Prim &x : ops[2 * k].prims)
+      if (x.type == BINE_PRIM_RECV) {
+        if (x.dst_buf != t.src_buf || x.count != t.count || x.dst_off < t.src_off ||
+            (x.dst_off - t.src_off) % t.count)
+          return false;
+        const uint64_t q = (x.dst_off - t.src_off) / t.count;
+        if (q >= (uint64_t)t.peer - 1) return false;
+        const int leaf = (int)q < t.pos ? (int)q : (int)q + 1;
+        if (ft.leaf[leaf] >= 0) return false;
+        ft.leaf[leaf] = (int8_t)n;
+        if (!add(x.peer, x.count * esz, false, nullptr, ptr(x.dst_buf, x.dst_off))) return false;
+        ft.nb++;
+      }
+    if (ft.nb != t.peer - 1) return false;
+    for (int p : ag_peers) {
+      if (!add(p, ft.nvec * 16, true, ft.out, nullptr)) return false;
+      ft.nc++;
+    }
+  }
+  // phase D: the allgather's receives, cut into slot-sized pieces -- the
+  // rounds DirectState::exchange cuts every message into, so each ordered
+  // pair sees the same messages whichever form each side issues
+  a.d0 = n;
+  if (ag) {
+    const uint64_t piece = d.slot;
+    for (const Prim &x : ops[nops - 1].prims)
+      if (x.type == BINE_PRIM_RECV) {
+        char *p = ptr(x.dst_buf, x.dst_off);
+        const uint64_t bytes = x.count * esz;
+        for (uint64_t off = 0; off < bytes; off += piece) {
+          const uint64_t len = std::min<uint64_t>(piece, bytes - off);
+          const Range r{p + off, p + off + len};
+          for (size_t k = 0; k < C; k++)
+            if (overlap(r, outs[k]) || overlap(r, owns[k])) return false;
+          for (const Range &y : a_src)
+            if (overlap(r, y) && (r.lo != y.lo || r.hi != y.hi)) return false;
+          if (len % 16 || !add(x.peer, len, false, nullptr, p + off)) return false;
+          a.nd++;
+        }
+      }
+    // our pieces are our trees' outputs: each exactly one slot but the last
+    for (size_t k = 0; k + 1 < C; k++)
+      if (a.t[k].nvec * 16 != d.slot) return false;
+  }
+  return dm_fused_check(a, dtype, op) == BINE_SUCCESS;
+}
+
+// k_dm_fused for the call if its schedule qualifies (build_fused): the
+// launch's status, or -1 (the caller issues the primitives)
+template <typename Ptr>
+static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
+                     hipStream_t K) {
+  DmFusedArgs a;
+  if (!build_fused(c, sc, ptr, esz, dtype, op, single, a)) return -1;
   const int rc = launch_dm_fused(a, dtype, op, K);
+  if (rc == BINE_SUCCESS && !single) c->fused_calls++;
   return rc == BINE_ERR_ARG || rc == BINE_ERR_UNSUPPORTED ? -1 : rc;  // not co-aligned etc.: the primitives
 }
 
@@ -1103,15 +1179,17 @@ static bool plan_dm_trees(const Transport &tx, bool on, const Schedule &sc, Ptr 
 // events at all, and graph mode captures it as one branch (§4.3 of DESIGN.md)
 static int execute(bine_comm *c, const Schedule &sc, const void *sbuf, void *rbuf, size_t esz, int dtype, int op,
                    hipStream_t K, bool single = false, bool joined = false, const Staging *stg = nullptr,
-                   const DmTreePlan *tpl = nullptr) {
+                   const DmTreePlan *tpl = nullptr, bool fused = false) {
   char *base[6];
   base[BINE_BUF_SBUF] = (char *)sbuf;
   base[BINE_BUF_RBUF] = (char *)rbuf;
   for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
   base[BINE_BUF_STAGE] = (char *)c->tmp[3];
   auto ptr = [&](int buf, uint64_t off) { return base[buf] + off * esz; };
-  if (single && !stg) {  // a small collective over the direct transport: one launch when its form allows
-    const int rc = try_fused(c, sc, ptr, esz, dtype, op, K);
+  // over the direct transport, a small collective (and a large one that
+  // run_collective found fusable, `fused`) is one launch when its form allows
+  if ((single || fused) && !stg) {
+    const int rc = try_fused(c, sc, ptr, esz, dtype, op, single, K);
     if (rc >= 0) return rc;
   }
   const bool solo = tpl && tpl->solo && !single && !stg;
@@ -1390,6 +1468,34 @@ static const DmTreePlan *tree_plan_for(bine_comm *c, const std::string &plan_key
   return it->second.any ? &it->second : nullptr;
 }
 
+// Whether a large call runs as ONE k_dm_fused launch (build_fused on the
+// call's buffers), cached per (plan, buffers, dtype, op, the direct
+// transport's settings)
+static bool fused_for(bine_comm *c, const std::string &plan_key_s, const Schedule &sc, const void *sbuf, void *rbuf,
+                      size_t esz, int dtype, int op) {
+  auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
+  // the large form belongs to the fused-tree setting (bine_comm_set_direct_tree);
+  // with it off the per-exchange launches and separate trees stay (A/B)
+  if (!rt || !rt->dm_on || !rt->dm || op < 0 || c->profile || !fused_large_on() || !c->dm_tree) return false;
+  char buf[256];
+  snprintf(buf, sizeof buf, "|%p|%p|%p|%p|%p|%p|%d|%d|%zu|%zu", sbuf, rbuf, c->tmp[0], c->tmp[1], c->tmp[2],
+           c->tmp[3], dtype, op, esz, rt->dm->slot);
+  const std::string key = plan_key_s + buf;
+  auto it = c->fused_cache.find(key);
+  if (it == c->fused_cache.end()) {
+    if (c->fused_cache.size() >= 256) c->fused_cache.clear();
+    char *base[6];
+    base[BINE_BUF_SBUF] = (char *)sbuf;
+    base[BINE_BUF_RBUF] = (char *)rbuf;
+    for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
+    base[BINE_BUF_STAGE] = (char *)c->tmp[3];
+    auto ptr = [&](int b, uint64_t off) { return base[b] + off * esz; };
+    DmFusedArgs a;
+    it = c->fused_cache.emplace(key, build_fused(c, sc, ptr, esz, dtype, op, false, a)).first;
+  }
+  return it->second;
+}
+
 // Graph mode: the first call for a (plan, buffers, dtype, op, stream,
 // transport options) key runs eagerly -- RCCL connects to new peers lazily and
 // the allgather option sizes its staging area, neither of which may happen
@@ -1400,8 +1506,8 @@ static const DmTreePlan *tree_plan_for(bine_comm *c, const std::string &plan_key
 // that key replays the graph with one hipGraphLaunch.  Work and ordering are
 // the eager schedule's, so results are bit-identical (GPU tests).
 static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule &sc, const void *sbuf, void *rbuf,
-                     size_t esz, int dtype, int op, hipStream_t K, bool single, const DmTreePlan *tpl) {
-  const bool one = single || (tpl && tpl->solo);  // the whole call on K: a one-branch graph
+                     size_t esz, int dtype, int op, hipStream_t K, bool single, const DmTreePlan *tpl, bool fused) {
+  const bool one = single || fused || (tpl && tpl->solo);  // the whole call on K: a one-branch graph
   const auto *rt = dynamic_cast<const RcclTransport *>(c->tx.get());
   char buf[192];
   snprintf(buf, sizeof buf, "|%p|%p|%d|%d|%p|%d|%d|%d|%d", sbuf, rbuf, dtype, op, (void *)K, (int)single,
@@ -1413,7 +1519,7 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
     HIP_TRY(hipGraphLaunch(it->second.x, K));
     return BINE_SUCCESS;
   }
-  int rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, false, nullptr, tpl);  // this call, eagerly
+  int rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, false, nullptr, tpl, fused);  // this call, eagerly
   if (rc) return rc;
   if (rt && rt->stage_gen != c->graph_stage_gen) {
     // the allgather option's staging area moved (freed after a synchronize of
@@ -1438,7 +1544,7 @@ static int run_graph(bine_comm *c, const std::string &plan_key_s, const Schedule
   const hipStream_t O = one ? K : c->cstream;
   HIP_TRY(hipStreamBeginCapture(O, hipStreamCaptureModeThreadLocal));
   if (!one) rc = stream_join(c, K, O);
-  if (!rc) rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, true, nullptr, tpl);
+  if (!rc) rc = execute(c, sc, sbuf, rbuf, esz, dtype, op, K, single, true, nullptr, tpl, fused);
   if (!rc && !one) rc = stream_join(c, O, K);
   const hipError_t ee = hipStreamEndCapture(O, &e.g);
   if (rc || ee != hipSuccess) {
@@ -1560,15 +1666,16 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     stg->rg = &sit->second;
   }
   const void *src = a.in_place ? rbuf : sbuf;
-  const DmTreePlan *tpl = single || stg ? nullptr : tree_plan_for(c, key, sc, src, rbuf, a.esz, dtype, op);
+  const bool fused = !single && !stg && fused_for(c, key, sc, src, rbuf, a.esz, dtype, op);
+  const DmTreePlan *tpl = single || stg || fused ? nullptr : tree_plan_for(c, key, sc, src, rbuf, a.esz, dtype, op);
   rc = order_begin(c, K);
   if (rc) {
   } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && !stg &&
              (multi_branch_graphs_ok() ||
-              ((single || (tpl && tpl->solo)) && hw_queues() >= (rccl_free(c) ? 2 : 4))))
-    rc = run_graph(c, key, sc, src, rbuf, a.esz, dtype, op, K, single, tpl);
+              ((single || fused || (tpl && tpl->solo)) && hw_queues() >= (rccl_free(c) ? 2 : 4))))
+    rc = run_graph(c, key, sc, src, rbuf, a.esz, dtype, op, K, single, tpl, fused);
   else
-    rc = execute(c, sc, src, rbuf, a.esz, dtype, op, K, single, false, stg, tpl);
+    rc = execute(c, sc, src, rbuf, a.esz, dtype, op, K, single, false, stg, tpl, fused);
   if (!rc) rc = order_end(c, K);
   if (roctx_on()) roctxRangePop();
   return rc;
@@ -2256,6 +2363,12 @@ int bine_comm_set_graphs(bine_comm_t c, int on) {
   return BINE_SUCCESS;
 }
 
+int64_t bine_comm_fused_calls(bine_comm_t c) {
+  if (!c) return -(int64_t)BINE_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return c->fused_calls;
+}
+
 int64_t bine_comm_graphs_cached(bine_comm_t c) {
   if (!c) return -(int64_t)BINE_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
@@ -2282,6 +2395,7 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
       r->dm_on = false;
       c->drop_graphs();  // captured launches carry the old inboxes
       c->tree_cache.clear();
+      c->fused_cache.clear();
       r->dm.reset();
     }
   }

@@ -1537,31 +1537,32 @@ __device__ __forceinline__ void copy_slice(const Msg &m, int wgs, bool push) {
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   using namespace dmf;
-  const int nm = a.na + a.nb + a.nc + a.nd;
-  // phase A: our blocks into the peers' inboxes (each slot's previous use
-  // acknowledged first)
+  const int nm = a.d0 + a.nd;
+  // phase A: our blocks of every chunk into the peers' inboxes (each slot's
+  // previous use acknowledged first)
   if (!wait_all(a, 0, a.na, false)) return;
   for (int i = 0; i < a.na; i++) copy_slice(resolve(a, a.m[i]), a.wgs, true);
   arrive_all(a, 0, a.na);
-  // phase B: the peers' blocks, read in place in our inbox as the tree's
-  // leaves; each result vector goes to `out` and, for the flat allgather
-  // (phase C's pushes), straight from registers into every peer's slot --
-  // whose previous use must have been acknowledged first
-  if (!wait_all(a, a.na, a.nb + a.nc, a.nb > 0)) return;
-  const u32x4 *lp[kMaxLeaves];
+  // phases B_c: the peers' blocks of chunk c, read in place in our inbox as
+  // the tree's leaves; each result vector goes to `out` and, for the flat
+  // allgather, straight from registers into every peer's slot -- whose
+  // previous use must have been acknowledged first
+  for (int ti = 0; ti < a.nt; ti++) {
+    const DmFusedTree &t = a.t[ti];
+    if (!wait_all(a, t.b0, t.nb + t.nc, t.nb > 0)) return;
+    const u32x4 *lp[kMaxLeaves];
 #pragma unroll
-  for (int j = 0; j < kMaxLeaves; j++)
-    lp[j] = j >= a.nl ? nullptr
-            : j == a.pos ? reinterpret_cast<const u32x4 *>(a.own_leaf)
-                         : resolve(a, a.m[a.leaf[j]]).src;
-  __amdgpu_buffer_rsrc_t cp[kMaxFusedPeers];
+    for (int j = 0; j < kMaxLeaves; j++)
+      lp[j] = j >= a.nl ? nullptr
+              : j == a.pos ? reinterpret_cast<const u32x4 *>(t.own_leaf)
+                           : resolve(a, a.m[t.leaf[j]]).src;
+    __amdgpu_buffer_rsrc_t cp[kMaxFusedPeers];
 #pragma unroll
-  for (int i = 0; i < kMaxFusedPeers; i++)
-    if (i < a.nc) cp[i] = wt_rsrc(resolve(a, a.m[a.na + a.nb + i]).dst);
-  {
-    u32x4 *out = reinterpret_cast<u32x4 *>(a.out);
+    for (int i = 0; i < kMaxFusedPeers; i++)
+      if (i < t.nc) cp[i] = wt_rsrc(resolve(a, a.m[t.b0 + t.nb + i]).dst);
+    u32x4 *out = reinterpret_cast<u32x4 *>(t.out);
     uint64_t lo, hi;
-    slice(a.nvec, a.wgs, &lo, &hi);
+    slice(t.nvec, a.wgs, &lo, &hi);
     for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
       u32x4 v[kMaxLeaves];
 #pragma unroll
@@ -1576,17 +1577,16 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
       out[i] = v[0];
 #pragma unroll
       for (int c = 0; c < kMaxFusedPeers; c++)
-        if (c < a.nc) st_wt(cp[c], i, v[0]);
+        if (c < t.nc) st_wt(cp[c], i, v[0]);
     }
+    // every leaf slice is read (the senders may reuse their slots) and every
+    // result slice is in the peers' inboxes
+    arrive_all(a, t.b0, t.nb + t.nc);
   }
-  // every leaf slice is read (the senders may reuse their slots) and every
-  // result slice is in the peers' inboxes
-  arrive_all(a, a.na, a.nb + a.nc);
-  // phase C: the peers' results out of our inbox
-  const int d0 = a.na + a.nb + a.nc;
-  if (!wait_all(a, d0, a.nd, true)) return;
-  for (int i = 0; i < a.nd; i++) copy_slice(resolve(a, a.m[d0 + i]), a.wgs, false);
-  arrive_all(a, d0, a.nd);
+  // phase D: the peers' results out of our inbox
+  if (!wait_all(a, a.d0, a.nd, true)) return;
+  for (int i = 0; i < a.nd; i++) copy_slice(resolve(a, a.m[a.d0 + i]), a.wgs, false);
+  arrive_all(a, a.d0, a.nd);
   // the launch's last workgroup advances the sequence bases (every workgroup
   // has read them: each resolve() happened before its launch-counter add)
   if (threadIdx.x == 0) {
@@ -1627,11 +1627,11 @@ bool dm_fused_supported(int dtype, int op) {
   return t && op >= BINE_SUM && op <= BINE_MIN;
 }
 
-int launch_dm_fused(const DmFusedArgs &a, int dtype, int op, void *stream) {
+int dm_fused_check(const DmFusedArgs &a, int dtype, int op) {
   if (!dm_fused_supported(dtype, op)) return BINE_ERR_UNSUPPORTED;
-  const int nm = a.na + a.nb + a.nc + a.nd;
+  const int nm = a.d0 + a.nd;
   if (a.wgs < 1 || !a.own || !a.slot || a.nl < 2 || a.nl > kMaxLeaves || a.pos < 0 || a.pos >= a.nl ||
-      a.nb != a.nl - 1 || nm > 4 * kMaxFusedPeers || !a.out || !a.own_leaf)
+      a.nt < 1 || a.nt > kMaxFusedTrees || a.na < 0 || a.nd < 0 || nm > kMaxFusedMsgs)
     return BINE_ERR_ARG;
   for (int i = 0; i < nm; i++) {
     const DmMsg &m = a.m[i];
@@ -1639,10 +1639,36 @@ int launch_dm_fused(const DmFusedArgs &a, int dtype, int op, void *stream) {
         m.bytes % 16 || ((uintptr_t)(m.push ? (const void *)m.src : (const void *)m.dst) & 15))
       return BINE_ERR_ARG;
   }
-  for (int j = 0; j < a.nl; j++)
-    if (j != a.pos && (a.leaf[j] < a.na || a.leaf[j] >= a.na + a.nb || a.m[a.leaf[j]].bytes != a.nvec * 16))
+  // the layout: A pushes, then each tree's leaf pulls and result pushes, then D pulls
+  int at = a.na;
+  for (int i = 0; i < a.na; i++)
+    if (!a.m[i].push) return BINE_ERR_ARG;
+  for (int ti = 0; ti < a.nt; ti++) {
+    const DmFusedTree &t = a.t[ti];
+    if (t.b0 != at || t.nb != a.nl - 1 || t.nc < 0 || !t.nvec || !t.out || !t.own_leaf ||
+        ((uintptr_t)t.out & 15) || ((uintptr_t)t.own_leaf & 15))
       return BINE_ERR_ARG;
-  if (((uintptr_t)a.out & 15) || ((uintptr_t)a.own_leaf & 15)) return BINE_ERR_ARG;
+    for (int i = t.b0; i < t.b0 + t.nb; i++)
+      if (a.m[i].push || a.m[i].bytes != t.nvec * 16) return BINE_ERR_ARG;
+    for (int i = t.b0 + t.nb; i < t.b0 + t.nb + t.nc; i++)
+      if (!a.m[i].push || a.m[i].bytes != t.nvec * 16) return BINE_ERR_ARG;
+    uint32_t seen = 0;
+    for (int j = 0; j < a.nl; j++) {
+      if (j == a.pos) continue;
+      const int i = t.leaf[j];
+      if (i < t.b0 || i >= t.b0 + t.nb || (seen >> (i - t.b0) & 1)) return BINE_ERR_ARG;
+      seen |= 1u << (i - t.b0);
+    }
+    at += t.nb + t.nc;
+  }
+  if (a.d0 != at) return BINE_ERR_ARG;
+  for (int i = a.d0; i < nm; i++)
+    if (a.m[i].push) return BINE_ERR_ARG;
+  return BINE_SUCCESS;
+}
+
+int launch_dm_fused(const DmFusedArgs &a, int dtype, int op, void *stream) {
+  if (int rc = dm_fused_check(a, dtype, op)) return rc;
   hipStream_t st = (hipStream_t)stream;
   hipError_t e;
   switch (dtype) {

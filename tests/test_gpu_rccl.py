@@ -154,3 +154,20 @@ def test_direct_transport_rebuilt_after_a_timeout():
                  timeout=280, ranks=2)
     assert r.returncode == 0, r.stdout[-3000:] + "\n" + r.stderr[-2000:]
     assert "RESULT P=2: ok" in r.stdout
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("P", [2, 4])
+def test_direct_fused_large_collectives(P):
+    """a whole flat-form collective over the direct
+    transport as ONE k_dm_fused launch -- several slot-sized chunks (1 MiB
+    slots), ragged last chunks, fp32 / fp64 / int64, SUM / MAX, in place,
+    allreduce (remap, static, rabenseifner) and reduce_scatter permute_remap
+    -- bit-exact vs the oracle on every rank, the fused launches counted, and
+    the per-exchange form interleaved with it (tools/dm_fused_check.py)"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "dm_fused_check.py"), str(P)], env=env,
+                    capture_output=True, text=True, timeout=280, ranks=P)
+    bad = [x for x in r.stdout.splitlines() if "MISMATCH" in x or "RESULT" in x or " ok, " in x]
+    assert r.returncode == 0, "\n".join(bad[:40]) + "\n" + r.stderr[-2000:]
+    assert f"RESULT P={P}" in r.stdout
