@@ -756,7 +756,8 @@ def _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem, stream, wo
 
 RELAY_MIN_BYTES = 256 << 10    # smallest relayed part when relay mode is on
 DM_WGS_TRIALS = (64, 256)      # direct transport: workgroups per message tried beside the default 128
-TREE_WGS_TRIALS = (128, 512)   # fused trees ("+dmt"): tree workgroups per launch tried beside the default 256
+TREE_WGS_TRIALS = (512, 1024)  # fused trees ("+dmt"): tree workgroups per launch tried beside the default 256
+#                               (a large flat call as one k_dm_fused launch: its whole grid)
 CHUNK_TRIALS = (4 << 20, 8 << 20, 16 << 20, 32 << 20, 64 << 20)   # pipelining chunks tried at N > 1
 MODES = {"off": ["direct"],
          # "+a2a" is not tried: RCCL runs ncclAllToAllv as the same grouped P2P kernel

@@ -29,8 +29,9 @@ struct DirectState {
   int P = 1, rank = 0, device = 0;
   size_t slot = (size_t)64 << 20;  // sub-message size (BINE_DIRECT_SLOT_BYTES; profiles/r4_dm_stamps_p2_sweep2.txt)
   int wgs = 128;                   // workgroups per message (BINE_DIRECT_WGS; bine_comm_set_direct_wgs)
-  int fused_wgs = 1024;            // workgroups of a large call's single k_dm_fused launch (BINE_DIRECT_FUSED_WGS;
-                                   // cut to the residency cap)
+  int fused_wgs = 0;               // workgroups of a large call's single k_dm_fused launch (BINE_DIRECT_FUSED_WGS;
+                                   // 0: tree_wgs -- every workgroup of that launch does tree work; cut to the
+                                   // residency cap, then to a multiple of the CUs)
   int env_wgs = 128;               // the value init() settled on (the setter's 0)
   int pull_wgs = 0;                // workgroups per copied pull (BINE_DIRECT_PULL_WGS; 0: wgs)
   // diagnostics (BINE_DIRECT_STAMPS=<records>): per-workgroup stamps of every

@@ -868,14 +868,21 @@ static bool fused_large_on() {
 // from one peer, more than kMaxFusedTrees chunks or kMaxFusedMsgs messages:
 // not this form.  Returns false when the schedule or the arguments do not
 // qualify (the caller then issues the primitives).
+// ops [o0, o1) of a schedule, indexed from 0
+struct OpSpan {
+  const SOp *p;
+  size_t n;
+  const SOp &operator[](size_t i) const { return p[i]; }
+  size_t size() const { return n; }
+};
+
 template <typename Ptr>
-static bool build_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
+static bool build_fused(bine_comm *c, OpSpan ops, Ptr ptr, size_t esz, int dtype, int op, bool single,
                         DmFusedArgs &a) {
   auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
   if (!rt || !rt->dm_on || !rt->dm || c->profile || !fused_on() || op < 0 || !dm_fused_supported(dtype, op))
     return false;
   if (!single && !fused_large_on()) return false;
-  const auto &ops = sc.ops;
   const size_t nops = ops.size();
   size_t C = 0, i = 0;
   while (i + 1 < nops && ops[i].xchg && !ops[i + 1].xchg) {
@@ -889,7 +896,7 @@ static bool build_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, i
   const Prim &t0 = ops[1].prims[0];
   if (t0.peer < 2 || t0.peer > kMaxLeaves || t0.pos < 0 || t0.pos >= t0.peer) return false;
   a = DmFusedArgs{};
-  a.wgs = single ? d.wgs : d.fused_wgs;
+  a.wgs = single ? d.wgs : d.fused_wgs ? d.fused_wgs : d.tree_wgs;
   a.share = d.share;
   a.rank = c->rank;
   a.slot = d.slot;
@@ -1009,16 +1016,51 @@ static bool build_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, i
   return dm_fused_check(a, dtype, op) == BINE_SUCCESS;
 }
 
-// k_dm_fused for the call if its schedule qualifies (build_fused): the
-// launch's status, or -1 (the caller issues the primitives)
+// The call's fused launches: the whole schedule as one k_dm_fused launch, or
+// -- a reduce-scatter of more chunks than one launch holds (no allgather
+// pieces) -- one launch per kMaxFusedTrees chunks.  Either way every ordered
+// pair sees the per-exchange form's messages in its order (chunk by chunk),
+// so the ranks' choices need not agree.  Empty: not this form.
+template <typename Ptr>
+static bool plan_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
+                       std::vector<DmFusedArgs> &out) {
+  out.assign(1, DmFusedArgs{});
+  const OpSpan all{sc.ops.data(), sc.ops.size()};
+  if (build_fused(c, all, ptr, esz, dtype, op, single, out[0])) return true;
+  out.clear();
+  const size_t n = sc.ops.size();
+  if (single || n % 2 || n <= 2 * (size_t)kMaxFusedTrees) return false;
+  for (size_t i = 0; i < n; i += 2)  // [X_c][tree_c] pairs only: no allgather exchange at the end
+    if (!sc.ops[i].xchg || sc.ops[i + 1].xchg) return false;
+  for (size_t o0 = 0; o0 < n; o0 += 2 * kMaxFusedTrees) {
+    out.emplace_back();
+    const OpSpan g{sc.ops.data() + o0, std::min(n - o0, 2 * (size_t)kMaxFusedTrees)};
+    if (!build_fused(c, g, ptr, esz, dtype, op, single, out.back())) {
+      out.clear();
+      return false;
+    }
+  }
+  return true;
+}
+
+// k_dm_fused for the call if its schedule qualifies (plan_fused): the
+// launches' status, or -1 (the caller issues the primitives)
 template <typename Ptr>
 static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
                      hipStream_t K) {
-  DmFusedArgs a;
-  if (!build_fused(c, sc, ptr, esz, dtype, op, single, a)) return -1;
-  const int rc = launch_dm_fused(a, dtype, op, K);
-  if (rc == BINE_SUCCESS && !single) c->fused_calls++;
-  return rc == BINE_ERR_ARG || rc == BINE_ERR_UNSUPPORTED ? -1 : rc;  // not co-aligned etc.: the primitives
+  std::vector<DmFusedArgs> v;
+  if (!plan_fused(c, sc, ptr, esz, dtype, op, single, v)) return -1;
+  for (size_t i = 0; i < v.size(); i++) {
+    const int rc = launch_dm_fused(v[i], dtype, op, K);
+    if (rc == BINE_ERR_ARG || rc == BINE_ERR_UNSUPPORTED) {
+      if (i == 0) return -1;  // not co-aligned etc.: the primitives
+      set_err("k_dm_fused: launch %zu of %zu refused after the first ran", i + 1, v.size());
+      return BINE_ERR_INTERNAL;
+    }
+    if (rc) return rc;
+  }
+  if (!single) c->fused_calls++;
+  return BINE_SUCCESS;
 }
 
 // Host staging of one call (bine_*_staged): the input buffer comes from
@@ -1490,8 +1532,8 @@ static bool fused_for(bine_comm *c, const std::string &plan_key_s, const Schedul
     for (int t = 0; t < 3; t++) base[BINE_BUF_TMP0 + t] = (char *)c->tmp[t];
     base[BINE_BUF_STAGE] = (char *)c->tmp[3];
     auto ptr = [&](int b, uint64_t off) { return base[b] + off * esz; };
-    DmFusedArgs a;
-    it = c->fused_cache.emplace(key, build_fused(c, sc, ptr, esz, dtype, op, false, a)).first;
+    std::vector<DmFusedArgs> v;
+    it = c->fused_cache.emplace(key, plan_fused(c, sc, ptr, esz, dtype, op, false, v)).first;
   }
   return it->second;
 }

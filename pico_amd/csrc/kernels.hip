@@ -1520,16 +1520,70 @@ __device__ __forceinline__ void slice(uint64_t n, int wgs, uint64_t *lo, uint64_
 }
 
 // a push writes the peer's slot through; a pull reads its own slot after
-// the acquire of wait_all
+// the acquire of wait_all.  U vectors per lane in flight (all loads, then
+// all stores): with one, every store waits for its own load and the slice
+// streams at a fraction of HBM bandwidth.
 __device__ __forceinline__ void copy_slice(const Msg &m, int wgs, bool push) {
+  constexpr int U = 4;
   uint64_t lo, hi;
   slice(m.nvec, wgs, &lo, &hi);
-  if (push) {
-    const __amdgpu_buffer_rsrc_t r = wt_rsrc(m.dst);
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) st_wt(r, i, __builtin_nontemporal_load(m.src + i));
-  } else {
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock)
-      __builtin_nontemporal_store(__builtin_nontemporal_load(m.src + i), m.dst + i);
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc(push ? m.dst : nullptr);
+  for (uint64_t b = lo + threadIdx.x; b < hi; b += (uint64_t)kBlock * U) {
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t i = b + (uint64_t)u * kBlock;
+      if (i < hi) x[u] = __builtin_nontemporal_load(m.src + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t i = b + (uint64_t)u * kBlock;
+      if (i < hi) {
+        if (push) st_wt(r, i, x[u]);
+        else __builtin_nontemporal_store(x[u], m.dst + i);
+      }
+    }
+  }
+}
+
+// this workgroup's slice [lo, hi) of a tree of NL leaves (own leaf at `pos`:
+// plain loads; the received ones in the inbox slots: non-temporal), each
+// result vector stored to `out` and pushed from registers into the nc
+// allgather slots; U vectors of every leaf per lane in flight, U x NL <= 8
+// (the registers of the kernel's other phases)
+template <typename T, int OP, int NL>
+__device__ __forceinline__ void tree_slice(const u32x4 *const *lp, int nl, int pos, unsigned swap, u32x4 *out,
+                                           const __amdgpu_buffer_rsrc_t *cp, int nc, uint64_t lo, uint64_t hi) {
+  constexpr int U = NL >= 8 ? 1 : 8 / NL;
+  for (uint64_t b = lo + threadIdx.x; b < hi; b += (uint64_t)kBlock * U) {
+    u32x4 v[U][NL];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t i = b + (uint64_t)u * kBlock;
+      if (i < hi) {
+#pragma unroll
+        for (int j = 0; j < NL; j++) {
+          if (j >= nl) continue;  // a tree of nl <= NL leaves (a non-power-of-two P's)
+          if (j == pos) v[u][j] = lp[j][i];
+          else v[u][j] = __builtin_nontemporal_load(lp[j] + i);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t i = b + (uint64_t)u * kBlock;
+      if (i >= hi) continue;
+      int lvl = 0;
+#pragma unroll
+      for (int w = 1; w < NL; w <<= 1, lvl++)
+#pragma unroll
+        for (int j = 0; j < NL; j += 2 * w)
+          if (j + w < nl) v[u][j] = comb16<T, OP>(v[u][j], v[u][j + w], (swap >> lvl) & 1);
+      out[i] = v[u][0];
+#pragma unroll
+      for (int c = 0; c < kMaxFusedPeers; c++)
+        if (c < nc) st_wt(cp[c], i, v[u][0]);
+    }
   }
 }
 }  // namespace dmf
@@ -1563,22 +1617,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
     u32x4 *out = reinterpret_cast<u32x4 *>(t.out);
     uint64_t lo, hi;
     slice(t.nvec, a.wgs, &lo, &hi);
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
-      u32x4 v[kMaxLeaves];
-#pragma unroll
-      for (int j = 0; j < kMaxLeaves; j++)
-        if (j < a.nl) v[j] = j == a.pos ? lp[j][i] : __builtin_nontemporal_load(lp[j] + i);
-      int lvl = 0;
-#pragma unroll
-      for (int w = 1; w < kMaxLeaves; w <<= 1, lvl++)
-#pragma unroll
-        for (int j = 0; j < kMaxLeaves; j += 2 * w)
-          if (j + w < a.nl) v[j] = comb16<T, OP>(v[j], v[j + w], (a.swap >> lvl) & 1);
-      out[i] = v[0];
-#pragma unroll
-      for (int c = 0; c < kMaxFusedPeers; c++)
-        if (c < t.nc) st_wt(cp[c], i, v[0]);
-    }
+    if (a.nl <= 2) tree_slice<T, OP, 2>(lp, a.nl, a.pos, a.swap, out, cp, t.nc, lo, hi);
+    else if (a.nl <= 4) tree_slice<T, OP, 4>(lp, a.nl, a.pos, a.swap, out, cp, t.nc, lo, hi);
+    else if (a.nl <= 8) tree_slice<T, OP, 8>(lp, a.nl, a.pos, a.swap, out, cp, t.nc, lo, hi);
+    else tree_slice<T, OP, 16>(lp, a.nl, a.pos, a.swap, out, cp, t.nc, lo, hi);
     // every leaf slice is read (the senders may reuse their slots) and every
     // result slice is in the peers' inboxes
     arrive_all(a, t.b0, t.nb + t.nc);
@@ -1604,11 +1646,31 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   }
 }
 
+// CUs of the current device (0: unknown), queried once per device
+static int dm_cus() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    cus[dev] = 0;
+  }
+  return cus[dev];
+}
+
 template <typename T, int OP>
 static hipError_t fused_launch(const DmFusedArgs &a0, hipStream_t st) {
   DmFusedArgs a = a0;
   int w = a.wgs;
   dm_fit_residency(&w, 1, nullptr, dm_cap((const void *)k_dm_fused<T, OP>, a.share));
+  // above one workgroup per CU, whole multiples of the CU count: every CU
+  // carries the same share of every phase (C3 at P = 2 on one GPU: 256 and
+  // 512 workgroups 0.41-0.42 ms, 320 / 384 / 640 0.47-0.54 ms)
+  const int cus = dm_cus();
+  if (cus > 0 && w > cus) w -= w % cus;
   a.wgs = w;
   hipLaunchKernelGGL((k_dm_fused<T, OP>), dim3((unsigned)a.wgs), dim3(kBlock), 0, st, a);
   return hipGetLastError();

@@ -8,7 +8,7 @@ into several slot-sized chunks -- the multi-chunk program of the kernel
 pushed from registers; D: the allgather's pulls).  Cases: allreduce
 bine_bdw_remap / bine_bdw_static / rabenseifner fp32, fp64, int64 SUM / MAX,
 exact and ragged chunk counts, in place; reduce_scatter bine_permute_remap
-(up to 4 chunks, no allgather); each output bit-exact vs the oracle, and the
+(up to 4 chunks per launch, more in several launches; no allgather); each output bit-exact vs the oracle, and the
 number of fused launches counted (bine_comm_fused_calls) -- with the fused
 trees off ("+dm") the same calls run the per-exchange launches, and calls of
 both forms are interleaved (the two forms move the same messages per pair).
@@ -38,6 +38,9 @@ def cases(P):
     out.append(("allreduce", "bine_bdw_remap", "float", "sum", 3 * P * per, False, False))    # 3 chunks + AG: > 4 slots
     out.append(("reduce_scatter", "bine_permute_remap", "float", "sum", 4 * per, False, True))  # 4 chunks, no AG
     out.append(("reduce_scatter", "bine_permute_remap", "double", "sum", 3 * (SLOT // 8) - 2, False, True))
+    # more chunks than one launch holds: one launch per 4 chunks
+    out.append(("reduce_scatter", "bine_permute_remap", "float", "sum", 6 * per, False, True))
+    out.append(("reduce_scatter", "bine_permute_remap", "int64", "sum", 9 * (SLOT // 8) + 2, False, True))
     return out
 
 
