@@ -285,6 +285,8 @@ struct DmFusedArgs {
   int nl = 0, pos = 0;
   unsigned swap = 0;
   DmFusedTree t[kMaxFusedTrees];
+  uint64_t *stamps = nullptr;          // DmArgs::stamps: one record per workgroup (kind 4: entry, end of the
+  uint32_t serial = 0;                 // first wait, end)
 };
 // BINE_ERR_UNSUPPORTED: (dtype, op) has no fused instantiation (the caller
 // issues the primitives one by one)

@@ -1050,7 +1050,10 @@ static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int 
                      hipStream_t K) {
   std::vector<DmFusedArgs> v;
   if (!plan_fused(c, sc, ptr, esz, dtype, op, single, v)) return -1;
+  auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
   for (size_t i = 0; i < v.size(); i++) {
+    v[i].stamps = rt->dm->stamps;
+    v[i].serial = rt->dm->serial++;
     const int rc = launch_dm_fused(v[i], dtype, op, K);
     if (rc == BINE_ERR_ARG || rc == BINE_ERR_UNSUPPORTED) {
       if (i == 0) return -1;  // not co-aligned etc.: the primitives

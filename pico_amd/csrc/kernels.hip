@@ -1592,9 +1592,11 @@ template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   using namespace dmf;
   const int nm = a.d0 + a.nd;
+  const uint64_t t0 = a.stamps ? wall_clock64() : 0;
   // phase A: our blocks of every chunk into the peers' inboxes (each slot's
   // previous use acknowledged first)
   if (!wait_all(a, 0, a.na, false)) return;
+  const uint64_t t1 = a.stamps ? wall_clock64() : 0;
   for (int i = 0; i < a.na; i++) copy_slice(resolve(a, a.m[i]), a.wgs, true);
   arrive_all(a, 0, a.na);
   // phases B_c: the peers' blocks of chunk c, read in place in our inbox as
@@ -1629,6 +1631,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   if (!wait_all(a, a.d0, a.nd, true)) return;
   for (int i = 0; i < a.nd; i++) copy_slice(resolve(a, a.m[a.d0 + i]), a.wgs, false);
   arrive_all(a, a.d0, a.nd);
+  if (threadIdx.x == 0 && a.stamps) dm_stamp(a.stamps, a.serial, 4, 255, blockIdx.x, t0, t1, wall_clock64());
   // the launch's last workgroup advances the sequence bases (every workgroup
   // has read them: each resolve() happened before its launch-counter add)
   if (threadIdx.x == 0) {

@@ -21,7 +21,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KIND = {0: "push", 1: "pull", 2: "tree"}
+KIND = {0: "push", 1: "pull", 2: "tree", 4: "fused"}   # fused: k_dm_fused, wait = its first phase's wait
 TICK_US = 0.01  # wall_clock64: 100 MHz
 
 
