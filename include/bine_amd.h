@@ -582,6 +582,13 @@ int64_t bine_plan_dm_trees(int algo, int nranks, int rank, size_t count, const i
 int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
                         size_t segsize, int in_place, size_t chunk_bytes, int mode, int kind, uint64_t *out,
                         int64_t cap);
+/* Whether the direct transport issues rank `rank`'s call as k_dm_fused
+ * launches (host only; the transport's slot `slot`, its fused trees on,
+ * `mode` as in bine_plan_schedule, `small` = a single-stream call): the
+ * number of launches, 0 when the call keeps its per-exchange launches, or
+ * -status. */
+int bine_plan_dm_fused(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                       int in_place, size_t chunk_bytes, int mode, size_t slot, int dtype, int op, int small);
 
 /* The direct transport's residency cut (host only): every launch's
  * workgroups -- `cw[0..n)` per copied message, *tw for a fused tree (NULL:

@@ -434,6 +434,22 @@ def dm_tree_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcount
     return list(host[:n]), list(defer[:n])
 
 
+def dm_fused_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, esz: int = 4,
+                  in_place: bool = False, chunk_bytes: int = 0, flat_ag=False, flat_rs: bool = False,
+                  slot: int = 64 << 20, dtype="float", op: str = "sum", small: bool = False) -> int:
+    """k_dm_fused launches the direct transport issues for rank `rank`'s call
+    (bine_plan_dm_fused, host only; fused trees on): 0 = the per-exchange
+    launches instead."""
+    a = _algo(coll, algo)
+    rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
+    mode = (2 if flat_ag else 0) | (4 if flat_rs else 0) | (8 if flat_ag == 2 else 0)
+    n = lib().bine_plan_dm_fused(a, nranks, rank, count, rc, 0, esz, int(in_place), chunk_bytes, mode, slot,
+                                 _dtype(dtype), OPS[op], int(small))
+    if n < 0:
+        raise BineError(int(-n), f"dm_fused_plan {coll}_{algo}")
+    return int(n)
+
+
 def stage_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, esz: int = 4,
                segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0, flat_ag=False, flat_rs: bool = False):
     """The host staging of rank `rank`'s schedule (bine_plan_stage; host only):
@@ -581,7 +597,7 @@ for _n in ALGOS["bcast"]:
     ENTRY_POINTS["bcast_" + _n] = _mk_bc(_n)
 globals().update(ENTRY_POINTS)
 
-__all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "reduce_local", "reduce3", "fill_pico", "checksum", "copy",
+__all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "dm_fused_plan", "reduce_local", "reduce3", "fill_pico", "checksum", "copy",
            "rccl_version",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "bcast", "loopback_bcast", "reduce_batch",

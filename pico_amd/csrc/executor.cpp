@@ -876,13 +876,17 @@ struct OpSpan {
   size_t size() const { return n; }
 };
 
+// the transport parameters a fused launch is built from (the live
+// DirectState, or bine_plan_dm_fused's host-only stand-in)
+struct FusedEnv {
+  int P = 1, rank = 0;
+  const DirectState *d = nullptr;
+  uint8_t *own = nullptr;  // the inbox base the kernel addresses (host-only planning: a stand-in)
+};
+
 template <typename Ptr>
-static bool build_fused(bine_comm *c, OpSpan ops, Ptr ptr, size_t esz, int dtype, int op, bool single,
+static bool build_fused(const FusedEnv &e, OpSpan ops, Ptr ptr, size_t esz, int dtype, int op, bool single,
                         DmFusedArgs &a) {
-  auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
-  if (!rt || !rt->dm_on || !rt->dm || c->profile || !fused_on() || op < 0 || !dm_fused_supported(dtype, op))
-    return false;
-  if (!single && !fused_large_on()) return false;
   const size_t nops = ops.size();
   size_t C = 0, i = 0;
   while (i + 1 < nops && ops[i].xchg && !ops[i + 1].xchg) {
@@ -892,15 +896,15 @@ static bool build_fused(bine_comm *c, OpSpan ops, Ptr ptr, size_t esz, int dtype
   }
   const bool ag = i < nops;
   if (C == 0 || C > (size_t)kMaxFusedTrees || (ag && (i + 1 != nops || !ops[i].xchg))) return false;
-  const DirectState &d = *rt->dm;
+  const DirectState &d = *e.d;
   const Prim &t0 = ops[1].prims[0];
   if (t0.peer < 2 || t0.peer > kMaxLeaves || t0.pos < 0 || t0.pos >= t0.peer) return false;
   a = DmFusedArgs{};
   a.wgs = single ? d.wgs : d.fused_wgs ? d.fused_wgs : d.tree_wgs;
   a.share = d.share;
-  a.rank = c->rank;
+  a.rank = e.rank;
   a.slot = d.slot;
-  a.own = (uint8_t *)d.own;
+  a.own = e.own;
   a.poison_host = d.hpoison_dev;
   a.timeout_ticks = d.timeout_ticks;
   a.nl = t0.peer;
@@ -923,10 +927,10 @@ static bool build_fused(bine_comm *c, OpSpan ops, Ptr ptr, size_t esz, int dtype
     owns.push_back({(const char *)ft.own_leaf, (const char *)ft.own_leaf + tb});
     for (int j = 0; j < kMaxLeaves; j++) ft.leaf[j] = -1;
   }
-  std::vector<int> js((size_t)c->size, 0), jr((size_t)c->size, 0);
+  std::vector<int> js((size_t)e.P, 0), jr((size_t)e.P, 0);
   int n = 0;
   auto add = [&](int peer, uint64_t bytes, bool push, const void *src, void *dst) -> bool {
-    if (n >= kMaxFusedMsgs || peer < 0 || peer >= c->size || peer == c->rank || bytes > d.slot || !bytes)
+    if (n >= kMaxFusedMsgs || peer < 0 || peer >= e.P || peer == e.rank || bytes > d.slot || !bytes)
       return false;
     int &j = push ? js[(size_t)peer] : jr[(size_t)peer];
     if (j >= dm::kSlots) return false;
@@ -1022,11 +1026,11 @@ static bool build_fused(bine_comm *c, OpSpan ops, Ptr ptr, size_t esz, int dtype
 // pair sees the per-exchange form's messages in its order (chunk by chunk),
 // so the ranks' choices need not agree.  Empty: not this form.
 template <typename Ptr>
-static bool plan_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
-                       std::vector<DmFusedArgs> &out) {
+static bool plan_fused_env(const FusedEnv &e, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op,
+                           bool single, std::vector<DmFusedArgs> &out) {
   out.assign(1, DmFusedArgs{});
   const OpSpan all{sc.ops.data(), sc.ops.size()};
-  if (build_fused(c, all, ptr, esz, dtype, op, single, out[0])) return true;
+  if (build_fused(e, all, ptr, esz, dtype, op, single, out[0])) return true;
   out.clear();
   const size_t n = sc.ops.size();
   if (single || n % 2 || n <= 2 * (size_t)kMaxFusedTrees) return false;
@@ -1035,12 +1039,28 @@ static bool plan_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, in
   for (size_t o0 = 0; o0 < n; o0 += 2 * kMaxFusedTrees) {
     out.emplace_back();
     const OpSpan g{sc.ops.data() + o0, std::min(n - o0, 2 * (size_t)kMaxFusedTrees)};
-    if (!build_fused(c, g, ptr, esz, dtype, op, single, out.back())) {
+    if (!build_fused(e, g, ptr, esz, dtype, op, single, out.back())) {
       out.clear();
       return false;
     }
   }
   return true;
+}
+
+template <typename Ptr>
+static bool plan_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
+                       std::vector<DmFusedArgs> &out) {
+  out.clear();
+  auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (!rt || !rt->dm_on || !rt->dm || c->profile || !fused_on() || op < 0 || !dm_fused_supported(dtype, op))
+    return false;
+  if (!single && !fused_large_on()) return false;
+  FusedEnv e;
+  e.P = c->size;
+  e.rank = c->rank;
+  e.d = rt->dm.get();
+  e.own = (uint8_t *)rt->dm->own;
+  return plan_fused_env(e, sc, ptr, esz, dtype, op, single, out);
 }
 
 // k_dm_fused for the call if its schedule qualifies (plan_fused): the
@@ -2340,6 +2360,30 @@ int64_t bine_plan_dm_trees(int algo, int nranks, int rank, size_t count, const i
     if (defer) defer[i] = pl.defer[(size_t)i];
   }
   return n;
+}
+
+int bine_plan_dm_fused(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
+                       int in_place, size_t chunk_bytes, int mode, size_t slot, int dtype, int op, int small) {
+  if (!esz || !slot) return -BINE_ERR_ARG;
+  PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, 0, in_place);
+  a.flat_ag = (mode & 2) != 0;
+  a.flat_rs = (mode & 4) != 0;
+  a.flat_ag_chunked = (mode & 8) != 0;
+  Plan p;
+  Schedule sc;
+  build(a, chunk_elems(chunk_bytes, esz), 0, (mode & 1) != 0, p, sc);
+  if (p.status != BINE_SUCCESS) return -p.status;
+  if (op < 0 || !dm_fused_supported(dtype, op)) return 0;
+  PlanOnlyTx tx;
+  tx.d.slot = slot;
+  FusedEnv e;
+  e.P = nranks;
+  e.rank = rank;
+  e.d = &tx.d;
+  e.own = (uint8_t *)((uintptr_t)15 << 40);  // stand-ins: 4 KiB-aligned, disjoint per buffer
+  auto ptr = [&](int buf, uint64_t off) { return (char *)((uintptr_t)(buf + 1) << 40) + off * esz; };
+  std::vector<DmFusedArgs> v;
+  return plan_fused_env(e, sc, ptr, esz, dtype, op, small != 0, v) ? (int)v.size() : 0;
 }
 
 int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,

@@ -20,7 +20,10 @@ in its N > 1 roofline).  Host only.
   receiving kernel).
 * launches: kernel launches per call (an exchange of r slot rounds: r
   launches when r = 1, else r + 1; a local op one; a fused tree none, or one
-  when it is hosted by itself) x the measured launch-to-launch gap.
+  when it is hosted by itself) x the measured launch-to-launch gap.  Over
+  the direct transport with fused trees a flat call whose chunks fit (round
+  5, bine_plan_dm_fused) is ONE k_dm_fused launch (a reduce-scatter: one
+  per 4 chunks), whose allgather pushes come from registers.
 
 On one GPU (P processes sharing it, the only multi-rank setting this pool
 offers) every rank's bytes go through the one HBM and no link is involved:
@@ -89,17 +92,40 @@ def _fused(coll, algo, P, rank, kw, slot):
     return leaf_ops, hosted, self_hosted
 
 
+def fused_launches(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0,
+                   rcounts=None, slot=SLOT_BYTES, one_launch=True):
+    """k_dm_fused launches of one large call (bine_plan_dm_fused): the whole
+    flat collective in one kernel (or one per 4 chunks of a reduce-scatter);
+    0 = the per-exchange launches (one_launch=False: BINE_DIRECT_FUSED_LARGE=0)"""
+    if not one_launch or not _flags(transport)[5] or P < 2:
+        return 0
+    import pico_amd
+    flat_ag, flat_rs = _flags(transport)[:2]
+    dt = {4: "float", 8: "double"}.get(esz, "float")
+    return pico_amd.dm_fused_plan(coll, algo, P, rank, count=count, rcounts=rcounts, esz=esz, chunk_bytes=chunk_bytes,
+                                  flat_ag=flat_ag, flat_rs=flat_rs, slot=slot, dtype=dt)
+
+
 def hbm_bytes(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0,
-              rcounts=None, slot=SLOT_BYTES):
-    """HBM bytes (reads + writes) one rank moves in one call (module doc)"""
+              rcounts=None, slot=SLOT_BYTES, one_launch=True):
+    """HBM bytes (reads + writes) one rank moves in one call (module doc).
+    In the one-launch form (fused_launches > 0) every exchange that feeds a
+    tree is read in place, and the allgather's sends are the trees' results
+    pushed from registers: no read of their source."""
     ops, kw = _schedule(coll, algo, P, rank, esz, transport, chunk_bytes, count, rcounts)
-    leaf_ops = _fused(coll, algo, P, rank, kw, slot)[0] if _flags(transport)[5] else set()
+    one = fused_launches(coll, algo, P, rank, esz, transport, chunk_bytes, count, rcounts, slot, one_launch) > 0
+    if one:
+        leaf_ops = {i for i in range(len(ops) - 1) if ops[i]["xchg"] and not ops[i + 1]["xchg"]}
+        ag_op = len(ops) - 1 if ops and ops[-1]["xchg"] else -1
+    else:
+        leaf_ops = _fused(coll, algo, P, rank, kw, slot)[0] if _flags(transport)[5] else set()
+        ag_op = -1
     b = 0
     for i, o in enumerate(ops):
         for p in o["prims"]:
             n = p["count"] * esz
-            b += {"SEND": n, "RECV": n + (0 if i in leaf_ops else 2 * n), "REDUCE_TREE": (p["peer"] + 1) * n,
-                  "COPY": 2 * n, "REDUCE": 3 * n, "REDUCE3": 3 * n}[p["type"]]
+            b += {"SEND": 0 if i == ag_op else n, "RECV": n + (0 if i in leaf_ops else 2 * n),
+                  "REDUCE_TREE": (p["peer"] + 1) * n, "COPY": 2 * n, "REDUCE": 3 * n, "REDUCE3": 3 * n}[p["type"]]
     return b
 
 
@@ -118,8 +144,11 @@ def link_bytes(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_
 
 
 def launches(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0,
-             rcounts=None, slot=SLOT_BYTES):
+             rcounts=None, slot=SLOT_BYTES, one_launch=True):
     """kernel launches per call (module doc)"""
+    nf = fused_launches(coll, algo, P, rank, esz, transport, chunk_bytes, count, rcounts, slot, one_launch)
+    if nf:
+        return nf
     ops, kw = _schedule(coll, algo, P, rank, esz, transport, chunk_bytes, count, rcounts)
     direct, fused = _flags(transport)[4:]
     hosted, self_hosted = (_fused(coll, algo, P, rank, kw, slot)[1:] if fused else (set(), set()))
@@ -138,13 +167,13 @@ def launches(coll, algo, P, rank=0, esz=4, transport="flatrs+flat+dmt", chunk_by
 
 def model_ms(coll, algo, P, esz=4, transport="flatrs+flat+dmt", chunk_bytes=16 << 20, count=0, rcounts=None,
              one_gpu=False, hbm_rate_gbs=HBM_RATE_GBS, link_gbs=LINK_GBS, t_boundary_us=T_BOUNDARY_US,
-             slot=SLOT_BYTES):
+             slot=SLOT_BYTES, one_launch=True):
     """expected ms of one call (module doc): {"model_ms", "t_link_ms", "t_hbm_ms", "launches", "hbm_bytes",
     "link_bytes"} (rank 0's schedule; the collectives are symmetric)"""
     kw = dict(esz=esz, transport=transport, chunk_bytes=chunk_bytes, count=count, rcounts=rcounts)
-    hb = hbm_bytes(coll, algo, P, slot=slot, **kw)
+    hb = hbm_bytes(coll, algo, P, slot=slot, one_launch=one_launch, **kw)
     lb = link_bytes(coll, algo, P, **kw) if P > 1 else 0
-    nl = launches(coll, algo, P, slot=slot, **kw)
+    nl = launches(coll, algo, P, slot=slot, one_launch=one_launch, **kw)
     t_hbm = (P if one_gpu else 1) * hb / (hbm_rate_gbs * 1e9) * 1e3
     t_link = 0.0 if one_gpu else lb / (link_gbs * 1e9) * 1e3
     return {"model_ms": round(max(t_link, t_hbm) + nl * t_boundary_us * 1e-3, 4), "t_link_ms": round(t_link, 4),

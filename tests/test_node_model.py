@@ -33,12 +33,13 @@ def test_hbm_bytes_table(P, fused, unfused):
 
 
 def test_launch_count_matches_the_stamped_runs():
+    # the per-exchange form (one_launch=False, BINE_DIRECT_FUSED_LARGE=0):
     # C3 at P = 2, 16 MiB chunks over flatrs+flat+dmt: 8 reduce-scatter
     # exchanges (each hosting the previous chunk's tree), the last tree by
     # itself, the 128 MiB allgather in 8 slot rounds (9 launches) = 18, the
     # launches per call tools/dm_stamps.py counted on the GPU; C4 33
     # (16 MiB slots, profiles/r4_dm_stamps_p2_solo.txt "base")
-    s16 = dict(slot=16 << 20)
+    s16 = dict(slot=16 << 20, one_launch=False)
     assert M.config_model("C3", 2, "flatrs+flat+dmt", **s16)["launches"] == 18
     assert M.config_model("C4", 2, "flatrs+flat+dmt", **s16)["launches"] == 33
     # P = 8: 2 exchanges of 16 MiB pieces, the last tree, the 32 MiB allgather
@@ -47,10 +48,34 @@ def test_launch_count_matches_the_stamped_runs():
     # the 64 MiB default slot (profiles/r4_dm_stamps_p2_sweep2.txt): the
     # allgather in 2 rounds at 16 MiB chunks (12), 4 + 1 + 1 at 64 MiB chunks
     # (6), C4 8 exchanges + the last tree (9); P = 8: the allgather in one
-    assert M.config_model("C3", 2, "flatrs+flat+dmt")["launches"] == 12
-    assert M.config_model("C3", 2, "flatrs+flat+dmt", 64 << 20)["launches"] == 6
-    assert M.config_model("C4", 2, "flatrs+flat+dmt", 64 << 20)["launches"] == 9
-    assert M.config_model("C3", 8, "flatrs+flat+dmt")["launches"] == 4
+    o = dict(one_launch=False)
+    assert M.config_model("C3", 2, "flatrs+flat+dmt", **o)["launches"] == 12
+    assert M.config_model("C3", 2, "flatrs+flat+dmt", 64 << 20, **o)["launches"] == 6
+    assert M.config_model("C4", 2, "flatrs+flat+dmt", 64 << 20, **o)["launches"] == 9
+    assert M.config_model("C3", 8, "flatrs+flat+dmt", **o)["launches"] == 4
+
+
+def test_one_launch_form():
+    """round 5's default (bine_plan_dm_fused): a flat call whose chunks are
+    slot-sized and fit one launch is ONE k_dm_fused launch -- C3 at P = 2 with
+    64 MiB chunks (2 chunks + 2 allgather pieces per peer: tools/dm_stamps.py
+    counted 1 launch per call, profiles/r5_dm_fused_p2.txt), C4 one launch per
+    4 chunks (2 at P = 2, stamped), P = 4 / 8 one; 16 MiB chunks below the
+    64 MiB slot keep the per-exchange launches.  The allgather's pushes come
+    from registers: 0.5 S less HBM traffic at P = 2 than the per-exchange
+    fused-tree form"""
+    c64 = 64 << 20
+    assert M.config_model("C3", 2, "flatrs+flat+dmt", c64)["launches"] == 1
+    assert M.config_model("C4", 2, "flatrs+flat+dmt", c64)["launches"] == 2
+    for P in (4, 8):
+        assert M.config_model("C3", P, "flatrs+flat+dmt", c64)["launches"] == 1
+        assert M.config_model("C4", P, "flatrs+flat+dmt", c64)["launches"] == 1
+        assert M.config_model("C5", P, "flatrs+flat+dmt", c64)["launches"] == 1
+    assert M.config_model("C3", 2, "flatrs+flat+dmt", 16 << 20)["launches"] == 12
+    one = M.hbm_bytes("allreduce", "bine_bdw_remap", 2, count=67_108_864, chunk_bytes=c64)
+    per = M.hbm_bytes("allreduce", "bine_bdw_remap", 2, count=67_108_864, chunk_bytes=c64, one_launch=False)
+    assert (one, per) == (4.0 * S3, 4.5 * S3)
+    assert M.hbm_bytes("allreduce", "bine_bdw_remap", 8, count=67_108_864, chunk_bytes=c64) == 5.5 * S3
 
 
 def test_model_arithmetic():
