@@ -69,7 +69,8 @@ typedef enum {
   BINE_ERR_RCCL = 5,         /* an RCCL call failed */
   BINE_ERR_UNSUPPORTED = 6,  /* algorithm / dtype / op not provided */
   BINE_ERR_INTERNAL = 7,
-  BINE_ERR_ROOT = 8          /* reference returns MPI_ERR_ROOT (bcast_bine_lat: root != 0) */
+  BINE_ERR_ROOT = 8,         /* reference returns MPI_ERR_ROOT (bcast_bine_lat: root != 0) */
+  BINE_ERR_COUNT = 9         /* reference returns MPI_ERR_COUNT (bandwidth bcasts: count < P) */
 } bine_status_t;
 
 /* Algorithms.  Names are the libbine function names without the collective
@@ -115,13 +116,13 @@ typedef enum {
   /* bcast, libbine_bcast.c (widening past section 8):
    * the latency trees; the scatter-allgather and bandwidth variants are not
    * provided yet (BINE_ERR_UNSUPPORTED) */
-  BINE_BC_SCATTER_ALLGATHER = 64,     /* :42   (not provided) */
+  BINE_BC_SCATTER_ALLGATHER = 64,     /* :42   */
   BINE_BC_BINE_LAT = 65,              /* :189  */
   BINE_BC_BINE_LAT_REVERSED = 66,     /* :281  */
   BINE_BC_BINE_LAT_NEW = 67,          /* :373  */
   BINE_BC_BINE_LAT_I_NEW = 68,        /* :408  */
-  BINE_BC_BINE_BDW_STATIC = 69,       /* :462  (not provided) */
-  BINE_BC_BINE_BDW_REMAP = 70         /* :649  (not provided) */
+  BINE_BC_BINE_BDW_STATIC = 69,       /* :462  */
+  BINE_BC_BINE_BDW_REMAP = 70         /* :649  */
 } bine_algo_t;
 
 /* the reference's MPI_IN_PLACE (mpi.h: (void *)-1) */
@@ -350,7 +351,13 @@ int bine_comm_set_flat_rs(bine_comm_t comm, int on);
  * BINE_DIRECT_WGS (workgroups per message, 128), BINE_DIRECT_MERGE (launch
  * structure: 3 = the mix above, 2 = one launch per round, 1 = pipelined, 0 =
  * separate push and pull launches).  At most 64 ranks.  Loopback:
- * UNSUPPORTED. */
+ * UNSUPPORTED.  Memory: each rank reserves one inbox of 320 KiB of flags +
+ * P x 4 slots x BINE_DIRECT_SLOT_BYTES (64 MiB default: 2 GiB at P = 8,
+ * 16 GiB at the 64-rank limit) at set-up, whatever the message sizes; set
+ * BINE_DIRECT_SLOT_BYTES lower for small messages or many ranks (a slot
+ * below the pipelining chunk only adds launch rounds).  Every launch's
+ * workgroups are cut to the GPU's resident capacity divided by the ranks
+ * sharing it (bine_dm_launch_cap). */
 int bine_comm_set_direct(bine_comm_t comm, int on);
 /* Workgroups per message of the direct transport's copy launches (0: the
  * default, BINE_DIRECT_WGS or 128).  Local, not collective; drops cached graphs

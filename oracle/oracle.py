@@ -197,6 +197,282 @@ def allgather(algo, sbufs, dtype, in_place_rbufs=None):
 ERR_ROOT = 7   # MPICH's MPI_ERR_ROOT
 
 
+ERR_COUNT = 2   # MPICH's MPI_ERR_COUNT
+BC_BDW = ("scatter_allgather", "bine_bdw_static", "bine_bdw_remap")
+
+
+class _Stuck(Exception):
+    pass
+
+
+def _replay(P, bufs, programs):
+    """Run one generator per rank -- a line-by-line restatement of a reference
+    function -- with MPI's point-to-point semantics: a send is buffered (its
+    bytes are snapshotted when posted, as MPI_Send / MPI_Isend of an unmodified
+    buffer deliver them), a receive takes the oldest message of its
+    (source, destination) pair, places it at its offset and reports its
+    element count (MPI_Get_count); a message longer than the receive's count
+    is MPI_ERR_TRUNCATE and ends the replay.  Yields: ("send", dst, off, n),
+    ("recv", src, off, maxn) -> n.  A rank's return value is its status.
+    Raises _Stuck when no rank can move (the reference would hang)."""
+    import collections
+    q = collections.defaultdict(collections.deque)
+    gens = [programs[r]() for r in range(P)]
+    rets = [None] * P
+    pending = [None] * P   # the op a rank waits on
+    val = [None] * P
+    while any(x is None for x in rets):
+        moved = False
+        for r in range(P):
+            while rets[r] is None:
+                if pending[r] is None:
+                    try:
+                        pending[r] = gens[r].send(val[r])
+                    except StopIteration as e:
+                        rets[r] = e.value if e.value is not None else OK
+                        moved = True
+                        break
+                    val[r] = None
+                    moved = True
+                op = pending[r]
+                if op[0] == "send":
+                    _, dst, off, n = op
+                    if off + n > bufs[r].size:
+                        raise ValueError("a send reads past the buffer")
+                    q[(r, dst)].append(np.array(bufs[r][off:off + n]))
+                    pending[r] = None
+                    moved = True
+                    continue
+                _, src, off, maxn = op
+                if not q[(src, r)]:
+                    break
+                m = q[(src, r)].popleft()
+                if m.size > maxn:
+                    raise ValueError("MPI_ERR_TRUNCATE")
+                if off + m.size > bufs[r].size:
+                    raise ValueError("a receive writes past the buffer")
+                bufs[r][off:off + m.size] = m
+                val[r] = m.size
+                pending[r] = None
+                moved = True
+        if not moved:
+            raise _Stuck()
+    return rets
+
+
+def _bc_scatter_allgather(P, count, root, bufs):
+    """bcast_scatter_allgather, libbine_bcast.c:42-187 (binomial-tree scatter,
+    recursive-doubling allgather with the non-power-of-two forwarding)"""
+    def prog(rank):
+        def g():
+            if P < 2:
+                return OK
+            if count < P:
+                return ERR_COUNT
+            u = lambda x: x % (1 << 64)   # the reference's size_t arithmetic (it wraps)
+            vrank = (rank - root + P) % P
+            sc = (count + P - 1) // P
+            curr = count if rank == root else 0
+            recv_count = 0
+            mask = 1
+            while mask < P:                                         # :73-91
+                if vrank & mask:
+                    parent = (rank - mask + P) % P
+                    recv_count = u(count - vrank * sc)
+                    if recv_count == 0:
+                        curr = 0
+                    else:
+                        curr = yield ("recv", parent, vrank * sc, recv_count)
+                    break
+                mask <<= 1
+            mask >>= 1
+            while mask > 0:                                         # :93-106
+                if vrank + mask < P:
+                    send_count = u(curr - sc * mask)
+                    if send_count > 0:
+                        yield ("send", (rank + mask) % P, sc * (vrank + mask), send_count)
+                        curr = u(curr - send_count)
+                mask >>= 1
+            rem = u(count - vrank * sc)                             # :112-115
+            curr = min(sc, rem)
+            mask = 1
+            while mask < P:                                         # :117-171
+                vremote = vrank ^ mask
+                remote = (vremote + root) % P
+                vtr = (vrank // mask) * mask
+                vrtr = (vremote // mask) * mask
+                if vremote < P:
+                    recv_count = u(count - vrtr * sc)
+                    yield ("send", remote, vtr * sc, curr)
+                    recv_count = yield ("recv", remote, vrtr * sc, recv_count)
+                    curr += recv_count
+                if vrtr + mask > P:
+                    nad = P - vtr - mask
+                    off = sc * (vtr + mask)
+                    rh = mask >> 1
+                    while rh > 0:
+                        vrem = vrank ^ rh
+                        rem_r = (vrem + root) % P
+                        tree_root = (vrank // (rh << 1)) * (rh << 1)
+                        if vrem > vrank and vrank < tree_root + nad and vrem >= tree_root + nad:
+                            yield ("send", rem_r, off, recv_count)
+                        elif vrem < vrank and vrem < tree_root + nad and vrank >= tree_root + nad:
+                            recv_count = yield ("recv", rem_r, off, count)
+                            curr += recv_count
+                        rh >>= 1
+                mask <<= 1
+            return OK
+        return g
+    return [prog(r) for r in range(P)]
+
+
+def _bc_bine_bdw_static(P, count, root, bufs):
+    """bcast_bine_bdw_static, libbine_bcast.c:462-647 (static-table scatter,
+    mirrored allgather)"""
+    steps = P.bit_length() - 1
+    tables = static_tables(P) if P >= 2 and P == 1 << steps else None
+
+    def prog(rank):
+        def g():
+            if P < 2:
+                return OK
+            if count < P:
+                return ERR_COUNT
+            if P != 1 << steps:
+                return ERR_SIZE
+            if root != 0:
+                return ERR_ROOT
+            received = [False] * P
+            received[root] = True
+            recv_step = -1
+            step = 0
+            while step < steps and not received[rank]:              # :519-530
+                for proc in range(P):
+                    if not received[proc]:
+                        continue
+                    dest = pi(proc, step, P)
+                    received[dest] = True
+                    if dest == rank:
+                        recv_step = step
+                        break
+                step += 1
+            split = count % P
+            small = count // P
+            big = small + (1 if split else 0)
+            _, sb, rb = tables
+            s_bm, r_bm = list(sb[rank]), list(rb[rank])
+
+            def cnt(b, w):
+                return w * big if b + w <= split else w * small if b >= split else w * small + (split - b)
+
+            def offs(b):
+                return b * big if b <= split else b * small + split
+            w = P >> 1
+            for step in range(steps):                               # :556-587
+                if rank != root and recv_step == step:
+                    yield ("recv", pi(rank, step, P), offs(r_bm[step]), cnt(r_bm[step], w))
+                if recv_step < step:
+                    yield ("send", pi(rank, step, P), offs(s_bm[step]), cnt(s_bm[step], w))
+                w >>= 1
+            w = 1
+            for step in range(steps - 1, -1, -1):                   # :606-632
+                dest = pi(rank, step, P)
+                if recv_step != step:
+                    yield ("send", dest, offs(r_bm[step]), cnt(r_bm[step], w))
+                if not recv_step < step:
+                    yield ("recv", dest, offs(s_bm[step]), cnt(s_bm[step], w))
+                w <<= 1
+            return OK
+        return g
+    return [prog(r) for r in range(P)]
+
+
+def _bc_bine_bdw_remap(P, count, root, bufs):
+    """bcast_bine_bdw_remap, libbine_bcast.c:649-760 (negabinary-remapped
+    scatter + allgather); root 0 only (:650 asserts)"""
+    steps = P.bit_length() - 1
+    nb2b = lambda x: ((x ^ 0xAAAAAAAA) - 0xAAAAAAAA) & 0xFFFFFFFF   # negabinary_to_binary
+
+    def sgn(v):
+        return v - (1 << 32) if v >= 1 << 31 else v
+
+    def prog(rank):
+        def g():
+            per, rem = count // P, count % P
+            displs = [per * i + (i if i < rem else rem) for i in range(P)]
+            rc = [per + (1 if i < rem else 0) for i in range(P)]
+            mask = 1
+            inv = 1 << (steps - 1) if steps else 0
+            bfm = ~(inv - 1) if inv else -1
+            rr = remap_rank(P, rank)
+            recv_mask = inv << 1
+            if rank != root:
+                recv_mask = rr & -rr
+            recvd = rank == root
+
+            def partner():
+                d = sgn(nb2b((mask << 1) - 1))
+                return (rank + d) % P if rank % 2 == 0 else (rank - d) % P
+            while mask < P:                                         # :689-716
+                pt = partner()
+                sf = remap_rank(P, pt) & bfm
+                sl = sf + inv - 1
+                scount = displs[sl] - displs[sf] + rc[sl]
+                rf = rr & bfm
+                rl = rf + inv - 1
+                rcount = displs[rl] - displs[rf] + rc[rl]
+                if recvd:
+                    yield ("send", pt, displs[sf], scount)
+                elif inv == recv_mask or pt == root:
+                    yield ("recv", pt, displs[rf], rcount)
+                    recvd = True
+                mask <<= 1
+                inv >>= 1
+                bfm >>= 1
+            mask >>= 1                                              # :719-751
+            inv = 1
+            bfm = -1
+            while mask > 0:
+                pt = partner()
+                rp = None if inv < recv_mask else pt
+                sp = None if inv == recv_mask else pt
+                if sp is not None:
+                    sf = rr & bfm
+                    sl = sf + inv - 1
+                    yield ("send", sp, displs[sf], displs[sl] - displs[sf] + rc[sl])
+                if rp is not None:
+                    rf = remap_rank(P, rp) & bfm
+                    rl = rf + inv - 1
+                    yield ("recv", rp, displs[rf], displs[rl] - displs[rf] + rc[rl])
+                mask >>= 1
+                inv <<= 1
+                bfm <<= 1
+            return OK
+        return g
+    return [prog(r) for r in range(P)]
+
+
+def bcast_bdw(algo, sbufs, dtype, root=0):
+    """the bandwidth bcasts (libbine_bcast.c:42, :462, :649), in place on each
+    rank's own input: (buffers after the broadcast, rets), by message-level
+    replay of the reference (_replay).  Where the reference crashes or hangs
+    (scatter_allgather's size_t counts wrap when a block starts past the
+    buffer's end, and a send then reads past it; bine_bdw_remap at root != 0
+    or non-power-of-two P): "crash" in every ret."""
+    P = len(sbufs)
+    bufs = [np.array(b, dtype=NP_DTYPES[dtype]).copy() for b in sbufs]
+    n = bufs[0].size if P else 0
+    if algo == "bine_bdw_remap" and (root != 0 or P & (P - 1)):
+        return bufs, ["crash"] * P
+    progs = {"scatter_allgather": _bc_scatter_allgather, "bine_bdw_static": _bc_bine_bdw_static,
+             "bine_bdw_remap": _bc_bine_bdw_remap}[algo](P, n, root, bufs)
+    try:
+        rets = _replay(P, bufs, progs)
+    except (_Stuck, ValueError):
+        return bufs, ["crash"] * P
+    return bufs, rets
+
+
 def bcast(algo, sbufs, dtype, root=0):
     """bcast latency trees, in place (each rank's buffer = its input); returns
     (buffers after the broadcast, rets).  Message-level replay of the

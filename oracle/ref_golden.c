@@ -79,6 +79,9 @@ static bc_fn pick_bcast(const char *a) {
   if (!strcmp(a, "bine_lat_reversed")) return bcast_bine_lat_reversed;
   if (!strcmp(a, "bine_lat_new")) return bcast_bine_lat_new;
   if (!strcmp(a, "bine_lat_i_new")) return bcast_bine_lat_i_new;
+  if (!strcmp(a, "scatter_allgather")) return bcast_scatter_allgather;
+  if (!strcmp(a, "bine_bdw_static")) return bcast_bine_bdw_static;
+  if (!strcmp(a, "bine_bdw_remap")) return bcast_bine_bdw_remap;
   return NULL;
 }
 

@@ -27,7 +27,7 @@ DTYPE_SIZE = {"int8": 1, "uint8": 1, "int16": 2, "uint16": 2, "int32": 4, "uint3
 OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "band": 5, "lor": 6, "bor": 7, "lxor": 8, "bxor": 9,
        "maxloc": 10, "minloc": 11}
 STATUS = {0: "SUCCESS", 1: "ERR_ARG", 2: "ERR_SIZE", 3: "ERR_NO_MEM", 4: "ERR_HIP", 5: "ERR_RCCL",
-          6: "ERR_UNSUPPORTED", 7: "ERR_INTERNAL", 8: "ERR_ROOT"}
+          6: "ERR_UNSUPPORTED", 7: "ERR_INTERNAL", 8: "ERR_ROOT", 9: "ERR_COUNT"}
 ALGOS = {
     "allreduce": {"recursivedoubling": 0, "ring": 1, "rabenseifner": 2, "bine_lat": 3,
                   "bine_bdw_static": 4, "bine_bdw_remap": 5, "bine_bdw_remap_segmented": 6,
@@ -41,9 +41,9 @@ ALGOS = {
                   "bine_block_by_block": 52, "bine_block_by_block_any_even": 53,
                   "bine_permute_static": 54, "bine_send_static": 55, "bine_permute_remap": 56,
                   "bine_send_remap": 57, "bine_2_blocks": 58, "bine_2_blocks_dtype": 59},
-    # the latency trees of libbine_bcast.c (scatter_allgather 64, bine_bdw_static 69,
-    # bine_bdw_remap 70: not provided)
-    "bcast": {"bine_lat": 65, "bine_lat_reversed": 66, "bine_lat_new": 67, "bine_lat_i_new": 68},
+    # libbine_bcast.c: the latency trees and (round 5) the bandwidth algorithms
+    "bcast": {"scatter_allgather": 64, "bine_lat": 65, "bine_lat_reversed": 66, "bine_lat_new": 67, "bine_lat_i_new": 68,
+              "bine_bdw_static": 69, "bine_bdw_remap": 70},
 }
 IN_PLACE = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)
 UNIQUE_ID_BYTES = 128

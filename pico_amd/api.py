@@ -181,7 +181,9 @@ class Comm:
 
     def set_direct(self, on: bool) -> None:
         """RCCL communicators on one node: exchanges through mapped peer memory
-        (bine_comm_set_direct); bit-identical; the first enable is collective."""
+        (bine_comm_set_direct); bit-identical.  EVERY call with on=True is
+        collective (all ranks, same point: set-up, or the rebuild of a
+        transport a timeout disabled on any rank); on=False is local."""
         check(lib().bine_comm_set_direct(self.handle, int(on)), "bine_comm_set_direct")
 
     def set_direct_wgs(self, wgs: int) -> None:

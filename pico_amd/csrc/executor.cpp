@@ -1787,6 +1787,7 @@ const char *bine_status_string(int s) {
     case BINE_ERR_RCCL: return "RCCL error";
     case BINE_ERR_UNSUPPORTED: return "unsupported algorithm, datatype or operator";
     case BINE_ERR_ROOT: return "unsupported root (reference: MPI_ERR_ROOT)";
+    case BINE_ERR_COUNT: return "count below the number of ranks (reference: MPI_ERR_COUNT)";
     default: return "internal error";
   }
 }

@@ -159,6 +159,7 @@ int to_mpi(int st) {
     case BINE_ERR_NO_MEM: return MPI_ERR_NO_MEM;
     case BINE_ERR_UNSUPPORTED: return MPI_ERR_UNSUPPORTED_OPERATION;
     case BINE_ERR_ROOT: return MPI_ERR_ROOT;
+    case BINE_ERR_COUNT: return MPI_ERR_COUNT;
     default:
       fprintf(stderr, "libbine(amd): %s: %s\n", bine_status_string(st), bine_last_error());
       return MPI_ERR_OTHER;
@@ -587,9 +588,24 @@ int do_bcast(int algo, void *buf, size_t count, MPI_Datatype dtype, int root, MP
   Entry *e;
   int rc = get_entry(comm, &e);
   if (rc) return rc;
+  // the bandwidth bcasts split the buffer into blocks of ELEMENTS (and refuse
+  // count < P, MPI_ERR_COUNT): they run on the type itself when the library
+  // has it with this extent, else on bytes with the element count checked
+  // here -- the blocks then fall elsewhere, the delivered bytes are the same
+  size_t n = bytes;
+  int dt = BINE_UINT8;
+  if (algo == BINE_BC_SCATTER_ALLGATHER || algo == BINE_BC_BINE_BDW_STATIC || algo == BINE_BC_BINE_BDW_REMAP) {
+    const int t = map_dtype(dtype);
+    if (t >= 0 && bine_dtype_size(t) == sz) {
+      n = count;
+      dt = t;
+    } else if (e->size > 1 && count < (size_t)e->size && algo != BINE_BC_BINE_BDW_REMAP) {
+      return MPI_ERR_COUNT;
+    }
+  }
   return with_buffers(e, MPI_IN_PLACE, 0, buf, bytes, true, 0, bytes,
                       [&](const void *, void *r, size_t, size_t, void *st) {
-                        return bine_bcast(e->comm, algo, r, bytes, BINE_UINT8, root, st);
+                        return bine_bcast(e->comm, algo, r, n, dt, root, st);
                       });
 }
 
@@ -597,7 +613,7 @@ int unsupported(const char *name) {
   static std::once_flag once;
   std::call_once(once, [&] {
     fprintf(stderr, "libbine(amd): %s is outside the reduce family this library provides "
-                    "(allreduce / reduce_scatter / reduce / allgather / the bcast latency trees); returning "
+                    "(allreduce / reduce_scatter / reduce / allgather / bcast); returning "
                     "MPI_ERR_UNSUPPORTED_OPERATION\n", name);
   });
   return MPI_ERR_UNSUPPORTED_OPERATION;
@@ -654,16 +670,16 @@ AG(allgather_bine_2_blocks_dtype, BINE_AG_BINE_2_BLOCKS_DTYPE)
 #undef AG
 
 NA(alltoall_bine, BINE_ALLGATHER_ARGS)
-NA(bcast_scatter_allgather, BINE_BCAST_ARGS)
 #define BC(fn, id) \
   int fn(BINE_BCAST_ARGS) { return do_bcast(id, buf, count, dtype, root, comm); }
 BC(bcast_bine_lat, BINE_BC_BINE_LAT)
 BC(bcast_bine_lat_reversed, BINE_BC_BINE_LAT_REVERSED)
 BC(bcast_bine_lat_new, BINE_BC_BINE_LAT_NEW)
 BC(bcast_bine_lat_i_new, BINE_BC_BINE_LAT_I_NEW)
+BC(bcast_scatter_allgather, BINE_BC_SCATTER_ALLGATHER)
+BC(bcast_bine_bdw_static, BINE_BC_BINE_BDW_STATIC)
+BC(bcast_bine_bdw_remap, BINE_BC_BINE_BDW_REMAP)
 #undef BC
-NA(bcast_bine_bdw_static, BINE_BCAST_ARGS)
-NA(bcast_bine_bdw_remap, BINE_BCAST_ARGS)
 NA(gather_bine, BINE_GATHER_ARGS)
 NA(scatter_bine, BINE_GATHER_ARGS)
 #undef NA

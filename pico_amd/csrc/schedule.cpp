@@ -1657,6 +1657,169 @@ void bc_bine_lat_new(Builder &b, const PlanArgs &a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// bcast, libbine_bcast.c: the bandwidth algorithms -- a scatter of the
+// root's buffer, then an allgather of the pieces.  In place in RB.
+// ---------------------------------------------------------------------------
+
+// bcast_scatter_allgather (:42-187): binomial-tree scatter of blocks of
+// sc = ceil(count / P) (vrank v's subtree gets blocks [v, v + lowbit(v))),
+// recursive-doubling allgather, and for a non-power-of-two P the forwarding
+// of an incomplete partner group's data by recursive halving (:149-169).
+// Every count is the size of the data it names, clamped to the buffer: the
+// reference computes them in size_t and its counts wrap when a block starts
+// past the buffer's end (e.g. count 9 at P = 8), where it then reads past
+// the buffer and crashes; here those blocks are empty and the broadcast
+// completes (tests/test_bcast.py: every such case delivers the root's
+// buffer).
+void bc_scatter_allgather(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  if (P < 2) return;
+  if (a.count < (uint64_t)P) { b.fail(BINE_ERR_COUNT); return; }
+  const uint64_t count = a.count, sc = (count + P - 1) / P;
+  const int v = pmod(r - a.root, P);
+  auto real = [&](int x) { return pmod(x + a.root, P); };
+  // the data of blocks [lo, lo + w) (vranks), clamped to the buffer
+  auto span = [&](int64_t lo, int64_t w) -> uint64_t {
+    const uint64_t s = std::min<uint64_t>(count, (uint64_t)lo * sc), e = std::min<uint64_t>(count, (uint64_t)(lo + w) * sc);
+    return e > s ? e - s : 0;
+  };
+  int top = 1;
+  while (top < P) top <<= 1;
+  const int low = v ? (v & -v) : top;  // the scatter's receive step (the root: none)
+  if (v) {  // :73-91
+    b.recv(real(v - low), RB, (uint64_t)v * sc, span(v, low));
+    b.end();
+  }
+  for (int m = low >> 1; m > 0; m >>= 1)  // :93-106, one blocking send per child
+    if (v + m < P) {
+      b.send(real(v + m), RB, (uint64_t)(v + m) * sc, span(v + m, m));
+      b.end();
+    }
+  for (int m = 1; m < P; m <<= 1) {  // :117-171
+    const int w = v ^ m;
+    const int64_t vtr = v / m * m, wtr = (int64_t)w / m * m;
+    if (w < P) {
+      b.send(real(w), RB, (uint64_t)vtr * sc, span(vtr, m));
+      b.recv(real(w), RB, (uint64_t)wtr * sc, span(wtr, m));
+      b.end();
+    }
+    if (wtr + m > P) {
+      const int64_t nad = P - vtr - m;
+      const uint64_t off = sc * (uint64_t)(vtr + m), fw = span(vtr + m, m);
+      for (int rh = m >> 1; rh > 0; rh >>= 1) {
+        const int x = v ^ rh;
+        const int64_t tr = v / (rh << 1) * (rh << 1);
+        if (x > v && v < tr + nad && x >= tr + nad) {
+          b.send(real(x), RB, off, fw);
+          b.end();
+        } else if (x < v && x < tr + nad && v >= tr + nad) {
+          b.recv(real(x), RB, off, fw);
+          b.end();
+        }
+      }
+    }
+  }
+}
+
+// bcast_bine_bdw_static (:462-647): the static tables' windows (libbine_utils_
+// bitmaps.c, regenerated by static_perm) of w = P >> (s + 1) blocks of the
+// COLL_BASE_COMPUTE_BLOCKCOUNT split; a rank receives its window at the step
+// the root's pi-tree reaches it (:519-530, replayed in the reference's own
+// order) and then forwards at every later step; the allgather mirrors it
+void bc_bine_bdw_static(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (P < 2) return;
+  if (a.count < (uint64_t)P) { b.fail(BINE_ERR_COUNT); return; }
+  if (!is_pow2(P)) { b.fail(BINE_ERR_SIZE); return; }
+  if (a.root != 0) { b.fail(BINE_ERR_ROOT); return; }
+  std::vector<char> got((size_t)P);
+  got[0] = 1;
+  int recv_step = -1;
+  for (int s = 0; s < steps && !got[(size_t)r]; s++)
+    for (int x = 0; x < P; x++) {
+      if (!got[(size_t)x]) continue;
+      const int d = pi(x, s, P);
+      got[(size_t)d] = 1;
+      if (d == r) { recv_step = s; break; }
+    }
+  std::vector<int> perm;
+  static_perm(P, perm);
+  auto rtab = [&](int x, int s) { const int w = P >> (s + 1); return perm[(size_t)x] & ~(w - 1); };
+  auto stab = [&](int x, int s) { return rtab(pi(x, s, P), s); };
+  const uint64_t small = a.count / P, split = a.count % P, big = small + (split ? 1 : 0);
+  auto cnt = [&](int blk, int w) -> uint64_t {
+    const uint64_t bb = (uint64_t)blk, ww = (uint64_t)w;
+    return bb + ww <= split ? ww * big : bb >= split ? ww * small : ww * small + (split - bb);
+  };
+  auto off = [&](int blk) -> uint64_t { const uint64_t bb = (uint64_t)blk; return bb <= split ? bb * big : bb * small + split; };
+  int w = P >> 1;
+  for (int s = 0; s < steps; s++, w >>= 1) {  // :556-587
+    if (r != 0 && recv_step == s) { b.recv(pi(r, s, P), RB, off(rtab(r, s)), cnt(rtab(r, s), w)); b.end(); }
+    if (recv_step < s) { b.send(pi(r, s, P), RB, off(stab(r, s)), cnt(stab(r, s), w)); b.end(); }
+  }
+  w = 1;
+  for (int s = steps - 1; s >= 0; s--, w <<= 1) {  // :606-632
+    const int d = pi(r, s, P);
+    if (recv_step != s) b.send(d, RB, off(rtab(r, s)), cnt(rtab(r, s), w));
+    if (!(recv_step < s)) b.recv(d, RB, off(stab(r, s)), cnt(stab(r, s), w));
+    b.end();
+  }
+}
+
+// bcast_bine_bdw_remap (:649-760): blocks in remapped (negabinary) order of
+// the count / P split with the remainder spread over the first blocks; the
+// partner at mask m is rank +- negabinary_to_binary(2m - 1); a rank receives
+// once, at the step given by the lowest set bit of its remapped rank, then
+// sends; the allgather mirrors it.  Root 0 and power-of-two P only (the
+// reference asserts root == 0 and is undefined elsewhere): BINE_ERR_ARG.
+void bc_bine_bdw_remap(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank, steps = log2_ceil(P);
+  if (P < 2) return;
+  if (!is_pow2(P) || a.root != 0) { b.fail(BINE_ERR_ARG); return; }
+  const uint64_t per = a.count / P, rem = a.count % P;
+  auto displ = [&](int i) { return per * (uint64_t)i + std::min<uint64_t>((uint64_t)i, rem); };
+  auto rc = [&](int i) { return per + ((uint64_t)i < rem ? 1 : 0); };
+  auto run = [&](int first, int last) { return displ(last) - displ(first) + rc(last); };
+  const int rr = (int)remap_rank((uint32_t)P, (uint32_t)r);
+  auto partner = [&](int mask) {
+    const int d = (int32_t)((((uint32_t)(mask << 1) - 1) ^ 0xAAAAAAAAu) - 0xAAAAAAAAu);  // negabinary_to_binary
+    return r % 2 == 0 ? pmod(r + d, P) : pmod(r - d, P);
+  };
+  int inv = 1 << (steps - 1), bfm = ~(inv - 1);
+  const int recv_mask = r == 0 ? inv << 1 : (rr & -rr);
+  bool recvd = r == 0;
+  int mask = 1;
+  for (; mask < P; mask <<= 1, inv >>= 1, bfm >>= 1) {  // :689-716
+    const int pt = partner(mask);
+    if (recvd) {
+      const int sf = (int)remap_rank((uint32_t)P, (uint32_t)pt) & bfm;
+      b.send(pt, RB, displ(sf), run(sf, sf + inv - 1));
+      b.end();
+    } else if (inv == recv_mask || pt == 0) {
+      const int rf = rr & bfm;
+      b.recv(pt, RB, displ(rf), run(rf, rf + inv - 1));
+      b.end();
+      recvd = true;
+    }
+  }
+  mask >>= 1;
+  inv = 1;
+  bfm = ~0;
+  for (; mask > 0; mask >>= 1, inv <<= 1, bfm <<= 1) {  // :719-751
+    const int pt = partner(mask);
+    if (inv != recv_mask) {
+      const int sf = rr & bfm;
+      b.send(pt, RB, displ(sf), run(sf, sf + inv - 1));
+    }
+    if (inv >= recv_mask) {
+      const int rf = (int)remap_rank((uint32_t)P, (uint32_t)pt) & bfm;
+      b.recv(pt, RB, displ(rf), run(rf, rf + inv - 1));
+    }
+    b.end();
+  }
+}
+
 Plan make_plan(const PlanArgs &a) {
   Builder b(a.rank);
   if (a.P < 1 || a.rank < 0 || a.rank >= a.P || a.esz == 0) { b.fail(BINE_ERR_ARG); return b.p; }
@@ -1702,6 +1865,9 @@ Plan make_plan(const PlanArgs &a) {
     case BINE_BC_BINE_LAT_REVERSED: bc_bine_lat(b, a, true); break;
     case BINE_BC_BINE_LAT_NEW:
     case BINE_BC_BINE_LAT_I_NEW: bc_bine_lat_new(b, a); break;
+    case BINE_BC_SCATTER_ALLGATHER: bc_scatter_allgather(b, a); break;
+    case BINE_BC_BINE_BDW_STATIC: bc_bine_bdw_static(b, a); break;
+    case BINE_BC_BINE_BDW_REMAP: bc_bine_bdw_remap(b, a); break;
     default: b.fail(BINE_ERR_UNSUPPORTED); break;
   }
   if (!b.pend_send.empty() || !b.pend_recv.empty()) b.end();

@@ -194,3 +194,38 @@ def config_model(cfg, P, transport, chunk_bytes=16 << 20, **kw):
         return model_ms(coll, algo, P, esz=esz, transport=transport, chunk_bytes=chunk_bytes, count=n, **kw)
     return model_ms(coll, algo, P, esz=esz, transport=transport, chunk_bytes=chunk_bytes, rcounts=[n // P] * P,
                     **kw)
+
+
+# ---- C1 end to end through the unchanged pico_core ----------
+# pico_core hands libbine host (malloc) buffers (pico_core_allreduce_utils.c:13-25):
+# a C1 call is H2D(1 MiB) -> the device collective -> D2H(1 MiB) on the
+# collective's stream (below two staging chunks nothing overlaps), every rank
+# on its own GPU and its own PCIe link on a node.
+T_HOST_RT_US = 66.0      # C1 at P = 1 through pico_core + libbine.so: the 1 MiB host round trip with the
+                         # page-locking and HIP calls around it (profiles/r4_e2e_c1.txt; the bare round
+                         # trip probe: 69-72 us)
+T_FLAG_US = 3.0          # one cross-GPU flag round trip of a k_dm_fused phase (system-scope store seen by
+                         # the peer's poll): NOT measured on xGMI -- the one assumed constant here
+C1_PHASES = 3            # k_dm_fused's flat allreduce: pushes, tree (+ allgather pushes), pulls
+C1_ONE_GPU_DEV_US = {2: 28.7, 4: 49.0}   # device-resident C1 with the ranks sharing ONE GPU (one HW queue
+                                          # each; profiles/r4_c1_fused_wgs.txt): the bench rehearsal's
+                                          # upper bound for a node
+C1_REFERENCE_CPU_US = {4: 215.0}         # the real reference libbine on the GPU box's host cores, C1 at
+                                          # P = 4 (BENCH_r04 cpu_baseline)
+
+
+def c1_e2e_us(P, t_host_rt_us=T_HOST_RT_US, t_flag_us=T_FLAG_US, t_boundary_us=T_BOUNDARY_US,
+              link_gbs=LINK_GBS):
+    """predicted C1 (fp32 allreduce_bine_bdw_remap, 262,144 elements per rank)
+    end to end at P ranks of one node, one GPU + one PCIe link each, over the
+    direct transport's one-launch flat form: {"e2e_us", "device_us",
+    "device_us_one_gpu_bound"}.  device = one launch + C1_PHASES flag round
+    trips + the busiest link's bytes; P = 1 is the measured host round trip
+    alone (the collective is the copy sbuf -> rbuf)."""
+    if P == 1:
+        return {"e2e_us": t_host_rt_us, "device_us": 0.0, "device_us_one_gpu_bound": None}
+    lb = link_bytes("allreduce", "bine_bdw_remap", P, transport="flatrs+flat+dmt", count=262_144,
+                    chunk_bytes=64 << 20)
+    dev = t_boundary_us + C1_PHASES * t_flag_us + lb / (link_gbs * 1e3)
+    return {"e2e_us": round(t_host_rt_us + dev, 2), "device_us": round(dev, 2),
+            "device_us_one_gpu_bound": C1_ONE_GPU_DEV_US.get(P)}

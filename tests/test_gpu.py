@@ -25,7 +25,7 @@ import pico_amd  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALL_DT = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64", "float", "double"]
-STATUS_OF_MPI = {12: 1, 51: 2, 7: 8}   # MPI_ERR_ARG / _SIZE / _ROOT -> BINE_ERR_ARG / _SIZE / _ROOT
+STATUS_OF_MPI = {12: 1, 51: 2, 7: 8, 2: 9}   # MPI_ERR_ARG / _SIZE / _ROOT / _COUNT -> BINE_ERR_*
 
 
 @pytest.fixture(scope="module")
@@ -179,11 +179,26 @@ def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, ro
     return outs, st
 
 
+def oracle_bcast(algo, sb, dt, root):
+    """(outputs, rets) the device path must give for a bcast: the oracle's
+    replay; where the reference crashes, the root's buffer everywhere
+    (scatter_allgather's wrapped counts) or MPI_ERR_ARG (bine_bdw_remap off
+    root 0 / a power-of-two P, where it asserts) -- DESIGN.md deviations"""
+    if algo not in O.BC_BDW:
+        return O.bcast(algo, sb, dt, root)
+    out, rets = O.bcast_bdw(algo, sb, dt, root)
+    if rets and rets[0] == "crash":
+        if algo == "bine_bdw_remap":
+            return [np.array(b).copy() for b in sb], [O.ERR_ARG] * len(sb)
+        return [np.array(sb[root]).copy() for _ in sb], [0] * len(sb)
+    return out, rets
+
+
 def oracle_outputs(coll, algo, sb, dt, op, rk, segsize, root=0):
     """the oracle's per-rank outputs of one collective (intended semantics:
     the reference's bugs are not reproduced)"""
     if coll == "bcast":
-        return O.bcast(algo, sb, dt, root)[0]
+        return oracle_bcast(algo, sb, dt, root)[0]
     if coll == "allgather":
         return O.allgather(algo, sb, dt)[0]
     if coll == "reduce_scatter":

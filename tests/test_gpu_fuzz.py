@@ -14,7 +14,7 @@ import pytest
 
 import pico_amd  # noqa: E402  (after torch, via test_gpu)
 from oracle import oracle as O
-from test_gpu import STATUS_OF_MPI, comms, run_loopback, sha
+from test_gpu import STATUS_OF_MPI, comms, oracle_bcast, run_loopback, sha
 
 pytestmark = pytest.mark.gpu
 
@@ -70,7 +70,7 @@ def _run(coll, algo, P, dt, op, n, o):
     sb = [mk(r) for r in range(P)]
     if coll == "bcast":   # pure data movement, in place; any root (the root-0-only trees: ERR_ROOT elsewhere)
         root = rng_root(P, n)
-        want, rets = O.bcast(algo, sb, dt, root)
+        want, rets = oracle_bcast(algo, sb, dt, root)
         for c in comms(P):
             c.set_flat_ag(o["flat_ag"])
         outs, st = run_loopback(coll, algo, sb, dt, root=root, relay=o["relay"])
@@ -137,9 +137,11 @@ def test_random_configurations_bit_exact(dev_fuzz, seed):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_random_bcast_bit_exact(dev_fuzz, seed):
-    """bcast latency trees: random P (non-powers of two: MPI_ERR_SIZE), root
-    (root-0-only trees: MPI_ERR_ROOT elsewhere), type, count, relay, vs the
-    oracle's message-level replay (tests/test_oracle.py pins it)"""
+    """bcast, latency trees and (round 5) the bandwidth algorithms: random P
+    (non-powers of two: MPI_ERR_SIZE where the reference says so), root
+    (root-0-only trees: MPI_ERR_ROOT elsewhere), type, count (below P:
+    MPI_ERR_COUNT for the bandwidth ones), relay, vs the oracle's
+    message-level replay (tests/test_oracle.py pins it)"""
     rng = random.Random(5000 + seed)
     bad = []
     try:

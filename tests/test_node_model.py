@@ -96,3 +96,23 @@ def test_bench_maps_trial_names_to_the_model():
     assert "error" not in a and a["model_ms"] == b["model_ms"]
     c = bench.node_model("C4", 8, "flatrs+flat+dm16", 64 << 20)
     assert "error" not in c and c["hbm_bytes"] == M.config_model("C4", 8, "flatrs+flat+dm", 64 << 20)["hbm_bytes"]
+
+
+def test_c1_end_to_end_model():
+    """C1 through the unchanged pico_core at P ranks with one
+    GPU and one PCIe link each = the measured 1 MiB host round trip (P = 1,
+    66 us) + one k_dm_fused launch + 3 flag round trips + the busiest link's
+    bytes.  Below the reference's own CPU libbine at P = 4 (215 us on the GPU
+    box's cores) even with the device part at its one-GPU measured bound
+    (49 us, ranks sharing one GPU); the one-GPU end-to-end runs (292-417 us at
+    P = 4) put all four ranks' copies on one PCIe link, which a node does not"""
+    assert M.c1_e2e_us(1)["e2e_us"] == M.T_HOST_RT_US
+    for P in (2, 4, 8):
+        m = M.c1_e2e_us(P)
+        lb = M.link_bytes("allreduce", "bine_bdw_remap", P, transport="flatrs+flat+dmt", count=262_144,
+                          chunk_bytes=64 << 20)
+        assert lb == 2 * (262_144 * 4) // P   # the flat phases: S / P on the busiest link, twice
+        assert m["device_us"] == pytest.approx(M.T_BOUNDARY_US + 3 * M.T_FLAG_US + lb / (M.LINK_GBS * 1e3), abs=0.01)
+        assert m["e2e_us"] < M.C1_REFERENCE_CPU_US[4]
+    hi = M.T_HOST_RT_US + M.C1_ONE_GPU_DEV_US[4]
+    assert hi < M.C1_REFERENCE_CPU_US[4]

@@ -35,7 +35,8 @@ def _run(c, ref_bugs=True):
         sb = G.inputs(c)
         return O.allgather(c["algo"], sb, dt)
     if c["coll"] == "bcast":
-        return O.bcast(c["algo"], G.inputs(c), dt, G.root(c))
+        f = O.bcast_bdw if c["algo"] in O.BC_BDW else O.bcast
+        return f(c["algo"], G.inputs(c), dt, G.root(c))
     sb = G.inputs(c)
     o, rets = O.reduce(c["algo"], sb, dt, c["op"])
     return [o] + [np.zeros(0)] * (P - 1), rets
@@ -196,3 +197,17 @@ def test_permute_remap_unequal_blocks_is_err_arg():
         sb = O.inputs("float", sum(rc), P)
         _, rets = O.reduce_scatter("bine_permute_remap", sb, rc, "float")
         assert rets == [O.ERR_ARG] * P
+
+
+def test_bcast_bdw_replay_predicts_the_reference_crashes():
+    """the bandwidth bcasts' replay (oracle.bcast_bdw) says "crash" exactly
+    where the reference produced no output -- scatter_allgather's wrapped
+    size_t counts (libbine_bcast.c:72, :97) -- and nowhere else"""
+    n = 0
+    for c in G.cases():
+        if c["coll"] != "bcast" or c["algo"] not in O.BC_BDW:
+            continue
+        _, rets = O.bcast_bdw(c["algo"], G.inputs(c), c["dtype"], G.root(c))
+        assert (rets[0] == "crash") == (c["status"] != "ok"), c["id"]
+        n += c["status"] != "ok"
+    assert n >= 100

@@ -134,6 +134,30 @@ def bcast_jobs():
     return jobs
 
 
+BC_BDW = ("scatter_allgather", "bine_bdw_static", "bine_bdw_remap")
+
+
+def bcast_bdw_jobs():
+    """the bandwidth bcasts (libbine_bcast.c:42, :462, :649 -- widening past
+    SURVEY.md 8(f)): scatter + allgather, in place on each rank's own input;
+    counts below P (MPI_ERR_COUNT), at and around P and multiples of it,
+    larger ones; scatter_allgather at every root, bine_bdw_static also at a
+    root != 0 (MPI_ERR_ROOT) and non-power-of-two P (MPI_ERR_SIZE),
+    bine_bdw_remap root 0 only (it asserts, :650)"""
+    jobs = []
+    for P in (1, 2, 3, 4, 5, 6, 8, 16):
+        ns = sorted({1, 3, P, P + 1, 2 * P, 2 * P + 1, 3 * P - 1, 13, 64, 333, 4099})
+        for a in BC_BDW:
+            if a == "bine_bdw_remap" and P & (P - 1):
+                continue   # non-power-of-two P: the reference's remap_rank is undefined there
+            roots = ["even"]
+            if a != "bine_bdw_remap":
+                roots += [f"root{r}" for r in sorted({r for r in (1, P - 1, P // 2) if 0 < r < P})]
+            for rk in roots:
+                jobs.append((P, "bcast", a, "sum", 0, rk, ["float", "int64", "int8"], ns, True))
+    return jobs
+
+
 def ops_jobs():
     """MPICH's logical and bitwise MPI_Ops through the reference's collectives
     (logical ops on sparsified inputs -- zeros, -0.0, NaN -- so that both truth
@@ -266,6 +290,11 @@ def main():
             keep = {c["id"] for c in index}
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(ops_jobs(), index, arrays)
+        if only == "bcast_bdw":
+            index = [c for c in old if not (c["coll"] == "bcast" and c["algo"] in BC_BDW)]
+            keep = {c["id"] for c in index}
+            arrays = {k: v for k, v in prev.items() if k in keep}
+            return capture(bcast_bdw_jobs(), index, arrays)
         index = [c for c in old if c["coll"] != only]
         arrays = {k: v for k, v in prev.items() if not k.startswith(only + ".")}
         jobs = {"allgather": allgather_jobs, "bcast": bcast_jobs}[only]()
@@ -312,6 +341,7 @@ def main():
     jobs += p16_jobs()
     jobs += inplace_jobs()
     jobs += bcast_jobs()
+    jobs += bcast_bdw_jobs()
     capture(jobs, [], {})
 
 
