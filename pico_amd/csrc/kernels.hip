@@ -1597,7 +1597,13 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   // previous use acknowledged first)
   if (!wait_all(a, 0, a.na, false)) return;
   const uint64_t t1 = a.stamps ? wall_clock64() : 0;
-  for (int i = 0; i < a.na; i++) copy_slice(resolve(a, a.m[i]), a.wgs, true);
+  // workgroup w starts at message w mod na and rotates: at any moment the
+  // workgroups spread over every peer's link instead of all pushing to the
+  // same peer first (on a node each peer is its own xGMI link)
+  for (int k = 0; k < a.na; k++) {
+    const int i = (int)((blockIdx.x + (unsigned)k) % (unsigned)a.na);
+    copy_slice(resolve(a, a.m[i]), a.wgs, true);
+  }
   arrive_all(a, 0, a.na);
   // phases B_c: the peers' blocks of chunk c, read in place in our inbox as
   // the tree's leaves; each result vector goes to `out` and, for the flat
@@ -1629,7 +1635,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   }
   // phase D: the peers' results out of our inbox
   if (!wait_all(a, a.d0, a.nd, true)) return;
-  for (int i = 0; i < a.nd; i++) copy_slice(resolve(a, a.m[a.d0 + i]), a.wgs, false);
+  for (int k = 0; k < a.nd; k++) {  // rotated as phase A (the slots lie in different HBM channels anyway)
+    const int i = (int)((blockIdx.x + (unsigned)k) % (unsigned)a.nd);
+    copy_slice(resolve(a, a.m[a.d0 + i]), a.wgs, false);
+  }
   arrive_all(a, a.d0, a.nd);
   if (threadIdx.x == 0 && a.stamps) dm_stamp(a.stamps, a.serial, 4, 255, blockIdx.x, t0, t1, wall_clock64());
   // the launch's last workgroup advances the sequence bases (every workgroup
