@@ -596,6 +596,12 @@ int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int 
  * -status. */
 int bine_plan_dm_fused(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
                        int in_place, size_t chunk_bytes, int mode, size_t slot, int dtype, int op, int small);
+/* The same, with the launches' messages in the order their sequence numbers
+ * are taken: 4 words each (launch, push, peer, bytes) into out (up to cap
+ * messages; *nmsgs = how many there are).  Returns the launches or -status. */
+int64_t bine_plan_dm_fused_msgs(int algo, int nranks, int rank, size_t count, const int *rcounts, int root,
+                                size_t esz, int in_place, size_t chunk_bytes, int mode, size_t slot, int dtype, int op,
+                                int small, uint64_t *out, int64_t cap, int64_t *nmsgs);
 
 /* The direct transport's residency cut (host only): every launch's
  * workgroups -- `cw[0..n)` per copied message, *tw for a fused tree (NULL:

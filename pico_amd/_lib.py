@@ -165,6 +165,8 @@ def lib():
                                 ctypes.POINTER(ctypes.c_int64), vp], ctypes.c_int64),
         "bine_plan_stage": ([i, i, i, sz, vp, i, sz, sz, i, sz, i, i, vp, ctypes.c_int64], ctypes.c_int64),
         "bine_plan_dm_fused": ([i, i, i, sz, vp, i, sz, i, sz, i, sz, i, i, i], i),
+        "bine_plan_dm_fused_msgs": ([i, i, i, sz, vp, i, sz, i, sz, i, sz, i, i, i, vp, ctypes.c_int64,
+                                     ctypes.POINTER(ctypes.c_int64)], ctypes.c_int64),
         "bine_plan_dm_trees": ([i, i, i, sz, vp, i, sz, i, sz, i, sz, i, i, i, vp, vp, ctypes.c_int64],
                                ctypes.c_int64),
         "bine_allreduce_staged": ([vp, i, vp, vp, vp, vp, sz, i, i, sz, sz, vp, vp, vp], i),

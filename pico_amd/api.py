@@ -452,6 +452,25 @@ def dm_fused_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcoun
     return int(n)
 
 
+def dm_fused_msgs(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, esz: int = 4,
+                  in_place: bool = False, chunk_bytes: int = 0, flat_ag=False, flat_rs: bool = False,
+                  slot: int = 64 << 20, dtype="float", op: str = "sum", small: bool = False):
+    """(launches, [(launch, push, peer, bytes), ...]) of the one-launch form
+    (bine_plan_dm_fused_msgs): the messages in sequence-number order"""
+    a = _algo(coll, algo)
+    rc = (ctypes.c_int * nranks)(*(rcounts or [0] * nranks))
+    mode = (2 if flat_ag else 0) | (4 if flat_rs else 0) | (8 if flat_ag == 2 else 0)
+    args = (a, nranks, rank, count, rc, 0, esz, int(in_place), chunk_bytes, mode, slot, _dtype(dtype), OPS[op],
+            int(small))
+    n = ctypes.c_int64(0)
+    nl = lib().bine_plan_dm_fused_msgs(*args, None, 0, ctypes.byref(n))
+    if nl < 0:
+        raise BineError(int(-nl), f"dm_fused_msgs {coll}_{algo}")
+    buf = (ctypes.c_uint64 * max(4 * n.value, 4))()
+    lib().bine_plan_dm_fused_msgs(*args, buf, n.value, ctypes.byref(n))
+    return int(nl), [tuple(int(x) for x in buf[4 * k:4 * k + 4]) for k in range(n.value)]
+
+
 def stage_plan(coll: str, algo, nranks: int, rank: int, count: int = 0, rcounts=None, esz: int = 4,
                segsize: int = 0, in_place: bool = False, chunk_bytes: int = 0, flat_ag=False, flat_rs: bool = False):
     """The host staging of rank `rank`'s schedule (bine_plan_stage; host only):
@@ -599,7 +618,7 @@ for _n in ALGOS["bcast"]:
     ENTRY_POINTS["bcast_" + _n] = _mk_bc(_n)
 globals().update(ENTRY_POINTS)
 
-__all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "dm_fused_plan", "reduce_local", "reduce3", "fill_pico", "checksum", "copy",
+__all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "dm_fused_plan", "dm_fused_msgs", "reduce_local", "reduce3", "fill_pico", "checksum", "copy",
            "rccl_version",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "bcast", "loopback_bcast", "reduce_batch",

@@ -2365,6 +2365,13 @@ int64_t bine_plan_dm_trees(int algo, int nranks, int rank, size_t count, const i
 
 int bine_plan_dm_fused(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,
                        int in_place, size_t chunk_bytes, int mode, size_t slot, int dtype, int op, int small) {
+  return (int)bine_plan_dm_fused_msgs(algo, nranks, rank, count, rcounts, root, esz, in_place, chunk_bytes, mode,
+                                      slot, dtype, op, small, nullptr, 0, nullptr);
+}
+
+int64_t bine_plan_dm_fused_msgs(int algo, int nranks, int rank, size_t count, const int *rcounts, int root,
+                                size_t esz, int in_place, size_t chunk_bytes, int mode, size_t slot, int dtype, int op,
+                                int small, uint64_t *out, int64_t cap, int64_t *nmsgs) {
   if (!esz || !slot) return -BINE_ERR_ARG;
   PlanArgs a = plan_args(algo, nranks, rank, count, rcounts, root, esz, 0, in_place);
   a.flat_ag = (mode & 2) != 0;
@@ -2384,7 +2391,21 @@ int bine_plan_dm_fused(int algo, int nranks, int rank, size_t count, const int *
   e.own = (uint8_t *)((uintptr_t)15 << 40);  // stand-ins: 4 KiB-aligned, disjoint per buffer
   auto ptr = [&](int buf, uint64_t off) { return (char *)((uintptr_t)(buf + 1) << 40) + off * esz; };
   std::vector<DmFusedArgs> v;
-  return plan_fused_env(e, sc, ptr, esz, dtype, op, small != 0, v) ? (int)v.size() : 0;
+  if (!plan_fused_env(e, sc, ptr, esz, dtype, op, small != 0, v)) v.clear();
+  // the launches' messages in the order their sequence numbers are taken
+  // (per peer and direction: j order = this order): launch, push, peer, bytes
+  int64_t n = 0;
+  for (size_t l = 0; l < v.size(); l++)
+    for (int i = 0; i < v[l].d0 + v[l].nd; i++, n++)
+      if (out && n < cap) {
+        uint64_t *o = out + 4 * n;
+        o[0] = l;
+        o[1] = (uint64_t)v[l].m[i].push;
+        o[2] = (uint64_t)v[l].m[i].peer;
+        o[3] = v[l].m[i].bytes;
+      }
+  if (nmsgs) *nmsgs = n;
+  return (int64_t)v.size();
 }
 
 int64_t bine_plan_stage(int algo, int nranks, int rank, size_t count, const int *rcounts, int root, size_t esz,

@@ -216,3 +216,80 @@ def test_fit_residency_library_matches_restatement():
             assert sum(pc) + (pt[0] if pt else 0) <= cap and min(pc + [1]) >= 1
         if rc == 0:
             assert pc == cw
+
+
+# ---- the one-launch form moves the per-exchange form's messages (round 5) ----------
+
+def _per_exchange_msgs(ops, esz, slot, rank_peer_kind):
+    """the per-exchange launches' messages of one rank in sequence order, per
+    (peer, push): each exchange's message to / from a peer cut into slot-sized
+    rounds (DirectState::exchange), exchanges in issue order (a deferred
+    tree's leaf pulls keep their place relative to the same peer's later
+    receives)"""
+    out = {}
+    for o in ops:
+        if not o["xchg"]:
+            continue
+        for p in o["prims"]:
+            if p["type"] not in ("SEND", "RECV") or not p["count"]:
+                continue
+            b = p["count"] * esz
+            key = (p["peer"], 1 if p["type"] == "SEND" else 0)
+            k = 0
+            while k * slot < b:
+                out.setdefault(key, []).append(min(slot, b - k * slot))
+                k += 1
+    return out
+
+
+FUSED_CASES = [
+    # (coll, algo, P, count or block, esz, chunk, slot, ragged)
+    ("allreduce", "bine_bdw_remap", 2, 67_108_864, 4, 64 << 20, 64 << 20, False),
+    ("allreduce", "bine_bdw_remap", 4, 67_108_864, 4, 64 << 20, 64 << 20, False),
+    ("allreduce", "bine_bdw_remap", 8, 67_108_864, 4, 64 << 20, 64 << 20, False),
+    ("allreduce", "bine_bdw_remap", 8, 33_554_432, 8, 64 << 20, 64 << 20, False),
+    ("allreduce", "bine_bdw_remap", 2, 2 * (262_144 + 64), 4, 1 << 20, 1 << 20, False),      # a short last chunk
+    ("allreduce", "bine_bdw_remap", 4, 4 * (262_144 + 4), 4, 1 << 20, 1 << 20, False),
+    ("allreduce", "bine_bdw_static", 8, 8 * 262_144 * 2, 4, 1 << 20, 1 << 20, False),
+    ("allreduce", "rabenseifner", 4, 4 * (131_072 + 2), 8, 1 << 20, 1 << 20, False),
+    ("reduce_scatter", "bine_permute_remap", 2, 6 * 262_144, 4, 1 << 20, 1 << 20, False),
+    ("reduce_scatter", "bine_permute_remap", 8, 268_435_456 // 8, 4, 64 << 20, 64 << 20, False),
+    ("reduce_scatter", "bine_send_remap", 4, 3 * 262_144, 4, 1 << 20, 1 << 20, True),
+]
+
+
+@pytest.mark.parametrize("case", FUSED_CASES, ids=lambda c: f"{c[0]}-{c[1]}-P{c[2]}-n{c[3]}")
+def test_one_launch_form_moves_the_per_exchange_messages(case):
+    """bine_plan_dm_fused_msgs vs the per-exchange form: for every rank and
+    peer the one-launch program pushes (and pulls) the same message sizes in
+    the same order as the per-exchange launches, and rank x's pushes to y are
+    rank y's pulls from x -- so every pair of ranks agrees on every sequence
+    number whichever form each rank takes (executor.cpp plan_fused)"""
+    import pico_amd
+    coll, algo, P, n, esz, chunk, slot, ragged = case
+    dt = {4: "float", 8: "double"}[esz]
+    kw = dict(esz=esz, chunk_bytes=chunk, flat_ag=coll == "allreduce", flat_rs=True)
+    if coll == "allreduce":
+        kw["count"] = n
+    else:
+        kw["rcounts"] = [n + (4 * (r % 3) if ragged else 0) for r in range(P)]   # ragged, 16-B blocks
+    seqs, n_fused = {}, 0
+    for r in range(P):
+        nl, msgs = pico_amd.dm_fused_msgs(coll, algo, P, r, slot=slot, dtype=dt, **kw)
+        ops = pico_amd.schedule(coll, algo, P, r, **kw)[0]
+        per = _per_exchange_msgs(ops, esz, slot, None)
+        seqs[r] = per
+        if nl == 0:
+            continue   # this rank keeps the per-exchange launches (e.g. ragged: a send-only last exchange)
+        n_fused += 1
+        got = {}
+        for _, push, peer, b in msgs:
+            got.setdefault((peer, push), []).append(b)
+        assert got == per, (case, r)
+        seqs[r] = got
+    assert n_fused >= 1, case
+    # every ordered pair agrees, whichever form each end takes
+    for x in range(P):
+        for y in range(P):
+            if x != y:
+                assert seqs[x].get((y, 1), []) == seqs[y].get((x, 0), []), (case, x, y)
