@@ -384,6 +384,12 @@ int bine_comm_set_direct_tree(bine_comm_t comm, int on);
  * cap), and with reset != 0 starts over.  BINE_ERR_UNSUPPORTED when stamps are
  * off. */
 int bine_comm_direct_stamps(bine_comm_t comm, uint64_t *out, size_t cap, size_t *n, int reset);
+/* 1 when a wait of this rank's direct transport timed out (the transport is
+ * disabled until the next collective bine_comm_set_direct(1) rebuilds it;
+ * a call in flight at that moment completed without its data), 0 otherwise
+ * or without a direct transport; -status on error.  Host-only read of the
+ * mapped poison word: call it after synchronizing. */
+int bine_comm_direct_timed_out(bine_comm_t comm);
 
 /* Graph mode (RCCL communicators): the first collective call for a given
  * (algorithm, arguments, buffers, dtype, op, stream) captures the whole issue

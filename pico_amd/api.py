@@ -197,6 +197,13 @@ class Comm:
         alike; bit-identical"""
         check(lib().bine_comm_set_direct_tree(self.handle, int(on)), "bine_comm_set_direct_tree")
 
+    def direct_timed_out(self) -> bool:
+        """a wait of this rank's direct transport timed out (bine_comm_direct_timed_out)"""
+        n = lib().bine_comm_direct_timed_out(self.handle)
+        if n < 0:
+            check(int(-n), "bine_comm_direct_timed_out")
+        return bool(n)
+
     def direct_stamps(self, reset: bool = True):
         """Direct-transport diagnostics (BINE_DIRECT_STAMPS=<records> at setup;
         bine_comm_direct_stamps): numpy uint64 array (n, 4) of per-workgroup

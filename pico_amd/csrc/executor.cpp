@@ -2543,6 +2543,12 @@ int bine_comm_set_direct(bine_comm_t c, int on) {
   return BINE_SUCCESS;
 }
 
+int bine_comm_direct_timed_out(bine_comm_t c) {
+  if (!c) return -BINE_ERR_ARG;
+  auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
+  return r && r->dm && r->dm->poisoned() ? 1 : 0;
+}
+
 int bine_comm_direct_stamps(bine_comm_t c, uint64_t *out, size_t cap, size_t *n, int reset) {
   if (!c || !n || (cap && !out)) return BINE_ERR_ARG;
   auto *r = dynamic_cast<RcclTransport *>(c->tx.get());

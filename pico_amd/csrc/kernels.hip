@@ -1660,12 +1660,14 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
 
 // CUs of the current device (0: unknown), queried once per device
 static int dm_cus() {
+  static std::mutex mu;
   static int cus[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
     (void)hipGetLastError();
     return 0;
   }
+  std::lock_guard<std::mutex> g(mu);
   if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     (void)hipGetLastError();
     cus[dev] = 0;

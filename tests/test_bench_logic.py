@@ -27,6 +27,14 @@ def test_pick_headline():
     assert bench.pick_headline(base, (fast, False), best, (slow, False, 2))[0] == base
 
 
+def test_runner_up_after_a_failed_pick():
+    inf = float("inf")
+    base, a, b, c = ("direct", 16, False), ("x+dmt", 32, False), ("x+dm", 32, False), ("x+dmt256", 32, False)
+    trials = {base: 300.0, a: 2.1, b: 19.0, c: inf}
+    assert bench.runner_up(trials, a, base) == b
+    assert bench.runner_up({base: 300.0, a: 2.1, c: inf}, a, base) is None
+
+
 def test_dm_wgs_mode_suffix():
     assert bench.dm_wgs("flatrs+flat") is None and bench.dm_wgs("trees") is None
     assert bench.dm_wgs("flatrs+flat+dm") == 0 and bench.dm_wgs("direct+dm") == 0
