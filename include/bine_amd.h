@@ -114,15 +114,21 @@ typedef enum {
   BINE_AG_BINE_2_BLOCKS = 58,         /* :892  */
   BINE_AG_BINE_2_BLOCKS_DTYPE = 59,   /* :999  */
   /* bcast, libbine_bcast.c (widening past section 8):
-   * the latency trees; the scatter-allgather and bandwidth variants are not
-   * provided yet (BINE_ERR_UNSUPPORTED) */
+   * the latency trees and the scatter + allgather bandwidth variants */
   BINE_BC_SCATTER_ALLGATHER = 64,     /* :42   */
   BINE_BC_BINE_LAT = 65,              /* :189  */
   BINE_BC_BINE_LAT_REVERSED = 66,     /* :281  */
   BINE_BC_BINE_LAT_NEW = 67,          /* :373  */
   BINE_BC_BINE_LAT_I_NEW = 68,        /* :408  */
   BINE_BC_BINE_BDW_STATIC = 69,       /* :462  */
-  BINE_BC_BINE_BDW_REMAP = 70         /* :649  */
+  BINE_BC_BINE_BDW_REMAP = 70,        /* :649  */
+  /* alltoall / gather / scatter: whole-block data
+   * movement; the plan refuses (BINE_ERR_ROOT at a power-of-two P, else
+   * BINE_ERR_SIZE) the (P, root) pairs at which the reference hangs, crashes
+   * or delivers a wrong result, and MPI_IN_PLACE (BINE_ERR_ARG) */
+  BINE_A2A_BINE = 80,                 /* alltoall_bine libbine_alltoall.c:14 */
+  BINE_GA_BINE = 81,                  /* gather_bine   libbine_gather.c:16   */
+  BINE_SC_BINE = 82                   /* scatter_bine  libbine_scatter.c:14  */
 } bine_algo_t;
 
 /* the reference's MPI_IN_PLACE (mpi.h: (void *)-1) */
@@ -469,6 +475,20 @@ int bine_allgather(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, siz
  * only (BINE_ERR_SIZE otherwise); bine_lat / bine_lat_reversed take root 0
  * only (BINE_ERR_ROOT), as the reference. */
 int bine_bcast(bine_comm_t comm, int algo, void *buf, size_t count, int dtype, int root, void *stream);
+/* gather_bine / scatter_bine / alltoall_bine (libbine.h:52, :63, :78; sendcount
+ * = recvcount = `count` elements per block, one type).  gather: sbuf `count`
+ * elements on every rank, rbuf P * count on the root (unused elsewhere, may be
+ * NULL); scatter: sbuf P * count on the root (unused elsewhere, may be NULL),
+ * rbuf `count`; alltoall: sbuf and rbuf P * count, block j of sbuf goes to
+ * rank j.  Pure data movement.  The literal schedules of the reference, or
+ * with bine_comm_set_flat_ag(1) one direct exchange (every block straight to
+ * its destination); refused (BINE_ERR_ROOT / BINE_ERR_SIZE) where the
+ * reference does not deliver the collective, BINE_ERR_ARG for MPI_IN_PLACE. */
+int bine_gather(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int root,
+                void *stream);
+int bine_scatter(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int root,
+                 void *stream);
+int bine_alltoall(bine_comm_t comm, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, void *stream);
 
 /* One group of point-to-point transfers on the communicator's transport (RCCL:
  * ncclSend / ncclRecv inside one ncclGroupStart/End) -- the MPI_Sendrecv /
@@ -506,6 +526,12 @@ int bine_loopback_run_allgather(bine_comm_t *comms, int nranks, int algo,
                                 int dtype, int *statuses);
 int bine_loopback_run_bcast(bine_comm_t *comms, int nranks, int algo, void *const *bufs,
                             size_t count, int dtype, int root, int *statuses);
+int bine_loopback_run_gather(bine_comm_t *comms, int nranks, int algo, const void *const *sbufs,
+                             void *const *rbufs, size_t count, int dtype, int root, int *statuses);
+int bine_loopback_run_scatter(bine_comm_t *comms, int nranks, int algo, const void *const *sbufs,
+                              void *const *rbufs, size_t count, int dtype, int root, int *statuses);
+int bine_loopback_run_alltoall(bine_comm_t *comms, int nranks, int algo, const void *const *sbufs,
+                               void *const *rbufs, size_t count, int dtype, int *statuses);
 
 /* ---- schedule introspection (host only, no GPU needed) ----------------------
  * A plan is the ordered list of primitives one rank executes. */

@@ -10,9 +10,10 @@
  *   allreduce_*                    :30-37     GPU path (bine_allreduce, RCCL + HIP kernels)
  *   reduce_bine_lat / _bdw         :64-65     GPU path (bine_reduce)
  *   reduce_scatter_*               :69-77     GPU path (bine_reduce_scatter)
- *   allgather_*, alltoall_bine, bcast_*,      exported so that pico_core links; return
- *   gather_bine, scatter_bine      :39-67     MPI_ERR_UNSUPPORTED_OPERATION (not on the
- *                                             reduce-family hot path)
+ *   allgather_*                    :39-50     GPU path (bine_allgather)
+ *   bcast_*                        :54-60     GPU path (bine_bcast)
+ *   alltoall_bine, gather_bine,    :52,63,78  GPU path (bine_alltoall / _gather /
+ *   scatter_bine                              _scatter); data movement, run on bytes
  *
  * Buffers may be host or device memory (hipPointerGetAttributes decides):
  * device buffers are used in place; host buffers (pico_core's default
@@ -71,7 +72,7 @@ int reduce_scatter_bine_permute_remap(BINE_REDUCE_SCATTER_ARGS);
 int reduce_scatter_bine_block_by_block(BINE_REDUCE_SCATTER_ARGS);
 int reduce_scatter_bine_block_by_block_any_even(BINE_REDUCE_SCATTER_ARGS);
 
-/* outside the reduce family: exported for link compatibility only */
+/* data movement: allgather, alltoall, bcast, gather, scatter */
 int allgather_k_bruck(BINE_ALLGATHER_ARGS);
 int allgather_recursivedoubling(BINE_ALLGATHER_ARGS);
 int allgather_ring(BINE_ALLGATHER_ARGS);

@@ -16,7 +16,9 @@
  * with PMPI_Allreduce / PMPI_Reduce_scatter / PMPI_Reduce.  And the pairs
  * MPICH rejects come back as MPI_ERR_OP.  Then the bcast latency trees
  * (bine_lat, _reversed at root 0; _new, _i_new at every root) vs PMPI_Bcast,
- * and four allgathers vs PMPI_Allgather, every type (P a power of two).
+ * four allgathers vs PMPI_Allgather, and gather_bine / scatter_bine /
+ * alltoall_bine vs PMPI_Gather / _Scatter / _Alltoall, every type (P a power
+ * of two).
  *   usage: mpiexec -n P op_check      (prints "OPCHECK ok <cases>" on rank 0)
  * P a power of two: the remap / block-by-block reduce-scatters report
  * MPI_ERR_ARG elsewhere (the reference hangs there; DESIGN.md deviations).
@@ -200,6 +202,43 @@ int main(int argc, char **argv) {
         }
         free(s); free(r); free(w);
       }
+  /* gather_bine / scatter_bine / alltoall_bine (whole blocks, every type) vs
+   * PMPI_Gather / PMPI_Scatter / PMPI_Alltoall, at root 0 and P / 2 (even, or
+   * P = 2: roots the reference serves); the root-only buffers NULL elsewhere,
+   * as pico_core passes them (pico_core_gather_utils.c, _scatter_utils.c) */
+  for (int which = 0; which < 3; which++)
+    for (size_t ti = 0; ti < sizeof types / sizeof *types; ti++)
+      for (size_t ci = 0; ci < sizeof counts / sizeof *counts; ci++)
+        for (int ri = 0; ri < (which == 2 || P == 1 ? 1 : 2); ri++) {
+          const type_t *t = &types[ti];
+          const size_t n = counts[ci], all = n * (size_t)P;
+          const int root = ri ? P / 2 : 0;
+          const size_t sn = which == 0 ? n : all, rn = which == 1 ? n : all;
+          char *s = malloc(sn * t->esz), *r = calloc(rn, t->esz), *w = calloc(rn, t->esz);
+          fill(s, t, sn, 777u + 29u * (unsigned)rank + (unsigned)(which * 11 + ti * 3 + ci));
+          int e, ew;
+          size_t on = rn;
+          if (which == 0) {
+            e = gather_bine(s, n, t->dt, rank == root ? r : NULL, n, t->dt, root, MPI_COMM_WORLD);
+            ew = PMPI_Gather(s, (int)n, t->dt, rank == root ? w : NULL, (int)n, t->dt, root, MPI_COMM_WORLD);
+            if (rank != root) on = 0;
+          } else if (which == 1) {
+            e = scatter_bine(rank == root ? s : NULL, n, t->dt, r, n, t->dt, root, MPI_COMM_WORLD);
+            ew = PMPI_Scatter(rank == root ? s : NULL, (int)n, t->dt, w, (int)n, t->dt, root, MPI_COMM_WORLD);
+          } else {
+            e = alltoall_bine(s, n, t->dt, r, n, t->dt, MPI_COMM_WORLD);
+            ew = PMPI_Alltoall(s, (int)n, t->dt, w, (int)n, t->dt, MPI_COMM_WORLD);
+          }
+          cases++;
+          if (e != MPI_SUCCESS || ew != MPI_SUCCESS || (on && !same(r, w, t, on))) {
+            bad++;
+            if (bad <= 40)
+              fprintf(stderr, "rank %d MISMATCH %s %s n=%zu root=%d rc=%d (mpich rc %d)\n", rank,
+                      which == 0 ? "gather_bine" : which == 1 ? "scatter_bine" : "alltoall_bine", t->name, n, root,
+                      e, ew);
+          }
+          free(s); free(r); free(w);
+        }
   int tot = 0;
   MPI_Allreduce(&bad, &tot, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
   if (rank == 0) printf(tot ? "OPCHECK FAILED %d of %d\n" : "OPCHECK ok %d cases\n", tot ? tot : cases, cases);

@@ -205,7 +205,7 @@ class _Stuck(Exception):
     pass
 
 
-def _replay(P, bufs, programs):
+def _replay(P, bufs, programs, leftover=None):
     """Run one generator per rank -- a line-by-line restatement of a reference
     function -- with MPI's point-to-point semantics: a send is buffered (its
     bytes are snapshotted when posted, as MPI_Send / MPI_Isend of an unmodified
@@ -213,7 +213,8 @@ def _replay(P, bufs, programs):
     (source, destination) pair, places it at its offset and reports its
     element count (MPI_Get_count); a message longer than the receive's count
     is MPI_ERR_TRUNCATE and ends the replay.  Yields: ("send", dst, off, n),
-    ("recv", src, off, maxn) -> n.  A rank's return value is its status.
+    ("recv", src, off, maxn) -> n on the rank's one buffer, or ("send", dst,
+    view) / ("recv", src, view) -> n naming the bytes of any buffer.  A rank's return value is its status.
     Raises _Stuck when no rank can move (the reference would hang)."""
     import collections
     q = collections.defaultdict(collections.deque)
@@ -235,6 +236,24 @@ def _replay(P, bufs, programs):
                     val[r] = None
                     moved = True
                 op = pending[r]
+                if len(op) == 3:
+                    # ("send", dst, view) / ("recv", src, view): a program over
+                    # several buffers names the bytes itself (_sl bounds-checks)
+                    if op[0] == "send":
+                        q[(r, op[1])].append(np.array(op[2]))
+                        pending[r] = None
+                        moved = True
+                        continue
+                    if not q[(op[1], r)]:
+                        break
+                    m = q[(op[1], r)].popleft()
+                    if m.size > op[2].size:
+                        raise ValueError("MPI_ERR_TRUNCATE")
+                    op[2][:m.size] = m
+                    val[r] = m.size
+                    pending[r] = None
+                    moved = True
+                    continue
                 if op[0] == "send":
                     _, dst, off, n = op
                     if off + n > bufs[r].size:
@@ -257,6 +276,8 @@ def _replay(P, bufs, programs):
                 moved = True
         if not moved:
             raise _Stuck()
+    if leftover is not None:   # messages sent and never received
+        leftover.extend(k for k, v in q.items() if v)
     return rets
 
 
@@ -471,6 +492,291 @@ def bcast_bdw(algo, sbufs, dtype, root=0):
     except (_Stuck, ValueError):
         return bufs, ["crash"] * P
     return bufs, rets
+
+
+# ---- gather / scatter / alltoall (libbine_gather.c, _scatter.c, _alltoall.c) ----
+_M32 = 0xFFFFFFFF
+
+
+def _b2nb(b):
+    """binary_to_negabinary (libbine_utils.h:509-513): int32 -> uint32"""
+    return _M32 if b > 0x55555555 else ((0xAAAAAAAA + b) & _M32) ^ 0xAAAAAAAA
+
+
+def _nb2b(n):
+    """negabinary_to_binary (libbine_utils.h:515-518): uint32 -> int32"""
+    v = ((0xAAAAAAAA ^ (n & _M32)) - 0xAAAAAAAA) & _M32
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+def _log2c(v):
+    """log_2 (libbine_utils.h:279-288): ceil(log2(v))"""
+    return (v - 1).bit_length() if v > 1 else 0
+
+
+def _nb_in_range(x, nbits):
+    """in_range (libbine_utils.h:524-526) over the smallest / largest
+    negabinary values of nbits digits (:47-50)"""
+    lo = -sum(1 << i for i in range(1, nbits, 2))
+    hi = sum(1 << i for i in range(0, nbits, 2))
+    return lo <= x <= hi
+
+
+def _remap_distance_doubling(num):
+    """remap_distance_doubling (libbine_utils.h:601-609)"""
+    num &= _M32
+    out = 0
+    while num > 0:
+        k = num.bit_length() - 1
+        out ^= 1 << k
+        num = (num ^ ((1 << (k + 1)) - 1)) & _M32
+    return out
+
+
+class _OOB(ValueError):
+    """the reference reads or writes past a buffer (undefined: it may crash or
+    run on with heap bytes)"""
+
+
+def _sl(buf, lo, hi):
+    """buf[lo:hi] in elements -- a view; a range past the buffer is the
+    reference reading / writing out of bounds (raised, not clipped)"""
+    if buf is None:
+        raise _Crash()
+    if lo < 0 or hi > buf.size or hi < lo:
+        raise _OOB()
+    return buf[lo:hi]
+
+
+def _uninit(n, dtype):
+    """a malloc'd temporary of the reference: zeros here; None (undefined) in a
+    symbolic run on object arrays (tests/rooted_util.defined)"""
+    return np.full(n, None, object) if dtype == object else np.zeros(n, dtype)
+
+
+class _Crash(Exception):
+    """the reference aborts (an assert) or dereferences NULL here"""
+
+
+def _gather_progs(P, n, root, sbufs, rbuf_root):
+    """gather_bine, libbine_gather.c:16-96: blocks gathered into a P-block
+    buffer (the root's rbuf, a temporary elsewhere), each rank extending its
+    resident run up or down at alternate steps (direction from the REAL rank's
+    parity, :33-36) and sending the whole run to its negabinary partner once
+    its low bits stop matching (:45-57)"""
+    def prog(rank):
+        def g():
+            rb = rbuf_root if rank == root else _uninit(P * n, sbufs[rank].dtype)
+            _sl(rb, rank * n, rank * n + n)[:] = sbufs[rank][:n]          # :28
+            lo = hi = rank
+            vrank = (rank - root) % P
+            ext = 1 if rank % 2 == 0 else -1
+            mask = 1
+            while mask < P:
+                nbv = _b2nb(vrank)
+                partner = (_nb2b(nbv ^ ((mask << 1) - 1)) + root) % P      # :39-40
+                mlsb = (mask << 2) - 1
+                lsbs = nbv & mlsb
+                equal = lsbs == 0 or lsbs == mlsb
+                if not equal or ((mask << 1) >= P and rank != root):       # :45-57
+                    if hi >= lo:
+                        yield ("send", partner, _sl(rb, lo * n, (hi + 1) * n))
+                    else:
+                        yield ("send", partner, _sl(rb, lo * n, P * n))
+                        yield ("send", partner, _sl(rb, 0, (hi + 1) * n))
+                    break
+                if ext == 1:                                                # :59-69
+                    rs, re = (hi + 1) % P, (hi + mask) % P
+                    hi = re
+                else:
+                    re, rs = (lo - 1) % P, (lo - mask) % P
+                    lo = rs
+                if re >= rs:                                                # :70-80
+                    yield ("recv", partner, _sl(rb, rs * n, (re + 1) * n))
+                else:
+                    yield ("recv", partner, _sl(rb, rs * n, P * n))
+                    yield ("recv", partner, _sl(rb, 0, (re + 1) * n))
+                ext = -ext
+                mask <<= 1
+            return OK
+        return g
+    return [prog(r) for r in range(P)]
+
+
+def _scatter_progs(P, n, root, sbuf_root, rbufs):
+    """scatter_bine, libbine_scatter.c:14-151: the gather's tree run backwards
+    -- resident block range [min, max] from the gather's end state
+    (:49-55), halved at every step; a non-root receives its subtree's blocks
+    once into a temporary (a leaf straight into rbuf, :110-126) and forwards
+    halves from there (relative block indices)"""
+    L = _log2c(P)
+
+    def prog(rank):
+        def g():
+            if P == 1:
+                raise _Crash()   # mask = 1 << (log_2(1) - 1): a negative shift (:57)
+            vrank = (rank - root) % P
+            hd = 1 if rank % 2 == 0 else -1
+            if L % 2 == 0:
+                hd = -hd
+            full = (1 << L) - 1
+            if rank % 2 == 0:                                               # :49-55
+                maxr = ((rank + 0x55555555) & full) % P
+                minr = ((rank - 0xAAAAAAAA) & full) % P
+            else:
+                minr = ((rank - 0x55555555) & full) % P
+                maxr = ((rank + 0xAAAAAAAA) & full) % P
+            mask = 1 << (L - 1)
+            off = rank
+            recvd, leaf, sb = False, False, None
+            if rank == root:
+                recvd, sb = True, sbuf_root
+            vnb = _b2nb(vrank)
+            while mask > 0:
+                partner = (_nb2b(vnb ^ ((mask << 1) - 1)) + root) % P      # :69-70
+                mlsb = (mask << 1) - 1
+                lsbs = vnb & mlsb
+                equal = lsbs == 0 or lsbs == mlsb
+                ts, te = minr, (minr + mask - 1) % P                         # :75-78
+                bs, be = (te + 1) % P, maxr
+                if hd == 1:
+                    ss, se, rs, re = bs, be, ts, te
+                    maxr = (maxr - mask) % P
+                else:
+                    ss, se, rs, re = ts, te, bs, be
+                    minr = (minr + mask) % P
+                if recvd:                                                    # :95-104
+                    if sb is None:
+                        raise _Crash()
+                    if se >= ss:
+                        yield ("send", partner, _sl(sb, ss * n, (se + 1) * n))
+                    else:
+                        yield ("send", partner, _sl(sb, ss * n, P * n))
+                        yield ("send", partner, _sl(sb, 0, (se + 1) * n))
+                elif equal:                                                  # :105-137
+                    nb = (re - rs + 1) % P
+                    if rs == re:
+                        rb, leaf = rbufs[rank], True
+                    else:
+                        sb = rb = _uninit(n * nb, rbufs[rank].dtype)
+                        minr, maxr = 0, nb - 1
+                        off = (rank - rs) % P
+                    if re >= rs:
+                        yield ("recv", partner, _sl(rb, 0, n * nb))
+                    else:
+                        yield ("recv", partner, _sl(rb, 0, n * (P - rs)))
+                        yield ("recv", partner, _sl(rb, n * (P - rs), n * (P - rs) + n * (re + 1)))
+                    recvd = True
+                mask >>= 1
+                hd = -hd
+            if not leaf:                                                     # :142-144
+                if sb is None:
+                    raise _Crash()
+                rbufs[rank][:n] = _sl(sb, off * n, off * n + n)
+            return OK
+        return g
+    return [prog(r) for r in range(P)]
+
+
+def _alltoall_progs(P, n, sbufs, rbufs):
+    """alltoall_bine, libbine_alltoall.c:14-147: log2(P) butterfly steps with
+    the negabinary partner; each step moves to rbuf the blocks whose
+    remapped destination falls in the partner's half (:71-94), compacts the
+    kept ones to the front of the temporary and receives the partner's into
+    its second half (:100-102); a final permutation by
+    remap_distance_doubling puts every source's block in place (:121-139)"""
+    L = _log2c(P)
+
+    def prog(rank):
+        def g():
+            tmp = np.array(sbufs[rank][:P * n])
+            rb = rbufs[rank]
+            resident = list(range(P))
+            nres = P
+            inv = 1 << (L - 1) if L else 0
+            bfm = ~(inv - 1)
+            mask = 1
+            while mask < P:
+                d = _nb2b((mask << 1) - 1)
+                partner = (rank + d) % P if rank % 2 == 0 else (rank - d) % P
+                mins = remap_rank(P, partner) & bfm
+                maxs = mins + inv - 1
+                nsend = nkeep = 0
+                nxt = []
+                for i in range(P):                                           # :71-94
+                    block = resident[i % nres]
+                    if mins <= remap_rank(P, block) <= maxs:
+                        _sl(rb, nsend * n, nsend * n + n)[:] = tmp[i * n:(i + 1) * n]
+                        nsend += 1
+                    else:
+                        if i != nkeep:
+                            tmp[nkeep * n:(nkeep + 1) * n] = tmp[i * n:(i + 1) * n]
+                        nkeep += 1
+                        nxt.append(block)
+                if nkeep != P // 2 or nsend != P // 2:
+                    raise _Crash()   # :95-96 assert
+                nres //= 2
+                yield ("send", partner, _sl(rb, 0, nsend * n))             # :100-102 Sendrecv
+                yield ("recv", partner, _sl(tmp, (P // 2) * n, (P // 2) * n + nsend * n))
+                resident[:nres] = nxt[:nres]
+                mask <<= 1
+                inv >>= 1
+                bfm >>= 1
+            for i in range(P):                                               # :121-139
+                rot = (i - rank) % P if rank % 2 == 0 else (rank - i) % P
+                rep = _b2nb(rot) if _nb_in_range(rot, L) else _b2nb(rot - P)
+                idx = _remap_distance_doubling(rep)
+                _sl(rb, i * n, (i + 1) * n)[:] = _sl(tmp, idx * n, (idx + 1) * n)
+            return OK
+        return g
+    return [prog(r) for r in range(P)]
+
+
+def _run_rooted(P, progs):
+    """rets of a rooted replay: "hang" (a deadlock), "crash" (an assert, a
+    NULL dereference, MPI_ERR_TRUNCATE -- fatal under MPICH's default
+    handler), "oob" (a read or write past a buffer: undefined), "dangling"
+    (completes but leaves a message unreceived, which MPICH delivers to the
+    next call's receive from that rank); else the MPI return codes"""
+    left = []
+    try:
+        rets = _replay(P, None, progs, left)
+    except _Stuck:
+        return ["hang"] * P
+    except _OOB:
+        return ["oob"] * P
+    except (ValueError, _Crash):
+        return ["crash"] * P
+    return ["dangling"] * P if left else rets
+
+
+def gather(sbufs, dtype, root=0):
+    """gather_bine by message-level replay: (the root's P * n buffer, rets);
+    where the reference does not complete cleanly every ret says why
+    (_run_rooted)"""
+    P, n = len(sbufs), sbufs[0].size
+    out = np.zeros(P * n, NP_DTYPES[dtype])
+    rets = _run_rooted(P, _gather_progs(P, n, root, sbufs, out))
+    return out, rets
+
+
+def scatter(sbuf_root, P, dtype, root=0):
+    """scatter_bine by message-level replay: sbuf_root holds P blocks of n;
+    (every rank's n-element rbuf, rets)"""
+    n = sbuf_root.size // P
+    rbufs = [np.zeros(n, NP_DTYPES[dtype]) for _ in range(P)]
+    rets = _run_rooted(P, _scatter_progs(P, n, root, np.array(sbuf_root), rbufs))
+    return rbufs, rets
+
+
+def alltoall(sbufs, dtype):
+    """alltoall_bine by message-level replay: sbufs[r] holds P blocks of n
+    (block j for rank j); (every rank's P * n rbuf, rets)"""
+    P = len(sbufs)
+    n = sbufs[0].size // P
+    rbufs = [np.zeros(P * n, NP_DTYPES[dtype]) for _ in range(P)]
+    rets = _run_rooted(P, _alltoall_progs(P, n, sbufs, rbufs))
+    return rbufs, rets
 
 
 def bcast(algo, sbufs, dtype, root=0):

@@ -19,6 +19,10 @@
  *                bcast: in place on each rank's input; rcounts "root<k>" = root k
  *                allgather: N = elements per rank (scount = rcount, same type,
  *                pico_core_utils.c:511-514), rbuf = P * N zeroed elements
+ *                gather / scatter: N = elements per block, root from "root<k>"
+ *                (else 0); gather: sbuf N, rbuf P * N on the root only (NULL
+ *                elsewhere, as pico_core passes it); scatter: sbuf P * N on the
+ *                root only, rbuf N; alltoall: sbuf and rbuf P * N
  *   rcounts_kind even   -> rcounts[i] = N / P  (pico_core_utils.c:535-536)
  *                ragged -> rcounts[i] = N / P + (i % 3)   (exercises displs)
  *                an "_inplace" suffix calls with MPI_IN_PLACE: the input is
@@ -273,7 +277,10 @@ int main(int argc, char **argv) {
         }
         outn = (size_t)rcounts[rank];
       }
-      if (!strcmp(coll, "allgather")) outn = N * (size_t)P;
+      const int root = !strncmp(rk, "root", 4) ? atoi(rk + 4) : 0;
+      if (!strcmp(coll, "allgather") || !strcmp(coll, "alltoall")) outn = N * (size_t)P;
+      if (!strcmp(coll, "alltoall") || !strcmp(coll, "scatter")) total = N * (size_t)P;
+      if (!strcmp(coll, "gather")) outn = rank == root ? N * (size_t)P : 0;
       void *sbuf = malloc(total * esz + 16);
       void *rbuf = calloc(outn * esz + total * esz + 16, 1);
       fill(sbuf, dts[d], total, seed_base + (unsigned)rank);
@@ -300,9 +307,16 @@ int main(int argc, char **argv) {
         /* in place on every rank's own input; root from "root<k>" (else 0) */
         bc_fn f = pick_bcast(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
-        const int root = !strncmp(rk, "root", 4) ? atoi(rk + 4) : 0;
         memcpy(rbuf, sbuf, total * esz);
         ret = f(rbuf, N, dt, root, MPI_COMM_WORLD);
+      } else if (!strcmp(coll, "gather")) {
+        /* pico_core: rbuf only on the root (pico_core_gather_utils.c) */
+        ret = gather_bine(sbuf, N, dt, rank == root ? rbuf : NULL, N, dt, root, MPI_COMM_WORLD);
+      } else if (!strcmp(coll, "scatter")) {
+        /* pico_core: sbuf only on the root (pico_core_scatter_utils.c) */
+        ret = scatter_bine(rank == root ? sbuf : NULL, N, dt, rbuf, N, dt, root, MPI_COMM_WORLD);
+      } else if (!strcmp(coll, "alltoall")) {
+        ret = alltoall_bine(sbuf, N, dt, rbuf, N, dt, MPI_COMM_WORLD);
       } else if (!strcmp(coll, "reduce")) {
         rd_fn f = pick_reduce(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);

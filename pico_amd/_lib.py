@@ -44,6 +44,10 @@ ALGOS = {
     # libbine_bcast.c: the latency trees and (round 5) the bandwidth algorithms
     "bcast": {"scatter_allgather": 64, "bine_lat": 65, "bine_lat_reversed": 66, "bine_lat_new": 67, "bine_lat_i_new": 68,
               "bine_bdw_static": 69, "bine_bdw_remap": 70},
+    # libbine_alltoall.c, libbine_gather.c, libbine_scatter.c (round 5)
+    "alltoall": {"bine": 80},
+    "gather": {"bine": 81},
+    "scatter": {"bine": 82},
 }
 IN_PLACE = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)
 UNIQUE_ID_BYTES = 128
@@ -139,6 +143,12 @@ def lib():
         "bine_loopback_run_allgather": ([vp, i, i, vp, vp, sz, i, vp], i),
         "bine_bcast": ([vp, i, vp, sz, i, i, vp], i),
         "bine_loopback_run_bcast": ([vp, i, i, vp, sz, i, i, vp], i),
+        "bine_gather": ([vp, i, vp, vp, sz, i, i, vp], i),
+        "bine_scatter": ([vp, i, vp, vp, sz, i, i, vp], i),
+        "bine_alltoall": ([vp, i, vp, vp, sz, i, vp], i),
+        "bine_loopback_run_gather": ([vp, i, i, vp, vp, sz, i, i, vp], i),
+        "bine_loopback_run_scatter": ([vp, i, i, vp, vp, sz, i, i, vp], i),
+        "bine_loopback_run_alltoall": ([vp, i, i, vp, vp, sz, i, vp], i),
         "bine_loopback_run_allreduce": ([vp, i, i, vp, vp, sz, i, i, sz, vp], i),
         "bine_loopback_run_reduce_scatter": ([vp, i, i, vp, vp, vp, i, i, vp], i),
         "bine_loopback_run_reduce": ([vp, i, i, vp, vp, sz, i, i, i, vp], i),

@@ -570,6 +570,47 @@ def loopback_bcast(comms, algo, bufs, count, dtype, root):
     return rc, list(st)
 
 
+def gather(algo, sbuf, rbuf, count: int, dtype, root: int, comm: Comm, stream=None) -> None:
+    """every rank's `count` elements of sbuf land in block r of the root's rbuf
+    (P * count elements; rbuf may be None elsewhere)."""
+    check(lib().bine_gather(comm.handle, _algo("gather", algo), _ptr(sbuf), _ptr(rbuf), count,
+                            _dtype(dtype, sbuf), root, _stream(stream, comm)), f"gather_{algo}")
+
+
+def scatter(algo, sbuf, rbuf, count: int, dtype, root: int, comm: Comm, stream=None) -> None:
+    """block r of the root's sbuf (P * count elements; sbuf may be None
+    elsewhere) lands in rank r's rbuf (`count` elements)."""
+    check(lib().bine_scatter(comm.handle, _algo("scatter", algo), _ptr(sbuf), _ptr(rbuf), count,
+                             _dtype(dtype, rbuf), root, _stream(stream, comm)), f"scatter_{algo}")
+
+
+def alltoall(algo, sbuf, rbuf, count: int, dtype, comm: Comm, stream=None) -> None:
+    """block j of rank r's sbuf lands in block r of rank j's rbuf (both P * count
+    elements)."""
+    check(lib().bine_alltoall(comm.handle, _algo("alltoall", algo), _ptr(sbuf), _ptr(rbuf), count,
+                              _dtype(dtype, rbuf), _stream(stream, comm)), f"alltoall_{algo}")
+
+
+def _loopback(fn, coll, comms, algo, sbufs, rbufs, count, dtype, *root):
+    st = (ctypes.c_int * len(comms))()
+    hs = (ctypes.c_void_p * len(comms))(*[c.handle.value for c in comms])
+    ref = next(b for b in list(rbufs) + list(sbufs) if b is not None)
+    rc = fn(hs, len(comms), _algo(coll, algo), _ptrs(sbufs), _ptrs(rbufs), count, _dtype(dtype, ref), *root, st)
+    return rc, list(st)
+
+
+def loopback_gather(comms, algo, sbufs, rbufs, count, dtype, root):
+    return _loopback(lib().bine_loopback_run_gather, "gather", comms, algo, sbufs, rbufs, count, dtype, root)
+
+
+def loopback_scatter(comms, algo, sbufs, rbufs, count, dtype, root):
+    return _loopback(lib().bine_loopback_run_scatter, "scatter", comms, algo, sbufs, rbufs, count, dtype, root)
+
+
+def loopback_alltoall(comms, algo, sbufs, rbufs, count, dtype):
+    return _loopback(lib().bine_loopback_run_alltoall, "alltoall", comms, algo, sbufs, rbufs, count, dtype)
+
+
 # ---- libbine-named entry points (include/libbine.h:30-78) --------------------------
 
 def _mk_ar(name):
@@ -623,11 +664,18 @@ for _n in ALGOS["allgather"]:
     ENTRY_POINTS["allgather_" + _n] = _mk_ag(_n)
 for _n in ALGOS["bcast"]:
     ENTRY_POINTS["bcast_" + _n] = _mk_bc(_n)
+ENTRY_POINTS["alltoall_bine"] = lambda sbuf, rbuf, count, dtype, comm, stream=None: \
+    alltoall("bine", sbuf, rbuf, count, dtype, comm, stream=stream)
+ENTRY_POINTS["gather_bine"] = lambda sbuf, rbuf, count, dtype, root, comm, stream=None: \
+    gather("bine", sbuf, rbuf, count, dtype, root, comm, stream=stream)
+ENTRY_POINTS["scatter_bine"] = lambda sbuf, rbuf, count, dtype, root, comm, stream=None: \
+    scatter("bine", sbuf, rbuf, count, dtype, root, comm, stream=stream)
 globals().update(ENTRY_POINTS)
 
 __all__ = ["Comm", "BineError", "IN_PLACE", "schedule", "dm_fused_plan", "dm_fused_msgs", "reduce_local", "reduce3", "fill_pico", "checksum", "copy",
            "rccl_version",
            "set_reduce_tuning", "allreduce", "reduce_scatter", "reduce", "loopback_allreduce",
            "loopback_reduce_scatter", "loopback_reduce", "plan", "allgather", "loopback_allgather", "bcast", "loopback_bcast", "reduce_batch",
+           "gather", "scatter", "alltoall", "loopback_gather", "loopback_scatter", "loopback_alltoall",
            "exchange", "vendor_allreduce", "reduce_tree", "allreduce_staged", "reduce_scatter_staged",
            "stage_plan", "dm_tree_plan"] + list(ENTRY_POINTS)

@@ -1860,6 +1860,10 @@ static const struct { int algo; const char *coll, *name, *selector; } kAlgos[] =
     {BINE_BC_BINE_LAT_I_NEW, "bcast", "bine_lat_i_new", "bine_lat_i_new_over"},
     {BINE_BC_BINE_BDW_STATIC, "bcast", "bine_bdw_static", "bine_bdw_static_over"},
     {BINE_BC_BINE_BDW_REMAP, "bcast", "bine_bdw_remap", "bine_bdw_remap_over"},
+    // pico_core_utils.c:152, :190, :245
+    {BINE_A2A_BINE, "alltoall", "bine", "bine_over"},
+    {BINE_GA_BINE, "gather", "bine", "bine_over"},
+    {BINE_SC_BINE, "scatter", "bine", "bine_over"},
 };
 
 int bine_algo_from_name(const char *coll, const char *name) {
@@ -2173,6 +2177,36 @@ int bine_bcast(bine_comm_t c, int algo, void *buf, size_t count, int dtype, int 
   return run_collective(c, a, BINE_IN_PLACE, buf, dtype, kOpNone, kCommChunk, stream);
 }
 
+// gather_bine / scatter_bine / alltoall_bine: `count` elements per block; pure
+// data movement (no operator)
+int bine_gather(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int root,
+                void *stream) {
+  if (algo != BINE_GA_BINE) return BINE_ERR_UNSUPPORTED;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  a.root = root;
+  return run_collective(c, a, sbuf, rbuf, dtype, kOpNone, kCommChunk, stream);
+}
+
+int bine_scatter(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, int root,
+                 void *stream) {
+  if (algo != BINE_SC_BINE) return BINE_ERR_UNSUPPORTED;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  a.root = root;
+  return run_collective(c, a, sbuf, rbuf, dtype, kOpNone, kCommChunk, stream);
+}
+
+int bine_alltoall(bine_comm_t c, int algo, const void *sbuf, void *rbuf, size_t count, int dtype, void *stream) {
+  if (algo != BINE_A2A_BINE) return BINE_ERR_UNSUPPORTED;
+  PlanArgs a;
+  a.algo = algo;
+  a.count = count;
+  return run_collective(c, a, sbuf, rbuf, dtype, kOpNone, kCommChunk, stream);
+}
+
 int bine_exchange(bine_comm_t c, int nsend, const int *send_peers, const void *const *sbufs, const size_t *sbytes,
                   int nrecv, const int *recv_peers, void *const *rbufs, const size_t *rbytes, void *stream) {
   if (!c || nsend < 0 || nrecv < 0) return BINE_ERR_ARG;
@@ -2255,6 +2289,30 @@ int bine_loopback_run_bcast(bine_comm_t *comms, int n, int algo, void *const *bu
   return run_threads(comms, n, statuses, [&](int r) {
     (void)hipSetDevice(comms[r]->device);
     return bine_bcast(comms[r], algo, bufs[r], count, dtype, root, comms[r]->stream);  // one stream per virtual rank
+  });
+}
+
+int bine_loopback_run_gather(bine_comm_t *comms, int n, int algo, const void *const *sbufs, void *const *rbufs,
+                             size_t count, int dtype, int root, int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_gather(comms[r], algo, sbufs[r], rbufs[r], count, dtype, root, comms[r]->stream);
+  });
+}
+
+int bine_loopback_run_scatter(bine_comm_t *comms, int n, int algo, const void *const *sbufs, void *const *rbufs,
+                              size_t count, int dtype, int root, int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_scatter(comms[r], algo, sbufs[r], rbufs[r], count, dtype, root, comms[r]->stream);
+  });
+}
+
+int bine_loopback_run_alltoall(bine_comm_t *comms, int n, int algo, const void *const *sbufs, void *const *rbufs,
+                               size_t count, int dtype, int *statuses) {
+  return run_threads(comms, n, statuses, [&](int r) {
+    (void)hipSetDevice(comms[r]->device);
+    return bine_alltoall(comms[r], algo, sbufs[r], rbufs[r], count, dtype, comms[r]->stream);
   });
 }
 

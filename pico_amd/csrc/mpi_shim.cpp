@@ -609,14 +609,33 @@ int do_bcast(int algo, void *buf, size_t count, MPI_Datatype dtype, int root, MP
                       });
 }
 
-int unsupported(const char *name) {
-  static std::once_flag once;
-  std::call_once(once, [&] {
-    fprintf(stderr, "libbine(amd): %s is outside the reduce family this library provides "
-                    "(allreduce / reduce_scatter / reduce / allgather / bcast); returning "
-                    "MPI_ERR_UNSUPPORTED_OPERATION\n", name);
-  });
-  return MPI_ERR_UNSUPPORTED_OPERATION;
+// alltoall_bine / gather_bine / scatter_bine: whole blocks of scount elements
+// (the reference asserts sendcount == recvcount and one type,
+// libbine_gather.c:17, libbine_scatter.c:17-18, libbine_alltoall.c:17-18:
+// unequal block sizes are MPI_ERR_ARG here), run on bytes.  gather: rbuf on
+// the root only (pico_core passes NULL elsewhere, pico_core_gather_utils.c);
+// scatter: sbuf on the root only.
+int do_blocks(int algo, const void *sbuf, size_t scount, MPI_Datatype sdtype, void *rbuf, size_t rcount,
+              MPI_Datatype rdtype, int root, MPI_Comm comm) {
+  Entry *e;
+  int rc = get_entry(comm, &e);
+  if (rc) return rc;
+  const bool has_s = algo != BINE_SC_BINE || e->rank == root;
+  const bool has_r = algo != BINE_GA_BINE || e->rank == root;
+  const size_t rsz = span(rdtype), ssz = has_s && sbuf != MPI_IN_PLACE ? span(sdtype) : rsz;
+  if (!rsz || !ssz) return MPI_ERR_TYPE;
+  const size_t bytes = rcount * rsz;
+  if (has_s && sbuf != MPI_IN_PLACE && scount * ssz != bytes) return MPI_ERR_ARG;
+  if (bytes == 0) return MPI_SUCCESS;
+  const size_t P = (size_t)e->size;
+  const size_t sbytes = has_s ? (algo == BINE_GA_BINE ? bytes : P * bytes) : 0;
+  const size_t rbytes = has_r ? (algo == BINE_SC_BINE ? bytes : P * bytes) : 0;
+  return with_buffers(e, has_s ? sbuf : nullptr, sbytes, has_r ? rbuf : nullptr, rbytes, false, 0, bytes,
+                      [&](const void *s, void *r, size_t, size_t, void *st) {
+                        if (algo == BINE_GA_BINE) return bine_gather(e->comm, algo, s, r, bytes, BINE_UINT8, root, st);
+                        if (algo == BINE_SC_BINE) return bine_scatter(e->comm, algo, s, r, bytes, BINE_UINT8, root, st);
+                        return bine_alltoall(e->comm, algo, s, r, bytes, BINE_UINT8, st);
+                      });
 }
 
 }  // namespace
@@ -651,8 +670,6 @@ RS(reduce_scatter_bine_block_by_block_any_even, BINE_RS_BINE_BLOCK_BY_BLOCK_ANY_
 int reduce_bine_lat(BINE_REDUCE_ARGS) { return do_reduce(BINE_RD_BINE_LAT, sbuf, rbuf, count, dtype, op, root, comm); }
 int reduce_bine_bdw(BINE_REDUCE_ARGS) { return do_reduce(BINE_RD_BINE_BDW, sbuf, rbuf, count, dtype, op, root, comm); }
 
-#define NA(fn, args) \
-  int fn(args) { return unsupported(#fn); }
 #define AG(fn, id) \
   int fn(BINE_ALLGATHER_ARGS) { return do_allgather(id, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm); }
 AG(allgather_k_bruck, BINE_AG_K_BRUCK)
@@ -669,7 +686,9 @@ AG(allgather_bine_2_blocks, BINE_AG_BINE_2_BLOCKS)
 AG(allgather_bine_2_blocks_dtype, BINE_AG_BINE_2_BLOCKS_DTYPE)
 #undef AG
 
-NA(alltoall_bine, BINE_ALLGATHER_ARGS)
+int alltoall_bine(BINE_ALLGATHER_ARGS) {
+  return do_blocks(BINE_A2A_BINE, sbuf, scount, sdtype, rbuf, rcount, rdtype, 0, comm);
+}
 #define BC(fn, id) \
   int fn(BINE_BCAST_ARGS) { return do_bcast(id, buf, count, dtype, root, comm); }
 BC(bcast_bine_lat, BINE_BC_BINE_LAT)
@@ -680,8 +699,11 @@ BC(bcast_scatter_allgather, BINE_BC_SCATTER_ALLGATHER)
 BC(bcast_bine_bdw_static, BINE_BC_BINE_BDW_STATIC)
 BC(bcast_bine_bdw_remap, BINE_BC_BINE_BDW_REMAP)
 #undef BC
-NA(gather_bine, BINE_GATHER_ARGS)
-NA(scatter_bine, BINE_GATHER_ARGS)
-#undef NA
+int gather_bine(BINE_GATHER_ARGS) {
+  return do_blocks(BINE_GA_BINE, sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm);
+}
+int scatter_bine(BINE_GATHER_ARGS) {
+  return do_blocks(BINE_SC_BINE, sbuf, scount, sdtype, rbuf, rcount, rdtype, root, comm);
+}
 
 }  // extern "C"

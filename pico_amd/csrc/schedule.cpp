@@ -22,7 +22,9 @@
 //    rbuf untouched at P = 1 (libbine_reduce_scatter.c:585, :1098).
 //  * assert()/hang cases of the reference return BINE_ERR_ARG.
 #include <algorithm>
+#include <array>
 #include <cstring>
+#include <map>
 
 #include "bine_internal.h"
 
@@ -1820,6 +1822,346 @@ void bc_bine_bdw_remap(Builder &b, const PlanArgs &a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// gather_bine / scatter_bine / alltoall_bine (libbine_gather.c, _scatter.c,
+// _alltoall.c): whole-block data movement.  No rank's program depends on the
+// data it receives, so the planner writes EVERY rank's program in block units
+// (a block = `count` elements), matches their messages per ordered pair in
+// posting order, runs them on block tags under rendezvous semantics --
+// checking bounds, message lengths (a longer message than its receive is
+// MPI_ERR_TRUNCATE), progress, and that every block lands where the
+// collective puts it -- and emits its own rank's program scaled by `count`,
+// each receive carrying its send's exact length.  Where the reference hangs,
+// aborts, reads or writes out of bounds or delivers something other than the
+// collective (non-power-of-two P; odd roots, and some even ones for scatter:
+// tests/golden pins which), the plan is refused -- BINE_ERR_ROOT at a
+// power-of-two P, BINE_ERR_SIZE otherwise -- instead of reproducing it.
+// ---------------------------------------------------------------------------
+namespace {
+
+enum { BS = 0, BR = 1, BT = 2 };  // sbuf, rbuf, the reference's malloc'd temporary
+
+struct BOp {
+  int kind;             // 0 copy, 1 send, 2 recv
+  int grp;              // send / recv: one blocking MPI call (Sendrecv: both) = one exchange
+  int peer;
+  int buf;              // send: source; recv / copy: destination
+  int64_t off, n;
+  int sbuf;             // copy source
+  int64_t soff;
+};
+
+struct BProg {
+  std::vector<BOp> ops;
+  int64_t size[3] = {0, 0, 0};  // blocks each buffer holds
+  bool crash = false;           // the reference aborts or dereferences NULL
+  int ngrp = 0;
+  void copy(int sb, int64_t so, int db, int64_t d, int64_t n) { ops.push_back({0, -1, -1, db, d, n, sb, so}); }
+  void send(int peer, int b, int64_t off, int64_t n) { ops.push_back({1, ngrp, peer, b, off, n, -1, 0}); }
+  void recv(int peer, int b, int64_t off, int64_t n) { ops.push_back({2, ngrp, peer, b, off, n, -1, 0}); }
+  void end() { ngrp++; }
+};
+
+int64_t pmod64(int64_t a, int64_t b) { int64_t r = a % b; return r < 0 ? r + b : r; }
+int nb_partner_root(uint32_t vnb, int mask, int root, int P) {  // e.g. libbine_gather.c:39-40
+  return pmod(from_nb(vnb ^ (uint32_t)((mask << 1) - 1)) + root, P);
+}
+
+// gather_bine, libbine_gather.c:16-96
+void ga_prog(int P, int root, int x, BProg &p) {
+  const int G = x == root ? BR : BT;  // non-roots gather into a P-block temporary (:23-26)
+  p.size[BS] = 1;
+  p.size[G] = P;
+  p.copy(BS, 0, G, x, 1);  // :28
+  int64_t lo = x, hi = x;
+  const uint32_t vnb = to_nb(pmod(x - root, P));
+  int ext = x % 2 ? -1 : 1;  // the REAL rank's parity (:33-36)
+  for (int mask = 1; mask < P; mask <<= 1) {
+    const int partner = nb_partner_root(vnb, mask, root, P);
+    const uint32_t mlsb = (uint32_t)(mask << 2) - 1, lsbs = vnb & mlsb;
+    if (!(lsbs == 0 || lsbs == mlsb) || ((mask << 1) >= P && x != root)) {  // :45-57
+      if (hi >= lo) { p.send(partner, G, lo, hi - lo + 1); p.end(); }  // one blocking call each
+      else { p.send(partner, G, lo, P - lo); p.end(); p.send(partner, G, 0, hi + 1); p.end(); }
+      return;
+    }
+    int64_t rs, re;  // :59-69
+    if (ext == 1) { rs = (hi + 1) % P; re = (hi + mask) % P; hi = re; }
+    else { re = pmod64(lo - 1, P); rs = pmod64(lo - mask, P); lo = rs; }
+    if (re >= rs) { p.recv(partner, G, rs, re - rs + 1); p.end(); }  // :70-80, one blocking
+    else { p.recv(partner, G, rs, P - rs); p.end(); p.recv(partner, G, 0, re + 1); p.end(); }  // call each
+    ext = -ext;
+  }
+}
+
+// scatter_bine, libbine_scatter.c:14-151
+void sc_prog(int P, int root, int x, BProg &p) {
+  p.size[BS] = x == root ? P : 0;
+  p.size[BR] = 1;
+  if (P == 1) { p.copy(BS, 0, BR, 0, 1); return; }  // the reference shifts by -1 here (:57)
+  const int L = log2_ceil(P);
+  int hd = x % 2 ? -1 : 1;
+  if (L % 2 == 0) hd = -hd;  // :38-40
+  const uint32_t full = (1u << L) - 1;
+  int64_t maxr, minr;  // :49-55
+  if (x % 2 == 0) { maxr = ((uint32_t)x + 0x55555555u) & full; minr = ((uint32_t)x - 0xAAAAAAAAu) & full; }
+  else { minr = ((uint32_t)x - 0x55555555u) & full; maxr = ((uint32_t)x + 0xAAAAAAAAu) & full; }
+  maxr %= P;
+  minr %= P;
+  int64_t off = x;
+  bool recvd = x == root, leaf = false;
+  int sb = x == root ? BS : -1;  // the buffer this rank forwards from
+  const uint32_t vnb = to_nb(pmod(x - root, P));
+  for (int mask = 1 << (L - 1); mask > 0; mask >>= 1, hd = -hd) {
+    const int partner = nb_partner_root(vnb, mask, root, P);
+    const uint32_t mlsb = (uint32_t)(mask << 1) - 1, lsbs = vnb & mlsb;
+    const int64_t ts = minr, te = pmod64(minr + mask - 1, P), bs = pmod64(te + 1, P), be = maxr;  // :75-93
+    int64_t ss, se, rs, re;
+    if (hd == 1) { ss = bs; se = be; rs = ts; re = te; maxr = pmod64(maxr - mask, P); }
+    else { ss = ts; se = te; rs = bs; re = be; minr = pmod64(minr + mask, P); }
+    if (recvd) {  // :95-104
+      if (sb < 0) { p.crash = true; return; }
+      if (se >= ss) { p.send(partner, sb, ss, se - ss + 1); p.end(); }
+      else { p.send(partner, sb, ss, P - ss); p.end(); p.send(partner, sb, 0, se + 1); p.end(); }
+    } else if (lsbs == 0 || lsbs == mlsb) {  // :105-137
+      const int64_t nb = pmod64(re - rs + 1, P);
+      int rb = BR;
+      if (rs == re) {
+        leaf = true;
+      } else {
+        rb = sb = BT;
+        p.size[BT] = nb;
+        minr = 0;
+        maxr = nb - 1;
+        off = pmod64(x - rs, P);
+      }
+      if (re >= rs) { p.recv(partner, rb, 0, nb); p.end(); }
+      else { p.recv(partner, rb, 0, P - rs); p.end(); p.recv(partner, rb, P - rs, re + 1); p.end(); }
+      recvd = true;
+    }
+  }
+  if (!leaf) {  // :142-144
+    if (sb < 0) { p.crash = true; return; }
+    p.copy(sb, off, BR, 0, 1);
+  }
+}
+
+int remap_distance_doubling(uint32_t num) {  // libbine_utils.h:601-609
+  int out = 0;
+  while (num > 0) {
+    const int k = 31 - __builtin_clz(num);
+    out ^= 1 << k;
+    num ^= (uint32_t)((1ull << (k + 1)) - 1);
+  }
+  return out;
+}
+
+// alltoall_bine, libbine_alltoall.c:14-147
+void a2a_prog(int P, int x, BProg &p) {
+  p.size[BS] = p.size[BR] = p.size[BT] = P;
+  p.copy(BS, 0, BT, 0, P);  // :50
+  const int L = log2_ceil(P);
+  std::vector<int> res((size_t)P), nxt;
+  for (int i = 0; i < P; i++) res[(size_t)i] = i;
+  int nres = P, inv = L ? 1 << (L - 1) : 0, bfm = ~(inv - 1);
+  for (int mask = 1; mask < P; mask <<= 1, inv >>= 1, bfm >>= 1) {
+    const int partner = nb_partner(x, mask, P);  // :59-64
+    const int64_t mins = remap_rank((uint32_t)P, (uint32_t)partner) & (uint32_t)bfm, maxs = mins + inv - 1;
+    int64_t ns = 0, nk = 0;
+    nxt.clear();
+    for (int i = 0; i < P; i++) {  // :71-94
+      const int blk = res[(size_t)(i % nres)];
+      const int64_t rb = remap_rank((uint32_t)P, (uint32_t)blk);
+      if (rb >= mins && rb <= maxs) {
+        p.copy(BT, i, BR, ns++, 1);
+      } else {
+        if (i != nk) p.copy(BT, i, BT, nk, 1);
+        nk++;
+        nxt.push_back(blk);
+      }
+    }
+    if (nk != P / 2 || ns != P / 2) { p.crash = true; return; }  // :95-96
+    nres /= 2;
+    p.send(partner, BR, 0, ns);  // :100-102, one MPI_Sendrecv
+    p.recv(partner, BT, P / 2, ns);
+    p.end();
+    for (int i = 0; i < nres; i++) res[(size_t)i] = nxt[(size_t)i];
+  }
+  for (int i = 0; i < P; i++) {  // :121-139
+    const int rot = x % 2 == 0 ? pmod(i - x, P) : pmod(x - i, P);
+    const uint32_t rep = nb_fits(rot, L) ? to_nb(rot) : to_nb(rot - P);
+    p.copy(BT, remap_distance_doubling(rep), BR, i, 1);
+  }
+}
+
+// Runs every rank's program on block tags (tag = source rank * P + block);
+// true when all of it completes in bounds and delivers the collective.
+bool blocks_run(int algo, int P, int root, std::vector<BProg> &pg, std::vector<std::vector<int>> &match) {
+  for (auto &p : pg)
+    if (p.crash) return false;
+  std::vector<std::array<std::vector<int64_t>, 3>> tag((size_t)P);
+  for (int x = 0; x < P; x++)
+    for (int b = 0; b < 3; b++) tag[(size_t)x][(size_t)b].assign((size_t)pg[(size_t)x].size[b], -1);
+  for (int x = 0; x < P; x++) {
+    auto &s = tag[(size_t)x][BS];
+    for (int64_t j = 0; j < (int64_t)s.size(); j++)
+      s[(size_t)j] = algo == BINE_GA_BINE ? (int64_t)x * P : algo == BINE_SC_BINE ? (int64_t)root * P + j
+                                                                                   : (int64_t)x * P + j;
+  }
+  auto in = [&](int x, int b, int64_t off, int64_t n) {
+    return off >= 0 && n >= 0 && off + n <= (int64_t)tag[(size_t)x][(size_t)b].size();
+  };
+  // match sends and receives per ordered pair, in posting order
+  std::map<std::pair<int, int>, std::vector<int>> sq, rq;
+  match.assign((size_t)P, {});
+  for (int x = 0; x < P; x++) {
+    match[(size_t)x].assign(pg[(size_t)x].ops.size(), -1);
+    for (int i = 0; i < (int)pg[(size_t)x].ops.size(); i++) {
+      const BOp &o = pg[(size_t)x].ops[(size_t)i];
+      if (o.kind == 1) sq[{x, o.peer}].push_back(i);
+      if (o.kind == 2) rq[{o.peer, x}].push_back(i);
+    }
+  }
+  for (auto &kv : sq) {
+    const auto &r = rq[kv.first];
+    if (r.size() != kv.second.size()) return false;
+    for (size_t k = 0; k < r.size(); k++) {
+      const BOp &s = pg[(size_t)kv.first.first].ops[(size_t)kv.second[k]];
+      const BOp &v = pg[(size_t)kv.first.second].ops[(size_t)r[k]];
+      if (s.n > v.n) return false;  // MPI_ERR_TRUNCATE
+      match[(size_t)kv.first.first][(size_t)kv.second[k]] = r[k];
+      match[(size_t)kv.first.second][(size_t)r[k]] = kv.second[k];
+    }
+  }
+  for (auto &kv : rq)
+    if (sq.find(kv.first) == sq.end() && !kv.second.empty()) return false;
+  // rendezvous run: a rank's copies run in order; the messages of its current
+  // exchange complete one by one as their peers reach the matching exchange
+  std::vector<size_t> pc((size_t)P, 0);
+  std::vector<std::vector<char>> done((size_t)P);
+  for (int x = 0; x < P; x++) done[(size_t)x].assign(pg[(size_t)x].ops.size(), 0);
+  auto grp_at = [&](int x) { const auto &o = pg[(size_t)x].ops; return pc[(size_t)x] < o.size() ? o[pc[(size_t)x]].grp : -2; };
+  for (bool moved = true; moved;) {
+    moved = false;
+    for (int x = 0; x < P; x++) {
+      auto &ops = pg[(size_t)x].ops;
+      while (pc[(size_t)x] < ops.size()) {
+        const BOp &o = ops[pc[(size_t)x]];
+        if (o.kind == 0) {
+          if (!in(x, o.sbuf, o.soff, o.n) || !in(x, o.buf, o.off, o.n)) return false;
+          auto &sv = tag[(size_t)x][(size_t)o.sbuf];
+          auto &dv = tag[(size_t)x][(size_t)o.buf];
+          std::vector<int64_t> t(sv.begin() + o.soff, sv.begin() + o.soff + o.n);
+          std::copy(t.begin(), t.end(), dv.begin() + o.off);
+          pc[(size_t)x]++;
+          moved = true;
+          continue;
+        }
+        size_t e = pc[(size_t)x];
+        while (e < ops.size() && ops[e].kind != 0 && ops[e].grp == o.grp) e++;
+        bool all = true;
+        for (size_t i = pc[(size_t)x]; i < e; i++) {
+          if (done[(size_t)x][i]) continue;
+          const BOp &m = ops[i];
+          const int j = match[(size_t)x][i];
+          const BOp &q = pg[(size_t)m.peer].ops[(size_t)j];
+          if (grp_at(m.peer) != q.grp || q.kind == 0) { all = false; continue; }
+          const BOp &s = m.kind == 1 ? m : q, &r = m.kind == 1 ? q : m;
+          const int sx = m.kind == 1 ? x : m.peer, rx = m.kind == 1 ? m.peer : x;
+          if (!in(sx, s.buf, s.off, s.n) || !in(rx, r.buf, r.off, s.n)) return false;
+          auto &sv = tag[(size_t)sx][(size_t)s.buf];
+          std::copy(sv.begin() + s.off, sv.begin() + s.off + s.n, tag[(size_t)rx][(size_t)r.buf].begin() + r.off);
+          done[(size_t)x][i] = done[(size_t)m.peer][(size_t)j] = 1;
+          moved = true;
+        }
+        if (!all) break;
+        pc[(size_t)x] = e;
+        moved = true;
+      }
+    }
+  }
+  for (int x = 0; x < P; x++)
+    if (pc[(size_t)x] < pg[(size_t)x].ops.size()) return false;  // a hang
+  for (int x = 0; x < P; x++) {
+    const auto &rb = tag[(size_t)x][BR];
+    if (algo == BINE_GA_BINE && x == root) {
+      for (int j = 0; j < P; j++)
+        if (rb[(size_t)j] != (int64_t)j * P) return false;
+    } else if (algo == BINE_SC_BINE) {
+      if (rb[0] != (int64_t)root * P + x) return false;
+    } else if (algo == BINE_A2A_BINE) {
+      for (int j = 0; j < P; j++)
+        if (rb[(size_t)j] != (int64_t)j * P + x) return false;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+void rooted_blocks(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  if (a.in_place) { b.fail(BINE_ERR_ARG); return; }  // the reference memcpy's from MPI_IN_PLACE
+  const bool rooted = a.algo != BINE_A2A_BINE;
+  if (rooted && (a.root < 0 || a.root >= P)) { b.fail(BINE_ERR_ROOT); return; }
+  std::vector<BProg> pg((size_t)P);
+  for (int x = 0; x < P; x++) {
+    if (a.algo == BINE_GA_BINE) ga_prog(P, a.root, x, pg[(size_t)x]);
+    else if (a.algo == BINE_SC_BINE) sc_prog(P, a.root, x, pg[(size_t)x]);
+    else a2a_prog(P, x, pg[(size_t)x]);
+  }
+  std::vector<std::vector<int>> match;
+  if (!blocks_run(a.algo, P, a.root, pg, match)) {
+    b.fail(is_pow2(P) && rooted ? BINE_ERR_ROOT : BINE_ERR_SIZE);
+    return;
+  }
+  const uint64_t c = a.count;
+  const int map[3] = {SB, RB, T0};
+  const BProg &me = pg[(size_t)r];
+  if (me.size[BT]) b.tmp(T0, (uint64_t)me.size[BT] * c);
+  for (size_t i = 0; i < me.ops.size(); i++) {
+    const BOp &o = me.ops[i];
+    if (o.kind == 0) {
+      b.copy(map[o.sbuf], (uint64_t)o.soff * c, map[o.buf], (uint64_t)o.off * c, (uint64_t)o.n * c);
+      continue;
+    }
+    if (o.kind == 1) {
+      b.send(o.peer, map[o.buf], (uint64_t)o.off * c, (uint64_t)o.n * c);
+    } else {  // the matching send's exact length
+      const BOp &s = pg[(size_t)o.peer].ops[(size_t)match[(size_t)r][i]];
+      b.recv(o.peer, map[o.buf], (uint64_t)o.off * c, (uint64_t)s.n * c);
+    }
+    if (i + 1 == me.ops.size() || me.ops[i + 1].kind == 0 || me.ops[i + 1].grp != o.grp) b.end();
+  }
+}
+
+// the direct forms (flat_ag): every block straight from its source to its
+// destination in one exchange -- one hop on every link of a fully connected
+// node; the same bytes land where the literal schedule puts them
+void rooted_flat(Builder &b, const PlanArgs &a) {
+  const int P = a.P, r = a.rank;
+  const uint64_t c = a.count;
+  if (a.algo == BINE_GA_BINE) {
+    if (r == a.root) {
+      b.copy(SB, 0, RB, (uint64_t)r * c, c);
+      for (int x = 0; x < P; x++) b.recv(x == r ? -1 : x, RB, (uint64_t)x * c, c);
+    } else {
+      b.send(a.root, SB, 0, c);
+    }
+  } else if (a.algo == BINE_SC_BINE) {
+    if (r == a.root) {
+      b.copy(SB, (uint64_t)r * c, RB, 0, c);
+      for (int x = 0; x < P; x++) b.send(x == r ? -1 : x, SB, (uint64_t)x * c, c);
+    } else {
+      b.recv(a.root, RB, 0, c);
+    }
+  } else {
+    b.copy(SB, (uint64_t)r * c, RB, (uint64_t)r * c, c);
+    for (int x = 0; x < P; x++) b.send(x == r ? -1 : x, SB, (uint64_t)x * c, c);
+    for (int x = 0; x < P; x++) b.recv(x == r ? -1 : x, RB, (uint64_t)x * c, c);
+  }
+  b.end();
+}
+
 Plan make_plan(const PlanArgs &a) {
   Builder b(a.rank);
   if (a.P < 1 || a.rank < 0 || a.rank >= a.P || a.esz == 0) { b.fail(BINE_ERR_ARG); return b.p; }
@@ -1868,6 +2210,16 @@ Plan make_plan(const PlanArgs &a) {
     case BINE_BC_SCATTER_ALLGATHER: bc_scatter_allgather(b, a); break;
     case BINE_BC_BINE_BDW_STATIC: bc_bine_bdw_static(b, a); break;
     case BINE_BC_BINE_BDW_REMAP: bc_bine_bdw_remap(b, a); break;
+    case BINE_A2A_BINE:
+    case BINE_GA_BINE:
+    case BINE_SC_BINE:
+      rooted_blocks(b, a);
+      if (a.flat_ag && a.P >= 2 && b.p.status == BINE_SUCCESS) {
+        Builder f(a.rank);
+        rooted_flat(f, a);
+        return f.p;
+      }
+      break;
     default: b.fail(BINE_ERR_UNSUPPORTED); break;
   }
   if (!b.pend_send.empty() || !b.pend_recv.empty()) b.end();

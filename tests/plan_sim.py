@@ -63,7 +63,13 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
     from the d2h pieces, each copied right after its op completed."""
     P = len(sbufs)
     esz = np.dtype(O.NP_DTYPES[dtype]).itemsize
-    count = sbufs[0].size
+    blocks = coll in ("gather", "scatter", "alltoall")
+    if coll != "scatter":
+        count = sbufs[0].size
+    if coll == "scatter":   # only the root's sbuf (P blocks) is read
+        count = sbufs[root].size // P
+    elif coll == "alltoall":
+        count = sbufs[0].size // P
     plans, bufs, stg, host_in, host_out = [], [], [], [], []
     for r in range(P):
         prims, tmp = pico_amd.plan(coll, algo, P, r, count=count, rcounts=rcounts, root=root, esz=esz,
@@ -78,7 +84,12 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             stg.append(pico_amd.stage_plan(coll, algo, P, r, count=count, rcounts=rcounts, esz=esz,
                                            segsize=segsize, in_place=in_place, chunk_bytes=chunk_bytes,
                                            flat_ag=flat_ag, flat_rs=flat_rs))
-        if coll == "allgather":
+        if blocks:
+            # gather: rbuf on the root only; scatter: sbuf on the root only
+            sb = sbufs[r].copy() if sbufs[r] is not None else np.zeros(0, O.NP_DTYPES[dtype])
+            rn = {"gather": P * count if r == root else 0, "scatter": count, "alltoall": P * count}[coll]
+            rb = poison(np.empty(rn, O.NP_DTYPES[dtype]))
+        elif coll == "allgather":
             # in place: rbufs[r] already holds the rank's block where the
             # algorithm expects it (P * count elements)
             rb = np.array(rbufs[r]).copy() if in_place else poison(np.empty(P * count, O.NP_DTYPES[dtype]))
@@ -89,7 +100,7 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
             rb = poison(np.empty(max(rcounts[r], 1), O.NP_DTYPES[dtype]))
         else:
             rb = poison(np.empty(max(count, 1), O.NP_DTYPES[dtype]))
-        if coll != "allgather":
+        if coll != "allgather" and not blocks:
             sb = sbufs[r].copy()
         if in_place and coll != "allgather":
             if coll == "reduce_scatter":
@@ -236,8 +247,10 @@ def run(coll, algo, sbufs, dtype, op="sum", rcounts=None, root=0, segsize=0, in_
         rb = host_out[r] if stage else bufs[r][RB]
         if coll == "reduce_scatter":
             outs.append(rb[:rcounts[r]])
-        elif coll == "allgather":
+        elif coll in ("allgather", "alltoall") or (coll == "gather" and r == root):
             outs.append(rb[:P * count])
+        elif coll == "gather":
+            outs.append(rb[:0])
         else:
             outs.append(rb[:count])
     return outs

@@ -16,6 +16,7 @@ import pytest
 
 import _sub
 import golden_util as G
+import rooted_util as R
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -168,6 +169,22 @@ def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, ro
         torch.cuda.synchronize()
         rc, st = pico_amd.loopback_bcast(comms(P), algo, ds, n, dtype, root)
         outs = [from_dev(d, dtype, n) for d in ds]
+    elif coll in R.ROOTED:
+        # n = elements per block; gather: rbuf on the root only, scatter: sbuf
+        # on the root only (the others pass NULL, as pico_core does)
+        n = n if coll == "gather" else n // P
+        rn = [P * n if (coll != "gather" or r == root) and coll != "scatter" else n if coll == "scatter" else 0
+              for r in range(P)]
+        dr = [torch.zeros(k * esz + 64, dtype=torch.uint8, device="cuda:0") if k else None for k in rn]
+        if coll == "scatter":
+            ds = [d if r == root else None for r, d in enumerate(ds)]
+        torch.cuda.synchronize()
+        if coll == "alltoall":
+            rc, st = pico_amd.loopback_alltoall(comms(P), algo, ds, dr, n, dtype)
+        else:
+            fn = pico_amd.loopback_gather if coll == "gather" else pico_amd.loopback_scatter
+            rc, st = fn(comms(P), algo, ds, dr, n, dtype, root)
+        outs = [from_dev(d, dtype, k) if k else np.zeros(0, O.NP_DTYPES[dtype]) for d, k in zip(dr, rn)]
     else:
         dr = [torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda:0") if r == root else None for r in range(P)]
         if in_place:   # MPI_IN_PLACE at the root: its input already sits in its receive buffer
@@ -232,7 +249,20 @@ def test_collectives_match_reference_goldens(dev, key, cs, relay):
         if relay and P < 3:
             continue
         rk = G.rcounts(c) if coll == "reduce_scatter" else None
-        sb = G.inputs(c, sum(rk) if rk else N)
+        sb = G.inputs(c, sum(rk) if rk else N * P if coll in ("scatter", "alltoall") else N)
+        if coll in R.ROOTED:
+            # the reference's result where it delivers the collective, else the
+            # product's refusal (tests/rooted_util.py)
+            root = G.root(c)
+            want, exp = R.expect(coll, sb, dt, root, P, N)
+            outs, st = run_loopback(coll, algo, sb, dt, root=root, relay=relay)
+            if st != [exp] * P:
+                bad.append((c["id"], "status", st, exp))
+            elif not exp and c["status"] == "ok" and G.check_rank_outputs(c, outs):
+                bad.append((c["id"], "ranks"))
+            elif not exp and any(o.tobytes() != (b"" if w is None else w.tobytes()) for o, w in zip(outs, want)):
+                bad.append((c["id"], "vs-oracle"))
+            continue
         if relay and c["segsize"] and N * sb[0].itemsize > 512 * c["segsize"]:
             continue
         ip = c["rcounts"].endswith("_inplace")   # MPI_IN_PLACE cases (the reference's in-place paths)
@@ -280,6 +310,32 @@ def test_collectives_match_reference_goldens(dev, key, cs, relay):
             if want is None or any(sha(outs[r]) != sha(want[r]) for r in miss):
                 bad.append((c["id"], "ranks", miss))
     assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("flat", [0, 1], ids=["literal", "direct"])
+@pytest.mark.parametrize("coll", R.ROOTED)
+def test_rooted_collectives_large(dev, coll, flat):
+    """gather / scatter / alltoall at sizes past the fixtures' (blocks of
+    65,537 fp32 and 3 int64 elements, P = 2, 4, 8, two roots) in the literal
+    schedule and the direct form (bine_comm_set_flat_ag): bit-exact vs the
+    collective (the reference delivers it at these (P, root), rooted_util)"""
+    bad = []
+    for P in (2, 4, 8):
+        for c in comms(P):
+            c.set_flat_ag(flat)
+        try:
+            for dt, n in (("float", 65537), ("int64", 3)):
+                for root in ([0] if coll == "alltoall" else [0, P // 2]):
+                    sb = R.inputs(coll, dt, n, P, seed_base=77)
+                    want, exp = R.expect(coll, sb, dt, root, P, n)
+                    assert exp == 0
+                    outs, st = run_loopback(coll, "bine", sb, dt, root=root)
+                    if any(st) or any(o.tobytes() != (b"" if w is None else w.tobytes()) for o, w in zip(outs, want)):
+                        bad.append((coll, P, dt, root, st))
+        finally:
+            for c in comms(P):
+                c.set_flat_ag(0)
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("relay", [0, 4096], ids=["direct", "relay"])
@@ -689,6 +745,9 @@ PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
     (2, "REDUCE", "bine_bdw_over", "float", False, "1048576"),
     (2, "BCAST", "bine_lat_over", "float", False, "1048576"),
     (2, "BCAST", "bine_lat_new_over", "int64", False, "1048576"),
+    (2, "GATHER", "bine_over", "float", False, "1048576"),
+    (2, "SCATTER", "bine_over", "int64", False, "1048576"),
+    (2, "ALLTOALL", "bine_over", "float", True, "1048576"),
 ])
 def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat, count):
     """the reference's UNCHANGED pico_core (integration/Makefile links it against
@@ -736,7 +795,8 @@ OP_CHECK = os.path.join(ROOT, "integration", "_build", "op_check")
 @pytest.mark.parametrize("np_,flat", [(1, False), (2, False), (2, True)])
 def test_mpi_typed_entry_points_match_mpich(dev, np_, flat):
     """integration/op_check: libbine.so's MPI-typed entry points (allreduce,
-    reduce_scatter, reduce; host buffers) equal MPICH's own PMPI_* collectives
+    reduce_scatter, reduce, bcast, allgather, gather, scatter, alltoall; host
+    buffers) equal MPICH's own PMPI_* collectives
     for every order-independent (type, op) pair, and return MPI_ERR_OP where
     MPICH rejects the pair; 2 ranks share the GPU as above"""
     env = dict(os.environ, BINE_FAKE_HOSTS="1")

@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 import golden_util as G
+import rooted_util as R
 from oracle import oracle as O
 
 TABLES = os.path.join(G.GOLDEN, "tables.json")
@@ -37,6 +38,10 @@ def _run(c, ref_bugs=True):
     if c["coll"] == "bcast":
         f = O.bcast_bdw if c["algo"] in O.BC_BDW else O.bcast
         return f(c["algo"], G.inputs(c), dt, G.root(c))
+    if c["coll"] in ("gather", "scatter", "alltoall"):
+        sb = G.inputs(c, N if c["coll"] == "gather" else N * P)
+        outs, rets = R.replay(c["coll"], sb, dt, G.root(c), P)
+        return [np.zeros(0) if o is None else o for o in outs], rets
     sb = G.inputs(c)
     o, rets = O.reduce(c["algo"], sb, dt, c["op"])
     return [o] + [np.zeros(0)] * (P - 1), rets
@@ -87,15 +92,49 @@ def test_oracle_matches_reference_goldens(key, cs):
             # variant's tmp_buf overflow at N=333 with 8-byte types,
             # libbine_allreduce.c:724); nothing to pin against
             continue
+        if rets and rets[0] in ("dangling", "oob"):
+            # the reference left a message unreceived in this (P, root) -- in
+            # the capture run (one mpiexec per (P, root)) the next case's
+            # receive from that rank takes it -- or read / wrote past a buffer
+            # and ran on: the outputs are not the case's own (the product
+            # refuses these pairs; test_rooted_replay_predicts_the_reference_failures)
+            continue
         if list(rets) != c["rets"]:
             bad.append((c["id"], "rets", rets, c["rets"]))
             continue
         if any(rets):
             continue
         miss = G.check_rank_outputs(c, out)
+        if miss and c["coll"] in R.ROOTED:
+            # where the reference returns a wrong result, part of it comes from
+            # its uninitialised temporaries: only the defined elements pin
+            exp = G.outputs(c)
+            mask = R.defined(c["coll"], c["P"], G.root(c), c["N"])
+            miss = [r for r in miss if exp is None or
+                    np.asarray(out[r])[:c["outn"][r]][mask[r]].tobytes() != exp[r][mask[r]].tobytes()]
         if miss:
             bad.append((c["id"], "ranks", miss))
     assert not bad, bad[:10]
+
+
+def test_rooted_replay_predicts_the_reference_failures():
+    """gather / scatter / alltoall: where the reference hung or crashed in the
+    capture (no output), the replay says hang, crash or out of bounds; where
+    it completed, the replay does not say hang or crash"""
+    seen = collections.Counter()
+    for c in G.cases():
+        if c["coll"] not in R.ROOTED:
+            continue
+        P, N = c["P"], c["N"]
+        sb = G.inputs(c, N if c["coll"] == "gather" else N * P)
+        _, rets = R.replay(c["coll"], sb, c["dtype"], G.root(c), P)
+        kind = rets[0] if isinstance(rets[0], str) else "ok"
+        seen[(c["status"], kind)] += 1
+        if c["status"] == "ok":
+            assert kind in ("ok", "dangling", "oob"), (c["id"], kind)
+        else:
+            assert kind in ("hang", "crash", "oob") or (c["coll"] == "scatter" and P == 1), (c["id"], kind)
+    assert seen[("ok", "ok")] >= 500 and seen[("no_output", "crash")] >= 100, seen
 
 
 def test_fill_matches_pico_core_generator():

@@ -158,6 +158,46 @@ def bcast_bdw_jobs():
     return jobs
 
 
+ROOTED = ("gather", "scatter", "alltoall")
+
+
+def _replay_hangs(O, coll, P, root):
+    """the oracle's message-level replay of the reference deadlocks here"""
+    n = 1
+    sb = [np.arange(n if coll == "gather" else n * P, dtype=np.int32) for _ in range(P)]
+    progs = (O._gather_progs(P, n, root, sb, np.zeros(P * n, np.int32)) if coll == "gather" else
+             O._scatter_progs(P, n, root, sb[root], [np.zeros(n, np.int32) for _ in range(P)])
+             if coll == "scatter" else O._alltoall_progs(P, n, sb, [np.zeros(P * n, np.int32) for _ in range(P)]))
+    try:
+        O._replay(P, None, progs)
+    except O._Stuck:
+        return True
+    except (ValueError, O._Crash):
+        pass
+    return False
+
+
+def rooted_jobs():
+    """gather_bine / scatter_bine / alltoall_bine (libbine_gather.c:16,
+    libbine_scatter.c:14, libbine_alltoall.c:14 -- SURVEY.md section 2 row 7):
+    N = elements per block; every root at P <= 8, a spread of roots at P = 16
+    (the reference is correct at some, hangs, crashes or returns a wrong
+    result at others: the fixtures pin which)"""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    jobs = []
+    for P in (1, 2, 3, 4, 5, 6, 7, 8, 16):
+        for coll in ROOTED:
+            roots = [0] if coll == "alltoall" else \
+                list(range(P)) if P <= 8 else [0, 1, 2, 4, 5, 8, 9, 14, 15]
+            for root in roots:
+                if _replay_hangs(O, coll, P, root):
+                    continue   # a deadlock: mpiexec would only time out (tests/test_oracle.py covers it)
+                jobs.append((P, coll, "bine", "sum", 0, f"root{root}", ["float", "int64", "int8"], [1, 2, 7, 64, 333],
+                             True))
+    return jobs
+
+
 def ops_jobs():
     """MPICH's logical and bitwise MPI_Ops through the reference's collectives
     (logical ops on sparsified inputs -- zeros, -0.0, NaN -- so that both truth
@@ -295,6 +335,11 @@ def main():
             keep = {c["id"] for c in index}
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(bcast_bdw_jobs(), index, arrays)
+        if only == "rooted":
+            index = [c for c in old if c["coll"] not in ROOTED]
+            keep = {c["id"] for c in index}
+            arrays = {k: v for k, v in prev.items() if k in keep}
+            return capture(rooted_jobs(), index, arrays)
         index = [c for c in old if c["coll"] != only]
         arrays = {k: v for k, v in prev.items() if not k.startswith(only + ".")}
         jobs = {"allgather": allgather_jobs, "bcast": bcast_jobs}[only]()
@@ -342,6 +387,7 @@ def main():
     jobs += inplace_jobs()
     jobs += bcast_jobs()
     jobs += bcast_bdw_jobs()
+    jobs += rooted_jobs()
     capture(jobs, [], {})
 
 
@@ -349,7 +395,9 @@ def capture(jobs, index, arrays):
     for (P, coll, algo, op, seg, rk, dts, ns, store) in jobs:
         # the reference hangs on some shapes (e.g. odd P in the any_even
         # variants): a short limit, then the cases are re-run one by one
-        recs = run_case(P, coll, algo, op, seg, rk, dts, ns, timeout=60 if coll in ("allgather", "bcast") else 120)
+        short = coll in ("allgather", "bcast")
+        # the rooted collectives' fixtures are tiny: a hang shows within seconds
+        recs = run_case(P, coll, algo, op, seg, rk, dts, ns, timeout=15 if coll in ROOTED else 60 if short else 120)
         if any(r[2] is None for r in recs):
             # one crashing case (e.g. the static variant's tmp_buf overflow,
             # libbine_allreduce.c:724 vs :749-765) kills the whole mpiexec:
@@ -358,7 +406,7 @@ def capture(jobs, index, arrays):
             for rec in recs:
                 if rec[2] is None:
                     rec = run_case(P, coll, algo, op, seg, rk, [rec[0]], [rec[1]],
-                                   timeout=20 if coll in ("allgather", "bcast") else 120)[0]
+                                   timeout=5 if coll in ROOTED else 20 if short else 120)[0]
                 fixed.append(rec)
             recs = fixed
         for dt, n, rets, outs, failed in recs:
