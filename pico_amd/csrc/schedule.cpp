@@ -2116,7 +2116,37 @@ void rooted_blocks(Builder &b, const PlanArgs &a) {
   }
   const uint64_t c = a.count;
   const int map[3] = {SB, RB, T0};
-  const BProg &me = pg[(size_t)r];
+  BProg &me = pg[(size_t)r];
+  // runs of block copies that continue each other (alltoall's staging and
+  // compaction, its final permutation) become one copy each -- unless the
+  // merged source and destination overlap in one buffer (a forward compaction
+  // must stay block by block); message matching is by index, so only copies
+  // are merged and the send / receive indices are remapped
+  {
+    std::vector<BOp> ops;
+    std::vector<int> idx(me.ops.size());
+    for (size_t i = 0; i < me.ops.size(); i++) {
+      const BOp &o = me.ops[i];
+      if (o.kind == 0 && !ops.empty()) {
+        BOp &q = ops.back();
+        const bool cont = q.kind == 0 && q.sbuf == o.sbuf && q.buf == o.buf && q.soff + q.n == o.soff &&
+                          q.off + q.n == o.off;
+        const bool apart = o.sbuf != o.buf || q.soff + q.n + o.n <= q.off || q.off + q.n + o.n <= q.soff;
+        if (cont && apart) {
+          q.n += o.n;
+          idx[i] = -1;
+          continue;
+        }
+      }
+      idx[i] = (int)ops.size();
+      ops.push_back(o);
+    }
+    std::vector<int> m2(ops.size(), -1);
+    for (size_t i = 0; i < me.ops.size(); i++)
+      if (idx[i] >= 0) m2[(size_t)idx[i]] = match[(size_t)r][i];
+    me.ops.swap(ops);
+    match[(size_t)r].swap(m2);
+  }
   if (me.size[BT]) b.tmp(T0, (uint64_t)me.size[BT] * c);
   for (size_t i = 0; i < me.ops.size(); i++) {
     const BOp &o = me.ops[i];

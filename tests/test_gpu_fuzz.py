@@ -167,6 +167,40 @@ def test_random_bcast_bit_exact(dev_fuzz, seed):
     assert not bad, bad[:6]
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_random_rooted_bit_exact(dev_fuzz, seed):
+    """gather / scatter / alltoall (round 5): random P, root, type, block size,
+    direct form, relay, vs the collective where the reference delivers it and
+    the refusal elsewhere (tests/rooted_util.py; tests/test_oracle.py pins the
+    replay that decides)"""
+    import rooted_util as R
+    rng = random.Random(7000 + seed)
+    bad = []
+    try:
+        for _ in range(30):
+            coll = rng.choice(R.ROOTED)
+            P = rng.choice([1, 2, 3, 4, 4, 6, 8, 8, 16])
+            root = 0 if coll == "alltoall" else rng.choice([0, 0, rng.randrange(P)])
+            dt = rng.choice(list(OPS_OF))
+            n = rng.choice([1, 2, 7, 64, 333, 1000, 4097, rng.randint(1, 20000)])
+            flat, relay = rng.random() < 0.4, rng.choice([0, 0, 64, 4096])
+            sb = R.inputs(coll, dt, n, P, seed_base=31 + seed)
+            want, exp = R.expect(coll, sb, dt, root, P, n)
+            for c in comms(P):
+                c.set_flat_ag(flat)
+            outs, st = run_loopback(coll, "bine", sb, dt, root=root, relay=relay)
+            if list(st) != [exp] * P:
+                bad.append((coll, P, root, dt, n, flat, relay, "status", st, exp))
+            elif not exp and any(o.tobytes() != (b"" if w is None else w.tobytes()) for o, w in zip(outs, want)):
+                bad.append((coll, P, root, dt, n, flat, relay, "data"))
+    finally:
+        for P in (1, 2, 3, 4, 6, 8, 16):
+            for c in comms(P):
+                c.set_relay(0)
+                c.set_flat_ag(False)
+    assert not bad, bad[:6]
+
+
 @pytest.fixture(scope="module")
 def dev_fuzz():
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
