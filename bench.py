@@ -1037,12 +1037,25 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         best = min(ok_c, key=trials.get) if ok_c else base_cfg
         if rank == 0:
             print(f"bench: the direct transport failed in trial {dm_dead[0]}; picking {tname(best)}", file=sys.stderr)
+    def full_run(cfg):
+        """(stats, ok, digest) of a full timed run of cfg; a library error
+        (e.g. a direct-transport wait that timed out: BINE_ERR_INTERNAL on the
+        next call) is a failed check, never the end of the bench"""
+        try:
+            apply_transport(comm, *cfg)
+            rbuf.fill_(float("nan"))
+            st_ = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
+            return (st_,) + parity(cfg[0])
+        except pico_amd.BineError as e:
+            if rank == 0:
+                print(f"bench: {tname(cfg)} failed in its full run: {e}", file=sys.stderr)
+            torch.cuda.synchronize()
+            return ({"median_ms": float("inf")}, False, None)
+
     run1 = None
     if best != base_cfg:
-        apply_transport(comm, *best)
-        rbuf.fill_(float("nan"))
-        st1 = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
-        run1 = (st1,) + parity(best[0])
+        run1 = full_run(best)
+        st1 = run1[0]
         if rank == 0 and (run1[1] is False or run1[0]["median_ms"] >= st0["median_ms"]):
             print(f"bench: the trials' pick {tname(best)} timed in full: {run1[0]['median_ms']:.4f} ms, parity "
                   f"{run1[1]}" + (" (a direct-transport wait timed out)" if dm_wgs(best[0]) is not None and
@@ -1054,10 +1067,8 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             nxt = runner_up(trials, best, base_cfg)
             if nxt is not None:
                 best = nxt
-                apply_transport(comm, *best)
-                rbuf.fill_(float("nan"))
-                st1 = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
-                run1 = (st1,) + parity(best[0])
+                run1 = full_run(best)
+                st1 = run1[0]
                 if rank == 0:
                     print(f"bench: runner-up {tname(best)} timed in full: {st1['median_ms']:.4f} ms, parity "
                           f"{run1[1]}", file=sys.stderr)

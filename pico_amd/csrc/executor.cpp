@@ -1071,6 +1071,10 @@ static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int 
   std::vector<DmFusedArgs> v;
   if (!plan_fused(c, sc, ptr, esz, dtype, op, single, v)) return -1;
   auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (rt->dm->poisoned()) {  // as exchange(): a dead transport's launches would exit at once, moving nothing
+    set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
+    return BINE_ERR_INTERNAL;
+  }
   for (size_t i = 0; i < v.size(); i++) {
     v[i].stamps = rt->dm->stamps;
     v[i].serial = rt->dm->serial++;

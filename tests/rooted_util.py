@@ -18,11 +18,18 @@ ERR_ROOT, ERR_SIZE = 8, 2   # bine_status_t
 
 def intended(coll, sbufs, root, P, n):
     """the collective itself: per-rank outputs (gather: the root's only)"""
+    dt = np.asarray(sbufs[root if coll == "scatter" else 0]).dtype   # (np.concatenate drops pair types' padding)
+
+    def cat(parts):
+        out = np.zeros(P * n, dt)
+        for k, x in enumerate(parts):
+            out[k * n:(k + 1) * n] = x
+        return out
     if coll == "gather":
-        return [np.concatenate([np.asarray(s)[:n] for s in sbufs]) if r == root else None for r in range(P)]
+        return [cat([np.asarray(s)[:n] for s in sbufs]) if r == root else None for r in range(P)]
     if coll == "scatter":
         return [np.asarray(sbufs[root])[r * n:(r + 1) * n] for r in range(P)]
-    return [np.concatenate([np.asarray(sbufs[s])[r * n:(r + 1) * n] for s in range(P)]) for r in range(P)]
+    return [cat([np.asarray(sbufs[s])[r * n:(r + 1) * n] for s in range(P)]) for r in range(P)]
 
 
 def replay(coll, sbufs, dt, root, P):
@@ -42,7 +49,7 @@ def expect(coll, sbufs, dt, root, P, n):
         return want, 0
     got, rets = replay(coll, sbufs, dt, root, P)
     ok = not isinstance(rets[0], str) and all(
-        (w is None) or (g is not None and np.asarray(g).tobytes() == np.asarray(w).tobytes())
+        (w is None) or (g is not None and O.canonical(np.asarray(g)) == O.canonical(np.asarray(w)))
         for g, w in zip(got, want))
     if ok:
         return want, 0

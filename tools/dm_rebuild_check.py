@@ -2,10 +2,11 @@
 """A direct transport disabled by a timed-out wait is rebuilt by the next
 bine_comm_set_direct(1) on every rank (executor.cpp): P processes on the one
 GPU; the wait limit is first set absurdly low (BINE_DIRECT_TIMEOUT_S=1e-7, so
-the first exchange times out and poisons the transport), the next call must
-report BINE_ERR_INTERNAL, then with the limit back at 10 s set_direct(1)
-rebuilds it and C3 allreduces (256 MiB fp32 per rank) match the committed
-oracle digest again.
+the first exchange times out and poisons the transport), a later call must
+report BINE_ERR_INTERNAL and bine_comm_direct_timed_out say so, then with the
+limit back at 10 s set_direct(1) rebuilds it and C3 allreduces (256 MiB fp32
+per rank) match the committed oracle digest again -- with per-exchange
+launches (16 MiB chunks) and with the one-launch k_dm_fused form (64 MiB).
 usage: python tools/dm_rebuild_check.py [P]   (exit 0 = every rank ok)"""
 import os
 import sys
@@ -40,29 +41,36 @@ def worker(rank, P, port, q):
         pico_amd.allreduce("bine_bdw_remap", sb, rb, n, "float", "sum", comm, stream=stream)
         stream.synchronize()
 
-    bench.apply_transport(comm, "flatrs+flat+dmt", 16 << 20)
-    poisoned = False
-    for _ in range(3):   # the first exchange times out; a later call reports it
+    # 16 MiB chunks: per-exchange launches; 64 MiB: the whole call as one
+    # k_dm_fused launch -- both must report a dead transport
+    for tag, chunk in (("", 16 << 20), ("_fused", 64 << 20)):
+        os.environ["BINE_DIRECT_TIMEOUT_S"] = "1e-7"
+        before = comm.fused_calls()
+        bench.apply_transport(comm, "flatrs+flat+dmt", chunk)   # (re)builds with the tiny limit
+        poisoned = False
+        for _ in range(3):   # the first exchange times out; a later call reports it
+            try:
+                call()
+            except pico_amd.BineError as e:
+                poisoned = "timed out" in str(e) or "poisoned" in str(e)
+                break
+        out["poisoned" + tag] = poisoned
+        out["timed_out" + tag] = comm.direct_timed_out()
+        torch.cuda.synchronize()
+        os.environ["BINE_DIRECT_TIMEOUT_S"] = "10"
         try:
-            call()
+            bench.apply_transport(comm, "flatrs+flat+dmt", chunk)   # rebuilds (collective)
+            ok = not comm.direct_timed_out()
+            for _ in range(3):
+                rb.fill_(float("nan"))
+                call()
+                o, _ = bench.check_digest(pico_amd, rb, n, "float", key, rank, stream)
+                ok = ok and bool(o)
+            out["rebuilt_ok" + tag] = ok
+            out["fused_launches" + tag] = comm.fused_calls() - before
         except pico_amd.BineError as e:
-            poisoned = "timed out" in str(e) or "poisoned" in str(e)
-            break
-    out["poisoned"] = poisoned
-    torch.cuda.synchronize()
-    os.environ["BINE_DIRECT_TIMEOUT_S"] = "10"
-    try:
-        bench.apply_transport(comm, "flatrs+flat+dmt", 16 << 20)   # rebuilds (collective)
-        ok = True
-        for _ in range(3):
-            rb.fill_(float("nan"))
-            call()
-            o, _ = bench.check_digest(pico_amd, rb, n, "float", key, rank, stream)
-            ok = ok and bool(o)
-        out["rebuilt_ok"] = ok
-    except pico_amd.BineError as e:
-        out["rebuilt_ok"] = False
-        out["error"] = str(e)
+            out["rebuilt_ok" + tag] = False
+            out["error" + tag] = str(e)
     comm.destroy()
     dist.destroy_process_group()
     q.put((rank, out))
@@ -86,6 +94,8 @@ if __name__ == "__main__":
     while not q.empty():
         r, o = q.get()
         res[r] = o
-    ok = len(res) == P and all(o["poisoned"] and o["rebuilt_ok"] for o in res.values())
+    ok = len(res) == P and all(o["poisoned"] and o["rebuilt_ok"] and o["poisoned_fused"] and o["rebuilt_ok_fused"]
+                               and o["timed_out"] and o["timed_out_fused"] and o["fused_launches_fused"] > 0
+                               for o in res.values())
     print(f"RESULT P={P}: {'ok' if ok else 'FAILED'} {res} exitcodes {[p.exitcode for p in ps]}", flush=True)
     sys.exit(0 if ok else 1)
