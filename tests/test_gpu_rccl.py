@@ -171,3 +171,16 @@ def test_direct_fused_large_collectives(P):
     bad = [x for x in r.stdout.splitlines() if "MISMATCH" in x or "RESULT" in x or " ok, " in x]
     assert r.returncode == 0, "\n".join(bad[:40]) + "\n" + r.stderr[-2000:]
     assert f"RESULT P={P}" in r.stdout
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("P", [2, 4])
+def test_rooted_collectives_processes(P):
+    """gather / scatter / alltoall (round 5) in P real processes: RCCL P2P
+    and the direct transport, literal schedule and direct form, graph mode;
+    bit-exact vs the collective (tools/rooted_check.py)"""
+    env = dict(os.environ, PYTHONPATH=ROOT, BINE_FAKE_HOSTS="1")
+    r = _sub.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rooted_check.py"), str(P)], env=env,
+                 timeout=280, ranks=P)
+    assert r.returncode == 0, r.stdout[-3000:] + "\n" + r.stderr[-2000:]
+    assert f"RESULT P={P}" in r.stdout

@@ -27,8 +27,6 @@ def worker(rank, P, port, q):
     import bench
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
-    with bench.quiet_stdout():
-        comm = pico_amd.Comm.from_torch_distributed(0)
     stream = torch.cuda.Stream()
     n = bench.C3_ELEMS
     sb = torch.empty(n, dtype=torch.float32, device="cuda:0")
@@ -44,7 +42,11 @@ def worker(rank, P, port, q):
     # 16 MiB chunks: per-exchange launches; 64 MiB: the whole call as one
     # k_dm_fused launch -- both must report a dead transport
     for tag, chunk in (("", 16 << 20), ("_fused", 64 << 20)):
+        # a fresh communicator per form: the wait limit is read when the
+        # transport is built, and a healthy transport is not rebuilt
         os.environ["BINE_DIRECT_TIMEOUT_S"] = "1e-7"
+        with bench.quiet_stdout():
+            comm = pico_amd.Comm.from_torch_distributed(0)
         before = comm.fused_calls()
         bench.apply_transport(comm, "flatrs+flat+dmt", chunk)   # (re)builds with the tiny limit
         poisoned = False
@@ -71,7 +73,8 @@ def worker(rank, P, port, q):
         except pico_amd.BineError as e:
             out["rebuilt_ok" + tag] = False
             out["error" + tag] = str(e)
-    comm.destroy()
+        torch.cuda.synchronize()
+        comm.destroy()
     dist.destroy_process_group()
     q.put((rank, out))
 
