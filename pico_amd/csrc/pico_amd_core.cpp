@@ -1,7 +1,8 @@
 // pico_amd_core.cpp -- device-resident benchmark driver for the MI355X library
 // with pico_core's command line, environment and output files, so the
 // reference's campaign scripts and plot/ tooling read its results unchanged
-// (SURVEY.md 8(f) rank 3).
+// (SURVEY.md 8(f) rank 3).  Every COLLECTIVE_TYPE of pico_core:
+// ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER, BCAST, GATHER, SCATTER, ALLTOALL.
 //
 //   mpiexec -n P pico_amd_core <count> <iterations> <algorithm> <dtype>
 //
@@ -56,7 +57,7 @@ const Dtype *find_dtype(const char *s) {
   return nullptr;
 }
 
-enum Coll { ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER };
+enum Coll { ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER, BCAST, GATHER, SCATTER, ALLTOALL };
 
 int fail(const char *msg) {
   fprintf(stderr, "pico_amd_core: %s. Aborting...\n", msg);
@@ -156,7 +157,11 @@ int main(int argc, char **argv) {
   else if (!strcmp(ct, "REDUCE_SCATTER")) { coll = REDUCE_SCATTER; cname = "reduce_scatter"; }
   else if (!strcmp(ct, "REDUCE")) { coll = REDUCE; cname = "reduce"; }
   else if (!strcmp(ct, "ALLGATHER")) { coll = ALLGATHER; cname = "allgather"; }
-  else return die("COLLECTIVE_TYPE not provided by this library (ALLREDUCE, REDUCE_SCATTER, REDUCE, ALLGATHER)");
+  else if (!strcmp(ct, "BCAST")) { coll = BCAST; cname = "bcast"; }
+  else if (!strcmp(ct, "GATHER")) { coll = GATHER; cname = "gather"; }
+  else if (!strcmp(ct, "SCATTER")) { coll = SCATTER; cname = "scatter"; }
+  else if (!strcmp(ct, "ALLTOALL")) { coll = ALLTOALL; cname = "alltoall"; }
+  else return die("unknown COLLECTIVE_TYPE");
 
   const int algo = bine_algo_from_name(cname, algorithm);
   if (algo < 0) return die("unknown algorithm");
@@ -186,9 +191,12 @@ int main(int argc, char **argv) {
   const char *dev_env = getenv("BINE_DEVICE");
   (void)hipSetDevice(dev_env ? atoi(dev_env) : lrank % ndev);
 
+  // sizes as pico_core's allocators (pico_core_*_utils.c): the root-only
+  // buffers (gather's rbuf, scatter's sbuf) are passed as NULL elsewhere;
+  // bcast runs in place on the send buffer
   const size_t local_count = count / (size_t)P;
-  const size_t s_elems = coll == ALLGATHER ? local_count : count;
-  const size_t r_elems = coll == REDUCE_SCATTER ? local_count : count;
+  const size_t s_elems = coll == ALLGATHER || coll == GATHER ? local_count : count;
+  const size_t r_elems = coll == REDUCE_SCATTER || coll == SCATTER ? local_count : coll == BCAST ? 0 : count;
   void *sbuf = nullptr, *rbuf = nullptr;
   if (hipMalloc(&sbuf, s_elems * dt->size + 16) != hipSuccess || hipMalloc(&rbuf, r_elems * dt->size + 16) != hipSuccess)
     return die("device allocation failed");
@@ -197,6 +205,8 @@ int main(int argc, char **argv) {
   const uint32_t seed = (uint32_t)(seed_env ? strtoul(seed_env, nullptr, 10) : (unsigned long)time(nullptr)) + (uint32_t)rank;
   if (bine_fill_pico(sbuf, s_elems, dt->bine, seed, nullptr) != BINE_SUCCESS) return die("input generation failed");
   (void)hipDeviceSynchronize();
+  std::vector<char> hs(s_elems * dt->size), hr(r_elems * dt->size), gt(r_elems * dt->size);
+  (void)hipMemcpy(hs.data(), sbuf, hs.size(), hipMemcpyDeviceToHost);  // the inputs (bcast: overwritten below)
 
   // ---- timed loop (one barrier before, one after every iteration) ----
   std::vector<int> rcounts((size_t)P, (int)local_count);
@@ -218,6 +228,20 @@ int main(int argc, char **argv) {
       case ALLGATHER:
         ret = ((int (*)(BINE_ALLGATHER_ARGS))fn)(sbuf, local_count, dt->mpi, rbuf, local_count, dt->mpi, comm);
         break;
+      case BCAST:
+        ret = ((int (*)(BINE_BCAST_ARGS))fn)(sbuf, count, dt->mpi, 0, comm);
+        break;
+      case GATHER:
+        ret = ((int (*)(BINE_GATHER_ARGS))fn)(sbuf, local_count, dt->mpi, rank == 0 ? rbuf : nullptr, local_count,
+                                              dt->mpi, 0, comm);
+        break;
+      case SCATTER:
+        ret = ((int (*)(BINE_GATHER_ARGS))fn)(rank == 0 ? sbuf : nullptr, local_count, dt->mpi, rbuf, local_count,
+                                              dt->mpi, 0, comm);
+        break;
+      case ALLTOALL:
+        ret = ((int (*)(BINE_ALLGATHER_ARGS))fn)(sbuf, local_count, dt->mpi, rbuf, local_count, dt->mpi, comm);
+        break;
     }
     times[(size_t)i] = MPI_Wtime() - t0;
     MPI_Barrier(comm);
@@ -228,8 +252,6 @@ int main(int argc, char **argv) {
   }
 
   // ---- ground truth: PMPI_* of the same MPI on host copies ----
-  std::vector<char> hs(s_elems * dt->size), hr(r_elems * dt->size), gt(r_elems * dt->size);
-  (void)hipMemcpy(hs.data(), sbuf, hs.size(), hipMemcpyDeviceToHost);
   (void)hipMemcpy(hr.data(), rbuf, hr.size(), hipMemcpyDeviceToHost);
   bool ok = true;
   switch (coll) {
@@ -248,6 +270,25 @@ int main(int argc, char **argv) {
     case ALLGATHER:
       PMPI_Allgather(hs.data(), (int)local_count, dt->mpi, gt.data(), (int)local_count, dt->mpi, comm);
       ok = same(hr.data(), gt.data(), local_count * (size_t)P, dt, P);
+      break;
+    case BCAST: {  // the root's input, broadcast by MPICH, vs every rank's buffer after the run
+      std::vector<char> now(hs.size());
+      (void)hipMemcpy(now.data(), sbuf, now.size(), hipMemcpyDeviceToHost);
+      PMPI_Bcast(hs.data(), (int)count, dt->mpi, 0, comm);
+      ok = memcmp(now.data(), hs.data(), hs.size()) == 0;
+      break;
+    }
+    case GATHER:
+      PMPI_Gather(hs.data(), (int)local_count, dt->mpi, gt.data(), (int)local_count, dt->mpi, 0, comm);
+      ok = rank != 0 || memcmp(hr.data(), gt.data(), count * dt->size) == 0;
+      break;
+    case SCATTER:
+      PMPI_Scatter(hs.data(), (int)local_count, dt->mpi, gt.data(), (int)local_count, dt->mpi, 0, comm);
+      ok = memcmp(hr.data(), gt.data(), local_count * dt->size) == 0;
+      break;
+    case ALLTOALL:
+      PMPI_Alltoall(hs.data(), (int)local_count, dt->mpi, gt.data(), (int)local_count, dt->mpi, comm);
+      ok = memcmp(hr.data(), gt.data(), count * dt->size) == 0;
       break;
   }
   int all_ok = 0, mine = ok ? 1 : 0;

@@ -703,7 +703,11 @@ def test_rccl_single_rank(dev):
 @pytest.mark.parametrize("coll,algo,dtype", [("ALLREDUCE", "bine_bdw_remap_over", "float"),
                                              ("REDUCE_SCATTER", "bine_permute_remap_over", "int64"),
                                              ("ALLGATHER", "k_bruck_over", "double"),
-                                             ("REDUCE", "bine_bdw_over", "int32")])
+                                             ("REDUCE", "bine_bdw_over", "int32"),
+                                             ("BCAST", "bine_lat_over", "float"),
+                                             ("GATHER", "bine_over", "int32"),
+                                             ("SCATTER", "bine_over", "double"),
+                                             ("ALLTOALL", "bine_over", "int64")])
 def test_pico_amd_core_writes_pico_core_csv(dev, tmp_path, coll, algo, dtype):
     """pico_amd_core: pico_core's CLI / env / ground-truth check / CSV layout,
     buffers in HBM, calls through libbine.so's libbine.h symbols.  One rank
@@ -720,6 +724,24 @@ def test_pico_amd_core_writes_pico_core_csv(dev, tmp_path, coll, algo, dtype):
     assert lines[0] == "highest,rank0" and len(lines) == 6
     assert all(int(x.split(",")[0]) > 0 for x in lines[1:])
     assert (tmp_path / "alloc_1_GPU.csv").read_text().startswith("MPI_Rank,allocation\n0,")
+
+
+@pytest.mark.parametrize("coll,algo,dtype", [("BCAST", "bine_bdw_remap_over", "float"),
+                                             ("GATHER", "bine_over", "int64"), ("SCATTER", "bine_over", "float"),
+                                             ("ALLTOALL", "bine_over", "int8"), ("ALLREDUCE", "bine_bdw_remap_over", "int32")])
+def test_pico_amd_core_two_ranks(dev, tmp_path, coll, algo, dtype):
+    """pico_amd_core with 2 ranks sharing the GPU (distinct RCCL host ids):
+    every rank's result checked against MPICH's PMPI_* collective, as
+    pico_core does, for the round-5 collectives"""
+    exe = os.path.join(ROOT, "pico_amd", "lib", "pico_amd_core")
+    env = dict(os.environ, COLLECTIVE_TYPE=coll, OUTPUT_DIR=str(tmp_path), DATA_DIR=str(tmp_path),
+               OUTPUT_LEVEL="summarized", LOCATION="local", SEGMENTED="no", PICO_SEED="99", BINE_FAKE_HOSTS="1",
+               PATH="/opt/conda/bin:" + os.environ.get("PATH", ""))
+    p = _sub.run_kw(["/opt/conda/bin/mpiexec", "-n", "2", exe, "1048576", "4", algo, dtype], env=env,
+                    capture_output=True, text=True, timeout=150, ranks=2)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "Last Iter Time" in p.stdout
+    assert len((tmp_path / f"1048576_{algo}_{dtype}.csv").read_text().splitlines()) == 5
 
 
 PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
