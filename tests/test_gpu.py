@@ -737,8 +737,11 @@ def test_pico_amd_core_two_ranks(dev, tmp_path, coll, algo, dtype):
     env = dict(os.environ, COLLECTIVE_TYPE=coll, OUTPUT_DIR=str(tmp_path), DATA_DIR=str(tmp_path),
                OUTPUT_LEVEL="summarized", LOCATION="local", SEGMENTED="no", PICO_SEED="99", BINE_FAKE_HOSTS="1",
                PATH="/opt/conda/bin:" + os.environ.get("PATH", ""))
-    p = _sub.run_kw(["/opt/conda/bin/mpiexec", "-n", "2", exe, "1048576", "4", algo, dtype], env=env,
-                    capture_output=True, text=True, timeout=150, ranks=2)
+    cmd = ["/opt/conda/bin/mpiexec"]
+    for r in range(2):   # one RCCL host id per rank: two ranks on ONE GPU (integration/run_pico_core.sh)
+        cmd += ([":"] if r else []) + ["-n", "1", "-env", "NCCL_HOSTID", f"fake-host-{r}", "-env",
+                                       "NCCL_SOCKET_IFNAME", "lo", exe, "1048576", "4", algo, dtype]
+    p = _sub.run_kw(cmd, env=env, capture_output=True, text=True, timeout=150, ranks=2)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "Last Iter Time" in p.stdout
     assert len((tmp_path / f"1048576_{algo}_{dtype}.csv").read_text().splitlines()) == 5
