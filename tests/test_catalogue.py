@@ -1,6 +1,7 @@
 """config/algorithm_config_mi355x.json (tools/make_catalogue.py): every entry
 resolves to a library algorithm through pico_core's selector string, and its
-comm_sz constraints are exactly the sizes the planner accepts (P = 1 ... 16), so
+comm_sz constraints are exactly the sizes the planner accepts (P = 1 ... 16; root 0,
+pico_core's), so
 the reference's parse_test.py never schedules a run the library refuses."""
 import json
 import os
@@ -55,4 +56,4 @@ def test_entries_resolve_and_constraints_match_planner():
                 # rules out the single-rank copy of reduce_scatter any_even)
                 assert planned == allowed or (P == 1 and planned and not allowed), (coll, sel, P)
             n += 1
-    assert n == 35   # 8 + 9 + 2 reduce family, 12 allgather, 4 bcast
+    assert n == 41   # 8 + 9 + 2 reduce family, 12 allgather, 7 bcast, alltoall, gather, scatter

@@ -82,6 +82,17 @@ ENTRIES = [
      "Bine binomial tree, negabinary partners, any root (:373)."),
     ("BCAST", "bine_lat_i_new", "bine_lat_i_new_over", [POW2], ["bine", "latency_optimal"],
      "Bine binomial tree, negabinary partners, non-blocking sends (:408)."),
+    ("BCAST", "scatter_allgather", "scatter_allgather_over", [COUNT_GE_P], ["bandwidth_optimal"],
+     "Binomial scatter + recursive-doubling allgather (:42)."),
+    ("BCAST", "bine_bdw_static", "bine_bdw_static_over", [POW2, COUNT_GE_P], ["bine", "bandwidth_optimal", "static"],
+     "Bine static-table scatter + allgather, root 0 (:462)."),
+    ("BCAST", "bine_bdw_remap", "bine_bdw_remap_over", [POW2], ["bine", "bandwidth_optimal", "remap"],
+     "Bine remapped scatter + allgather, root 0 (:649)."),
+    ("ALLTOALL", "bine", "bine_over", [POW2], ["bine"], "Bine butterfly (libbine_alltoall.c:14)."),
+    ("GATHER", "bine", "bine_over", [POW2], ["bine"],
+     "Bine tree, root 0 and the even roots the reference serves (libbine_gather.c:16)."),
+    ("SCATTER", "bine", "bine_over", [POW2], ["bine"],
+     "Bine tree, root 0 and the roots the reference serves (libbine_scatter.c:14)."),
 ]
 
 
