@@ -39,6 +39,10 @@ CASES = [
     ("allgather", "k_bruck", "double", 7),
     ("allgather", "sparbit", "float", 5),
     ("allgather", "bine_block_by_block", "float", 9),
+    # gather / scatter / alltoall (round 5): n = elements per block, root 0
+    ("gather", "bine", "float", 7),
+    ("scatter", "bine", "int64", 5),
+    ("alltoall", "bine", "float", 3),
 ]
 # the flat reduce-scatter + flat allgather phases (one all-peers exchange per
 # phase, REDUCE_TREE on the owner), executed from the issue schedule
@@ -59,6 +63,9 @@ FLAT_CASES = [
     ("reduce_scatter", "bine_block_by_block_any_even", "float", 64),
     ("allreduce", "ring", "float", 1000),
     ("reduce_scatter", "ring", "double", 64),
+    ("gather", "bine", "int8", 9),
+    ("scatter", "bine", "float", 4),
+    ("alltoall", "bine", "int64", 2),
 ]
 
 
@@ -77,6 +84,7 @@ def _worker(rank, P, port, q):
     import torch.distributed as dist
     import pico_amd
     from oracle import oracle as O
+    import rooted_util as R
     dist.init_process_group("gloo", rank=rank, world_size=P, init_method=f"tcp://127.0.0.1:{port}")
     bad = []
     for flat, (coll, algo, dtype, n) in [(False, c) for c in CASES] + [(True, c) for c in FLAT_CASES]:
@@ -85,7 +93,10 @@ def _worker(rank, P, port, q):
         rc = [n // P] * P if coll == "reduce_scatter" else None
         total = sum(rc) if rc else n
         sb = O.inputs(dtype, total, P)
-        if coll == "allgather":
+        if coll in R.ROOTED:
+            sb = R.inputs(coll, dtype, n, P)
+            want = R.expect(coll, sb, dtype, 0, P, n)[0][rank]
+        elif coll == "allgather":
             want = O.allgather(algo, sb, dtype)[0][rank]
         elif coll == "allreduce":
             want = O.allreduce(algo, sb, dtype, segsize=64)[0][rank]
@@ -100,7 +111,8 @@ def _worker(rank, P, port, q):
                                                 chunk_bytes=128, flat_rs=True, flat_ag=True, info=True)
             prims = [dict(x, group=k) for k, o in enumerate(ops) for x in o["prims"]]
             tmp = info["tmp_elems"]
-        out_n = rc[rank] if rc else (P * n if coll == "allgather" else n)
+        out_n = rc[rank] if rc else (P * n if coll in ("allgather", "alltoall") or (coll == "gather" and rank == 0)
+                                     else 0 if coll == "gather" else n)
         bufs = [sb[rank].copy(), np.zeros(max(out_n, 1), npdt)] + [np.zeros(int(t) + 1, npdt) for t in tmp]
 
         def v(b, off, cnt):
