@@ -1788,18 +1788,19 @@ void bc_bine_bdw_remap(Builder &b, const PlanArgs &a) {
     const int d = (int32_t)((((uint32_t)(mask << 1) - 1) ^ 0xAAAAAAAAu) - 0xAAAAAAAAu);  // negabinary_to_binary
     return r % 2 == 0 ? pmod(r + d, P) : pmod(r - d, P);
   };
-  int inv = 1 << (steps - 1), bfm = ~(inv - 1);
+  int inv = 1 << (steps - 1);
+  uint32_t bfm = ~(uint32_t)(inv - 1);  // (unsigned: the mask's shifts below are well defined; remaps are < P)
   const int recv_mask = r == 0 ? inv << 1 : (rr & -rr);
   bool recvd = r == 0;
   int mask = 1;
   for (; mask < P; mask <<= 1, inv >>= 1, bfm >>= 1) {  // :689-716
     const int pt = partner(mask);
     if (recvd) {
-      const int sf = (int)remap_rank((uint32_t)P, (uint32_t)pt) & bfm;
+      const int sf = (int)(remap_rank((uint32_t)P, (uint32_t)pt) & bfm);
       b.send(pt, RB, displ(sf), run(sf, sf + inv - 1));
       b.end();
     } else if (inv == recv_mask || pt == 0) {
-      const int rf = rr & bfm;
+      const int rf = (int)((uint32_t)rr & bfm);
       b.recv(pt, RB, displ(rf), run(rf, rf + inv - 1));
       b.end();
       recvd = true;
@@ -1807,15 +1808,15 @@ void bc_bine_bdw_remap(Builder &b, const PlanArgs &a) {
   }
   mask >>= 1;
   inv = 1;
-  bfm = ~0;
+  bfm = ~0u;
   for (; mask > 0; mask >>= 1, inv <<= 1, bfm <<= 1) {  // :719-751
     const int pt = partner(mask);
     if (inv != recv_mask) {
-      const int sf = rr & bfm;
+      const int sf = (int)((uint32_t)rr & bfm);
       b.send(pt, RB, displ(sf), run(sf, sf + inv - 1));
     }
     if (inv >= recv_mask) {
-      const int rf = (int)remap_rank((uint32_t)P, (uint32_t)pt) & bfm;
+      const int rf = (int)(remap_rank((uint32_t)P, (uint32_t)pt) & bfm);
       b.recv(pt, RB, displ(rf), run(rf, rf + inv - 1));
     }
     b.end();
@@ -1962,10 +1963,11 @@ void a2a_prog(int P, int x, BProg &p) {
   const int L = log2_ceil(P);
   std::vector<int> res((size_t)P), nxt;
   for (int i = 0; i < P; i++) res[(size_t)i] = i;
-  int nres = P, inv = L ? 1 << (L - 1) : 0, bfm = ~(inv - 1);
+  int nres = P, inv = L ? 1 << (L - 1) : 0;
+  uint32_t bfm = ~(uint32_t)(inv - 1);
   for (int mask = 1; mask < P; mask <<= 1, inv >>= 1, bfm >>= 1) {
     const int partner = nb_partner(x, mask, P);  // :59-64
-    const int64_t mins = remap_rank((uint32_t)P, (uint32_t)partner) & (uint32_t)bfm, maxs = mins + inv - 1;
+    const int64_t mins = remap_rank((uint32_t)P, (uint32_t)partner) & bfm, maxs = mins + inv - 1;
     int64_t ns = 0, nk = 0;
     nxt.clear();
     for (int i = 0; i < P; i++) {  // :71-94

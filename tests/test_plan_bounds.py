@@ -1,6 +1,7 @@
 """Host sanitizer sweep of the planner and the issue scheduler
 (tools/plan_bounds.cpp): schedule.cpp / issue.cpp / trees.cpp built with g++
--fsanitize=address,undefined, every algorithm of the four families x P x rank x
+-fsanitize=address,undefined, every algorithm (reduce family, allgather, bcast,
+gather / scatter / alltoall) x P x rank (x root) x
 sizes (ragged reduce-scatter blocks) x in / out of place x transport settings
 (flat allgather, flat reduce-scatter, multi-tree, relay, chunked), every
 primitive of the plan and of the issue schedule checked to stay inside the
@@ -19,7 +20,7 @@ CSRC = os.path.join(ROOT, "pico_amd", "csrc")
 EXE = os.path.join(ROOT, "tools", "_build", "plan_bounds")
 
 ALGOS = [0, 1, 2, 3, 4, 5, 6, 7, 16, 17, 18, 19, 20, 21, 22, 23, 24, 32, 33,
-         48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59]
+         48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 64, 65, 66, 67, 68, 69, 70, 80, 81, 82]
 # the flat reduce-scatter / multi-tree algorithms also up to P = 16 (16-leaf trees)
 P16 = [4, 5, 6, 20, 21, 22, 33]
 

@@ -3,7 +3,8 @@
 // and UndefinedBehaviorSanitizer (tests/test_plan_bounds.py builds and runs it;
 // no GPU, no HIP runtime).
 //
-// For every algorithm of the four families, P = 1..16, every rank, ragged and
+// For every algorithm (reduce family, allgather, bcast, gather / scatter /
+// alltoall), P = 1..16, every rank (and roots 0, P / 2, P - 1), ragged and
 // even sizes, in and out of place, and every transport setting (flat
 // allgather / flat reduce-scatter / multi-tree / relay, chunked or not) it
 // checks that each primitive of the plan AND of the issue schedule stays
@@ -73,14 +74,19 @@ void check_prim(const char *what, const PlanArgs &a, const Prim &p, const Bounds
 // the caller's buffers in elements, per the collective's MPI signature
 Bounds caller_bounds(const PlanArgs &a, const Plan &plan, uint64_t stage) {
   Bounds b{};
-  const int fam = a.algo / 16;  // 0 allreduce, 1 reduce_scatter, 2 reduce, 3 allgather
+  const int fam = a.algo / 16;  // 0 allreduce, 1 reduce_scatter, 2 reduce, 3 allgather, 4 bcast, 5 a2a/gather/scatter
   uint64_t total = 0;
   for (int x : a.rcounts) total += (uint64_t)x;
   uint64_t s = 0, r = 0;
+  const uint64_t all = (uint64_t)a.P * a.count;
   if (fam == 0) s = r = a.count;
   else if (fam == 1) { s = total; r = a.in_place ? total : (uint64_t)a.rcounts[(size_t)a.rank]; }
   else if (fam == 2) { s = a.count; r = a.rank == a.root || a.in_place ? a.count : 0; }
-  else { s = a.count; r = (uint64_t)a.P * a.count; }
+  else if (fam == 3) { s = a.count; r = all; }
+  else if (fam == 4) s = r = a.count;  // in place on the one buffer
+  else if (a.algo == BINE_GA_BINE) { s = a.count; r = a.rank == a.root ? all : 0; }  // rbuf on the root only
+  else if (a.algo == BINE_SC_BINE) { s = a.rank == a.root ? all : 0; r = a.count; }  // sbuf on the root only
+  else s = r = all;
   // MPI_IN_PLACE: the executor maps SBUF onto the receive buffer (executor.cpp run_collective)
   b.lim[BINE_BUF_SBUF] = a.in_place ? r : s;
   b.lim[BINE_BUF_RBUF] = r;
@@ -125,7 +131,7 @@ int main(int argc, char **argv) {
   const int maxP = argc > 1 ? atoi(argv[1]) : 16;
   const int only = argc > 2 ? atoi(argv[2]) : -1;  // one algorithm id (-1: all)
   const int algos[] = {0, 1, 2, 3, 4, 5, 6, 7, 16, 17, 18, 19, 20, 21, 22, 23, 24, 32, 33,
-                       48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59};
+                       48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 64, 65, 66, 67, 68, 69, 70, 80, 81, 82};
   const size_t counts[] = {0, 1, 13, 1000};
   long plans = 0;
   for (int algo : algos)
@@ -134,11 +140,16 @@ int main(int argc, char **argv) {
         for (int rag = 0; rag < 2; rag++)
           for (int ip = 0; ip < 2; ip++)
             for (int mode = 0; mode < 8; mode++)
-              for (int rank = 0; rank < P; rank++) {
+              for (int rank = 0; rank < P; rank++)
+               for (int root : {0, P / 2, P - 1}) {
                 const int fam = algo / 16;
                 if (rag && fam != 1) continue;  // ragged blocks: reduce_scatter only
                 if (ip && fam == 2 && rank != 0) continue;  // in place only at the root (bine_reduce: ERR_ARG)
+                if (root && fam < 4) continue;  // rooted sweeps: bcast, gather, scatter
+                if (fam == 4 && !ip) continue;  // bcast: in place by definition
+                if ((root == P / 2 && P / 2 == 0) || (root == P - 1 && (P - 1 == P / 2 || P - 1 == 0))) continue;
                 PlanArgs a;
+                a.root = root;
                 a.algo = algo;
                 a.P = P;
                 a.rank = rank;
