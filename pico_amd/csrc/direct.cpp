@@ -165,6 +165,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (const char *e = getenv("BINE_DIRECT_SLOT_BYTES")) slot = (size_t)strtoull(e, nullptr, 10);
   if (const char *e = getenv("BINE_DIRECT_WGS")) wgs = atoi(e);
   if (const char *e = getenv("BINE_DIRECT_PULL_WGS")) pull_wgs = std::max(0, atoi(e));
+  if (const char *e = getenv("BINE_DIRECT_AUTOSCALE")) autoscale = atoi(e) != 0;
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
   if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
   if (const char *e = getenv("BINE_DIRECT_MCAST")) mcast = atoi(e) != 0;
@@ -441,7 +442,7 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
   const TreeSpec *ltree = tree;  // the tree of the launch being built
   // the messages that get workgroups of their own: standalone copies and the
   // leaders of push groups (members ride with their leader, leaves with the tree)
-  auto index_copies = [&]() {
+  auto index_copies = [&](bool plain) {
     a.ncopy = 0;
     a.ncw = 0;
     for (int i = 0; i < a.nmsg; i++) {
@@ -453,6 +454,26 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       a.cidx[a.ncopy] = i;
       a.cwgs[a.ncopy] = (m.push || !pull_wgs ? a.wgs : pull_wgs) * members;
       a.ncw += a.cwgs[a.ncopy++];
+    }
+    // a plain k_dm_move launch of few messages (one push and one pull of a
+    // Bine step, a rooted collective's single message) would leave most of
+    // the GPU idle at `wgs` workgroups each: every copy takes the same whole
+    // multiple of its workgroups that the resident capacity allows, keeping
+    // at least 64 KiB per workgroup.  The protocol does not care how many
+    // workgroups a copy has (each launch counts its own arrivals).
+    if (plain && autoscale && a.ncw > 0) {
+      const int cap = dm_launch_cap(0, 0, 0, 0, share);
+      const int k = cap > 0 ? cap / a.ncw : 1;
+      if (k > 1) {
+        a.ncw = 0;
+        for (int c = 0; c < a.ncopy; c++) {
+          const uint64_t by = a.m[a.cidx[c]].bytes >> 16;
+          const int lim = (int)std::min<uint64_t>((uint64_t)a.cwgs[c] * (uint64_t)k,
+                                                  std::max<uint64_t>((uint64_t)a.cwgs[c], by));
+          a.cwgs[c] = lim;
+          a.ncw += a.cwgs[c];
+        }
+      }
     }
   };
   auto flush = [&]() -> int {
@@ -471,12 +492,12 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
       for (int j = 0; j < kMaxLeaves; j++) t.leaf_msg[j] = -1;
       for (int i = 0; i < a.nmsg; i++)
         if (a.m[i].leaf >= 0) t.leaf_msg[a.m[i].leaf] = i;
-      index_copies();
+      index_copies(false);
       rc = launch_dm_move_tree(a, t, ltree->dtype, ltree->op, st);
       tree_round = -1;
       ltree = tree;
     } else {
-      index_copies();
+      index_copies(true);
       rc = launch_dm_move(a, st);
     }
     a.nmsg = 0;

@@ -34,6 +34,8 @@ struct DirectState {
                                    // residency cap, then to a multiple of the CUs)
   int env_wgs = 128;               // the value init() settled on (the setter's 0)
   int pull_wgs = 0;                // workgroups per copied pull (BINE_DIRECT_PULL_WGS; 0: wgs)
+  bool autoscale = true;           // a k_dm_move launch below the GPU's resident capacity scales its
+                                   // messages' workgroups up (BINE_DIRECT_AUTOSCALE=0: off)
   // diagnostics (BINE_DIRECT_STAMPS=<records>): per-workgroup stamps of every
   // launch (DmArgs::stamps), read back with bine_comm_direct_stamps
   uint64_t *stamps = nullptr;
