@@ -277,6 +277,29 @@ def p16_jobs():
     return jobs
 
 
+def large_p_jobs():
+    """P = 32 and 64 (five and six Bine steps: beyond one node, the scale the
+    reference's own campaigns run at) for the main algorithm of every family
+    and the classic baselines"""
+    jobs = []
+    for P in (32, 64):
+        for a in ("bine_bdw_remap", "bine_bdw_static", "bine_lat", "ring", "rabenseifner", "recursivedoubling"):
+            jobs.append((P, "allreduce", a, "sum", 0, "even", FEW_DT, [13, 4099], True))
+        jobs.append((P, "allreduce", "bine_bdw_remap_segmented", "sum", 64, "even", FEW_DT, [13, 4099], True))
+        for a in ("bine_permute_remap", "bine_send_remap", "bine_static", "bine_block_by_block", "butterfly", "ring"):
+            jobs.append((P, "reduce_scatter", a, "sum", 0, "even", FEW_DT, [P * 3, P * 100], True))
+        for a in ("bine_bdw", "bine_lat"):
+            jobs.append((P, "reduce", a, "sum", 0, "even", FEW_DT, [13, 4099], True))
+        for a in ("bine_permute_remap", "bine_send_static", "bine_2_blocks", "k_bruck", "ring"):
+            jobs.append((P, "allgather", a, "sum", 0, "even", FEW_DT, [3, 200], True))
+        for a in ("bine_lat", "bine_bdw_remap", "bine_bdw_static", "scatter_allgather"):
+            jobs.append((P, "bcast", a, "sum", 0, "even", FEW_DT, [7, P + 1, 4099], True))
+        jobs.append((P, "bcast", "bine_lat_new", "sum", 0, f"root{P - 1}", FEW_DT, [7, 4099], True))
+        for coll in ROOTED:
+            jobs.append((P, coll, "bine", "sum", 0, "root0", FEW_DT, [1, 33], True))
+    return jobs
+
+
 def inplace_jobs():
     """MPI_IN_PLACE through every reduce-family algorithm (the reference's own
     in-place code paths, e.g. libbine_allreduce.c:849-852,
@@ -335,6 +358,11 @@ def main():
             keep = {c["id"] for c in index}
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(bcast_bdw_jobs(), index, arrays)
+        if only == "largep":
+            index = [c for c in old if c["P"] not in (32, 64)]
+            keep = {c["id"] for c in index}
+            arrays = {k: v for k, v in prev.items() if k in keep}
+            return capture(large_p_jobs(), index, arrays)
         if only == "rooted":
             index = [c for c in old if c["coll"] not in ROOTED]
             keep = {c["id"] for c in index}
@@ -388,6 +416,7 @@ def main():
     jobs += bcast_jobs()
     jobs += bcast_bdw_jobs()
     jobs += rooted_jobs()
+    jobs += large_p_jobs()
     capture(jobs, [], {})
 
 
