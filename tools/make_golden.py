@@ -297,6 +297,17 @@ def large_p_jobs():
         jobs.append((P, "bcast", "bine_lat_new", "sum", 0, f"root{P - 1}", FEW_DT, [7, 4099], True))
         for coll in ROOTED:
             jobs.append((P, coll, "bine", "sum", 0, "root0", FEW_DT, [1, 33], True))
+    # non-power-of-two sizes past 8 for the algorithms that run at any P (the
+    # others' error returns / refusals are pinned at P = 3, 5, 6, 7)
+    for P in (12, 24):
+        for a in ("ring", "rabenseifner", "bine_lat", "recursivedoubling"):
+            jobs.append((P, "allreduce", a, "sum", 0, "even", FEW_DT, [13, 4099], True))
+        jobs.append((P, "allreduce", "bine_bdw_remap_segmented", "sum", 64, "even", FEW_DT, [13, 4099], True))
+        for a in ("ring", "butterfly", "recursivehalving", "bine_send_remap"):
+            jobs.append((P, "reduce_scatter", a, "sum", 0, "even", FEW_DT, [P * 3, P * 100], True))
+        for a in ("ring", "k_bruck", "sparbit"):
+            jobs.append((P, "allgather", a, "sum", 0, "even", FEW_DT, [3, 200], True))
+        jobs.append((P, "bcast", "scatter_allgather", "sum", 0, "even", FEW_DT, [7, P + 1, 4099], True))
     return jobs
 
 
@@ -359,7 +370,7 @@ def main():
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(bcast_bdw_jobs(), index, arrays)
         if only == "largep":
-            index = [c for c in old if c["P"] not in (32, 64)]
+            index = [c for c in old if c["P"] not in (12, 24, 32, 64)]
             keep = {c["id"] for c in index}
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(large_p_jobs(), index, arrays)
