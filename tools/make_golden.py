@@ -297,6 +297,16 @@ def large_p_jobs():
         jobs.append((P, "bcast", "bine_lat_new", "sum", 0, f"root{P - 1}", FEW_DT, [7, 4099], True))
         for coll in ROOTED:
             jobs.append((P, coll, "bine", "sum", 0, "root0", FEW_DT, [1, 33], True))
+    # the operators' semantics through deeper trees: P = 16 and 32
+    for P in (16, 32):
+        for op, rk, dts in (("max", "even_sparse", ["float", "double"]), ("min", "even_sparse", ["float"]),
+                            ("prod", "even", ["float", "int32"]), ("land", "even_sparse", ["float", "int8"]),
+                            ("bxor", "even", ["int64", "int16"]), ("maxloc", "even_sparse", PAIR_DT),
+                            ("minloc", "even_sparse", PAIR_DT)):
+            for a in ("bine_bdw_remap", "bine_lat"):
+                jobs.append((P, "allreduce", a, op, 0, rk, dts, [13, 1000], True))
+            jobs.append((P, "reduce_scatter", "bine_permute_remap", op, 0, rk, dts, [P * 3, P * 64], True))
+            jobs.append((P, "reduce", "bine_bdw", op, 0, rk, dts, [13, 1000], True))
     # non-power-of-two sizes past 8 for the algorithms that run at any P (the
     # others' error returns / refusals are pinned at P = 3, 5, 6, 7)
     for P in (12, 24):
@@ -370,7 +380,8 @@ def main():
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(bcast_bdw_jobs(), index, arrays)
         if only == "largep":
-            index = [c for c in old if c["P"] not in (12, 24, 32, 64)]
+            index = [c for c in old if c["P"] not in (12, 24, 32, 64) and
+                     not (c["P"] == 16 and c["op"] != "sum")]
             keep = {c["id"] for c in index}
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(large_p_jobs(), index, arrays)
