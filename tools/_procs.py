@@ -15,3 +15,16 @@ def join_ranks(ps, timeout_s):
         if p.is_alive():
             p.terminate()
         p.join(30)
+
+
+def rank_device(rank):
+    """the GPU a probe's rank uses: 0 (every rank on the box's one GPU, RCCL
+    told the ranks are on different hosts so it moves bytes over sockets), or
+    with BINE_RANK_DEVICES=1 on a multi-GPU node rank % the visible GPUs, RCCL
+    left to find xGMI (tools/node_check.sh)"""
+    import os
+    if os.environ.get("BINE_RANK_DEVICES") == "1":
+        import torch
+        return rank % max(1, torch.cuda.device_count())
+    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    return 0

@@ -45,7 +45,8 @@ def cases(P):
 
 
 def worker(rank, P, port, q):
-    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    from tools._procs import rank_device
+    dev = rank_device(rank)   # (sets the fake RCCL host id on the one-GPU box)
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ["BINE_DIRECT_SLOT_BYTES"] = str(SLOT)
@@ -56,9 +57,9 @@ def worker(rank, P, port, q):
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle as O
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
-    comm = pico_amd.Comm.from_torch_distributed(0)
+    comm = pico_amd.Comm.from_torch_distributed(dev)
     comm.set_direct(True)
     comm.set_flat_ag(True)
     comm.set_flat_rs(True)
@@ -81,8 +82,8 @@ def worker(rank, P, port, q):
                 want = want[rank]
                 total, outn = n * P, n
             assert not any(rets)
-            s = torch.from_numpy(sb[rank].view(np.uint8).copy()).to("cuda:0")
-            r = torch.full((outn * esz,), 0xA5, dtype=torch.uint8, device="cuda:0")
+            s = torch.from_numpy(sb[rank].view(np.uint8).copy()).to("cuda")
+            r = torch.full((outn * esz,), 0xA5, dtype=torch.uint8, device="cuda")
             if inplace:
                 r = s.clone()
             torch.cuda.synchronize()

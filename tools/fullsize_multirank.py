@@ -33,7 +33,8 @@ TRANSPORTS = [("flatrs+flat+dm", ("C3", "C4", "C5")), ("flatrs+flat+dmt", ("C3",
 
 
 def worker(rank, P, port, gold, q):
-    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    from tools._procs import rank_device
+    dev = rank_device(rank)   # (sets the fake RCCL host id on the one-GPU box)
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
@@ -41,9 +42,9 @@ def worker(rank, P, port, gold, q):
     import torch.distributed as dist
     import pico_amd
     import bench
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
-    comm = pico_amd.Comm.from_torch_distributed(0)
+    comm = pico_amd.Comm.from_torch_distributed(dev)
     st = torch.cuda.Stream()
     tdt = {"float": torch.float32, "double": torch.float64, "int64": torch.int64}
     bad = []
@@ -53,10 +54,10 @@ def worker(rank, P, port, gold, q):
             if cfg not in which:
                 continue
             key = f"{cfg}/{coll}/{algo}/{dt}/N{n}/P{P}"
-            sb = torch.empty(n, dtype=tdt[dt], device="cuda:0")
+            sb = torch.empty(n, dtype=tdt[dt], device="cuda")
             pico_amd.fill_pico(sb, n, dt, 1234 + rank)
             on = n if coll == "allreduce" else n // P
-            rb = torch.empty(on, dtype=tdt[dt], device="cuda:0")
+            rb = torch.empty(on, dtype=tdt[dt], device="cuda")
             rb.fill_(float("nan") if dt != "int64" else -1)
             torch.cuda.synchronize()
             dist.barrier()

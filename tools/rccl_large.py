@@ -90,7 +90,8 @@ def locate(r, count, path, want_all):
 
 
 def worker(rank, P, port, want, dts, q, xdir):
-    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    from tools._procs import rank_device
+    dev = rank_device(rank)   # (sets the fake RCCL host id on the one-GPU box)
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
@@ -98,9 +99,9 @@ def worker(rank, P, port, want, dts, q, xdir):
     import torch
     import torch.distributed as dist
     import bench
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
-    comm = pico_amd.Comm.from_torch_distributed(0)
+    comm = pico_amd.Comm.from_torch_distributed(dev)
     bad, n_ok = [], 0
     side = torch.cuda.Stream()   # graph mode needs a non-NULL caller stream
     modes = [m for m in MODES if (m in bench.transport_modes("auto", P) or m in ("flatrs+flat+a2a", "relay+flat+dm",
@@ -110,8 +111,8 @@ def worker(rank, P, port, want, dts, q, xdir):
         if dt not in dts:
             continue
         tdt = {"float": torch.float32, "double": torch.float64}[dt]
-        s = torch.empty(n, dtype=tdt, device="cuda:0")
-        r = torch.empty(n, dtype=tdt, device="cuda:0")
+        s = torch.empty(n, dtype=tdt, device="cuda")
+        r = torch.empty(n, dtype=tdt, device="cuda")
         pico_amd.fill_pico(s, n, dt, 1234 + rank)
         torch.cuda.synchronize()
         din = pico_amd.checksum(s, n, dt)
@@ -139,8 +140,8 @@ def worker(rank, P, port, want, dts, q, xdir):
             print(f"rank {rank} allreduce {dt} {m} (eager + graph): {'ok' if not bad else 'BAD'}", flush=True)
         del s, r
     bench.apply_transport(comm, "direct", 0)
-    s = torch.empty(N32, dtype=torch.float32, device="cuda:0")
-    r = torch.empty(N32 // P, dtype=torch.float32, device="cuda:0")
+    s = torch.empty(N32, dtype=torch.float32, device="cuda")
+    r = torch.empty(N32 // P, dtype=torch.float32, device="cuda")
     pico_amd.fill_pico(s, N32, "float", 1234 + rank)
     torch.cuda.synchronize()
     din = pico_amd.checksum(s, N32, "float")

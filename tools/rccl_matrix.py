@@ -47,7 +47,8 @@ SETTINGS = (("direct", 0, 0, 0, 0), ("chunk4KiB", 0, 4096, 0, 0), ("relay", 64, 
 
 
 def worker(rank, P, port, q):
-    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    from tools._procs import rank_device
+    dev = rank_device(rank)   # (sets the fake RCCL host id on the one-GPU box)
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
@@ -56,15 +57,15 @@ def worker(rank, P, port, q):
     import torch
     import torch.distributed as dist
     from oracle import oracle as O
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
-    comm = pico_amd.Comm.from_torch_distributed(0)
+    comm = pico_amd.Comm.from_torch_distributed(dev)
     npdt = O.NP_DTYPES
     bad, n_ok = [], 0
 
     def dev(a):
         t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
-        return t if t.numel() else torch.zeros(16, dtype=torch.uint8, device="cuda:0")
+        return t if t.numel() else torch.zeros(16, dtype=torch.uint8, device="cuda")
 
     def host(t, dt, n):
         return t[: n * np.dtype(npdt[dt]).itemsize].cpu().numpy().view(npdt[dt]).copy()
@@ -113,7 +114,7 @@ def worker(rank, P, port, q):
             sb = O.inputs(dt, n, P)
             for algo in pico_amd.ALGOS["allreduce"]:
                 want, rets = O.allreduce(algo, sb, dt, segsize=256)
-                r = torch.zeros(n * esz + 16, dtype=torch.uint8, device="cuda:0")
+                r = torch.zeros(n * esz + 16, dtype=torch.uint8, device="cuda")
                 s = dev(sb[rank])
                 run(f"{sname} allreduce_{algo} {dt} n={n}", rets[rank], want[rank],
                     lambda: pico_amd.allreduce(algo, s, r, n, dt, "sum", comm, segsize=256), r, dt, n)
@@ -121,19 +122,19 @@ def worker(rank, P, port, q):
             sbr = O.inputs(dt, sum(rc), P)
             for algo in pico_amd.ALGOS["reduce_scatter"]:
                 want, rets = O.reduce_scatter(algo, sbr, rc, dt)
-                r = torch.zeros(rc[rank] * esz + 16, dtype=torch.uint8, device="cuda:0")
+                r = torch.zeros(rc[rank] * esz + 16, dtype=torch.uint8, device="cuda")
                 s = dev(sbr[rank])
                 run(f"{sname} reduce_scatter_{algo} {dt} ragged", rets[rank], want[rank],
                     lambda: pico_amd.reduce_scatter(algo, s, r, rc, dt, "sum", comm), r, dt, rc[rank])
             for algo in pico_amd.ALGOS["reduce"]:
                 want, rets = O.reduce(algo, sb, dt)
-                r = torch.zeros(n * esz + 16, dtype=torch.uint8, device="cuda:0")
+                r = torch.zeros(n * esz + 16, dtype=torch.uint8, device="cuda")
                 s = dev(sb[rank])
                 run(f"{sname} reduce_{algo} {dt}", rets[rank], want if rank == 0 else None,
                     lambda: pico_amd.reduce(algo, s, r if rank == 0 else None, n, dt, "sum", 0, comm), r, dt, n)
             for algo in pico_amd.ALGOS["allgather"]:
                 want, rets = O.allgather(algo, sb, dt)
-                r = torch.zeros(P * n * esz + 16, dtype=torch.uint8, device="cuda:0")
+                r = torch.zeros(P * n * esz + 16, dtype=torch.uint8, device="cuda")
                 s = dev(sb[rank])
                 run(f"{sname} allgather_{algo} {dt}", rets[rank], want[rank],
                     lambda: pico_amd.allgather(algo, s, r, n, dt, comm), r, dt, P * n)
@@ -142,13 +143,13 @@ def worker(rank, P, port, q):
     comm.set_direct(False)
     # the raw P2P primitive (bine_exchange): ring shift, then all peers at once
     nb = 100003
-    mine = torch.full((nb,), rank + 1, dtype=torch.uint8, device="cuda:0")
-    got = torch.zeros(nb, dtype=torch.uint8, device="cuda:0")
+    mine = torch.full((nb,), rank + 1, dtype=torch.uint8, device="cuda")
+    got = torch.zeros(nb, dtype=torch.uint8, device="cuda")
     pico_amd.exchange(comm, [((rank + 1) % P, mine, nb)], [((rank - 1) % P, got, nb)])
     torch.cuda.synchronize()
     ok = bool((got == (rank - 1) % P + 1).all())
     peers = [p for p in range(P) if p != rank]
-    allr = torch.zeros(len(peers) * nb, dtype=torch.uint8, device="cuda:0")
+    allr = torch.zeros(len(peers) * nb, dtype=torch.uint8, device="cuda")
     pico_amd.exchange(comm, [(p, mine, nb) for p in peers], [(p, allr[i * nb:], nb) for i, p in enumerate(peers)])
     torch.cuda.synchronize()
     ok &= all(bool((allr[i * nb:(i + 1) * nb] == p + 1).all()) for i, p in enumerate(peers))
@@ -158,8 +159,8 @@ def worker(rank, P, port, q):
         bad.append(("exchange", "data"))
     # RCCL's own allreduce (the bench's vendor baseline): int64 SUM is order-free
     vi = [O.fill("int64", nb, 1234 + r) for r in range(P)]
-    vs = torch.from_numpy(vi[rank]).to("cuda:0")
-    vr = torch.zeros(nb, dtype=torch.int64, device="cuda:0")
+    vs = torch.from_numpy(vi[rank]).to("cuda")
+    vr = torch.zeros(nb, dtype=torch.int64, device="cuda")
     pico_amd.vendor_allreduce(vs, vr, nb, "int64", "sum", comm)
     torch.cuda.synchronize()
     want_v = vi[0].copy()

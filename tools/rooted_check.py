@@ -20,7 +20,8 @@ MODES = [("rccl", False, False, False), ("rccl", True, False, False), ("rccl", F
 
 
 def worker(rank, P, port, q):
-    os.environ["NCCL_HOSTID"] = f"bine-fake-host-{rank}"
+    from tools._procs import rank_device
+    dev = rank_device(rank)   # (sets the fake RCCL host id on the one-GPU box)
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(P))
@@ -30,9 +31,9 @@ def worker(rank, P, port, q):
     import torch.distributed as dist
     import rooted_util as R
     from oracle import oracle as O
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
-    comm = pico_amd.Comm.from_torch_distributed(0)
+    comm = pico_amd.Comm.from_torch_distributed(dev)
     stream = torch.cuda.Stream()
     bad, n_ok = [], 0
     for name, flat, direct, graphs in MODES:
@@ -47,8 +48,8 @@ def worker(rank, P, port, q):
                     esz = np.dtype(O.NP_DTYPES[dt]).itemsize
                     rn = {"gather": P * n if rank == root else 0, "scatter": n, "alltoall": P * n}[coll]
                     has_s = coll != "scatter" or rank == root
-                    s = torch.from_numpy(sb[rank].view(np.uint8).copy()).to("cuda:0") if has_s else None
-                    r = torch.full((rn * esz,), 0xA5, dtype=torch.uint8, device="cuda:0") if rn else None
+                    s = torch.from_numpy(sb[rank].view(np.uint8).copy()).to("cuda") if has_s else None
+                    r = torch.full((rn * esz,), 0xA5, dtype=torch.uint8, device="cuda") if rn else None
                     torch.cuda.synchronize()
                     tag = f"{name} flat={flat} graphs={graphs} {coll} {dt} n={n} root={root}"
                     try:
