@@ -307,6 +307,15 @@ def large_p_jobs():
                 jobs.append((P, "allreduce", a, op, 0, rk, dts, [13, 1000], True))
             jobs.append((P, "reduce_scatter", "bine_permute_remap", op, 0, rk, dts, [P * 3, P * 64], True))
             jobs.append((P, "reduce", "bine_bdw", op, 0, rk, dts, [13, 1000], True))
+    # MPI_IN_PLACE and ragged blocks through P = 16's four steps
+    for a in AR_BINE + AR_CLASSIC:
+        jobs.append((16, "allreduce", a, "sum", 0, "even_inplace", FEW_DT, [13, 4099], True))
+    for a in RS_BINE + RS_CLASSIC:
+        jobs.append((16, "reduce_scatter", a, "sum", 0, "even_inplace", FEW_DT, [16 * 3, 16 * 100], True))
+        if a in RS_RAGGED_OK:
+            jobs.append((16, "reduce_scatter", a, "sum", 0, "ragged", FEW_DT, [16 * 4, 16 * 50], True))
+    for a in ("bine_lat", "bine_bdw"):
+        jobs.append((16, "reduce", a, "sum", 0, "even_inplace", FEW_DT, [13, 4099], True))
     # non-power-of-two sizes past 8 for the algorithms that run at any P (the
     # others' error returns / refusals are pinned at P = 3, 5, 6, 7)
     for P in (12, 24):
@@ -381,7 +390,7 @@ def main():
             return capture(bcast_bdw_jobs(), index, arrays)
         if only == "largep":
             index = [c for c in old if c["P"] not in (12, 24, 32, 64) and
-                     not (c["P"] == 16 and c["op"] != "sum")]
+                     not (c["P"] == 16 and (c["op"] != "sum" or c["rcounts"] in ("even_inplace", "ragged")))]
             keep = {c["id"] for c in index}
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(large_p_jobs(), index, arrays)
