@@ -18,6 +18,7 @@
  *   coll         allreduce | reduce_scatter | reduce | allgather | bcast | fill (dump the inputs)
  *                bcast: in place on each rank's input; rcounts "root<k>" = root k
  *                allgather: N = elements per rank (scount = rcount, same type,
+ *                "_inplace": MPI_IN_PLACE, the own block at block `rank` of rbuf;
  *                pico_core_utils.c:511-514), rbuf = P * N zeroed elements
  *                gather / scatter: N = elements per block, root from "root<k>"
  *                (else 0); gather: sbuf N, rbuf P * N on the root only (NULL
@@ -302,7 +303,9 @@ int main(int argc, char **argv) {
       } else if (!strcmp(coll, "allgather")) {
         ag_fn f = pick_allgather(algo);
         if (!f) MPI_Abort(MPI_COMM_WORLD, 5);
-        ret = f(sbuf, N, dt, rbuf, N, dt, MPI_COMM_WORLD);
+        /* MPI_IN_PLACE: the rank's own block already at block `rank` of rbuf */
+        if (inplace) memcpy((char *)rbuf + (size_t)rank * N * esz, sbuf, N * esz);
+        ret = f(inplace ? MPI_IN_PLACE : sbuf, N, dt, rbuf, N, dt, MPI_COMM_WORLD);
       } else if (!strcmp(coll, "bcast")) {
         /* in place on every rank's own input; root from "root<k>" (else 0) */
         bc_fn f = pick_bcast(algo);

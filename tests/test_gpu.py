@@ -162,6 +162,10 @@ def run_loopback(coll, algo, sbufs, dtype, op="sum", rcounts=None, segsize=0, ro
         outs = [from_dev(d, dtype, c) for d, c in zip(dr, rcounts)]
     elif coll == "allgather":
         dr = [torch.zeros(P * n * esz + 64, dtype=torch.uint8, device="cuda:0") for _ in range(P)]
+        if in_place:   # MPI_IN_PLACE: the own block already at block r of rbuf
+            for r in range(P):
+                dr[r][r * n * esz:(r + 1) * n * esz] = ds[r][:n * esz]
+            ds = [pico_amd.IN_PLACE] * P
         torch.cuda.synchronize()
         rc, st = pico_amd.loopback_allgather(comms(P), algo, ds, dr, n, dtype)
         outs = [from_dev(d, dtype, P * n) for d in dr]
@@ -211,13 +215,24 @@ def oracle_bcast(algo, sb, dt, root):
     return out, rets
 
 
-def oracle_outputs(coll, algo, sb, dt, op, rk, segsize, root=0):
+def in_place_rbufs(sb, dt):
+    """allgather with MPI_IN_PLACE: every rank's rbuf holding its own block"""
+    P, n = len(sb), sb[0].size
+    out = []
+    for r in range(P):
+        b = np.zeros(P * n, O.NP_DTYPES[dt])
+        b[r * n:(r + 1) * n] = sb[r]
+        out.append(b)
+    return out
+
+
+def oracle_outputs(coll, algo, sb, dt, op, rk, segsize, root=0, in_place=False):
     """the oracle's per-rank outputs of one collective (intended semantics:
     the reference's bugs are not reproduced)"""
     if coll == "bcast":
         return oracle_bcast(algo, sb, dt, root)[0]
     if coll == "allgather":
-        return O.allgather(algo, sb, dt)[0]
+        return O.allgather(algo, sb, dt, in_place_rbufs=in_place_rbufs(sb, dt) if in_place else None)[0]
     if coll == "reduce_scatter":
         return O.reduce_scatter(algo, sb, rk, dt, op)[0]
     if coll == "reduce":
@@ -289,7 +304,7 @@ def test_collectives_match_reference_goldens(dev, key, cs, relay):
             else:
                 # the reference crashed (e.g. MPI_IN_PLACE in the block-by-block
                 # and remap variants, which read it as a buffer): vs the oracle
-                want = oracle_outputs(coll, algo, sb, dt, c["op"], rk, c["segsize"], root)
+                want = oracle_outputs(coll, algo, sb, dt, c["op"], rk, c["segsize"], root, in_place=ip)
                 if coll == "reduce_scatter" and P == 1 and algo in ("butterfly", "bine_block_by_block"):
                     want = [sb[0][: rk[0]]]   # the P = 1 copy the reference omits (DESIGN.md deviations)
                 if any(sha(o) != sha(w) for o, w in zip(outs, want)):

@@ -307,6 +307,10 @@ def large_p_jobs():
                 jobs.append((P, "allreduce", a, op, 0, rk, dts, [13, 1000], True))
             jobs.append((P, "reduce_scatter", "bine_permute_remap", op, 0, rk, dts, [P * 3, P * 64], True))
             jobs.append((P, "reduce", "bine_bdw", op, 0, rk, dts, [13, 1000], True))
+    # the allgather family with MPI_IN_PLACE (the own block already in rbuf)
+    for P in (1, 2, 3, 4, 8):
+        for a in AG_ALGOS:
+            jobs.append((P, "allgather", a, "sum", 0, "even_inplace", ["float", "int64"], [7, 333], True))
     # MPI_IN_PLACE and ragged blocks through P = 16's four steps
     for a in AR_BINE + AR_CLASSIC:
         jobs.append((16, "allreduce", a, "sum", 0, "even_inplace", FEW_DT, [13, 4099], True))
@@ -390,7 +394,8 @@ def main():
             return capture(bcast_bdw_jobs(), index, arrays)
         if only == "largep":
             index = [c for c in old if c["P"] not in (12, 24, 32, 64) and
-                     not (c["P"] == 16 and (c["op"] != "sum" or c["rcounts"] in ("even_inplace", "ragged")))]
+                     not (c["P"] == 16 and (c["op"] != "sum" or c["rcounts"] in ("even_inplace", "ragged"))) and
+                     not (c["coll"] == "allgather" and c["rcounts"] == "even_inplace")]
             keep = {c["id"] for c in index}
             arrays = {k: v for k, v in prev.items() if k in keep}
             return capture(large_p_jobs(), index, arrays)
