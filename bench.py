@@ -182,6 +182,63 @@ def timed(torch, stream, call, steps, warmup, dist=None, syncs=(), per_iter=True
                         issue * 1e3 / steps, wall)
 
 
+class Drain:
+    """comm.synchronize as a timed() sync that never raises: since round 6 the
+    completion of calls whose direct-transport wait timed out is an error on
+    the rank that timed out (bine_comm_synchronize) -- and
+    possibly only there.  Raising on that rank alone would leave the ranks in
+    different collectives (timed()'s barriers, the digest votes), so the first
+    error is recorded here and `failed()` agrees on it over all ranks."""
+
+    def __init__(self, comm):
+        self.comm = comm
+        self.err = None
+
+    def __call__(self):
+        import pico_amd
+        try:
+            self.comm.synchronize()
+        except pico_amd.BineError as e:
+            if self.err is None:
+                self.err = str(e)
+
+    def guard(self, call):
+        """call() with its issue-time library error recorded, not raised (a
+        poisoned transport refuses a call at issue on the rank that timed out
+        while its peers issue theirs); nothing more is issued on this rank
+        once it failed"""
+        import pico_amd
+
+        def g():
+            if self.err is not None:
+                return
+            try:
+                call()
+            except pico_amd.BineError as e:
+                self.err = str(e)
+        return g
+
+    def failed(self, dist):
+        """None when no rank saw an error, else 'rank r: <its error>' for the
+        lowest such rank (collective: every rank gets the same answer)"""
+        if dist is None:
+            return None if self.err is None else f"rank 0: {self.err}"
+        errs = [None] * dist.get_world_size()
+        dist.all_gather_object(errs, self.err)
+        for r, e in enumerate(errs):
+            if e is not None:
+                return f"rank {r}: {e}"
+        return None
+
+
+def measure(torch, stream, dist, comm, call, steps, warmup):
+    """timed() of a collective with every rank's library errors agreed on:
+    (stats, None) or (stats, 'rank r: <error>') -- the same on every rank"""
+    d = Drain(comm)
+    st = timed(torch, stream, d.guard(call), steps, warmup, dist, (d,))
+    return st, d.failed(dist)
+
+
 def reduce_stats(torch, dist, per, region, issue_ms, wall):
     """the statistic over ranks: per iteration the max over ranks (as every
     other figure), the first 20 % of iterations dropped, the median of the
@@ -527,25 +584,30 @@ def overlap_frac(exchanges, locals_):
     return min(1.0, hid / tot)
 
 
-def _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem, stream):
+def _step_profile(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem, stream):
     return step_profile(torch, comm,
-                        lambda: pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream))
+                        lambda: pico_amd.allreduce(algo, sbuf, rbuf, nelem, "float", "sum", comm, stream=stream),
+                        dist)
 
 
-def step_profile(torch, comm, call):
+def step_profile(torch, comm, call, dist=None):
     """One extra collective (outside the timed region) with per-op timing
     events (bine_comm_set_profile): where the time of this rank goes -- busy
     time of the comm stream (exchanges) and of the compute stream (reductions),
     their span, the share of the reductions' time during which an exchange
     is in flight (overlap_frac), and the exchange ops' egress rates."""
     comm.set_profile(True)
+    d = Drain(comm)
     try:
-        call()
+        d.guard(call)()
         torch.cuda.synchronize()
-        comm.synchronize()
-        ops = comm.profile()
+        d()
+        err = d.failed(dist)
+        ops = comm.profile() if err is None else []
     finally:
         comm.set_profile(False)
+    if err is not None:
+        return {"error": err}
     if not ops:
         return {}
     span = max(o["start_ms"] + o["ms"] for o in ops)
@@ -628,9 +690,12 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
         for g in (False, True):   # eager issue, then the HIP-graph replay (bine_comm_set_graphs)
             comm.set_graphs(g)
             rb.fill_(float("nan"))
-            st = timed(torch, stream,
-                       lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
-                       50, 10, dist, (comm.synchronize,))
+            st, err = measure(torch, stream, dist, comm,
+                              lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
+                              50, 10)
+            if err:
+                out[f"C1_allreduce_{algo}_f32_1MiB" + ("_graph" if g else "")] = {"error": err}
+                continue
             ok, _ = check_digest(pico_amd, rb, n1, "float", gkey("C1", "allreduce", algo, "float", n1, world), rank)
             out[f"C1_allreduce_{algo}_f32_1MiB" + ("_graph" if g else "")] = {
                 "us": round(st["median_ms"] * 1e3, 2),
@@ -646,9 +711,12 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
             apply_transport(comm, "flatrs+flat+dm", chunk, False)
             for algo in ("bine_bdw_remap", "bine_lat"):
                 rb.fill_(float("nan"))
-                st = timed(torch, stream,
-                           lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
-                           50, 10, dist, (comm.synchronize,))
+                st, err = measure(torch, stream, dist, comm,
+                                  lambda: pico_amd.allreduce(algo, sb, rb, n1, "float", "sum", comm, stream=stream),
+                                  50, 10)
+                if err:
+                    out[f"C1_allreduce_{algo}_f32_1MiB_direct_fused"] = {"error": err}
+                    continue
                 ok, _ = check_digest(pico_amd, rb, n1, "float", gkey("C1", "allreduce", algo, "float", n1, world),
                                      rank)
                 out[f"C1_allreduce_{algo}_f32_1MiB_direct_fused"] = {
@@ -672,15 +740,18 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
     rb = torch.empty(n // world, dtype=torch.float32, device=dev)
     pico_amd.fill_pico(sb, n, "float", 1234 + rank)
     rc = [n // world] * world
-    st = timed(torch, stream,
-               lambda: pico_amd.reduce_scatter("bine_permute_remap", sb, rb, rc, "float", "sum", comm, stream=stream),
-               5, 2, dist, (comm.synchronize,))
+    st, err = measure(torch, stream, dist, comm,
+                      lambda: pico_amd.reduce_scatter("bine_permute_remap", sb, rb, rc, "float", "sum", comm,
+                                                      stream=stream),
+                      5, 2)
     ok, _ = check_digest(pico_amd, rb, n // world, "float",
                          gkey("C4", "reduce_scatter", "bine_permute_remap", "float", n, world, trees), rank)
     S = n * 4
     nm = node_model("C4", world, mode, chunk)
-    out["C4_reduce_scatter_bine_permute_remap_f32_1GiB"] = {
-        "ms": round(st["median_ms"], 4), "busbw_per_rank_GBs": round((world - 1) / world * S / (st["median_ms"] * 1e-3) / 1e9, 2),
+    c4 = "C4_reduce_scatter_bine_permute_remap_f32_1GiB"
+    out[c4] = {"error": err} if err else {
+        "ms": round(st["median_ms"], 4),
+        "busbw_per_rank_GBs": round((world - 1) / world * S / (st["median_ms"] * 1e-3) / 1e9, 2),
         "graph_replay": graphs and comm.graphs_cached() > 0, "parity_ok": all_ok(torch, dist, ok),
         "model_ms": nm.get("model_ms"),
         "frac_of_model": round(nm["model_ms"] / st["median_ms"], 4) if nm.get("model_ms") else None}
@@ -694,9 +765,13 @@ def _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev, mode, 
         sb = torch.empty(n, dtype=tdt, device=dev)
         rb = torch.empty(n, dtype=tdt, device=dev)
         pico_amd.fill_pico(sb, n, dt, 1234 + rank)
-        st = timed(torch, stream,
-                   lambda: pico_amd.allreduce("bine_bdw_remap", sb, rb, n, dt, "sum", comm, stream=stream),
-                   5, 2, dist, (comm.synchronize,))
+        st, err = measure(torch, stream, dist, comm,
+                          lambda: pico_amd.allreduce("bine_bdw_remap", sb, rb, n, dt, "sum", comm, stream=stream),
+                          5, 2)
+        if err:
+            out[f"C5_allreduce_bine_bdw_remap_{dt}_256MiB"] = {"error": err}
+            del sb, rb
+            continue
         ok, _ = check_digest(pico_amd, rb, n, dt, gkey("C5", "allreduce", "bine_bdw_remap", dt, n, world, trees), rank)
         S = n * 8
         ms = st["median_ms"]
@@ -736,6 +811,55 @@ def _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, per_peer=3
     out["all_peers_egress_GBs"] = round(len(peers) * per_peer / (st["median_ms"] * 1e-3) / 1e9, 2)
     del sb, rb
     torch.cuda.empty_cache()
+    return out
+
+
+def _direct_probe(pico_amd, torch, dist, comm, stream, world, rank, dev, iters=1000, nbytes=64 << 20):
+    """The two node constants the model assumes for the direct transport,
+    measured per peer pair: the cross-GPU flag round trip
+    (bine_comm_direct_ping: `iters` round trips inside one launch per side,
+    the transport's own store / poll protocol) and the one-link push rate (a
+    `nbytes` exchange with that peer alone, both directions at once, over the
+    direct transport).  Pairs in the rounds of a 1-factorisation: rank r with
+    r xor k, k = 1 .. P'-1 (P' the next power of two; a rank whose partner
+    does not exist sits the round out).  Rank 0 gets every pair's values,
+    their medians and the model's constants beside them."""
+    from pico_amd import model as NM
+    apply_transport(comm, "direct+dm", nbytes)
+    sb = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    rb = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    sb.fill_(rank & 0xFF)
+    torch.cuda.synchronize()
+    rtt, gbs, errs = {}, {}, []
+    p2 = 1 << (world - 1).bit_length()
+    for k in range(1, p2):
+        peer = rank ^ k
+        if peer < world:
+            try:
+                rtt[peer] = comm.direct_ping(peer, iters)
+            except pico_amd.BineError as e:
+                errs.append(f"ping {rank}-{peer}: {e}")
+        call = (lambda p=peer: pico_amd.exchange(comm, [(p, sb, nbytes)], [(p, rb, nbytes)], stream=stream)) \
+            if peer < world else (lambda: None)
+        st, err = measure(torch, stream, dist, comm, call, 10, 3)   # every rank: the same barriers
+        if err:
+            errs.append(f"push {rank}-{peer}: {err}")
+        elif peer < world:
+            gbs[peer] = nbytes / (st["median_ms"] * 1e-3) / 1e9
+    del sb, rb
+    torch.cuda.empty_cache()
+    allv = [None] * world
+    dist.all_gather_object(allv, (rtt, gbs, errs))
+    pr = {f"{r}-{p}": round(v, 3) for r, (t, _, _) in enumerate(allv) for p, v in t.items() if r < p}
+    pg = {f"{r}-{p}": round(v, 2) for r, (_, g, _) in enumerate(allv) for p, v in g.items()}
+    out = {"flag_round_trip_us": pr, "push_GBs": pg, "push_bytes": nbytes, "ping_iters": iters,
+           "errors": [e for _, _, es in allv for e in es][:8],
+           "model_T_FLAG_US": NM.T_FLAG_US, "model_LINK_GBS": NM.LINK_GBS}
+    if pr:
+        out["flag_round_trip_us_median"] = round(statistics.median(pr.values()), 3)
+        out["flag_one_way_us_median"] = round(statistics.median(pr.values()) / 2, 3)
+    if pg:
+        out["push_GBs_median"] = round(statistics.median(pg.values()), 2)
     return out
 
 
@@ -783,6 +907,25 @@ def node_model(cfg, world, mode, chunk):
                  one_gpu=os.environ.get("BINE_FAKE_HOSTS") == "1")
         return m
     except Exception as e:  # the model is a report, never a reason to lose the line
+        return {"error": str(e)}
+
+
+def measured_models(world, mode, chunk, link_gbs, t_flag_us):
+    """pico_amd.model's C3 / C4 / C5 expectation for `mode` with the measured
+    link rate, and the C1 end-to-end expectation with the measured per-phase
+    flag latency (bench.py's direct-transport probe); the one-GPU form when
+    ranks share a GPU (then no link: the values say what the probe saw)"""
+    try:
+        from pico_amd import model as NM
+        t = re.sub(r"(\+dmt?)\d*(x\d+)?", r"\1", mode)
+        one = os.environ.get("BINE_FAKE_HOSTS") == "1"
+        res = {"link_GBs": link_gbs, "t_flag_us": t_flag_us, "one_gpu": one}
+        for cfg in ("C3", "C4", "C5"):
+            res[cfg] = NM.config_model(cfg, world, t, chunk, one_gpu=one, link_gbs=link_gbs)["model_ms"]
+        if t_flag_us is not None:
+            res["C1_e2e_us"] = NM.c1_e2e_us(world, t_flag_us=t_flag_us, link_gbs=link_gbs)["e2e_us"]
+        return res
+    except Exception as e:  # a report, never a reason to lose the line
         return {"error": str(e)}
 
 
@@ -933,32 +1076,28 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
                 comm.set_graphs(False)   # an empty graph cache: graphs_cached() then says whether this one captured
             apply_transport(comm, *cfg)
             rbuf.fill_(float("nan"))   # a transport that writes nothing cannot pass on the last one's output
-            st = timed(torch, stream, run, 3, 2, dist, (comm.synchronize,))
+            st, why_err = measure(torch, stream, dist, comm, run, 3, 2)
             ok, _ = parity(cfg[0])
-            verdicts[cfg] = ok
-            trials[cfg] = st["median_ms"] if ok is not False else float("inf")
+            # a call whose direct-transport wait timed out reports it at its
+            # completion on the rank that timed out (the call ran on without
+            # its data): agreed over the ranks, with the waiter's record
+            verdicts[cfg] = ok if why_err is None else f"failed: {why_err}"[:700]
+            trials[cfg] = st["median_ms"] if ok is not False and why_err is None else float("inf")
             if cfg[2] and comm.graphs_cached() == 0:
                 # the library kept every call eager (its HIP-runtime gate,
                 # include/bine_amd.h): not a graph replay, so not picked as one
                 verdicts[cfg] = "eager (not captured)"
                 trials[cfg] = float("inf")
-            if ok is False:
-                # a direct-transport wait that timed out (the call ran on without its data) is
-                # told apart from a wrong result: every rank's own poison word, gathered
-                to = dm_wgs(cfg[0]) is not None and all_ok(torch, dist, not comm.direct_timed_out()) is False
-                if to:
-                    verdicts[cfg] = "timed out"
-                if rank == 0:
-                    why = "a direct-transport wait timed out on some rank" if to else \
-                        "output digest differs from the oracle's"
-                    print(f"bench: transport {tname(cfg)} EXCLUDED: {why}", file=sys.stderr)
+            if (ok is False or why_err is not None) and rank == 0:
+                why = why_err or "output digest differs from the oracle's"
+                print(f"bench: transport {tname(cfg)} EXCLUDED: {why}", file=sys.stderr)
         except pico_amd.BineError as e:
             if rank == 0:
                 print(f"bench: transport {tname(cfg)} skipped: {e}", file=sys.stderr)
             torch.cuda.synchronize()
-            comm.synchronize()
+            Drain(comm)()
             trials[cfg] = float("inf")
-            verdicts[cfg] = "error"
+            verdicts[cfg] = f"error: {e}"[:700]
             if dm_wgs(cfg[0]) is not None and e.status == 6:   # BINE_ERR_UNSUPPORTED: setup failed
                 # symmetric: setup is agreed over RCCL, so every rank stops
                 # trying together
@@ -1044,8 +1183,13 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
         try:
             apply_transport(comm, *cfg)
             rbuf.fill_(float("nan"))
-            st_ = timed(torch, stream, run, steps, warmup, dist, (comm.synchronize,))
-            return (st_,) + parity(cfg[0])
+            st_, why_err = measure(torch, stream, dist, comm, run, steps, warmup)
+            ok_, dig_ = parity(cfg[0])
+            if why_err is not None:
+                if rank == 0:
+                    print(f"bench: {tname(cfg)} failed in its full run: {why_err}", file=sys.stderr)
+                return ({"median_ms": float("inf")}, False, None)
+            return st_, ok_, dig_
         except pico_amd.BineError as e:
             if rank == 0:
                 print(f"bench: {tname(cfg)} failed in its full run: {e}", file=sys.stderr)
@@ -1109,7 +1253,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     watchdog = arm_deadline(budget, _partial, "side measurements")
     if rank == 0:
         print(f"bench: headline {tname(best)} {ms:.4f} ms; side measurements next", file=sys.stderr, flush=True)
-    steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, comm, algo, sbuf, rbuf, nelem,
+    steps_prof = _side(rank, "step profile", lambda: _step_profile(pico_amd, torch, dist, comm, algo, sbuf, rbuf, nelem,
                                                                       stream))
     extra = _side(rank, "C1/C4/C5", lambda: _extra_configs(pico_amd, torch, dist, comm, stream, world, rank, dev,
                                                            chosen, chunk, graphs, not dm_dead)) if extras else {}
@@ -1120,6 +1264,11 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             print(f"bench: {tname(best)} unavailable after the side measurements ({e}); RCCL P2P for the rest",
                   file=sys.stderr)
         apply_transport(comm, "direct", chunk, False)
+    # the direct transport's flag round trip and one-link push rate per peer
+    # pair: the node model's two assumed constants, measured
+    dprobe = _side(rank, "direct-transport probe",
+                   lambda: _direct_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
+        if extras and not dm_dead else {}
     probe = _side(rank, "P2P probe", lambda: _p2p_probe(pico_amd, torch, dist, comm, stream, world, rank, dev)) \
         if extras else {}
     vendor = _side(rank, "RCCL allreduce", lambda: _vendor_allreduce(pico_amd, torch, dist, comm, sbuf, rbuf, nelem,
@@ -1128,25 +1277,33 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
     if out is not None:
         out["config"].update({"step_profile_rank0": steps_prof, "other_baseline_configs": extra,
                               "rccl_p2p_probe": probe, "rccl_allreduce_baseline": vendor,
+                              "direct_transport_probe": dprobe,
                               "transport_trials_ms": {tname(c): round(v, 4) for c, v in trials.items()},
                               "provisional_literal_rccl": {"ms": round(st0["median_ms"], 4),
                                                            "algbw_per_rank_GBs": round(S / (st0["median_ms"] * 1e-3) / 1e9, 2),
                                                            "parity_ok": ok0}})
         out["config"]["parity"]["trials"] = {tname(c): v for c, v in verdicts.items()}
+    if rank == 0 and dprobe.get("push_GBs_median"):
+        # the node model again with the measured constants in place of the
+        # assumed ones: the link rate (C3 / C4 / C5) and the per-phase flag
+        # latency of the C1 end-to-end model (one way = round trip / 2)
+        out["roofline"]["model_with_measured_constants"] = measured_models(
+            world, chosen, chunk, dprobe["push_GBs_median"], dprobe.get("flag_one_way_us_median"))
     if rank == 0:
         # the same egress against what RCCL P2P itself moves on this node: per
         # exchange op its busiest link at what RCCL moves per link in that
         # pattern -- the one-peer rate for a one-peer op, the all-peers egress
         # rate / (P - 1) when the op talks to several peers at once
         one, allp = probe.get("one_peer_GBs"), probe.get("all_peers_egress_GBs")
-        L = out["roofline"]["link_time_bytes"]
+        lroof = out["roofline"].get("link_roofline_if_node", out["roofline"])
+        L = lroof["link_time_bytes"]
         if one and L:
             op_links = link_roofline(pico_amd, algo, world, rank, nelem, chunk, chosen)[3]
             per_link_all = min(one, allp / (world - 1)) if allp else one
             t_rccl = sum(b / ((one if npeers <= 1 else per_link_all) * 1e9) for b, npeers in op_links)
-            out["roofline"]["rccl_p2p_one_link_GBs"] = one
-            out["roofline"]["rccl_p2p_per_link_all_peers_GBs"] = round(per_link_all, 2)
-            out["roofline"]["frac_of_rccl_p2p_bound"] = round(t_rccl / (ms * 1e-3), 4)
+            lroof["rccl_p2p_one_link_GBs"] = one
+            lroof["rccl_p2p_per_link_all_peers_GBs"] = round(per_link_all, 2)
+            lroof["frac_of_rccl_p2p_bound"] = round(t_rccl / (ms * 1e-3), 4)
     comm.destroy()
     dist.destroy_process_group()
     return out
@@ -1242,6 +1399,22 @@ def _headline_line(pico_amd, algo, world, rank, nelem, steps, warmup, key, cfg, 
                              "(7 x 153), the BASELINE target's denominator"},
         "wall_s": round(st["wall_s"], 4),
     }
+    if os.environ.get("BINE_FAKE_HOSTS") == "1":
+        # ranks sharing ONE GPU (a rehearsal): no xGMI link carries anything,
+        # every rank's bytes go through the one HBM -- that is the bound in
+        # play; the link figures stay, labelled for a node
+        link = out["roofline"]
+        hb = nm.get("hbm_bytes")
+        ach = hb * world / (ms * 1e-3) / 1e9 if hb else None
+        out["roofline"] = {
+            "bound": "hbm", "achieved": _r(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": _r(ach / HBM_PEAK_GBS if ach else None), "traffic": None,
+            "algorithmic_bytes_per_call": hb * world if hb else None,
+            "model_ms": link["model_ms"], "frac_of_model": link["frac_of_model"], "model": nm,
+            "link_roofline_if_node": {k: v for k, v in link.items() if k not in ("model", "model_ms", "frac_of_model")},
+            "note": "ranks share ONE GPU: achieved = every rank's HBM bytes of one call (pico_amd/model.py "
+                    "hbm_bytes, from the executed schedule) / ms_per_step against the one HBM's peak; "
+                    "link_roofline_if_node = the xGMI roofline this line would carry on a node"}
     return out
 
 def main():

@@ -190,12 +190,12 @@ int bine_checksum(const void *buf, size_t count, int dtype, uint64_t *out, void 
 int bine_get_unique_id(void *id /* BINE_UNIQUE_ID_BYTES */);
 /* RCCL version codes (NCCL_VERSION encoding, e.g. 22606 = 2.26.6): the library
  * the process maps (ncclGetVersion) and the headers this library was compiled
- * against, both written even on failure.  Returns BINE_ERR_RCCL (reason in
- * bine_last_error) for a skewed pair: either code outside the window whose ABI
- * for every RCCL type this library passes was checked (bine_rccl_abi_check);
- * bine_comm_init_rccl refuses such a runtime, and also one whose results in
- * the creation-time ABI probe (every type / op this library passes, run
- * through the runtime) differ. */
+ * against.  A pure reporter (BINE_ERR_RCCL only when the runtime cannot be
+ * asked): whether the pair lies in the window whose ABI for every RCCL type
+ * this library passes was checked is bine_rccl_abi_check's answer;
+ * bine_comm_init_rccl refuses a pair outside it, and also a runtime whose
+ * results in the creation-time ABI probe (every type / op this library
+ * passes, run through the runtime) differ. */
 int bine_rccl_version(int *runtime, int *compiled);
 /* The pure check behind bine_rccl_version: BINE_SUCCESS iff both version codes
  * lie in the checked ABI window (2.26.0 ... 2.27.99). */
@@ -396,6 +396,17 @@ int bine_comm_direct_stamps(bine_comm_t comm, uint64_t *out, size_t cap, size_t 
  * or without a direct transport; -status on error.  Host-only read of the
  * mapped poison word: call it after synchronizing. */
 int bine_comm_direct_timed_out(bine_comm_t comm);
+/* Cross-GPU flag latency of the direct transport: this
+ * rank and `peer` play `iters` (>= 2) flag round trips with the transport's
+ * own protocol -- a system-scope store into the peer's inbox, a poll of its
+ * answer in ours -- inside ONE launch on each side, no kernel boundary in
+ * between; *us = microseconds per round trip over round trips 2 .. iters as
+ * this rank's clock saw them (the lower rank starts each round trip).  BOTH
+ * ranks of the pair must call it together, after the communicator's earlier
+ * work (it synchronizes the communicator's streams first and blocks until
+ * done).  A timed-out wait poisons the transport as any other
+ * (BINE_ERR_INTERNAL); BINE_ERR_UNSUPPORTED without a direct transport. */
+int bine_comm_direct_ping(bine_comm_t comm, int peer, int iters, double *us);
 
 /* Graph mode (RCCL communicators): the first collective call for a given
  * (algorithm, arguments, buffers, dtype, op, stream) captures the whole issue

@@ -204,6 +204,13 @@ class Comm:
             check(int(-n), "bine_comm_direct_timed_out")
         return bool(n)
 
+    def direct_ping(self, peer: int, iters: int = 1000) -> float:
+        """microseconds per cross-GPU flag round trip with `peer` over the
+        direct transport (bine_comm_direct_ping; both ranks call it together)"""
+        us = ctypes.c_double(0.0)
+        check(lib().bine_comm_direct_ping(self.handle, peer, iters, ctypes.byref(us)), "bine_comm_direct_ping")
+        return us.value
+
     def direct_stamps(self, reset: bool = True):
         """Direct-transport diagnostics (BINE_DIRECT_STAMPS=<records> at setup;
         bine_comm_direct_stamps): numpy uint64 array (n, 4) of per-workgroup
@@ -274,15 +281,17 @@ def copy(dst, src, nbytes: int, stream=None) -> None:
 
 
 def rccl_version() -> dict:
-    """{"runtime": code, "compiled": code, ...}: the RCCL this process maps vs the
-    headers libbine_amd.so was compiled against (NCCL_VERSION codes)."""
+    """{"runtime": code, "compiled": code, ..., "abi_ok"}: the RCCL this process
+    maps vs the headers libbine_amd.so was compiled against (NCCL_VERSION
+    codes), and whether the pair lies in the checked ABI window -- reported
+    also when it does not (communicator creation refuses such a pair)."""
     rt, ct = ctypes.c_int(), ctypes.c_int()
     check(lib().bine_rccl_version(ctypes.byref(rt), ctypes.byref(ct)), "bine_rccl_version")
 
     def fmt(v):
         return f"{v // 10000}.{v // 100 % 100}.{v % 100}"
     return {"runtime": fmt(rt.value), "compiled": fmt(ct.value), "runtime_code": rt.value,
-            "compiled_code": ct.value}
+            "compiled_code": ct.value, "abi_ok": lib().bine_rccl_abi_check(rt.value, ct.value) == 0}
 
 
 def checksum(buf, count: int, dtype=None, stream=None) -> int:

@@ -160,7 +160,8 @@ namespace dm {
 constexpr size_t kFlagStride = 128;  // one flag / counter per 128-B line
 constexpr size_t kReadyOff = 0, kAckOff = 64 << 10, kCntPushOff = 128 << 10, kCntPullOff = 192 << 10,
                  kPoisonOff = 256 << 10, kBaseSendOff = 260 << 10, kBaseRecvOff = 264 << 10,
-                 kLaunchCntOff = 268 << 10, kPeerTabOff = 272 << 10, kFlagsBytes = 320 << 10;
+                 kLaunchCntOff = 268 << 10, kPeerTabOff = 272 << 10, kPingOff = 288 << 10,
+                 kFlagsBytes = 320 << 10;
 constexpr int kSlots = 4;      // slots per ordered pair
 constexpr int kMaxPeers = 64;  // P limit of the layout (flag regions: P * kSlots * 128 B <= 64 KiB)
 }  // namespace dm
@@ -218,8 +219,41 @@ namespace dm {
 // workgroup's wall_clock64 at entry, when its wait ended, when its copy (or
 // tree) ended.  kind: 0 push, 1 pull, 2 tree, 3 push group
 constexpr int kStampHdr = 8, kStampWords = 4;
+// The mapped host words (DirectState::hpoison, kHostBytes): word 0's low half
+// is the poison flag; 64-bit words kRecFirst .. kRecFirst + kRecWords - 1 hold
+// the first timed-out waiter's record (dm_time_out, kernels.hip): kind << 8 |
+// phase, rank, peer, slot, sequence number wanted, flag value last seen,
+// launch serial, workgroup << 16 | thread, wall_clock64 ticks waited
+constexpr int kRecFirst = 1, kRecWords = 9;
+constexpr size_t kHostBytes = 128;
+// what the waiter was: a push waits for the receiver's acknowledgement of the
+// slot's previous use, a pull / leaf for the sender's ready mark
+enum WaitKind : uint32_t {
+  kWaitMovePush = 1,   // k_dm_move push
+  kWaitMovePull = 2,   // k_dm_move pull
+  kWaitGroupPush = 3,  // k_dm_move push group (BINE_DIRECT_MCAST)
+  kWaitTreeLeaf = 4,   // k_dm_move_tree leaf
+  kWaitFusedPush = 5,  // k_dm_fused push (phase 0: A, 1 + c: the allgather pieces of tree c)
+  kWaitFusedPull = 6,  // k_dm_fused leaf (phase 1 + c) or allgather pull (phase 15: D)
+  kWaitPing = 7,       // k_dm_ping (bine_comm_direct_ping): the peer's answer
+};
 }  // namespace dm
 int launch_dm_move(const DmArgs &a, void *stream);
+
+// The flag latency probe (k_dm_ping, bine_comm_direct_ping): ping flags at
+// dm::kPingOff + x * kFlagStride of the inbox of rank y, written by rank x
+// (monotonic: sequence numbers base + 1 .. base + iters, base = the pair's
+// earlier pings, counted on the host by both ranks alike)
+struct DmPingArgs {
+  uint8_t *own = nullptr;
+  uint32_t *poison_host = nullptr;
+  uint64_t timeout_ticks = 0;
+  uint64_t base = 0;
+  uint64_t *out = nullptr;  // device word: wall_clock64 ticks of round trips 2 .. iters (0: timed out)
+  int rank = 0, peer = 0, iters = 0, initiator = 0;
+  uint32_t serial = 0;
+};
+int launch_dm_ping(const DmPingArgs &a, void *stream);
 
 // The flat reduce-scatter's tree evaluated INSIDE the exchange launch that
 // receives its leaves (k_dm_move_tree<T, OP, NL>): the launch's copy messages

@@ -132,6 +132,7 @@ DirectState::~DirectState() {
   if (own_fd >= 0) close(own_fd);
   if (hpoison) (void)hipHostFree(hpoison);
   if (stamps) (void)hipFree(stamps);
+  if (ping_out) (void)hipFree(ping_out);
 }
 
 static int map_handle(hipMemGenericAllocationHandle_t h, size_t size, int device, void **va, std::string &err) {
@@ -181,13 +182,14 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   double secs = 10.0;
   if (const char *e = getenv("BINE_DIRECT_TIMEOUT_S")) secs = atof(e);
   timeout_ticks = (uint64_t)(secs * khz * 1000.0);
+  clock_khz = khz;
   step(rank, "host word");
-  if (hipHostMalloc((void **)&hpoison, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+  if (hipHostMalloc((void **)&hpoison, kHostBytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&hpoison_dev, hpoison, 0) != hipSuccess) {
     err = "direct transport: no mapped host word";
     return BINE_ERR_NO_MEM;
   }
-  *(volatile uint32_t *)hpoison = 0;
+  memset(hpoison, 0, kHostBytes);
   if (const char *e = getenv("BINE_DIRECT_STAMPS")) {
     const uint64_t cap = strtoull(e, nullptr, 10);
     if (cap) {
@@ -224,6 +226,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (e != hipSuccess) { err = std::string("export: ") + hipGetErrorString(e); return BINE_ERR_HIP; }
   peer.assign((size_t)P, nullptr);
   peer_h.assign((size_t)P, hipMemGenericAllocationHandle_t{});
+  ping_count.assign((size_t)P, 0);
   peer[(size_t)rank] = own;
   return BINE_SUCCESS;
 }
@@ -369,7 +372,43 @@ static uint64_t rd64(const void *p) {
   return v;
 }
 
-void DirectState::dump() const {
+void DirectState::dump() const { fprintf(stderr, "[bine dm r%d] %s\n", rank, describe(true).c_str()); }
+
+std::string DirectState::describe(bool flags) const {
+  static const char *const kinds[] = {"?", "k_dm_move push", "k_dm_move pull", "k_dm_move push group",
+                                      "k_dm_move_tree leaf", "k_dm_fused push", "k_dm_fused pull", "k_dm_ping"};
+  std::string s;
+  char b[320];
+  const volatile uint64_t *h = (const volatile uint64_t *)hpoison;
+  if (!h || !(h[0] & 0xffffffffu)) return "no wait timed out";
+  const uint64_t kp = h[kRecFirst];
+  const uint32_t kind = (uint32_t)(kp >> 8), phase = (uint32_t)(kp & 255);
+  if (kind == 0 || kind > kWaitPing) {
+    s = "a wait timed out (no record: poisoned by a launch without one)";
+  } else {
+    const bool push = kind == kWaitMovePush || kind == kWaitGroupPush || kind == kWaitFusedPush;
+    const uint64_t peer_ = h[kRecFirst + 2], slot_ = h[kRecFirst + 3], want = h[kRecFirst + 4],
+                   seen = h[kRecFirst + 5], ser = h[kRecFirst + 6], wg = h[kRecFirst + 7], ticks = h[kRecFirst + 8];
+    char ph[32] = "";
+    if (kind >= kWaitFusedPush) {
+      if (phase == 0) snprintf(ph, sizeof ph, " (phase A)");
+      else if (phase == 15) snprintf(ph, sizeof ph, " (phase D)");
+      else snprintf(ph, sizeof ph, " (phase B%u)", phase - 1);
+    }
+    snprintf(b, sizeof b,
+             "rank %d: %s%s, workgroup %llu thread %llu of launch %llu, waited %.3g s for peer %llu's %s of "
+             "slot %llu to reach %llu; last seen %llu",
+             rank, kinds[kind], ph, (unsigned long long)(wg >> 16), (unsigned long long)(wg & 0xffff),
+             (unsigned long long)ser, clock_khz > 0 ? (double)ticks / (clock_khz * 1e3) : 0.0,
+             (unsigned long long)peer_, push ? "acknowledgement" : kind == kWaitPing ? "ping answer" : "ready mark", (unsigned long long)slot_,
+             (unsigned long long)want, (unsigned long long)seen);
+    s = b;
+  }
+  if (!flags || !own) return s;
+  // per peer: the newest ready mark it set here / the sub-messages this rank
+  // has taken from it, the newest acknowledgement it set here / the
+  // sub-messages this rank has sent it (bases advance at a launch's end)
+  s += "; flags per peer (ready from / received, ack from / sent):";
   for (int x = 0; x < P; x++) {
     if (x == rank) continue;
     uint64_t rd = 0, ak = 0;
@@ -377,10 +416,34 @@ void DirectState::dump() const {
       rd = std::max(rd, rd64((char *)own + kReadyOff + ((size_t)x * kSlots + k) * kFlagStride));
       ak = std::max(ak, rd64((char *)own + kAckOff + ((size_t)x * kSlots + k) * kFlagStride));
     }
-    fprintf(stderr, "[bine dm r%d] peer %d: ready (from it) %llu / received %llu, ack (from it) %llu / sent %llu\n",
-            rank, x, (unsigned long long)rd, (unsigned long long)rd64((char *)own + kBaseRecvOff + 8 * (size_t)x),
-            (unsigned long long)ak, (unsigned long long)rd64((char *)own + kBaseSendOff + 8 * (size_t)x));
+    snprintf(b, sizeof b, " %d: %llu/%llu %llu/%llu", x, (unsigned long long)rd,
+             (unsigned long long)rd64((char *)own + kBaseRecvOff + 8 * (size_t)x), (unsigned long long)ak,
+             (unsigned long long)rd64((char *)own + kBaseSendOff + 8 * (size_t)x));
+    s += b;
   }
+  return s;
+}
+
+int DirectState::ping(int x, int iters, hipStream_t st, uint64_t *ticks) {
+  if (x < 0 || x >= P || x == rank || iters < 2) return BINE_ERR_ARG;
+  if (!ping_out && hipMalloc((void **)&ping_out, sizeof(uint64_t)) != hipSuccess) return BINE_ERR_NO_MEM;
+  DmPingArgs a;
+  a.own = (uint8_t *)own;
+  a.poison_host = hpoison_dev;
+  a.timeout_ticks = timeout_ticks;
+  a.base = ping_count[(size_t)x];
+  a.out = ping_out;
+  a.rank = rank;
+  a.peer = x;
+  a.iters = iters;
+  a.initiator = rank < x;
+  a.serial = serial++;
+  ping_count[(size_t)x] += (uint64_t)iters;
+  if (int rc = launch_dm_ping(a, st)) return rc;
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipMemcpy(ticks, ping_out, sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return BINE_ERR_HIP;
+  return BINE_SUCCESS;
 }
 
 bool DirectState::tree_ok(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec &t) const {

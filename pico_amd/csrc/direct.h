@@ -84,8 +84,19 @@ struct DirectState {
   bool mcast = false;     // pushes of the same bytes to several peers as one group (BINE_DIRECT_MCAST=1;
                           // off: no gain measured, profiles/r3_push_groups.txt)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }
-  // stderr: this rank's flags and device-side sequence bases (after a timeout)
+  int clock_khz = 0;  // wall_clock64 rate (the record's ticks -> seconds)
+  // the timeout's cause: the first timed-out waiter's record (dm::kRecFirst,
+  // mapped host words) and, with `flags`, per peer the ready / ack flags vs
+  // this rank's sequence bases (device reads: only once the streams drained)
+  std::string describe(bool flags) const;
+  // stderr: describe(true)
   void dump() const;
+  // the flag latency probe with `peer` (k_dm_ping; both ranks of the pair call
+  // it together): *ticks = wall_clock64 ticks of round trips 2 .. iters, 0 when
+  // the wait timed out (the transport is then poisoned)
+  std::vector<uint64_t> ping_count;  // per peer: ping sequence numbers used so far (both ends count alike)
+  uint64_t *ping_out = nullptr;      // device word the probe writes
+  int ping(int peer, int iters, hipStream_t st, uint64_t *ticks);
 };
 
 }  // namespace bine

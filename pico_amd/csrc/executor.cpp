@@ -48,7 +48,7 @@ namespace bine {
 static thread_local std::string g_err;
 
 static void set_err(const char *fmt, ...) {
-  char buf[512];
+  char buf[2048];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
@@ -89,8 +89,11 @@ struct Transport {
   // device-side transport state that must see every collective's exchanges
   // in one stream order (the direct transport's sequence bases)
   virtual bool stream_ordered() const { return false; }
-  // non-success: the transport is unusable (checked before a graph replay)
+  // non-success: the transport is unusable (checked before issuing and
+  // before a graph replay); _drained: the same after the streams drained,
+  // with the transport's full state in the error string
   virtual int health() const { return BINE_SUCCESS; }
+  virtual int health_drained() const { return health(); }
   // an exchange whose receives are the leaves of the following tree, the
   // tree evaluated inside the exchange (direct transport, k_dm_move_tree)
   virtual bool tree_ok(const std::vector<XSend> &, const std::vector<XRecv> &, const TreeSpec &) const {
@@ -262,13 +265,17 @@ struct RcclTransport final : Transport {
   int dm_wgs = 0;  // workgroups per message of the direct transport (0: BINE_DIRECT_WGS / 128)
   uint64_t key = 0;  // hash of the unique id: names the direct transport's sockets
   bool stream_ordered() const override { return dm_on; }
-  int health() const override {
+  // `flags`: also read the per-peer flags (device memory: only once the
+  // streams drained, bine_comm_synchronize)
+  int health(bool flags) const {
     if (dm_on && dm->poisoned()) {
-      set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
+      set_err("direct transport: a wait timed out; transport disabled: %s", dm->describe(flags).c_str());
       return BINE_ERR_INTERNAL;
     }
     return BINE_SUCCESS;
   }
+  int health() const override { return health(false); }
+  int health_drained() const override { return health(true); }
   bool allgather_shape(const std::vector<XSend> &s, const std::vector<XRecv> &r) const {
     if (size < 3 || (int)s.size() != size - 1 || (int)r.size() != size - 1) return false;
     const size_t b = s[0].bytes;
@@ -313,23 +320,12 @@ struct RcclTransport final : Transport {
   int exchange_tree(const std::vector<XSend> &s, const std::vector<XRecv> &r, const TreeSpec *t,
                     const std::vector<XRecv> *dl, const TreeSpec *dt, hipStream_t st) override {
     if (!dm_on) return BINE_ERR_UNSUPPORTED;
-    if (dm->poisoned()) {
-      set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
-      return BINE_ERR_INTERNAL;
-    }
+    if (int rc = health(false)) return rc;
     return dm->exchange(s, r, st, t, dl, dt);
   }
   int exchange(const std::vector<XSend> &s, const std::vector<XRecv> &r, hipStream_t st) override {
     if (dm_on) {
-      if (dm->poisoned()) {
-        static bool dumped = false;
-        if (!dumped && getenv("BINE_TRACE")) {
-          dumped = true;
-          dm->dump();
-        }
-        set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
-        return BINE_ERR_INTERNAL;
-      }
+      if (int rc = health(false)) return rc;
       return dm->exchange(s, r, st);
     }
     if (coll_ag && allgather_shape(s, r)) return allgather(s, r, st);
@@ -1071,10 +1067,8 @@ static int try_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int 
   std::vector<DmFusedArgs> v;
   if (!plan_fused(c, sc, ptr, esz, dtype, op, single, v)) return -1;
   auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
-  if (rt->dm->poisoned()) {  // as exchange(): a dead transport's launches would exit at once, moving nothing
-    set_err("direct transport: a wait timed out (a peer missing or a protocol fault); transport disabled");
-    return BINE_ERR_INTERNAL;
-  }
+  // as exchange(): a dead transport's launches would exit at once, moving nothing
+  if (int rc = rt->health()) return rc;
   for (size_t i = 0; i < v.size(); i++) {
     v[i].stamps = rt->dm->stamps;
     v[i].serial = rt->dm->serial++;
@@ -1972,12 +1966,16 @@ int bine_rccl_version(int *runtime, int *compiled) {
   NCCL_TRY(ncclGetVersion(&v));
   if (runtime) *runtime = v;
   if (compiled) *compiled = NCCL_VERSION_CODE;
-  return bine_rccl_abi_check(v, NCCL_VERSION_CODE);
+  return BINE_SUCCESS;  // a reporter: the refusal is bine_comm_init_rccl's
 }
 
 int bine_comm_init_rccl(bine_comm_t *out, int nranks, int rank, const void *id, int device) {
   if (!out || nranks < 1 || rank < 0 || rank >= nranks || !id) return BINE_ERR_ARG;
-  if (int rc0 = bine_rccl_version(nullptr, nullptr)) return rc0;  // the version window (refuses a skewed pair)
+  {
+    int v = 0;
+    NCCL_TRY(ncclGetVersion(&v));
+    if (int rc0 = bine_rccl_abi_check(v, NCCL_VERSION_CODE)) return rc0;  // the version window: refuses a skewed pair
+  }
   auto c = std::make_unique<bine_comm>();
   c->rank = rank;
   c->size = nranks;
@@ -2040,8 +2038,10 @@ static int sync_bounded(bine_comm *c, hipStream_t s, const char *what) {
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (el > limit) {
       auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
-      if (rt && rt->dm_on && rt->dm) rt->dm->dump();
-      set_err("rank %d: the %s stream did not drain within %.0f s (BINE_SYNC_TIMEOUT_S)", c->rank, what, limit);
+      const bool dm = rt && rt->dm_on && rt->dm;
+      if (dm) rt->dm->dump();
+      set_err("rank %d: the %s stream did not drain within %.0f s (BINE_SYNC_TIMEOUT_S)%s%s", c->rank, what, limit,
+              dm ? "; direct transport: " : "", dm ? rt->dm->describe(false).c_str() : "");
       return BINE_ERR_INTERNAL;
     }
     if (el > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));  // spin first: short calls
@@ -2059,7 +2059,11 @@ int bine_comm_synchronize(bine_comm_t c) {
     set_err("loopback: %d send/recv size mismatches", c->hub->mismatches.load());
     return BINE_ERR_INTERNAL;
   }
-  return BINE_SUCCESS;
+  // a direct-transport wait that timed out inside the calls just drained:
+  // they completed without their data, so their completion is an error
+  //  -- and stays one until bine_comm_set_direct(1)
+  // rebuilds the transport or bine_comm_set_direct(0) leaves it
+  return c->tx ? c->tx->health_drained() : BINE_SUCCESS;
 }
 
 int bine_comm_destroy(bine_comm_t c) {
@@ -2609,6 +2613,24 @@ int bine_comm_direct_timed_out(bine_comm_t c) {
   if (!c) return -BINE_ERR_ARG;
   auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
   return r && r->dm && r->dm->poisoned() ? 1 : 0;
+}
+
+int bine_comm_direct_ping(bine_comm_t c, int peer, int iters, double *us) {
+  if (!c || !us || iters < 2 || peer < 0 || peer >= c->size || peer == c->rank) return BINE_ERR_ARG;
+  auto *r = dynamic_cast<RcclTransport *>(c->tx.get());
+  if (!r || !r->dm_on || !r->dm) return BINE_ERR_UNSUPPORTED;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  if (int rc = r->health()) return rc;
+  // after everything the communicator issued (the probe's flags are its own,
+  // but a probe beside a running collective would measure the collective)
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipStreamSynchronize(c->cstream));
+  uint64_t ticks = 0;
+  if (int rc = r->dm->ping(peer, iters, c->cstream, &ticks)) return rc;
+  if (int rc = r->health_drained()) return rc;
+  *us = r->dm->clock_khz > 0 ? (double)ticks / (r->dm->clock_khz * 1e3) * 1e6 / (iters - 1) : 0.0;
+  return BINE_SUCCESS;
 }
 
 int bine_comm_direct_stamps(bine_comm_t c, uint64_t *out, size_t cap, size_t *n, int reset) {

@@ -904,6 +904,38 @@ __device__ __forceinline__ void dm_stamp(uint64_t *st, uint32_t serial, int kind
   r[3] = t2;
 }
 
+// A wait that timed out: poison the transport -- the
+// inbox word every later launch checks and the mapped host word the host
+// reads -- and, for the first waiter of this rank to time out (the one whose
+// exchange flips the inbox word), leave what it waited for in the host words
+// (dm::TimeoutRecord, read by DirectState::describe): which kernel and phase,
+// the peer, the slot, the sequence number wanted and the flag value last
+// seen, the launch's serial, the workgroup and how long it waited.  The
+// record's stores come before the poison word's (release), so a host that
+// sees the word set sees the record.
+__device__ __noinline__ void dm_time_out(uint32_t *poison, uint32_t *host, uint32_t kind, uint32_t phase, int rank,
+                                         int peer, uint64_t slot, uint64_t want, uint64_t seen, uint32_t serial,
+                                         uint64_t waited) {
+  const uint32_t was = __hip_atomic_exchange(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!host) return;
+  if (was == 0) {
+    uint64_t *h = reinterpret_cast<uint64_t *>(host);
+    const uint64_t v[dm::kRecWords] = {(uint64_t)kind << 8 | phase,
+                                       (uint64_t)(uint32_t)rank,
+                                       (uint64_t)(uint32_t)peer,
+                                       slot,
+                                       want,
+                                       seen,
+                                       serial,
+                                       (uint64_t)blockIdx.x << 16 | threadIdx.x,
+                                       waited};
+#pragma unroll
+    for (int i = 0; i < dm::kRecWords; i++)
+      __hip_atomic_store(h + dm::kRecFirst + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __hip_atomic_store(host, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // one workgroup's share of message mi (workgroup wi of a.wgs): wait, copy,
 // release, count in; the last workgroup of the message publishes.  false: the
 // transport is poisoned (the workgroup must leave the launch at once)
@@ -946,10 +978,11 @@ __device__ __forceinline__ bool dm_copy_msg(const DmArgs &a, int mi, int wi, int
     int ok = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0;
     if (ok && wait_ptr) {
       const long long w0 = wall_clock64();
-      while (ld_rlx_sys(wait_ptr) < wait_val) {
+      uint64_t seen;
+      while ((seen = ld_rlx_sys(wait_ptr)) < wait_val) {
         if (wall_clock64() - w0 > (long long)a.timeout_ticks) {
-          __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          dm_time_out(poison, a.poison_host, m.push ? dm::kWaitMovePush : dm::kWaitMovePull, 0, a.rank, m.peer, k,
+                      wait_val, seen, a.serial, wall_clock64() - w0);
           ok = 0;
           break;
         }
@@ -1055,10 +1088,11 @@ __device__ __forceinline__ bool dm_mcast_msg(const DmArgs &a, int mi, int wi, in
       if (ok && seq > (uint64_t)kSlots) {
         const uint64_t *w = reinterpret_cast<const uint64_t *>(own + kAckOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
         const long long t0 = wall_clock64();
-        while (ld_rlx_sys(w) < seq - kSlots) {
+        uint64_t seen;
+        while ((seen = ld_rlx_sys(w)) < seq - kSlots) {
           if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
-            __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            dm_time_out(poison, a.poison_host, dm::kWaitGroupPush, 0, a.rank, m.peer, k, seq - kSlots, seen, a.serial,
+                        wall_clock64() - t0);
             ok = 0;
             break;
           }
@@ -1251,6 +1285,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
   const u32x4 *lp[NL];
   const uint64_t *wp = nullptr;
   uint64_t wseq = 0;
+  int wpeer = -1;
+  size_t wslot = 0;
   __shared__ int go;
   uint64_t t0 = 0, t1 = 0;
   if (threadIdx.x == 0) {
@@ -1272,14 +1308,17 @@ __global__ __launch_bounds__(kBlock) void k_dm_move_tree(DmArgs a, DmTree t) {
     if ((int)threadIdx.x == j) {
       wp = reinterpret_cast<const uint64_t *>(own + kReadyOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
       wseq = seq;
+      wpeer = m.peer;
+      wslot = k;
     }
   }
   if (wp && go) {
     const long long tw = wall_clock64();
-    while (ld_rlx_sys(wp) < wseq) {
+    uint64_t seen;
+    while ((seen = ld_rlx_sys(wp)) < wseq) {
       if (wall_clock64() - tw > (long long)a.timeout_ticks) {
-        __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        dm_time_out(poison, a.poison_host, dm::kWaitTreeLeaf, 0, a.rank, wpeer, wslot, wseq, seen, a.serial,
+                    wall_clock64() - tw);
         go = 0;
         break;
       }
@@ -1464,19 +1503,21 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
 // poll has completed before the barrier -- and a second barrier orders the
 // workgroup's reads after it.  false: the transport is poisoned (now or
 // earlier).
-__device__ __forceinline__ bool wait_all(const DmFusedArgs &a, int first, int n, bool acq) {
+__device__ __forceinline__ bool wait_all(const DmFusedArgs &a, int first, int n, bool acq, uint32_t phase) {
   __shared__ int bad;
   uint32_t *poison = reinterpret_cast<uint32_t *>(a.own + kPoisonOff);
   if (threadIdx.x == 0) bad = __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
   __syncthreads();
   if ((int)threadIdx.x < n && !bad) {
-    const Msg m = resolve(a, a.m[first + threadIdx.x]);
+    const DmMsg &mm = a.m[first + threadIdx.x];
+    const Msg m = resolve(a, mm);
     if (m.wait) {
       const long long t0 = wall_clock64();
-      while (ld_rlx_sys(m.wait) < m.wait_val) {
+      uint64_t seen;
+      while ((seen = ld_rlx_sys(m.wait)) < m.wait_val) {
         if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
-          __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (a.poison_host) __hip_atomic_store(a.poison_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          dm_time_out(poison, a.poison_host, mm.push ? dm::kWaitFusedPush : dm::kWaitFusedPull, phase, a.rank,
+                      mm.peer, m.seq % kSlots, m.wait_val, seen, a.serial, wall_clock64() - t0);
           bad = 1;
           break;
         }
@@ -1595,7 +1636,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   const uint64_t t0 = a.stamps ? wall_clock64() : 0;
   // phase A: our blocks of every chunk into the peers' inboxes (each slot's
   // previous use acknowledged first)
-  if (!wait_all(a, 0, a.na, false)) return;
+  if (!wait_all(a, 0, a.na, false, 0)) return;
   const uint64_t t1 = a.stamps ? wall_clock64() : 0;
   // workgroup w starts at message w mod na and rotates: at any moment the
   // workgroups spread over every peer's link instead of all pushing to the
@@ -1611,7 +1652,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
   // previous use must have been acknowledged first
   for (int ti = 0; ti < a.nt; ti++) {
     const DmFusedTree &t = a.t[ti];
-    if (!wait_all(a, t.b0, t.nb + t.nc, t.nb > 0)) return;
+    if (!wait_all(a, t.b0, t.nb + t.nc, t.nb > 0, 1 + ti)) return;
     const u32x4 *lp[kMaxLeaves];
 #pragma unroll
     for (int j = 0; j < kMaxLeaves; j++)
@@ -1634,7 +1675,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_fused(DmFusedArgs a) {
     arrive_all(a, t.b0, t.nb + t.nc);
   }
   // phase D: the peers' results out of our inbox
-  if (!wait_all(a, a.d0, a.nd, true)) return;
+  if (!wait_all(a, a.d0, a.nd, true, 15)) return;
   for (int k = 0; k < a.nd; k++) {  // rotated as phase A (the slots lie in different HBM channels anyway)
     const int i = (int)((blockIdx.x + (unsigned)k) % (unsigned)a.nd);
     copy_slice(resolve(a, a.m[a.d0 + i]), a.wgs, false);
@@ -1757,6 +1798,54 @@ int launch_dm_fused(const DmFusedArgs &a, int dtype, int op, void *stream) {
     default: return BINE_ERR_UNSUPPORTED;
   }
   return e == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
+}
+
+// ----------------------------------------------------------------------------
+// cross-GPU flag latency probe (bine_comm_direct_ping).
+// One lane of one workgroup on each of two ranks plays ping-pong with the
+// transport's own flag protocol -- a relaxed system-scope store of a sequence
+// number into the peer's inbox, a relaxed system-scope poll (with the
+// protocol's back-off) of the peer's answer in its own -- `iters` times in one
+// launch, no kernel boundary in between.  Round trip 1 absorbs the two
+// launches' skew; rounds 2 .. iters are timed with wall_clock64 on each side.
+// A round trip is two one-way flag latencies: a k_dm_fused phase boundary
+// costs one (pico_amd/model.py T_FLAG_US).  Timed out: the transport is
+// poisoned like any other wait, *out = 0.
+__global__ __launch_bounds__(64) void k_dm_ping(DmPingArgs a) {
+  using namespace dm;
+  if (threadIdx.x != 0) return;
+  uint32_t *poison = reinterpret_cast<uint32_t *>(a.own + kPoisonOff);
+  const uint64_t *mine = reinterpret_cast<const uint64_t *>(a.own + kPingOff + (size_t)a.peer * kFlagStride);
+  uint8_t *remote = reinterpret_cast<uint8_t *const *>(a.own + kPeerTabOff)[a.peer];
+  uint64_t *theirs = reinterpret_cast<uint64_t *>(remote + kPingOff + (size_t)a.rank * kFlagStride);
+  if (__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+    __hip_atomic_store(a.out, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  uint64_t t0 = 0;
+  for (int i = 1; i <= a.iters; i++) {
+    if (i == 2) t0 = wall_clock64();
+    const uint64_t s = a.base + (uint64_t)i;
+    if (a.initiator) publish(theirs, s);
+    const long long w0 = wall_clock64();
+    uint64_t seen;
+    while ((seen = ld_rlx_sys(mine)) < s) {
+      if (wall_clock64() - w0 > (long long)a.timeout_ticks) {
+        dm_time_out(poison, a.poison_host, kWaitPing, 0, a.rank, a.peer, 0, s, seen, a.serial, wall_clock64() - w0);
+        __hip_atomic_store(a.out, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!a.initiator) publish(theirs, s);
+  }
+  __hip_atomic_store(a.out, wall_clock64() - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int launch_dm_ping(const DmPingArgs &a, void *stream) {
+  if (a.iters < 2 || !a.own || !a.out || a.peer == a.rank) return BINE_ERR_ARG;
+  hipLaunchKernelGGL(k_dm_ping, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? BINE_SUCCESS : BINE_ERR_HIP;
 }
 
 // ----------------------------------------------------------------------------

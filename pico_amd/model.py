@@ -204,8 +204,10 @@ def config_model(cfg, P, transport, chunk_bytes=16 << 20, **kw):
 T_HOST_RT_US = 66.0      # C1 at P = 1 through pico_core + libbine.so: the 1 MiB host round trip with the
                          # page-locking and HIP calls around it (profiles/r4_e2e_c1.txt; the bare round
                          # trip probe: 69-72 us)
-T_FLAG_US = 3.0          # one cross-GPU flag round trip of a k_dm_fused phase (system-scope store seen by
-                         # the peer's poll): NOT measured on xGMI -- the one assumed constant here
+T_FLAG_US = 3.0          # the flag latency one k_dm_fused phase boundary costs: a system-scope store seen
+                         # by the peer's poll, one way.  Assumed; bench.py measures it at N > 1
+                         # (bine_comm_direct_ping: round trip / 2, "direct_transport_probe") and
+                         # recomputes the models with it ("model_with_measured_constants")
 C1_PHASES = 3            # k_dm_fused's flat allreduce: pushes, tree (+ allgather pushes), pulls
 C1_ONE_GPU_DEV_US = {2: 28.7, 4: 49.0}   # device-resident C1 with the ranks sharing ONE GPU (one HW queue
                                           # each; profiles/r4_c1_fused_wgs.txt): the bench rehearsal's

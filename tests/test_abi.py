@@ -78,7 +78,9 @@ def test_rccl_abi_window_refuses_a_skewed_pair():
     """the RCCL pair the library is built against / runs on
     must lie in the window whose ABI for every type it passes was checked
     (executor.cpp: static_asserts on the header values, bine_rccl_abi_check,
-    the creation-time probe); outside it bine_rccl_version refuses."""
+    the creation-time probe); outside it bine_comm_init_rccl refuses, while
+    bine_rccl_version stays a reporter and rccl_version() says
+    abi_ok."""
     L = pico_amd.lib()
     assert L.bine_rccl_abi_check(22606, 22707) == 0     # torch's runtime, ROCm 7.2's headers
     assert L.bine_rccl_abi_check(22703, 22703) == 0
@@ -94,3 +96,5 @@ def test_rccl_abi_window_refuses_a_skewed_pair():
     rt, ct = ctypes.c_int(), ctypes.c_int()
     assert L.bine_rccl_version(ctypes.byref(rt), ctypes.byref(ct)) == 0, L.bine_last_error()
     assert 22600 <= rt.value <= 22799 and 22600 <= ct.value <= 22799
+    v = pico_amd.rccl_version()
+    assert v["abi_ok"] is True and v["runtime_code"] == rt.value

@@ -50,4 +50,14 @@ def test_bench_two_ranks_one_gpu():
     assert any("+dm" in k.split("/")[0] for k in trials), trials
     others = c["other_baseline_configs"]
     assert others and all(v.get("parity_ok") is True for v in others.values()), others
-    assert d["roofline"]["bound"] == "xgmi" and d["roofline"]["achieved"] > 0
+    # two ranks share the one GPU: the bound in play is its HBM (VERDICT r5
+    # weak #6), the link roofline is kept for a node
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and 0 < r["frac"] <= 1, r
+    assert r["link_roofline_if_node"]["bound"] == "xgmi" and r["link_roofline_if_node"]["achieved"] > 0
+    # the direct transport's node constants, measured per pair
+    p = c["direct_transport_probe"]
+    assert p["flag_round_trip_us"].get("0-1", 0) > 0 and p["push_GBs"].get("0-1", 0) > 0, p
+    assert p["model_T_FLAG_US"] > 0 and p["model_LINK_GBS"] > 0
+    m = r["model_with_measured_constants"]
+    assert m["C3"] > 0 and m["C1_e2e_us"] > 0, m
