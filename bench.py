@@ -219,16 +219,43 @@ class Drain:
         return g
 
     def failed(self, dist):
-        """None when no rank saw an error, else 'rank r: <its error>' for the
-        lowest such rank (collective: every rank gets the same answer)"""
+        """None when no rank saw an error, else every such rank's error --
+        'rank r: <its error>' joined by ' || ', lowest rank first; a
+        direct-transport timeout carries the waiter's record and both ends'
+        flags and bases (DirectState::describe), so the line says which wait
+        of which rank stalled on what -- plus the box's queue census
+        (VERDICT r5 item 3).  Collective: every rank gets the same answer."""
         if dist is None:
-            return None if self.err is None else f"rank 0: {self.err}"
-        errs = [None] * dist.get_world_size()
-        dist.all_gather_object(errs, self.err)
-        for r, e in enumerate(errs):
-            if e is not None:
-                return f"rank {r}: {e}"
-        return None
+            errs = [self.err]
+        else:
+            errs = [None] * dist.get_world_size()
+            dist.all_gather_object(errs, self.err)
+        bad = [f"rank {r}: {e[:1500]}" for r, e in enumerate(errs) if e is not None]
+        if not bad:
+            return None
+        return " || ".join(bad) + " || " + queue_census()
+
+
+def queue_census():
+    """compute queues per process on the box's GPUs (KFD sysfs), in one line:
+    how many user-mode queues the scheduler has to place when a wait times
+    out (past the hardware's slots it time-slices them)"""
+    try:
+        base = "/sys/class/kfd/kfd/proc"
+        per = []
+        for pid in sorted(os.listdir(base)):
+            qd = os.path.join(base, pid, "queues")
+            if not os.path.isdir(qd):
+                continue
+            n = 0
+            for q in os.listdir(qd):
+                with open(os.path.join(qd, q, "type")) as f:
+                    n += f.read().strip() == "0"
+            if n:
+                per.append(n)
+        return f"KFD compute queues: {sum(per)} in {len(per)} processes {per}"
+    except OSError as e:
+        return f"KFD compute queues: unreadable ({e})"
 
 
 def measure(torch, stream, dist, comm, call, steps, warmup):
@@ -301,9 +328,12 @@ def cpu_baseline(gpu_digest=None, budget_s: float = 5.0):
     reference sources against MPICH 3.3.2) on 256 MiB fp32 per rank at P = 1
     (`value`: the single-GPU line's comparison), and at P = 2, 4, 8 host ranks
     (one per core), same statistic; its output digest is compared with the
-    GPU's and the oracle's.  Plus C1 (the reference's own CPU configuration)
-    and MPICH's MPI_Reduce_local on C2 (libbine's arithmetic).  Falls back to
-    the oracle's restatement (kind "port") when the reference build is absent."""
+    GPU's and the oracle's.  Plus C1 (the reference's own CPU configuration),
+    C4 (reduce_scatter_bine_permute_remap, 1 GiB fp32 per rank) and C5
+    (allreduce_bine_bdw_remap fp64 / int64, 256 MiB per rank) at P = 8 host
+    ranks, each digest-checked, and MPICH's MPI_Reduce_local on C2 (libbine's
+    arithmetic).  Falls back to the oracle's restatement (kind "port") when
+    the reference build is absent."""
     S = C3_ELEMS * 4
     host = host_info()
     if not (os.path.exists(REF_BENCH) and os.path.exists(MPIEXEC)):
@@ -339,6 +369,35 @@ def cpu_baseline(gpu_digest=None, budget_s: float = 5.0):
     if c1 and c1.get("rc") == 0:
         out["libbine_allreduce_bine_bdw_remap_c1_P4"] = {"us": round(c1["median_s"] * 1e6, 2), "cores": 4,
                                                           "iterations": 200}
+    # BASELINE configs C4 and C5 on the host cores: the
+    # reference's reduce_scatter_bine_permute_remap on 1 GiB fp32 per rank and
+    # its allreduce_bine_bdw_remap on 256 MiB of fp64 / int64 per rank, both
+    # at P = 8 host ranks (one per core), the same statistic, rank 0's output
+    # digest against the committed oracle digest
+    for name, args, key, S_ in (
+            ("libbine_reduce_scatter_bine_permute_remap_c4_P8",
+             ["reduce_scatter", "bine_permute_remap", C4_ELEMS, 3],
+             gkey("C4", "reduce_scatter", "bine_permute_remap", "float", C4_ELEMS, 8), C4_ELEMS * 4),
+            ("libbine_allreduce_bine_bdw_remap_c5_double_P8",
+             ["allreduce", "bine_bdw_remap", C5_ELEMS, 5, "double"],
+             gkey("C5", "allreduce", "bine_bdw_remap", "double", C5_ELEMS, 8), C5_ELEMS * 8),
+            ("libbine_allreduce_bine_bdw_remap_c5_int64_P8",
+             ["allreduce", "bine_bdw_remap", C5_ELEMS, 5, "int64"],
+             gkey("C5", "allreduce", "bine_bdw_remap", "int64", C5_ELEMS, 8), C5_ELEMS * 8)):
+        try:
+            r = _ref_bench(8, args, 180)
+        except Exception:
+            r = None
+        if r and r.get("rc") == 0:
+            t = r["median_s"]
+            want = golden(key)
+            rs = args[0] == "reduce_scatter"
+            out[name] = {"ms": round(t * 1e3, 3), "cores": 8, "iterations": r["iters"],
+                         ("busbw_per_rank_GBs" if rs else "algbw_per_rank_GBs"):
+                             round((7 / 8 if rs else 1.0) * S_ / t / 1e9, 3),
+                         "output_digest_equals_oracle": None if want is None else int(r["digest"]) == int(want[0])}
+        else:
+            out[name] = {"error": "ref_bench failed" if r is None else f"rc {r.get('rc')}"}
     try:
         rl = _ref_bench(1, ["reduce_local", C2_ELEMS, budget_s], budget_s + 60)
     except Exception:
@@ -1081,7 +1140,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             # a call whose direct-transport wait timed out reports it at its
             # completion on the rank that timed out (the call ran on without
             # its data): agreed over the ranks, with the waiter's record
-            verdicts[cfg] = ok if why_err is None else f"failed: {why_err}"[:700]
+            verdicts[cfg] = ok if why_err is None else f"failed: {why_err}"[:16000]
             trials[cfg] = st["median_ms"] if ok is not False and why_err is None else float("inf")
             if cfg[2] and comm.graphs_cached() == 0:
                 # the library kept every call eager (its HIP-runtime gate,
@@ -1097,7 +1156,7 @@ def bench_allreduce(steps: int, warmup: int, nelem: int, algo: str, relay: str, 
             torch.cuda.synchronize()
             Drain(comm)()
             trials[cfg] = float("inf")
-            verdicts[cfg] = f"error: {e}"[:700]
+            verdicts[cfg] = f"error: {e}"[:2000]
             if dm_wgs(cfg[0]) is not None and e.status == 6:   # BINE_ERR_UNSUPPORTED: setup failed
                 # symmetric: setup is agreed over RCCL, so every rank stops
                 # trying together

@@ -252,8 +252,9 @@ int bine_comm_set_chunk(bine_comm_t comm, size_t bytes);
  * :898-906).  On a fully connected node that is one hop on every link at once.
  * The allgather family (out of place) becomes one all-peers exchange after
  * its own plan has decided the status.  Pure data movement: results
- * identical bit for bit.  Off by default (the literal schedule;
- * BINE_FLAT_AG=1 turns it on); collective.  on = 2 (BINE_FLAT_AG=2): with
+ * identical bit for bit.  Off by default in the core (the literal schedule;
+ * BINE_FLAT_AG=1 turns it on; libbine.so turns it on, bine_dropin_defaults);
+ * collective.  on = 2 (BINE_FLAT_AG=2): with
  * the flat reduce-scatter too, the allreduces' allgather is cut with the
  * reduce-scatter's chunks, chunk k's results leaving right after chunk k+1's
  * reduce-scatter exchange, so the output completes chunk by chunk. */
@@ -332,8 +333,24 @@ int bine_comm_set_coll_a2a(bine_comm_t comm, int on);
  * (BINE_PRIM_REDUCE_TREE: reads P blocks, writes one).  Results identical bit
  * for bit to the literal schedule.  Chunked like the other pipelined steps
  * (the transfer of chunk k+1 overlaps the tree of chunk k).  Off by default
- * (BINE_FLAT_RS=1 turns it on); collective. */
+ * in the core (BINE_FLAT_RS=1 turns it on; libbine.so turns it on,
+ * bine_dropin_defaults); collective. */
 int bine_comm_set_flat_rs(bine_comm_t comm, int on);
+/* The forms libbine.so (the libbine.h drop-in) gives each communicator it
+ * creates for the unchanged pico_core, host only, from
+ * the environment at the call: by default the fastest bit-identical forms --
+ * the flat reduce-scatter and flat allgather phases (the planner applies them
+ * where they exist: power-of-two P, the Bine remap / static / rabenseifner
+ * allreduces, the remap / static reduce-scatters, reduce_bine_bdw, the
+ * one-shot latency forms; elsewhere the literal schedule) and, at P > 1, the
+ * direct peer-memory transport (its fused trees and, where a call's plan fits,
+ * the whole call as ONE k_dm_fused launch -- C1 and C3 do); a communicator
+ * whose ranks cannot set the direct transport up keeps RCCL P2P.
+ * BINE_LITERAL=1: the reference's literal schedule over RCCL P2P (all three
+ * off).  BINE_FLAT_RS, BINE_FLAT_AG (0 / 1 / 2) and BINE_DIRECT (0 / 1)
+ * override one setting each.  The choice depends on P and the environment
+ * only -- the same on every rank. */
+int bine_dropin_defaults(int P, int *flat_rs, int *flat_ag, int *direct);
 
 /* Direct peer-memory transport (RCCL communicators, one node): exchanges
  * move through device memory every rank maps from every peer (VMM

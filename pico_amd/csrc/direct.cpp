@@ -405,20 +405,34 @@ std::string DirectState::describe(bool flags) const {
     s = b;
   }
   if (!flags || !own) return s;
-  // per peer: the newest ready mark it set here / the sub-messages this rank
-  // has taken from it, the newest acknowledgement it set here / the
-  // sub-messages this rank has sent it (bases advance at a launch's end)
-  s += "; flags per peer (ready from / received, ack from / sent):";
+  // per peer x, read here and -- through the mapping every rank holds of
+  // every peer's inbox -- in x's own inbox: the ready marks x set in our
+  // slots 0..3, the sub-messages we have taken from x (our base) against the
+  // ones x has sent us (x's base), the acknowledgements x set for our slots,
+  // our sends against x's receives, and whether x itself timed out.  Bases
+  // advance at a launch's end, so between calls both ends of a pair agree; a
+  // disagreement is an accounting fault, a lagging peer a peer that never
+  // ran its part.
+  auto u = [](uint64_t v) { return (unsigned long long)v; };
+  const uint32_t lc = (uint32_t)rd64((char *)own + kLaunchCntOff);
+  snprintf(b, sizeof b, "; launch counter %u; per peer x (ready x->us slots 0-3, bases us-recv/x-send, "
+                        "ack x->us slots 0-3, bases us-send/x-recv, x poisoned):", lc);
+  s += b;
   for (int x = 0; x < P; x++) {
     if (x == rank) continue;
-    uint64_t rd = 0, ak = 0;
+    uint64_t rd[kSlots], ak[kSlots];
     for (int k = 0; k < kSlots; k++) {
-      rd = std::max(rd, rd64((char *)own + kReadyOff + ((size_t)x * kSlots + k) * kFlagStride));
-      ak = std::max(ak, rd64((char *)own + kAckOff + ((size_t)x * kSlots + k) * kFlagStride));
+      rd[k] = rd64((char *)own + kReadyOff + ((size_t)x * kSlots + k) * kFlagStride);
+      ak[k] = rd64((char *)own + kAckOff + ((size_t)x * kSlots + k) * kFlagStride);
     }
-    snprintf(b, sizeof b, " %d: %llu/%llu %llu/%llu", x, (unsigned long long)rd,
-             (unsigned long long)rd64((char *)own + kBaseRecvOff + 8 * (size_t)x), (unsigned long long)ak,
-             (unsigned long long)rd64((char *)own + kBaseSendOff + 8 * (size_t)x));
+    const char *px = x < (int)peer.size() ? (const char *)peer[(size_t)x] : nullptr;
+    const uint64_t xs = px ? rd64(px + kBaseSendOff + 8 * (size_t)rank) : ~0ull,
+                   xr = px ? rd64(px + kBaseRecvOff + 8 * (size_t)rank) : ~0ull,
+                   xp = px ? rd64(px + kPoisonOff) & 0xffffffffu : ~0ull;
+    snprintf(b, sizeof b, " %d: r[%llu %llu %llu %llu] %llu/%llu a[%llu %llu %llu %llu] %llu/%llu p%llu;", x,
+             u(rd[0]), u(rd[1]), u(rd[2]), u(rd[3]), u(rd64((char *)own + kBaseRecvOff + 8 * (size_t)x)), u(xs),
+             u(ak[0]), u(ak[1]), u(ak[2]), u(ak[3]), u(rd64((char *)own + kBaseSendOff + 8 * (size_t)x)), u(xr),
+             u(xp));
     s += b;
   }
   return s;
@@ -523,9 +537,13 @@ int DirectState::exchange(const std::vector<XSend> &s, const std::vector<XRecv> 
     // the GPU idle at `wgs` workgroups each: every copy takes the same whole
     // multiple of its workgroups that the resident capacity allows, keeping
     // at least 64 KiB per workgroup.  The protocol does not care how many
-    // workgroups a copy has (each launch counts its own arrivals).
-    if (plain && autoscale && a.ncw > 0) {
-      const int cap = dm_launch_cap(0, 0, 0, 0, share);
+    // workgroups a copy has (each launch counts its own arrivals).  Bounded
+    // (ADVICE r5): launches of at most two copies (the measured gains: one
+    // push and one pull, a rooted collective's single message), and to half
+    // the resident capacity, so a direct launch of this rank in flight on
+    // another stream (a tree, a fused call) keeps room beside it.
+    if (plain && autoscale && a.ncw > 0 && a.ncopy <= 2) {
+      const int cap = dm_launch_cap(0, 0, 0, 0, share) / 2;
       const int k = cap > 0 ? cap / a.ncw : 1;
       if (k > 1) {
         a.ncw = 0;

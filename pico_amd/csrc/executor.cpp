@@ -48,7 +48,7 @@ namespace bine {
 static thread_local std::string g_err;
 
 static void set_err(const char *fmt, ...) {
-  char buf[2048];
+  char buf[4096];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
@@ -923,6 +923,15 @@ static bool build_fused(const FusedEnv &e, OpSpan ops, Ptr ptr, size_t esz, int 
     owns.push_back({(const char *)ft.own_leaf, (const char *)ft.own_leaf + tb});
     for (int j = 0; j < kMaxLeaves; j++) ft.leaf[j] = -1;
   }
+  // a tree's own leaf written by ANOTHER chunk's tree: there is
+  // no grid barrier between the phases, so that is only safe when the bytes
+  // a workgroup reads are the bytes it wrote itself -- the same range cut
+  // into the same slices (equal nvec); anything else is not this form
+  for (size_t k = 0; k < C; k++)
+    for (size_t k2 = 0; k2 < C; k2++)
+      if (k2 != k && overlap(owns[k2], outs[k]) &&
+          (owns[k2].lo != outs[k].lo || owns[k2].hi != outs[k].hi || a.t[k2].nvec != a.t[k].nvec))
+        return false;
   std::vector<int> js((size_t)e.P, 0), jr((size_t)e.P, 0);
   int n = 0;
   auto add = [&](int peer, uint64_t bytes, bool push, const void *src, void *dst) -> bool {
@@ -2681,6 +2690,19 @@ int bine_comm_set_direct_tree(bine_comm_t c, int on) {
   c->dm_tree_wgs = w;
   if (auto *r = dynamic_cast<RcclTransport *>(c->tx.get()))
     if (r->dm) r->dm->tree_wgs = w ? w : r->dm->tree_wgs_env;
+  return BINE_SUCCESS;
+}
+
+int bine_dropin_defaults(int P, int *flat_rs, int *flat_ag, int *direct) {
+  if (P < 1 || !flat_rs || !flat_ag || !direct) return BINE_ERR_ARG;
+  auto env = [](const char *k) -> const char * {
+    const char *v = getenv(k);
+    return v && *v ? v : nullptr;
+  };
+  const bool literal = env("BINE_LITERAL") && atoi(env("BINE_LITERAL")) != 0;
+  *flat_rs = env("BINE_FLAT_RS") ? atoi(env("BINE_FLAT_RS")) != 0 : !literal;
+  *flat_ag = env("BINE_FLAT_AG") ? std::max(0, std::min(atoi(env("BINE_FLAT_AG")), 2)) : !literal;
+  *direct = P > 1 && (env("BINE_DIRECT") ? atoi(env("BINE_DIRECT")) > 0 : !literal);
   return BINE_SUCCESS;
 }
 

@@ -43,7 +43,44 @@ struct Entry {
   hipStream_t h2d = nullptr, d2h = nullptr;
   std::vector<hipEvent_t> ev;
   size_t ev_next = 0;
+  // page-locked bounce buffers for small host buffers (bounce_bytes())
+  void *bounce[2] = {nullptr, nullptr};
+  size_t bounce_cap[2] = {0, 0};
 };
+
+// Small host buffers go through two page-locked bounce buffers the
+// communicator owns: the caller's bytes are memcpy'd into
+// them (and the result out of them) on the CPU, so the call registers nothing
+// -- per-call hipHostRegister / hipHostUnregister of a 1 MiB buffer costs
+// more than its PCIe transfer (C1 at P = 1: 66 us of which ~38 us are the
+// 2 MiB on the link).  Nothing outlives the call: the bounce
+// buffers belong to the library, the caller's pages are never pinned.  Calls
+// whose host buffers are larger keep the per-call registration (memcpy
+// through a bounce buffer is slower than DMA from registered pages there,
+// profiles/r4_host_stage_probe.txt).  BINE_HOST_BOUNCE_BYTES (default 4 MiB;
+// 0 = off) is the largest buffer that bounces.
+size_t bounce_bytes() {
+  static const size_t v = getenv("BINE_HOST_BOUNCE_BYTES") ? (size_t)strtoull(getenv("BINE_HOST_BOUNCE_BYTES"),
+                                                                              nullptr, 10)
+                                                           : (size_t)4 << 20;
+  return v;
+}
+
+// bounce buffer `slot` of at least `bytes` (grown on demand, kept); nullptr
+// when it cannot be allocated (the call then registers, as a large one)
+void *bounce_buf(Entry *e, int slot, size_t bytes) {
+  if (e->bounce_cap[slot] < bytes) {
+    if (e->bounce[slot]) (void)hipHostFree(e->bounce[slot]);
+    e->bounce[slot] = nullptr;
+    e->bounce_cap[slot] = 0;
+    if (hipHostMalloc(&e->bounce[slot], bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    e->bounce_cap[slot] = bytes;
+  }
+  return e->bounce[slot];
+}
 
 // Host buffers page-locked for ONE call.  A permanent
 // registration cache is unsafe in a general MPI library: a buffer freed and
@@ -130,8 +167,10 @@ void release(Entry *e) {
     bine_comm_synchronize(e->comm);
     bine_comm_destroy(e->comm);
   }
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < 2; i++) {
     if (e->dev[i]) (void)hipFree(e->dev[i]);
+    if (e->bounce[i]) (void)hipHostFree(e->bounce[i]);
+  }
   if (e->h2d) (void)hipStreamDestroy(e->h2d);
   if (e->d2h) (void)hipStreamDestroy(e->d2h);
   for (auto x : e->ev) (void)hipEventDestroy(x);
@@ -250,15 +289,26 @@ int get_entry(MPI_Comm comm, Entry **out) {
   MPI_Bcast(id, BINE_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
   st = bine_comm_init_rccl(&e->comm, e->size, e->rank, id, device);
   if (st != BINE_SUCCESS) { delete e; return to_mpi(st); }
-  // BINE_DIRECT=1: exchanges over the direct peer-memory transport instead of
-  // RCCL P2P (bine_comm_set_direct; collective, and every rank of a pico_core
-  // run sees the same environment).  Setup is agreed over RCCL, so a failure
-  // is the same on every rank: then the communicator keeps RCCL.
-  const char *dm = getenv("BINE_DIRECT");
-  if (e->size > 1 && dm && atoi(dm) > 0) {
+  // The drop-in's forms (bine_dropin_defaults): the
+  // fastest bit-identical ones unless the environment says otherwise -- the
+  // flat phases, and exchanges over the direct peer-memory transport instead
+  // of RCCL P2P (bine_comm_set_direct; collective, and every rank of a
+  // pico_core run sees the same environment).  Setup is agreed over RCCL, so
+  // a failure is the same on every rank: then the communicator keeps RCCL.
+  int frs = 0, fag = 0, dm = 0;
+  if ((st = bine_dropin_defaults(e->size, &frs, &fag, &dm)) == BINE_SUCCESS &&
+      (st = bine_comm_set_flat_rs(e->comm, frs)) == BINE_SUCCESS)
+    st = bine_comm_set_flat_ag(e->comm, fag);
+  if (st != BINE_SUCCESS) {
+    bine_comm_destroy(e->comm);
+    delete e;
+    return to_mpi(st);
+  }
+  if (dm) {
     const int dst = bine_comm_set_direct(e->comm, 1);
     if (dst != BINE_SUCCESS && e->rank == 0)
-      fprintf(stderr, "libbine(amd): BINE_DIRECT=1 but the direct transport is unavailable (%d); using RCCL\n", dst);
+      fprintf(stderr, "libbine(amd): the direct transport is unavailable (%d: %s); using RCCL P2P\n", dst,
+              bine_last_error());
   }
   MPI_Comm_set_attr(comm, g_keyval, e);
   g_entries.insert(e);
@@ -359,26 +409,43 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
   bool stage_r = rbuf && rbytes && !on_device(rbuf);
   int rc;
   if ((rc = copy_streams(e))) return rc;
+  const size_t ch = esz ? stage_chunk_bytes() / esz * esz : 0;
+  const size_t total = count * esz;
+  const bool piped = ch && total >= 2 * ch && (stage_s || stage_r) && (!stage_s || sbytes == total) &&
+                     (!stage_r || rbytes == total);
+  // small host buffers: through the communicator's page-locked bounce buffers
+  // (nothing registered); the caller's input is copied in on the CPU now
+  void *bs = nullptr, *br = nullptr;
+  const bool fill_r = stage_r && (in_place || read_rbuf);  // (every earlier call has drained all three streams)
+  if (!piped && (stage_s || stage_r) && std::max(stage_s ? sbytes : 0, stage_r ? rbytes : 0) <= bounce_bytes()) {
+    bs = stage_s ? bounce_buf(e, 0, sbytes) : nullptr;
+    br = stage_r ? bounce_buf(e, 1, rbytes) : nullptr;
+    if ((stage_s && !bs) || (stage_r && !br)) bs = br = nullptr;  // no bounce memory: register as a large call
+  }
+  const bool bounced = bs || br;
   CallPins pins;
   if (stage_s) {
     void *d;
     if ((rc = stage(e, 0, sbytes, &d))) return rc;
     ds = d;
-    pins.add(sbuf, sbytes);
+    if (bounced) memcpy(bs, sbuf, sbytes);
+    else pins.add(sbuf, sbytes);
   }
   if (stage_r) {
     void *d;
     if ((rc = stage(e, 1, rbytes, &d))) return rc;
     dr = d;
-    pins.add(rbuf, rbytes);
+    if (bounced) {
+      if (fill_r) memcpy(br, rbuf, rbytes);
+    } else {
+      pins.add(rbuf, rbytes);
+    }
   }
   pins.commit();
-  const bool fill_r = stage_r && (in_place || read_rbuf);  // (every earlier call has drained all three streams)
-  const size_t ch = esz ? stage_chunk_bytes() / esz * esz : 0;
-  const size_t total = count * esz;
+  const void *hs = bounced && stage_s ? bs : sbuf;  // the host side of the copies
+  void *hr = bounced && stage_r ? br : rbuf;
   auto issue = [&]() -> int {
-    if (ch && total >= 2 * ch && (stage_s || stage_r) && (!stage_s || sbytes == total) &&
-        (!stage_r || rbytes == total)) {
+    if (piped) {
       for (size_t off = 0; off < total; off += ch) {
         const size_t len = std::min(ch, total - off);
         if (stage_s && hipMemcpyAsync((char *)ds + off, (const char *)sbuf + off, len, hipMemcpyHostToDevice,
@@ -401,18 +468,21 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
     // unpipelined: copy in, collective, copy out depend on each other in
     // turn, so they share the collective's stream -- no cross-stream event
     // hops (a small call's latency is mostly such hops: C1 end to end)
-    if (stage_s && hipMemcpyAsync((void *)ds, sbuf, sbytes, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (stage_s && hipMemcpyAsync((void *)ds, hs, sbytes, hipMemcpyHostToDevice, st) != hipSuccess)
       return MPI_ERR_OTHER;
-    if (fill_r && hipMemcpyAsync(dr, rbuf, rbytes, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (fill_r && hipMemcpyAsync(dr, hr, rbytes, hipMemcpyHostToDevice, st) != hipSuccess)
       return MPI_ERR_OTHER;
     if (int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st)) return to_mpi(bst);
-    if (stage_r && hipMemcpyAsync(rbuf, dr, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess) return MPI_ERR_OTHER;
+    if (stage_r && hipMemcpyAsync(hr, dr, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess) return MPI_ERR_OTHER;
     return MPI_SUCCESS;
   };
   rc = issue();
   // drain whatever was issued (also after an error: the registrations must
   // outlive every copy that uses them)
   const int rc2 = finish(e, pins, {{e->h2d, "host-to-device"}, {e->d2h, "device-to-host"}, {st, "collective"}});
+  // a bounced result reaches the caller's buffer only from a call that
+  // completed (an error leaves rbuf as it was)
+  if (!rc && !rc2 && bounced && stage_r) memcpy(rbuf, br, rbytes);
   return rc ? rc : rc2;
 }
 

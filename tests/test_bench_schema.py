@@ -124,7 +124,7 @@ def test_library_errors_agreed_over_ranks():
     assert all(p.exitcode == 0 for p in ps)
     for r in (0, 1):
         a, b, c, ncalls = res[r]
-        assert a is not None and a.startswith("rank 1: ")
+        assert a is not None and a.startswith("rank 1: ") and "KFD compute queues" in a and "rank 0:" not in a
         assert b is not None and b.startswith("rank 0: ")
         assert c is None
         assert ncalls == (1 if r == 0 else 2)

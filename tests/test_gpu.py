@@ -713,6 +713,57 @@ def test_rccl_single_rank(dev):
         c.destroy()
 
 
+def test_unordered_fill_of_the_round4_harness_races(dev):
+    """DESIGN.md 7.1, candidate (i): the round-4 form of
+    tools/rccl_large.py filled the collective's input with fill_pico on
+    torch's default stream (the legacy NULL stream) and issued the collective
+    inside `with torch.cuda.stream(side)` -- a torch pool stream, created
+    non-blocking, so nothing ordered the two.  Here the NULL stream is held
+    busy first (torch.cuda._sleep), which makes the race certain instead of
+    rare: in the round-4 form the collective (P = 1: the copy sbuf -> rbuf)
+    reads the input before the fill and the output's digest is wrong; with
+    the ordering the harness has now (torch.cuda.synchronize() between fill
+    and collective) it is right.  The race can touch only the FIRST call
+    after a fill -- every later call of that harness came after a
+    device-wide synchronize -- so it cannot be the round-4 failure of all 16
+    calls."""
+    n = 1 << 24   # 64 MiB fp32
+    want = pico_amd.checksum(_filled(n), n, "float")
+    uid = pico_amd.Comm.unique_id()
+    c = pico_amd.Comm.rccl(0, 1, uid, 0)
+    side = torch.cuda.Stream()
+    s = torch.zeros(n, dtype=torch.float32, device=dev)
+    r = torch.zeros(n, dtype=torch.float32, device=dev)
+    try:
+        def run(ordered):
+            s.zero_()
+            r.fill_(float("nan"))
+            with torch.cuda.stream(side):   # warm: plans and workspace exist, nothing implicit syncs
+                pico_amd.allreduce("bine_bdw_remap", s, r, n, "float", "sum", c)
+            torch.cuda.synchronize()
+            c.synchronize()
+            torch.cuda._sleep(200_000_000)                 # the NULL stream busy for ~0.1 s
+            pico_amd.fill_pico(s, n, "float", 1234)       # on the NULL stream, after the sleep
+            if ordered:
+                torch.cuda.synchronize()
+            with torch.cuda.stream(side):
+                pico_amd.allreduce("bine_bdw_remap", s, r, n, "float", "sum", c)
+            torch.cuda.synchronize()
+            c.synchronize()
+            return pico_amd.checksum(r, n, "float") == want
+        assert run(ordered=False) is False   # the round-4 form reads the input before its fill
+        assert run(ordered=True) is True
+    finally:
+        c.destroy()
+
+
+def _filled(n):
+    t = torch.empty(n, dtype=torch.float32, device="cuda:0")
+    pico_amd.fill_pico(t, n, "float", 1234)
+    torch.cuda.synchronize()
+    return t
+
+
 # ---- pico_core-compatible device-resident driver (SURVEY.md 8(f) rank 3) ----------
 
 @pytest.mark.parametrize("coll,algo,dtype", [("ALLREDUCE", "bine_bdw_remap_over", "float"),
@@ -765,41 +816,50 @@ def test_pico_amd_core_two_ranks(dev, tmp_path, coll, algo, dtype):
 PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
 
 
+# libbine.so's forms (bine_dropin_defaults): "default" = no
+# BINE_* setting at all (the flat phases over the direct transport, the whole
+# call as one k_dm_fused launch where its plan fits); "literal" = BINE_LITERAL=1
+# (the reference's literal schedule over RCCL P2P); "rccl" = BINE_DIRECT=0 (the
+# flat phases over RCCL P2P).  BINE_FAKE_HOSTS is the harness's (two ranks on
+# one GPU need distinct RCCL host ids, integration/run_pico_core.sh).
+FORMS = {"default": {}, "literal": {"BINE_LITERAL": "1"}, "rccl": {"BINE_DIRECT": "0"}}
+
+
 @pytest.mark.skipif(not os.path.exists(PICO_CORE), reason="reference pico_core not built (integration/Makefile)")
-@pytest.mark.parametrize("np_,coll,algo,dtype,flat,count", [
-    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "1048576"),
+@pytest.mark.parametrize("np_,coll,algo,dtype,form,count", [
+    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", "default", "1048576"),
     # staged in pipelined chunks (libbine.so with_buffers): P = 1 is a copy, int64
     # SUM is exact in any association -- both cut the buffer into 16 MiB chunks
-    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "67108864"),
-    (2, "ALLREDUCE", "bine_bdw_remap_over", "int64", False, "8388608"),
-    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", False, "16777216"),
+    (1, "ALLREDUCE", "bine_bdw_remap_over", "float", "default", "67108864"),
+    (2, "ALLREDUCE", "bine_bdw_remap_over", "int64", "default", "8388608"),
+    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", "literal", "16777216"),
     # floating point at P > 1: the staging pipelined into the collective
-    # (bine_allreduce_staged / bine_reduce_scatter_staged), over RCCL and over
-    # the direct peer-memory transport (BINE_DIRECT=1)
-    (4, "ALLREDUCE", "bine_bdw_remap_over", "float", "dm", "16777216"),
-    (4, "ALLREDUCE", "bine_bdw_static_over", "double", "dm", "8388608"),
-    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "float", False, "16777216"),
-    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", True, "1048576"),
-    (2, "ALLREDUCE", "bine_lat_over", "double", True, "1048576"),
-    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "int64", True, "1048576"),
-    (2, "REDUCE", "bine_bdw_over", "float", False, "1048576"),
-    (2, "BCAST", "bine_lat_over", "float", False, "1048576"),
-    (2, "BCAST", "bine_lat_new_over", "int64", False, "1048576"),
-    (2, "GATHER", "bine_over", "float", False, "1048576"),
-    (2, "SCATTER", "bine_over", "int64", False, "1048576"),
-    (2, "ALLTOALL", "bine_over", "float", True, "1048576"),
+    # (bine_allreduce_staged / bine_reduce_scatter_staged), over the direct
+    # peer-memory transport (the default) and over RCCL
+    (4, "ALLREDUCE", "bine_bdw_remap_over", "float", "default", "16777216"),
+    (4, "ALLREDUCE", "bine_bdw_static_over", "double", "default", "8388608"),
+    (4, "ALLREDUCE", "bine_bdw_remap_over", "float", "literal", "16777216"),
+    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "float", "literal", "16777216"),
+    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "float", "default", "16777216"),
+    (2, "ALLREDUCE", "bine_bdw_remap_over", "float", "rccl", "1048576"),
+    (2, "ALLREDUCE", "bine_lat_over", "double", "default", "1048576"),
+    (2, "REDUCE_SCATTER", "bine_permute_remap_over", "int64", "default", "1048576"),
+    (2, "REDUCE", "bine_bdw_over", "float", "literal", "1048576"),
+    (2, "REDUCE", "bine_bdw_over", "float", "default", "1048576"),
+    (2, "BCAST", "bine_lat_over", "float", "default", "1048576"),
+    (2, "BCAST", "bine_lat_new_over", "int64", "literal", "1048576"),
+    (2, "GATHER", "bine_over", "float", "default", "1048576"),
+    (2, "SCATTER", "bine_over", "int64", "default", "1048576"),
+    (2, "ALLTOALL", "bine_over", "float", "rccl", "1048576"),
 ])
-def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat, count):
+def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, form, count):
     """the reference's UNCHANGED pico_core (integration/Makefile links it against
     libbine.so) drives the GPU path through the libbine.h symbols and checks
     every result against MPICH's own PMPI_* collective (pico_core_utils.c:
     553-610), aborting on a mismatch; 2 ranks share the GPU through RCCL's
-    socket transport (distinct NCCL_HOSTIDs), optionally with the flat phases"""
-    env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
-    if flat == "dm":
-        env.update(BINE_DIRECT="1")
-    elif flat:
-        env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
+    socket transport (distinct NCCL_HOSTIDs), in libbine.so's default forms,
+    the literal schedule, or the flat phases over RCCL"""
+    env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1", **FORMS[form])
     p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), str(np_), coll, count,
                         "5", algo, dtype], env=env, capture_output=True, text=True, timeout=150, ranks=np_)
     assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
@@ -807,18 +867,21 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, flat,
 
 
 @pytest.mark.skipif(not os.path.exists(PICO_CORE), reason="reference pico_core not built (integration/Makefile)")
-@pytest.mark.parametrize("algo,flat", [("bine_bdw_remap_over", False), ("bine_bdw_remap_over", True),
-                                       ("bine_lat_over", False)])
-def test_reference_pico_core_c1(dev, tmp_path, algo, flat):
+@pytest.mark.parametrize("algo,form", [("bine_bdw_remap_over", "default"), ("bine_bdw_remap_over", "literal"),
+                                       ("bine_bdw_remap_over", "rccl"), ("bine_lat_over", "default")])
+def test_reference_pico_core_c1(dev, tmp_path, algo, form):
     """BASELINE configs[0] (C1) through the GPU path exactly as the reference
     runs it: the unchanged pico_core, 4 ranks, 262,144 fp32 elements (1 MiB)
     per rank, allreduce SUM (pico_core_utils.h:262), 20 iterations, every one
     checked by pico_core against MPICH's PMPI_Allreduce (pico_core_utils.c:
     553-610, 960-992); the 4 ranks share the GPU through RCCL's socket
-    transport (distinct NCCL_HOSTIDs); host buffers, staged by libbine.so"""
-    env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1")
-    if flat:
-        env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
+    transport (distinct NCCL_HOSTIDs); host buffers, staged by libbine.so.
+    "default": no BINE_* setting -- libbine.so's own choice (VERDICT r5 item
+    4: the flat phases over the direct transport, one k_dm_fused launch)"""
+    env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1", **FORMS[form])
+    for k in ("BINE_LITERAL", "BINE_DIRECT", "BINE_FLAT_RS", "BINE_FLAT_AG"):
+        if k not in FORMS[form]:
+            env.pop(k, None)
     p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_pico_core.sh"), "4", "ALLREDUCE", "262144",
                         "20", algo, "float"], env=env, capture_output=True, text=True, timeout=150, ranks=4)
     assert p.returncode == 0, (p.stdout[-1500:], p.stderr[-1500:])
@@ -832,16 +895,14 @@ OP_CHECK = os.path.join(ROOT, "integration", "_build", "op_check")
 
 
 @pytest.mark.skipif(not os.path.exists(OP_CHECK), reason="integration/op_check not built (integration/Makefile)")
-@pytest.mark.parametrize("np_,flat", [(1, False), (2, False), (2, True)])
-def test_mpi_typed_entry_points_match_mpich(dev, np_, flat):
+@pytest.mark.parametrize("np_,form", [(1, "default"), (2, "literal"), (2, "default"), (2, "rccl")])
+def test_mpi_typed_entry_points_match_mpich(dev, np_, form):
     """integration/op_check: libbine.so's MPI-typed entry points (allreduce,
     reduce_scatter, reduce, bcast, allgather, gather, scatter, alltoall; host
     buffers) equal MPICH's own PMPI_* collectives
     for every order-independent (type, op) pair, and return MPI_ERR_OP where
     MPICH rejects the pair; 2 ranks share the GPU as above"""
-    env = dict(os.environ, BINE_FAKE_HOSTS="1")
-    if flat:
-        env.update(BINE_FLAT_RS="1", BINE_FLAT_AG="1")
+    env = dict(os.environ, BINE_FAKE_HOSTS="1", **FORMS[form])
     p = _sub.run_kw(["bash", os.path.join(ROOT, "integration", "run_op_check.sh"), str(np_)], env=env,
                        capture_output=True, text=True, timeout=150, ranks=np_)
     assert p.returncode == 0 and "OPCHECK ok" in p.stdout, (p.stdout[-1500:], p.stderr[-1500:])

@@ -274,3 +274,28 @@ def test_bcast_bdw_replay_predicts_the_reference_crashes():
         assert (rets[0] == "crash") == (c["status"] != "ok"), c["id"]
         n += c["status"] != "ok"
     assert n >= 100
+
+
+def test_checker_never_rebuilt_outside_the_build_container(tmp_path, monkeypatch):
+    """oracle.build() accepts liboracle.so only when its
+    stamp names the sha256 of the sources beside it; a missing or stale
+    checker is compiled in the build container (/root/reference present) and
+    is an ERROR anywhere else -- the GPU box never rebuilds it silently."""
+    import importlib.util
+    import shutil
+    src = os.path.dirname(os.path.abspath(O.__file__))
+    for f in ("bine_oracle.c", "bine_oracle.h", "Makefile", "oracle.py", "liboracle.so", "liboracle.so.sha256"):
+        shutil.copy2(os.path.join(src, f), tmp_path / f)
+    spec = importlib.util.spec_from_file_location("oracle_copy", tmp_path / "oracle.py")
+    M = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(M)
+    real_isdir = os.path.isdir
+    monkeypatch.setattr(os.path, "isdir", lambda p: False if p == "/root/reference" else real_isdir(p))
+    assert M.build() == str(tmp_path / "liboracle.so")          # stamp matches: used as shipped
+    with open(tmp_path / "bine_oracle.c", "a") as f:
+        f.write("\n/* edited after the build */\n")
+    with pytest.raises(RuntimeError, match="never rebuilt"):
+        M.build()                                                   # stale: refused, not recompiled
+    os.remove(tmp_path / "liboracle.so.sha256")
+    with pytest.raises(RuntimeError):
+        M.build()

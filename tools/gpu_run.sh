@@ -4,10 +4,10 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-W="BINE_DIRECT_WGS=64,BINE_DIRECT_TREE_WGS=128"
+T="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread"
+R="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 bash tools/gpu_steps.sh \
- "ab2c:150:python -u tools/dm_tree_ab.py 2 16,64 6" \
- "stamps2c:700:python -u tools/dm_stamps.py 2 8 base: w64t128:$W w64t128g:$W,DM_STAMPS_GRAPHS=1 w64t128c64:$W,BINE_CHUNK_BYTES=67108864 w64t128c64s64:$W,BINE_CHUNK_BYTES=67108864,BINE_DIRECT_SLOT_BYTES=67108864 w64t128c64s64g:$W,BINE_CHUNK_BYTES=67108864,BINE_DIRECT_SLOT_BYTES=67108864,DM_STAMPS_GRAPHS=1 w128t256c64s64:BINE_DIRECT_WGS=128,BINE_DIRECT_TREE_WGS=256,BINE_CHUNK_BYTES=67108864,BINE_DIRECT_SLOT_BYTES=67108864" \
- "rcclc:600:$T tests/test_gpu_rccl.py" \
- "full8c:400:$T tests/test_gpu_fullsize.py -k eight_processes"
+ "r6b_rebuild:300:$T tests/test_gpu_rccl.py -k rebuilt_after" \
+ "r6b_dmto:200:$T tests/test_gpu.py -k timed_out_call" \
+ "r6b_b2:400:GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 2 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 > gpurun_out/r6b_b2.json" \
+ "r6b_b8:600:GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 8 --master-port 29515 bench.py --gpus 8 --steps 20 --warmup 5 > gpurun_out/r6b_b8.json"
