@@ -242,18 +242,24 @@ def queue_census():
     out (past the hardware's slots it time-slices them)"""
     try:
         base = "/sys/class/kfd/kfd/proc"
-        per = []
+        per = {}   # gpu_id -> [compute queues of each process on it]
         for pid in sorted(os.listdir(base)):
             qd = os.path.join(base, pid, "queues")
             if not os.path.isdir(qd):
                 continue
-            n = 0
+            mine = {}
             for q in os.listdir(qd):
                 with open(os.path.join(qd, q, "type")) as f:
-                    n += f.read().strip() == "0"
-            if n:
-                per.append(n)
-        return f"KFD compute queues: {sum(per)} in {len(per)} processes {per}"
+                    if f.read().strip() != "0":
+                        continue
+                with open(os.path.join(qd, q, "gpuid")) as f:
+                    g = f.read().strip()
+                mine[g] = mine.get(g, 0) + 1
+            for g, n in mine.items():
+                per.setdefault(g, []).append(n)
+        # KFD's sysfs is the host's: other jobs on the host's other GPUs show too
+        return "KFD compute queues per GPU (gpu_id: total in processes [per process]): " + "; ".join(
+            f"{g}: {sum(v)} in {len(v)} {v}" for g, v in sorted(per.items()))
     except OSError as e:
         return f"KFD compute queues: unreadable ({e})"
 

@@ -161,9 +161,32 @@ constexpr size_t kFlagStride = 128;  // one flag / counter per 128-B line
 constexpr size_t kReadyOff = 0, kAckOff = 64 << 10, kCntPushOff = 128 << 10, kCntPullOff = 192 << 10,
                  kPoisonOff = 256 << 10, kBaseSendOff = 260 << 10, kBaseRecvOff = 264 << 10,
                  kLaunchCntOff = 268 << 10, kPeerTabOff = 272 << 10, kPingOff = 288 << 10,
-                 kFlagsBytes = 320 << 10;
+                 kGeomOff = 296 << 10;
+// Slice flags of k_dm_fused (round 6): workgroup w of a launch of `wgs`
+// workgroups owns slice w of every message (slice(): [n w / wgs, n (w+1) / wgs)
+// of its n vectors), so a receiver's workgroup w needs only the SENDER's
+// workgroup w to be done with slice w, not the whole message.  Per (ordered
+// pair, slot, slice) a ready flag (in the receiver's inbox, set by the sender's
+// workgroup w after its stores of slice w were acknowledged) and an ack flag
+// (in the sender's inbox, set by the receiver's workgroup w after its reads of
+// slice w completed); value = seq << kSliceWgsBits | wgs of the setter's launch
+// -- a slice flag stands for slice w only when both ends cut the message with
+// the same wgs (the message sizes match by construction).  The whole-message
+// flags are still published (the last arriver), so a peer issuing another
+// form waits on those.  kGeomOff: per (peer, slot) the sequence number and
+// vector count of this rank's last k_dm_fused push into that slot (local), so
+// a push can tell whether the receiver's slice acks of the slot's previous use
+// cover the bytes it is about to overwrite.
+constexpr int kSliceMax = 1024, kSliceWgsBits = 12;
+constexpr size_t kSliceReadyOff = 320 << 10,
+                 kSliceAckOff = kSliceReadyOff + (size_t)64 * 4 * kSliceMax * 8,   // kMaxPeers x kSlots x kSliceMax
+                 kFlagsBytes = kSliceAckOff + (size_t)64 * 4 * kSliceMax * 8;
 constexpr int kSlots = 4;      // slots per ordered pair
 constexpr int kMaxPeers = 64;  // P limit of the layout (flag regions: P * kSlots * 128 B <= 64 KiB)
+static_assert(kSliceAckOff - kSliceReadyOff == (size_t)kMaxPeers * kSlots * kSliceMax * 8 &&
+                  kFlagsBytes - kSliceAckOff == (size_t)kMaxPeers * kSlots * kSliceMax * 8 &&
+                  kGeomOff + (size_t)kMaxPeers * kSlots * 16 <= kSliceReadyOff && kFlagsBytes % 4096 == 0,
+              "inbox layout");
 }  // namespace dm
 struct DmMsg {
   const uint8_t *src;  // push: the data to send (pull: unused -- the slot)

@@ -1463,7 +1463,20 @@ struct Msg {
   uint64_t *sig;
   uint32_t *cnt;
   uint64_t seq, nvec;
+  // this workgroup's slice flags (bine_internal.h dm::kSliceReadyOff; null
+  // when the launch has more workgroups than the layout holds): the one it
+  // may wait on instead of `wait`, the one it sets after its slice, and (a
+  // push) this rank's record of the slot's previous use
+  const uint64_t *swait;
+  uint64_t *ssig;
+  uint64_t *geom;
+  int k;
 };
+
+// a slice flag's value: the sequence number and the setter's workgroup count
+__device__ __forceinline__ uint64_t slice_val(uint64_t seq, int wgs) {
+  return seq << kSliceWgsBits | (uint64_t)wgs;
+}
 
 __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
   Msg r;
@@ -1471,8 +1484,11 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
   const uint64_t *base = reinterpret_cast<const uint64_t *>(own + (m.push ? kBaseSendOff : kBaseRecvOff)) + m.peer;
   r.seq = __hip_atomic_load(base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)m.j + 1;
   const size_t k = (size_t)(r.seq % kSlots);
+  r.k = (int)k;
   uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
   r.nvec = m.bytes / 16;
+  const bool sl = a.wgs <= kSliceMax;
+  const size_t w = blockIdx.x;
   if (m.push) {
     r.src = reinterpret_cast<const u32x4 *>(m.src);
     r.dst = reinterpret_cast<u32x4 *>(remote + kFlagsBytes + ((size_t)a.rank * kSlots + k) * a.slot);
@@ -1482,6 +1498,13 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
     r.wait_val = r.seq - kSlots;
     r.sig = reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
     r.cnt = reinterpret_cast<uint32_t *>(own + kCntPushOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+    r.swait = sl ? reinterpret_cast<const uint64_t *>(own + kSliceAckOff +
+                                                      (((size_t)m.peer * kSlots + k) * kSliceMax + w) * 8)
+                 : nullptr;
+    r.ssig = sl ? reinterpret_cast<uint64_t *>(remote + kSliceReadyOff +
+                                               (((size_t)a.rank * kSlots + k) * kSliceMax + w) * 8)
+                : nullptr;
+    r.geom = reinterpret_cast<uint64_t *>(own + kGeomOff + ((size_t)m.peer * kSlots + k) * 16);
   } else {
     r.src = reinterpret_cast<const u32x4 *>(own + kFlagsBytes + ((size_t)m.peer * kSlots + k) * a.slot);
     r.dst = reinterpret_cast<u32x4 *>(m.dst);
@@ -1489,8 +1512,30 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
     r.wait_val = r.seq;
     r.sig = reinterpret_cast<uint64_t *>(remote + kAckOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
     r.cnt = reinterpret_cast<uint32_t *>(own + kCntPullOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
+    r.swait = sl ? reinterpret_cast<const uint64_t *>(own + kSliceReadyOff +
+                                                      (((size_t)m.peer * kSlots + k) * kSliceMax + w) * 8)
+                 : nullptr;
+    r.ssig = sl ? reinterpret_cast<uint64_t *>(remote + kSliceAckOff +
+                                               (((size_t)a.rank * kSlots + k) * kSliceMax + w) * 8)
+                : nullptr;
+    r.geom = nullptr;
   }
   return r;
+}
+
+// whether this workgroup may go on with message m: the whole message's flag,
+// or -- when both ends cut it with this launch's workgroup count -- the flag
+// of its own slice.  A push's slice of the slot's previous use was acked by
+// the receiver's workgroup w only for the bytes THAT message's cut gave it:
+// usable when this rank's record says that use was a k_dm_fused push of the
+// same vector count (same wgs: in the ack's value).  `seen` = the whole
+// flag's last value (the time-out record's).
+__device__ __forceinline__ bool flag_ok(const DmFusedArgs &a, const Msg &m, bool push, bool geom_ok, uint64_t *seen) {
+  *seen = ld_rlx_sys(m.wait);
+  if (*seen >= m.wait_val) return true;
+  if (!m.swait || (push && !geom_ok)) return false;
+  const uint64_t v = ld_rlx_sys(m.swait);
+  return (v >> kSliceWgsBits) >= m.wait_val && (v & ((1u << kSliceWgsBits) - 1)) == (uint64_t)a.wgs;
 }
 
 // The waits and arrivals of a phase's messages run side by side, one thread
@@ -1514,7 +1559,11 @@ __device__ __forceinline__ bool wait_all(const DmFusedArgs &a, int first, int n,
     if (m.wait) {
       const long long t0 = wall_clock64();
       uint64_t seen;
-      while ((seen = ld_rlx_sys(m.wait)) < m.wait_val) {
+      // a push's slice acks cover this push's slice only if the slot's
+      // previous use was a k_dm_fused push of the same vector count
+      const bool geom_ok = mm.push && m.swait && ld_rlx_sys(m.geom) == m.wait_val &&
+                           ld_rlx_sys(m.geom + 1) == m.nvec;
+      while (!flag_ok(a, m, mm.push, geom_ok, &seen)) {
         if (wall_clock64() - t0 > (long long)a.timeout_ticks) {
           dm_time_out(poison, a.poison_host, mm.push ? dm::kWaitFusedPush : dm::kWaitFusedPull, phase, a.rank,
                       mm.peer, m.seq % kSlots, m.wait_val, seen, a.serial, wall_clock64() - t0);
@@ -1544,10 +1593,17 @@ __device__ __forceinline__ void arrive_all(const DmFusedArgs &a, int first, int 
   vm_wait();
   __syncthreads();
   if ((int)threadIdx.x < n) {
-    const Msg m = resolve(a, a.m[first + threadIdx.x]);
+    const DmMsg &mm = a.m[first + threadIdx.x];
+    const Msg m = resolve(a, mm);
+    // this workgroup's slice is done: its flag (the peer's workgroup w may go on)
+    if (m.ssig) publish(m.ssig, slice_val(m.seq, a.wgs));
     const uint32_t old = __hip_atomic_fetch_add(m.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (old + 1 == (uint32_t)a.wgs) {
       __hip_atomic_store(m.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the slot's next use
+      if (mm.push) {  // the use this push made of the slot (read by the slot's next push, a later launch)
+        __hip_atomic_store(m.geom, m.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(m.geom + 1, m.nvec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       publish(m.sig, m.seq);
     }
   }
