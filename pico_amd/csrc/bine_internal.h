@@ -177,14 +177,22 @@ constexpr size_t kReadyOff = 0, kAckOff = 64 << 10, kCntPushOff = 128 << 10, kCn
 // vector count of this rank's last k_dm_fused push into that slot (local), so
 // a push can tell whether the receiver's slice acks of the slot's previous use
 // cover the bytes it is about to overwrite.
+// Layout [w][x][k]: one 128-B line per (slice w, pair x) holds that pair's
+// kSlots flags of slice w -- written only by one sender workgroup, polled
+// only by one receiver workgroup (flags of different workgroups in one line
+// made the phases contend for it: C3 at P = 2 0.385 -> 0.412 ms).
 constexpr int kSliceMax = 1024, kSliceWgsBits = 12;
+constexpr size_t kSliceLine = 128;
 constexpr size_t kSliceReadyOff = 320 << 10,
-                 kSliceAckOff = kSliceReadyOff + (size_t)64 * 4 * kSliceMax * 8,   // kMaxPeers x kSlots x kSliceMax
-                 kFlagsBytes = kSliceAckOff + (size_t)64 * 4 * kSliceMax * 8;
+                 kSliceAckOff = kSliceReadyOff + (size_t)kSliceMax * 64 * kSliceLine,   // x kMaxPeers
+                 kFlagsBytes = kSliceAckOff + (size_t)kSliceMax * 64 * kSliceLine;
+// the slice flag of (slice w, pair x, slot k) from a region's base
+constexpr size_t slice_off(size_t w, size_t x, size_t k) { return (w * 64 + x) * kSliceLine + k * 8; }
 constexpr int kSlots = 4;      // slots per ordered pair
 constexpr int kMaxPeers = 64;  // P limit of the layout (flag regions: P * kSlots * 128 B <= 64 KiB)
-static_assert(kSliceAckOff - kSliceReadyOff == (size_t)kMaxPeers * kSlots * kSliceMax * 8 &&
-                  kFlagsBytes - kSliceAckOff == (size_t)kMaxPeers * kSlots * kSliceMax * 8 &&
+static_assert(kSliceAckOff - kSliceReadyOff == (size_t)kMaxPeers * kSliceMax * kSliceLine &&
+                  kFlagsBytes - kSliceAckOff == (size_t)kMaxPeers * kSliceMax * kSliceLine &&
+                  kSlots * 8 <= kSliceLine &&
                   kGeomOff + (size_t)kMaxPeers * kSlots * 16 <= kSliceReadyOff && kFlagsBytes % 4096 == 0,
               "inbox layout");
 }  // namespace dm
@@ -344,6 +352,7 @@ struct DmFusedArgs {
   DmFusedTree t[kMaxFusedTrees];
   uint64_t *stamps = nullptr;          // DmArgs::stamps: one record per workgroup (kind 4: entry, end of the
   uint32_t serial = 0;                 // first wait, end)
+  int slices = 1;                      // per-slice flags (dm::kSliceReadyOff; BINE_DIRECT_SLICE_FLAGS=0: off)
 };
 // BINE_ERR_UNSUPPORTED: (dtype, op) has no fused instantiation (the caller
 // issues the primitives one by one)

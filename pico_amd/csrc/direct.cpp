@@ -170,6 +170,7 @@ int DirectState::init(int P_, int rank_, int device_, std::string &err) {
   if (const char *e = getenv("BINE_DIRECT_MERGE")) merge = std::min(3, std::max(0, atoi(e)));
   if (const char *e = getenv("BINE_DIRECT_TREE_WGS")) tree_wgs = std::max(1, atoi(e));
   if (const char *e = getenv("BINE_DIRECT_MCAST")) mcast = atoi(e) != 0;
+  if (const char *e = getenv("BINE_DIRECT_SLICE_FLAGS")) slice_flags = atoi(e) != 0;
   if (const char *e = getenv("BINE_DIRECT_FUSED_WGS")) fused_wgs = std::max(1, atoi(e));
   tree_wgs_env = tree_wgs;
   if (slot < (1 << 20)) slot = 1 << 20;

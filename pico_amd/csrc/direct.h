@@ -81,6 +81,7 @@ struct DirectState {
   // co-located ranks' current launches are resident together.  Round 4's
   // share / 2 cut of the workgroup counts is subsumed by the cap.
   int share = 1;
+  bool slice_flags = true;  // k_dm_fused's per-slice flags (BINE_DIRECT_SLICE_FLAGS=0: whole-message flags only)
   bool mcast = false;     // pushes of the same bytes to several peers as one group (BINE_DIRECT_MCAST=1;
                           // off: no gain measured, profiles/r3_push_groups.txt)
   bool poisoned() const { return hpoison && *(volatile uint32_t *)hpoison != 0; }

@@ -903,6 +903,7 @@ static bool build_fused(const FusedEnv &e, OpSpan ops, Ptr ptr, size_t esz, int 
   a.own = e.own;
   a.poison_host = d.hpoison_dev;
   a.timeout_ticks = d.timeout_ticks;
+  a.slices = d.slice_flags ? 1 : 0;
   a.nl = t0.peer;
   a.pos = t0.pos;
   a.swap = (unsigned)t0.flags >> 8;

@@ -1487,7 +1487,7 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
   r.k = (int)k;
   uint8_t *remote = reinterpret_cast<uint8_t *const *>(own + kPeerTabOff)[m.peer];
   r.nvec = m.bytes / 16;
-  const bool sl = a.wgs <= kSliceMax;
+  const bool sl = a.slices && a.wgs <= kSliceMax;
   const size_t w = blockIdx.x;
   if (m.push) {
     r.src = reinterpret_cast<const u32x4 *>(m.src);
@@ -1498,12 +1498,9 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
     r.wait_val = r.seq - kSlots;
     r.sig = reinterpret_cast<uint64_t *>(remote + kReadyOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
     r.cnt = reinterpret_cast<uint32_t *>(own + kCntPushOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
-    r.swait = sl ? reinterpret_cast<const uint64_t *>(own + kSliceAckOff +
-                                                      (((size_t)m.peer * kSlots + k) * kSliceMax + w) * 8)
+    r.swait = sl ? reinterpret_cast<const uint64_t *>(own + kSliceAckOff + slice_off(w, (size_t)m.peer, k))
                  : nullptr;
-    r.ssig = sl ? reinterpret_cast<uint64_t *>(remote + kSliceReadyOff +
-                                               (((size_t)a.rank * kSlots + k) * kSliceMax + w) * 8)
-                : nullptr;
+    r.ssig = sl ? reinterpret_cast<uint64_t *>(remote + kSliceReadyOff + slice_off(w, (size_t)a.rank, k)) : nullptr;
     r.geom = reinterpret_cast<uint64_t *>(own + kGeomOff + ((size_t)m.peer * kSlots + k) * 16);
   } else {
     r.src = reinterpret_cast<const u32x4 *>(own + kFlagsBytes + ((size_t)m.peer * kSlots + k) * a.slot);
@@ -1512,12 +1509,9 @@ __device__ __forceinline__ Msg resolve(const DmFusedArgs &a, const DmMsg &m) {
     r.wait_val = r.seq;
     r.sig = reinterpret_cast<uint64_t *>(remote + kAckOff + ((size_t)a.rank * kSlots + k) * kFlagStride);
     r.cnt = reinterpret_cast<uint32_t *>(own + kCntPullOff + ((size_t)m.peer * kSlots + k) * kFlagStride);
-    r.swait = sl ? reinterpret_cast<const uint64_t *>(own + kSliceReadyOff +
-                                                      (((size_t)m.peer * kSlots + k) * kSliceMax + w) * 8)
+    r.swait = sl ? reinterpret_cast<const uint64_t *>(own + kSliceReadyOff + slice_off(w, (size_t)m.peer, k))
                  : nullptr;
-    r.ssig = sl ? reinterpret_cast<uint64_t *>(remote + kSliceAckOff +
-                                               (((size_t)a.rank * kSlots + k) * kSliceMax + w) * 8)
-                : nullptr;
+    r.ssig = sl ? reinterpret_cast<uint64_t *>(remote + kSliceAckOff + slice_off(w, (size_t)a.rank, k)) : nullptr;
     r.geom = nullptr;
   }
   return r;

@@ -48,21 +48,20 @@ struct Entry {
   size_t bounce_cap[2] = {0, 0};
 };
 
-// Small host buffers go through two page-locked bounce buffers the
-// communicator owns: the caller's bytes are memcpy'd into
-// them (and the result out of them) on the CPU, so the call registers nothing
-// -- per-call hipHostRegister / hipHostUnregister of a 1 MiB buffer costs
-// more than its PCIe transfer (C1 at P = 1: 66 us of which ~38 us are the
-// 2 MiB on the link).  Nothing outlives the call: the bounce
-// buffers belong to the library, the caller's pages are never pinned.  Calls
-// whose host buffers are larger keep the per-call registration (memcpy
-// through a bounce buffer is slower than DMA from registered pages there,
-// profiles/r4_host_stage_probe.txt).  BINE_HOST_BOUNCE_BYTES (default 4 MiB;
-// 0 = off) is the largest buffer that bounces.
+// Small host buffers MAY go through two page-locked bounce buffers the
+// communicator owns: the caller's bytes memcpy'd into
+// them (and the result out of them) on the CPU, so the call registers
+// nothing.  Measured through the unchanged pico_core (C1, 1 MiB fp32,
+// profiles/r6_e2e_c1.txt): 115 us per call at P = 1 against 66 us with the
+// per-call hipHostRegister / hipHostUnregister, 488 vs 419 us at P = 4 on one
+// GPU -- the two 1 MiB CPU copies cost more than the registration they save
+// (as HIP's own pageable staging does: 115 us).  So it is off by default;
+// BINE_HOST_BOUNCE_BYTES=<bytes> turns it on for buffers up to that size
+// (a host whose memcpy is faster than its page-locking).
 size_t bounce_bytes() {
   static const size_t v = getenv("BINE_HOST_BOUNCE_BYTES") ? (size_t)strtoull(getenv("BINE_HOST_BOUNCE_BYTES"),
                                                                               nullptr, 10)
-                                                           : (size_t)4 << 20;
+                                                           : 0;
   return v;
 }
 
