@@ -257,11 +257,34 @@ def queue_census():
                 mine[g] = mine.get(g, 0) + 1
             for g, n in mine.items():
                 per.setdefault(g, []).append(n)
+        hqd = hw_queue_slots()
         # KFD's sysfs is the host's: other jobs on the host's other GPUs show too
-        return "KFD compute queues per GPU (gpu_id: total in processes [per process]): " + "; ".join(
-            f"{g}: {sum(v)} in {len(v)} {v}" for g, v in sorted(per.items()))
+        return ("KFD compute queues per GPU (gpu_id: total in processes [per process], HW queue slots): "
+                + "; ".join(f"{g}: {sum(v)} in {len(v)} {v}, slots {hqd.get(g, '?')}" for g, v in sorted(per.items())))
     except OSError as e:
         return f"KFD compute queues: unreadable ({e})"
+
+
+def hw_queue_slots():
+    """gpu_id -> the compute queue slots KFD reports for that GPU
+    (topology `num_cp_queues`): past that many user queues on one GPU the
+    scheduler time-slices them"""
+    out = {}
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "gpu_id")) as f:
+                    g = f.read().strip()
+                with open(os.path.join(base, node, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if g != "0" and "num_cp_queues" in props:
+                out[g] = int(props["num_cp_queues"])
+    except OSError:
+        pass
+    return out
 
 
 def measure(torch, stream, dist, comm, call, steps, warmup):

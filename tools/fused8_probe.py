@@ -46,7 +46,7 @@ def worker(rank, P, port, batches, per, q):
     torch.cuda.synchronize()
     bench.apply_transport(comm, "flatrs+flat+dmt", 64 << 20)
     key = bench.gkey("C3", "allreduce", "bine_bdw_remap", "float", n, P)
-    times, err, ok = [], None, None
+    times, err, ok, census = [], None, None, None
     fused0 = comm.fused_calls()
     for b in range(batches):
         dist.barrier()
@@ -58,6 +58,8 @@ def worker(rank, P, port, batches, per, q):
         torch.cuda.synchronize()
         d()
         times.append((time.perf_counter() - t0) * 1e3)
+        if b == 0 and rank == 0:
+            census = bench.queue_census()   # every rank's queues exist by now
         why = d.failed(dist)
         if why is not None:
             err = d.err
@@ -66,7 +68,7 @@ def worker(rank, P, port, batches, per, q):
         ok = bool(bench.check_digest(pico_amd, rb, n, "float", key, rank, stream)[0])
     out = {"rank": rank, "batches": len(times), "batch_ms_median": round(statistics.median(times), 3) if times else None,
            "batch_ms_max": round(max(times), 3) if times else None, "fused_launches": comm.fused_calls() - fused0,
-           "digest_ok": ok, "error": err[:2500] if err else None}
+           "digest_ok": ok, "error": err[:2500] if err else None, "census_after_batch0": census}
     comm.destroy()
     dist.destroy_process_group()
     q.put(out)
