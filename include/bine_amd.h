@@ -666,17 +666,24 @@ int64_t bine_plan_dm_fused_msgs(int algo, int nranks, int rank, size_t count, co
 /* The direct transport's residency cut (host only): every launch's
  * workgroups -- `cw[0..n)` per copied message, *tw for a fused tree (NULL:
  * none) -- are scaled proportionally, each >= 1, to sum to at most `cap` =
- * CUs x resident blocks per CU of the launched kernel / ranks sharing the GPU,
- * so that every waiting workgroup of every co-located rank's current launch
- * is resident at once and no waiter can hold the slot its producer needs.
+ * CUs x (resident blocks per CU of the launched kernel - margin) / ranks
+ * sharing the GPU (bine_dm_residency_cap), so that every waiting workgroup of
+ * every co-located rank's current launch is resident at once, with a margin
+ * for other waves, and no waiter can hold the slot its producer needs.
  * Returns 0 (unchanged: fits, or cap <= 0), 1 (scaled) or -1 (the parts alone
  * exceed cap; unchanged). */
 int bine_dm_fit_residency(int *cw, int n, int *tw, int cap);
 /* That cap on the current device (needs a GPU): kind 0 = k_dm_move, 1 =
  * k_dm_move_tree for (dtype, op, nl leaves), 2 = k_dm_fused for (dtype, op);
- * CUs x resident blocks per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor)
- * / share.  -1: no such kernel; 0: the device could not be queried. */
+ * bine_dm_residency_cap(CUs, resident blocks per CU
+ * (hipOccupancyMaxActiveBlocksPerMultiprocessor), margin, share) with the
+ * margin of BINE_DIRECT_RESIDENCY_MARGIN (default 1).  -1: no such kernel; 0:
+ * the device could not be queried. */
 int bine_dm_launch_cap(int kind, int dtype, int op, int nl, int share);
+/* The rule itself (host only): cus x max(1, per_cu - margin) / share -- the
+ * margin is the blocks per CU left to waves other than the transport's
+ * spinning ones; 0 when cus or per_cu <= 0. */
+int bine_dm_residency_cap(int cus, int per_cu, int margin, int share);
 
 #ifdef __cplusplus
 }

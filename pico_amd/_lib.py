@@ -126,6 +126,7 @@ def lib():
         "bine_comm_direct_ping": ([vp, i, i, ctypes.POINTER(ctypes.c_double)], i),
         "bine_dropin_defaults": ([i, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)], i),
         "bine_dm_launch_cap": ([i, i, i, i, i], i),
+        "bine_dm_residency_cap": ([i, i, i, i], i),
         "bine_checksum": ([vp, sz, i, ctypes.POINTER(u64), vp], i),
         "bine_get_unique_id": ([vp], i),
         "bine_comm_init_rccl": ([ctypes.POINTER(vp), i, i, vp, i], i),

@@ -216,11 +216,24 @@ struct DmMsg {
 // scheduler's time slicing resolves it slowly, or a wait times out).  So every
 // launch is cut to fit: its workgroups (each copy entry's cwgs, the tree's
 // twgs, the fused kernel's wgs) are scaled so that they sum to at most
-// cap = CUs x resident blocks per CU of the kernel (hipOccupancy...) / share.
+// cap = CUs x (resident blocks per CU of the kernel (hipOccupancy...) - margin)
+// / share (dm_residency_cap).  The margin (one workgroup per CU,
+// BINE_DIRECT_RESIDENCY_MARGIN) is what any other wave on the GPU may hold
+// while the spinning ones hold theirs: with 8 ranks on one GPU at the exact
+// cap (8 x 160 = 1,280 = 256 CUs x 5) a producer's last workgroups got a slot
+// only after the first waiter timed out.
 // dm_fit_residency: scale `cw[0..n)` and *tw (null: none) proportionally,
 // each >= 1, to sum <= cap.  0: unchanged (already fits or cap <= 0),
 // 1: scaled, -1: n parts (+ the tree) alone exceed cap (left unchanged).
 int dm_fit_residency(int *cw, int n, int *tw, int cap);
+// the cap from the device's CUs, the kernel's resident blocks per CU, the
+// margin (blocks per CU left free; never below one resident block per CU)
+// and the ranks sharing the GPU; 0 when unknown (cus or per_cu <= 0)
+inline int dm_residency_cap(int cus, int per_cu, int margin, int share) {
+  if (cus <= 0 || per_cu <= 0) return 0;
+  const int per = per_cu - margin >= 1 ? per_cu - margin : 1;
+  return cus * per / (share >= 1 ? share : 1);
+}
 // the cap itself on the current device: kind 0 k_dm_move, 1 k_dm_move_tree for
 // (dtype, op, nl), 2 k_dm_fused for (dtype, op); -1: no such kernel, 0: unknown
 int dm_launch_cap(int kind, int dtype, int op, int nl, int share);

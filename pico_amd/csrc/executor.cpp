@@ -2762,6 +2762,10 @@ int bine_comm_set_relay(bine_comm_t c, size_t min_part_bytes) {
 
 int bine_set_reduce_tuning(int unroll, int maxblocks, int nontemporal);
 
+int bine_dm_residency_cap(int cus, int per_cu, int margin, int share) {
+  return dm_residency_cap(cus, per_cu, margin, share);
+}
+
 int bine_dm_launch_cap(int kind, int dtype, int op, int nl, int share) {
   return dm_launch_cap(kind, dtype, op, nl, share);
 }

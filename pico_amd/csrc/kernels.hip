@@ -1227,13 +1227,23 @@ static bool dm_args_ok(const DmArgs &a, bool leaves_ok) {
   return true;
 }
 
+// blocks per CU a direct-transport launch leaves free (dm_residency_cap)
+static int dm_margin() {
+  static const int m = [] {
+    const char *e = getenv("BINE_DIRECT_RESIDENCY_MARGIN");
+    return e && *e ? std::max(0, atoi(e)) : 1;
+  }();
+  return m;
+}
+
 // Workgroup slots one direct-transport launch may take on the current device
-// (bine_internal.h dm_fit_residency): CUs x resident blocks per CU of kernel
-// `k` (the occupancy API: registers, LDS, wave slots) / share; 0 if unknown.
-// Both factors are queried once per kernel and device.
+// (bine_internal.h dm_fit_residency, dm_residency_cap): CUs x (resident blocks
+// per CU of kernel `k` (the occupancy API: registers, LDS, wave slots) -
+// margin) / share; 0 if unknown.  Both factors are queried once per kernel
+// and device.
 static int dm_cap(const void *k, int share) {
   static std::mutex mu;
-  static std::map<std::pair<const void *, int>, int> cache;
+  static std::map<std::pair<const void *, int>, std::pair<int, int>> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
     (void)hipGetLastError();
@@ -1248,9 +1258,9 @@ static int dm_cap(const void *k, int share) {
       (void)hipGetLastError();
       cus = per = 0;
     }
-    it = cache.emplace(std::make_pair(k, dev), cus * per).first;
+    it = cache.emplace(std::make_pair(k, dev), std::make_pair(cus, per)).first;
   }
-  return it->second / std::max(1, share);
+  return dm_residency_cap(it->second.first, it->second.second, dm_margin(), share);
 }
 
 int launch_dm_move(const DmArgs &a0, void *stream) {

@@ -450,3 +450,51 @@ def fit(cw, tw, cap):
             cw[i] -= 1
         s -= 1
     return 1
+
+
+def fused_residency(P, W, slots, held=0, slices=True, order="rr"):
+    """k_dm_fused's residency on ONE GPU shared by P ranks:
+    each rank launches W workgroups; workgroup w does phase A (its pushes, no
+    wait at a fresh slot), then waits for phase B's leaves, then for phase D's
+    pieces, holding its slot until the end.  With slice flags (`slices`)
+    workgroup w waits only for the peers' workgroup w; with whole-message
+    flags for every workgroup of every peer.  The GPU has `slots` workgroup
+    slots, `held` of them taken for the whole run by other waves; each rank's
+    workgroups are dispatched in blockIdx order ("rr": one from each rank in
+    turn, "seq": rank 0's launch first, ...).  Returns (completed, the most
+    transport workgroups resident at once)."""
+    state = [[0] * W for _ in range(P)]   # 0 not dispatched, 1 past A, 2 past B, 3 done
+    nxt = [0] * P
+    free = slots - held
+    most = 0
+    turn = 0
+
+    def past(w, k):
+        if slices:
+            return all(state[r][w] >= k for r in range(P))
+        return all(s >= k for row in state for s in row)
+
+    progress = True
+    while progress:
+        progress = False
+        while free > 0:
+            cands = [r for r in range(P) if nxt[r] < W]
+            if not cands:
+                break
+            r = cands[turn % len(cands)] if order == "rr" else cands[0]
+            turn += 1
+            state[r][nxt[r]] = 1
+            nxt[r] += 1
+            free -= 1
+            progress = True
+        most = max(most, sum(1 for row in state for s in row if s in (1, 2)))
+        for r in range(P):
+            for w in range(nxt[r]):
+                if state[r][w] == 1 and past(w, 1):
+                    state[r][w] = 2
+                    progress = True
+                if state[r][w] == 2 and past(w, 2):
+                    state[r][w] = 3
+                    free += 1
+                    progress = True
+    return all(s == 3 for row in state for s in row), most

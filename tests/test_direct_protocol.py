@@ -218,6 +218,42 @@ def test_fit_residency_library_matches_restatement():
             assert pc == cw
 
 
+def test_fused_residency_margin_and_slice_flags():
+    """k_dm_fused with 8 ranks on one MI355X (256 CUs x 5
+    resident blocks = 1,280 slots).  Round 5's cap (CUs x blocks / share =
+    160 per rank) demands exactly 1,280: with whole-message flags every
+    workgroup of every rank must be resident at once, so ONE slot held by any
+    other wave stalls the call until a waiter times out -- the rehearsal's
+    record (the producers' marks arrived after the time-out).  The bound: the
+    margin (one block per CU left free: 128 per rank, 1,024 slots) completes
+    with up to one held slot per CU; slice flags (a workgroup waits only for
+    its peers' same slice, dispatch in blockIdx order) complete at the old
+    cap with up to W - 1 held slots."""
+    import pico_amd
+    L = pico_amd.lib()
+    cus, per = 256, 5
+    assert L.bine_dm_residency_cap(cus, per, 0, 8) == 160          # round 5's rule
+    assert L.bine_dm_residency_cap(cus, per, 1, 8) == 128          # the margin
+    assert L.bine_dm_residency_cap(cus, per, 1, 2) == 512          # P = 2 keeps its 512 workgroups
+    assert L.bine_dm_residency_cap(cus, per, 1, 1) == 1024         # a node: above every default launch
+    assert L.bine_dm_residency_cap(cus, 1, 1, 1) == cus            # never below one block per CU
+    assert L.bine_dm_residency_cap(0, per, 1, 1) == 0               # unknown device
+    for share in range(1, 17):
+        for p in range(2, 9):
+            for m in (0, 1, 2):
+                cap = L.bine_dm_residency_cap(cus, p, m, share)
+                assert cap == cus * max(1, p - m) // share
+                assert share * cap <= cus * p - (cus * m if p - m >= 1 else 0)
+    slots = cus * per
+    for order in ("rr", "seq"):
+        assert dm_sim.fused_residency(8, 160, slots, 0, slices=False, order=order) == (True, 1280)
+        assert dm_sim.fused_residency(8, 160, slots, 1, slices=False, order=order) == (False, 1279)
+        assert dm_sim.fused_residency(8, 128, slots, cus, slices=False, order=order) == (True, 1024)
+        assert not dm_sim.fused_residency(8, 128, slots, cus + 1, slices=False, order=order)[0]
+        assert dm_sim.fused_residency(8, 160, slots, 159, slices=True, order=order)[0]
+        assert dm_sim.fused_residency(8, 128, slots, cus, slices=True, order=order)[0]
+
+
 # ---- the one-launch form moves the per-exchange form's messages (round 5) ----------
 
 def _per_exchange_msgs(ops, esz, slot, rank_peer_kind):

@@ -1124,10 +1124,11 @@ def test_vendor_allreduce_needs_rccl():
 
 def test_direct_transport_launch_caps(dev):
     """the residency cap of every direct-transport kernel on this device
-    (bine_dm_launch_cap: CUs x resident blocks per CU / share): k_dm_move's
-    32 VGPRs hold 8 workgroups per CU, k_dm_move_tree<float, SUM, 8>'s 96
-    hold 5 -- 2048 and 1280 slots on MI355X's 256 CUs; every launch is cut to
-    its cap / ranks on the GPU (tests/test_direct_protocol.py)"""
+    (bine_dm_launch_cap: CUs x (resident blocks per CU - 1) / share):
+    k_dm_move's 32 VGPRs hold 8 workgroups per CU, k_dm_move_tree<float, SUM,
+    8>'s 96 hold 5 -- 1792 and 1024 slots on MI355X's 256 CUs with one block
+    per CU left free; every launch is cut to its cap / ranks on the GPU
+    (tests/test_direct_protocol.py)"""
     L = pico_amd.lib()
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     mv = L.bine_dm_launch_cap(0, 0, 0, 0, 1)
@@ -1138,4 +1139,7 @@ def test_direct_transport_launch_caps(dev):
     assert mv % cus == 0 and tr8 % cus == 0 and fu % cus == 0
     assert mv >= tr8                     # the tree's registers cost residency
     assert L.bine_dm_launch_cap(0, 0, 0, 0, 8) == mv // 8
+    props = torch.cuda.get_device_properties(0)
+    if props.multi_processor_count == 256 and "gfx950" in props.gcnArchName:
+        assert (mv, tr8, fu) == (1792, 1024, 1024)
     assert L.bine_dm_launch_cap(1, pico_amd.DTYPES["float"], pico_amd.OPS["sum"], 3, 1) == -1
