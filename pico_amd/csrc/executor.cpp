@@ -664,7 +664,10 @@ static int comm_setup(bine_comm *c) {
   int lo = 0, hi = 0;
   HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi));
+  // the comm stream at the highest priority (BINE_COMM_PRIORITY=0: the
+  // default priority, a diagnostic for ranks sharing one GPU)
+  const char *cp = getenv("BINE_COMM_PRIORITY");
+  HIP_TRY(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, cp && atoi(cp) == 0 ? lo : hi));
   c->ev.resize(1024);
   for (auto &e : c->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));

@@ -44,7 +44,8 @@ def worker(rank, P, port, batches, per, q):
     rb = torch.empty(n, dtype=torch.float32, device="cuda:0")
     pico_amd.fill_pico(sb, n, "float", 1234 + rank)
     torch.cuda.synchronize()
-    bench.apply_transport(comm, "flatrs+flat+dmt", 64 << 20)
+    bench.apply_transport(comm, os.environ.get("PROBE_TRANSPORT", "flatrs+flat+dmt"),
+                          int(os.environ.get("PROBE_CHUNK_MIB", "64")) << 20)
     key = bench.gkey("C3", "allreduce", "bine_bdw_remap", "float", n, P)
     times, err, ok, census = [], None, None, None
     fused0 = comm.fused_calls()
@@ -99,7 +100,8 @@ if __name__ == "__main__":
     res = []
     while not q.empty():
         res.append(q.get())
-    env = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "BINE_DIRECT_TIMEOUT_S", "BINE_DIRECT_FUSED_WGS")}
+    env = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "BINE_DIRECT_TIMEOUT_S", "BINE_DIRECT_FUSED_WGS",
+                                          "PROBE_TRANSPORT", "PROBE_CHUNK_MIB", "BINE_COMM_PRIORITY")}
     ok = len(res) == P and all(r["error"] is None and r["digest_ok"] for r in res)
     print(json.dumps({"P": P, "env": env, "ok": ok, "census_while_running": census,
                       "ranks": sorted(res, key=lambda r: r["rank"])}), flush=True)

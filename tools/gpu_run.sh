@@ -4,7 +4,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-R="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 bash tools/gpu_steps.sh \
- "r6j_b8m0:560:BINE_DIRECT_RESIDENCY_MARGIN=0 GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 8 --master-port 29515 bench.py --gpus 8 --steps 20 --warmup 5 > gpurun_out/r6j_b8m0.json" \
- "r6j_b8s0:560:BINE_DIRECT_SLICE_FLAGS=0 GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 8 --master-port 29517 bench.py --gpus 8 --steps 20 --warmup 5 > gpurun_out/r6j_b8s0.json"
+ "r6k_suite:800:python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
+ "r6k_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "r6k_dmhi:150:PROBE_TRANSPORT=direct+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6k_dmhi.json" \
+ "r6k_dmlo:150:BINE_COMM_PRIORITY=0 PROBE_TRANSPORT=direct+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6k_dmlo.json"
