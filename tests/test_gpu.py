@@ -726,12 +726,16 @@ def test_unordered_fill_of_the_round4_harness_races(dev):
     and collective) it is right.  The race can touch only the FIRST call
     after a fill -- every later call of that harness came after a
     device-wide synchronize -- so it cannot be the round-4 failure of all 16
-    calls."""
+    calls.  The side stream is a high-priority one: HIP keeps
+    a separate HW queue pool per priority, so it cannot share a hardware
+    queue with the NULL stream -- which, with the suite's few queues per
+    process (tests/conftest.py), would order the two by accident and hide
+    the race."""
     n = 1 << 24   # 64 MiB fp32
     want = pico_amd.checksum(_filled(n), n, "float")
     uid = pico_amd.Comm.unique_id()
     c = pico_amd.Comm.rccl(0, 1, uid, 0)
-    side = torch.cuda.Stream()
+    side = torch.cuda.Stream(priority=-1)
     s = torch.zeros(n, dtype=torch.float32, device=dev)
     r = torch.zeros(n, dtype=torch.float32, device=dev)
     try:
