@@ -18,6 +18,7 @@ per-exchange launches (16 MiB chunks) and with the one-launch k_dm_fused form
 usage: python tools/dm_rebuild_check.py [P]   (exit 0 = every rank ok)"""
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -64,6 +65,14 @@ def worker(rank, P, port, q):
         errs, first_ok = [], None
         for i in range(2):   # the first call's completion reports the timeout; the second fails too
             rb.fill_(float("nan"))
+            torch.cuda.synchronize()
+            dist.barrier()
+            if i == 0 and rank > 0:
+                # rank 0 issues first and waits for data its peers send only
+                # later, so its wait times out for certain (with every rank
+                # issuing together, all of a call's flags may be set before
+                # anybody looks)
+                time.sleep(0.5)
             try:
                 call()
                 errs.append(None)
