@@ -1011,7 +1011,13 @@ def measured_models(world, mode, chunk, link_gbs, t_flag_us):
         for cfg in ("C3", "C4", "C5"):
             res[cfg] = NM.config_model(cfg, world, t, chunk, one_gpu=one, link_gbs=link_gbs)["model_ms"]
         if t_flag_us is not None:
-            res["C1_e2e_us"] = NM.c1_e2e_us(world, t_flag_us=t_flag_us, link_gbs=link_gbs)["e2e_us"]
+            # ranks sharing one GPU: the push figure is no link rate (DESIGN.md
+            # 7.2), so the node's C1 takes the measured flag latency with the
+            # model's link rate
+            res["C1_e2e_us"] = NM.c1_e2e_us(world, t_flag_us=t_flag_us,
+                                            link_gbs=NM.LINK_GBS if one else link_gbs)["e2e_us"]
+            if one:
+                res["C1_note"] = "one GPU: C1_e2e_us = the node model with the measured flag latency and the assumed link rate"
         return res
     except Exception as e:  # a report, never a reason to lose the line
         return {"error": str(e)}

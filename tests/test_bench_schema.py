@@ -68,6 +68,10 @@ def test_model_with_measured_constants(monkeypatch):
     assert base["C3"] == bench.node_model("C3", 8, "flatrs+flat+dmt", 64 << 20)["model_ms"]
     assert base["C1_e2e_us"] == M.c1_e2e_us(8)["e2e_us"]
     assert slow["C3"] > base["C3"] and slow["C4"] > base["C4"] and slow["C1_e2e_us"] > base["C1_e2e_us"]
+    # ranks sharing one GPU: the push figure is no link rate -- C1 keeps the assumed link rate
+    monkeypatch.setenv("BINE_FAKE_HOSTS", "1")
+    one = bench.measured_models(8, "flatrs+flat+dmt", 64 << 20, 0.41, M.T_FLAG_US)
+    assert one["one_gpu"] and one["C1_e2e_us"] == M.c1_e2e_us(8)["e2e_us"] and "C1_note" in one
 
 
 class _Comm:
