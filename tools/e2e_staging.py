@@ -69,15 +69,13 @@ if __name__ == "__main__":
         out["transport"] = "direct peer memory (BINE_DIRECT=1)" if os.environ.get("BINE_DIRECT") == "1" else "RCCL"
     if len(sys.argv) > 5 and sys.argv[5] == "c1":
         # round 6: libbine.so's defaults (bine_dropin_defaults: flat phases over the
-        # direct transport, one k_dm_fused launch) and the small host buffers
-        # bounced through page-locked library buffers (BINE_HOST_BOUNCE_BYTES)
-        cfgs = [("default (no BINE_* setting): flat phases, direct transport, bounce buffers", {}),
-                ("default, per-call page-locking instead of bounce buffers", {"BINE_HOST_BOUNCE_BYTES": "0"}),
-                ("default, pageable (HIP's own staging)", {"BINE_HOST_BOUNCE_BYTES": "0", "BINE_HOST_REGISTER": "0"}),
+        # direct transport, one k_dm_fused launch; host buffers page-locked per
+        # call) against the variants: bounce buffers, pageable, RCCL, literal
+        cfgs = [("default (no BINE_* setting): flat phases, direct transport, per-call page-locking", {}),
+                ("default forms, bounce buffers (BINE_HOST_BOUNCE_BYTES=4 MiB)", {"BINE_HOST_BOUNCE_BYTES": str(4 << 20)}),
+                ("default forms, pageable (HIP's own staging)", {"BINE_HOST_REGISTER": "0"}),
                 ("flat phases over RCCL (BINE_DIRECT=0)", {"BINE_DIRECT": "0"}),
-                ("literal schedule over RCCL (BINE_LITERAL=1)", {"BINE_LITERAL": "1"}),
-                ("literal schedule over RCCL, per-call page-locking (round 5's default)",
-                 {"BINE_LITERAL": "1", "BINE_HOST_BOUNCE_BYTES": "0"})]
+                ("literal schedule over RCCL (BINE_LITERAL=1, round 5's default)", {"BINE_LITERAL": "1"})]
     for name, env in cfgs:
         r = run(np_, dtype, count, iters, env)
         if "ms_median" in r:
