@@ -4,10 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
 bash tools/gpu_steps.sh \
- "r6m_fix:200:python -u -m pytest tests/test_gpu_rccl.py tests/test_gpu.py -k 'rebuilt_after_a_timeout or round4_harness' -v --timeout 150 --timeout-method thread -p no:cacheprovider" \
- "bench:240:python -u bench.py > gpurun_out/bench.json" \
- "prof:200:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline" \
- "pmcf:70:BENCH_NO_SMALL_WINDOWS=1 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --no-cpu-baseline" \
- "pmcw:70:BENCH_NO_SMALL_WINDOWS=1 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --no-cpu-baseline"
+ "r6o_suite:900:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
+ "r6o_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "r6o_bench:240:python -u bench.py > gpurun_out/r6o_bench.json"
