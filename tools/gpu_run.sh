@@ -5,6 +5,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
- "r6o_suite:900:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
- "r6o_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
- "r6o_bench:240:python -u bench.py > gpurun_out/r6o_bench.json"
+ "r6p_wt:60:./tools/bin/wt_store_probe > gpurun_out/r6p_wt.json"
