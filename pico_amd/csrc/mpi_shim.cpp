@@ -423,15 +423,6 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
   }
   const bool bounced = bs || br;
   CallPins pins;
-  // a small call's output buffer only receives the final copy: registered
-  // after the input's copy and the collective were issued, so the GPU works
-  // meanwhile (pages of its own: a page shared with the input is registered
-  // with the input, up front)
-  CallPins late;
-  const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
-  const bool split = !piped && !bounced && stage_s && stage_r && !fill_r &&
-                     (((uintptr_t)rbuf + rbytes + pg - 1) / pg <= (uintptr_t)sbuf / pg ||
-                      ((uintptr_t)sbuf + sbytes + pg - 1) / pg <= (uintptr_t)rbuf / pg);
   if (stage_s) {
     void *d;
     if ((rc = stage(e, 0, sbytes, &d))) return rc;
@@ -446,7 +437,7 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
     if (bounced) {
       if (fill_r) memcpy(br, rbuf, rbytes);
     } else {
-      (split ? late : pins).add(rbuf, rbytes);
+      pins.add(rbuf, rbytes);
     }
   }
   pins.commit();
@@ -481,7 +472,6 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
     if (fill_r && hipMemcpyAsync(dr, hr, rbytes, hipMemcpyHostToDevice, st) != hipSuccess)
       return MPI_ERR_OTHER;
     if (int bst = body(in_place ? BINE_IN_PLACE : ds, dr, (size_t)0, count, (void *)st)) return to_mpi(bst);
-    late.commit();
     if (stage_r && hipMemcpyAsync(hr, dr, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess) return MPI_ERR_OTHER;
     return MPI_SUCCESS;
   };
@@ -489,7 +479,6 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
   // drain whatever was issued (also after an error: the registrations must
   // outlive every copy that uses them)
   const int rc2 = finish(e, pins, {{e->h2d, "host-to-device"}, {e->d2h, "device-to-host"}, {st, "collective"}});
-  late.drained = pins.drained;
   // a bounced result reaches the caller's buffer only from a call that
   // completed (an error leaves rbuf as it was)
   if (!rc && !rc2 && bounced && stage_r) memcpy(rbuf, br, rbytes);
