@@ -46,6 +46,10 @@ struct Entry {
   // page-locked bounce buffers for small host buffers (bounce_bytes())
   void *bounce[2] = {nullptr, nullptr};
   size_t bounce_cap[2] = {0, 0};
+  // every collective of this communicator runs as kernels end to end (P = 1,
+  // or the direct transport): small host buffers may be read and written by
+  // those kernels in place (zero_copy_bytes())
+  bool kernels_only = false;
 };
 
 // Small host buffers MAY go through two page-locked bounce buffers the
@@ -79,6 +83,21 @@ void *bounce_buf(Entry *e, int slot, size_t bytes) {
     e->bounce_cap[slot] = bytes;
   }
   return e->bounce[slot];
+}
+
+// Small host buffers in place (zero copy): on a communicator whose
+// collectives are kernels end to end (Entry::kernels_only), a call whose
+// host buffers are at most this many bytes (BINE_HOST_ZERO_COPY_BYTES,
+// default 4 MiB; 0 = off) page-locks them for the call, mapped into the GPU's
+// address space, and hands their device addresses to the collective: its
+// kernels read the input and write the result over PCIe themselves -- no
+// staging copies, no device workspace round trip (C1: one k_dm_fused launch
+// instead of copy in, launch, copy out).
+size_t zero_copy_bytes() {
+  static const size_t v = getenv("BINE_HOST_ZERO_COPY_BYTES")
+                              ? (size_t)strtoull(getenv("BINE_HOST_ZERO_COPY_BYTES"), nullptr, 10)
+                              : (size_t)4 << 20;
+  return v;
 }
 
 // Host buffers page-locked for ONE call.  A permanent
@@ -127,6 +146,7 @@ int drain(hipStream_t s, const char *what, int rank) {
 struct CallPins {
   std::vector<std::pair<uintptr_t, uintptr_t>> want, regs;  // [lo, hi), page-rounded
   bool drained = true;  // false: a copy may still read / write the pages (never unregister then)
+  unsigned flags = hipHostRegisterDefault;  // hipHostRegisterMapped: kernels address the pages (zero copy)
   void add(const void *p, size_t n) {
     if (!register_on() || !p || p == MPI_IN_PLACE || !n) return;
     hipPointerAttribute_t a;
@@ -141,7 +161,7 @@ struct CallPins {
     for (size_t i = 0; i < want.size();) {
       uintptr_t lo = want[i].first, hi = want[i].second;
       for (i++; i < want.size() && want[i].first <= hi; i++) hi = std::max(hi, want[i].second);
-      if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterDefault) == hipSuccess) regs.emplace_back(lo, hi);
+      if (hipHostRegister((void *)lo, hi - lo, flags) == hipSuccess) regs.emplace_back(lo, hi);
       else (void)hipGetLastError();  // stays pageable: HIP stages those copies itself
     }
   }
@@ -154,7 +174,27 @@ struct CallPins {
     for (const auto &r : regs) (void)hipHostUnregister((void *)r.first);
     (void)hipGetLastError();
   }
+  // whether every wanted range got registered (a failed one stays pageable)
+  bool covered() const {
+    for (const auto &w : want) {
+      bool in = false;
+      for (const auto &r : regs) in = in || (r.first <= w.first && w.second <= r.second);
+      if (!in) return false;
+    }
+    return true;
+  }
 };
+
+// the device address of host memory the GPU can address (registered mapped,
+// or the caller's own page-locked memory); nullptr if it cannot
+void *host_dev_ptr(const void *p) {
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
 
 int g_keyval = MPI_KEYVAL_INVALID;
 int g_self_keyval = MPI_KEYVAL_INVALID;
@@ -303,11 +343,13 @@ int get_entry(MPI_Comm comm, Entry **out) {
     delete e;
     return to_mpi(st);
   }
+  e->kernels_only = e->size == 1;
   if (dm) {
     const int dst = bine_comm_set_direct(e->comm, 1);
     if (dst != BINE_SUCCESS && e->rank == 0)
       fprintf(stderr, "libbine(amd): the direct transport is unavailable (%d: %s); using RCCL P2P\n", dst,
               bine_last_error());
+    e->kernels_only = e->kernels_only || dst == BINE_SUCCESS;
   }
   MPI_Comm_set_attr(comm, g_keyval, e);
   g_entries.insert(e);
@@ -422,6 +464,23 @@ int with_buffers(Entry *e, const void *sbuf, size_t sbytes, void *rbuf, size_t r
     if ((stage_s && !bs) || (stage_r && !br)) bs = br = nullptr;  // no bounce memory: register as a large call
   }
   const bool bounced = bs || br;
+  // zero copy: the collective's kernels address the host buffers themselves
+  if (!piped && !bounced && e->kernels_only && register_on() && (stage_s || stage_r) &&
+      std::max(stage_s ? sbytes : 0, stage_r ? rbytes : 0) <= zero_copy_bytes()) {
+    CallPins zp;
+    zp.flags = hipHostRegisterMapped;
+    if (stage_s) zp.add(sbuf, sbytes);
+    if (stage_r) zp.add(rbuf, rbytes);
+    zp.commit();
+    const void *zs = stage_s ? host_dev_ptr(sbuf) : ds;
+    void *zr = stage_r ? host_dev_ptr(rbuf) : dr;
+    if (zp.covered() && zs && zr) {
+      const int bst = body(in_place ? BINE_IN_PLACE : zs, zr, (size_t)0, count, (void *)st);
+      const int rz = finish(e, zp, {{st, "collective"}});
+      return bst ? to_mpi(bst) : rz;
+    }
+    // not addressable: staged as any other call (zp unregisters on return)
+  }
   CallPins pins;
   if (stage_s) {
     void *d;

@@ -198,12 +198,13 @@ def config_model(cfg, P, transport, chunk_bytes=16 << 20, **kw):
 
 # ---- C1 end to end through the unchanged pico_core ----------
 # pico_core hands libbine host (malloc) buffers (pico_core_allreduce_utils.c:13-25):
-# a C1 call is H2D(1 MiB) -> the device collective -> D2H(1 MiB) on the
-# collective's stream (below two staging chunks nothing overlaps), every rank
-# on its own GPU and its own PCIe link on a node.
-T_HOST_RT_US = 66.0      # C1 at P = 1 through pico_core + libbine.so: the 1 MiB host round trip with the
-                         # page-locking and HIP calls around it (profiles/r4_e2e_c1.txt; the bare round
-                         # trip probe: 69-72 us)
+# a C1 call's kernels read the input and write the result in the page-locked
+# host buffers over PCIe (libbine.so zero copy, round 6), every rank on its
+# own GPU and its own PCIe link on a node.
+T_HOST_RT_US = 54.0      # C1 at P = 1 through pico_core + libbine.so: the 1 MiB host round trip, the
+                         # kernel reading and writing the page-locked host buffers over PCIe itself
+                         # (round 6 zero copy; profiles/r6_e2e_c1_zero_copy.txt; staged through device
+                         # buffers: 66 us, profiles/r4_e2e_c1.txt)
 T_FLAG_US = 3.0          # the flag latency one k_dm_fused phase boundary costs: a system-scope store seen
                          # by the peer's poll, one way.  Assumed; bench.py measures it at N > 1
                          # (bine_comm_direct_ping: round trip / 2, "direct_transport_probe") and

@@ -101,11 +101,12 @@ def test_bench_maps_trial_names_to_the_model():
 def test_c1_end_to_end_model():
     """C1 through the unchanged pico_core at P ranks with one
     GPU and one PCIe link each = the measured 1 MiB host round trip (P = 1,
-    66 us) + one k_dm_fused launch + 3 flag round trips + the busiest link's
-    bytes.  Below the reference's own CPU libbine at P = 4 (215 us on the GPU
-    box's cores) even with the device part at its one-GPU measured bound
-    (49 us, ranks sharing one GPU); the one-GPU end-to-end runs (292-417 us at
-    P = 4) put all four ranks' copies on one PCIe link, which a node does not"""
+    54 us with the kernels addressing the host buffers, round 6) + one
+    k_dm_fused launch + 3 flag round trips + the busiest link's bytes.  Below
+    the reference's own CPU libbine at P = 4 (215 us on the GPU box's cores)
+    even with the device part at its one-GPU measured bound (49 us, ranks
+    sharing one GPU); the one-GPU end-to-end runs (263 us at P = 4) put all
+    four ranks' PCIe traffic on one link, which a node does not"""
     assert M.c1_e2e_us(1)["e2e_us"] == M.T_HOST_RT_US
     for P in (2, 4, 8):
         m = M.c1_e2e_us(P)

@@ -71,7 +71,9 @@ if __name__ == "__main__":
         # round 6: libbine.so's defaults (bine_dropin_defaults: flat phases over the
         # direct transport, one k_dm_fused launch; host buffers page-locked per
         # call) against the variants: bounce buffers, pageable, RCCL, literal
-        cfgs = [("default (no BINE_* setting): flat phases, direct transport, per-call page-locking", {}),
+        cfgs = [("default (no BINE_* setting): flat phases, direct transport, host buffers in place (zero copy)", {}),
+                ("default forms, staged through device buffers (BINE_HOST_ZERO_COPY_BYTES=0)",
+                 {"BINE_HOST_ZERO_COPY_BYTES": "0"}),
                 ("default forms, bounce buffers (BINE_HOST_BOUNCE_BYTES=4 MiB)", {"BINE_HOST_BOUNCE_BYTES": str(4 << 20)}),
                 ("default forms, pageable (HIP's own staging)", {"BINE_HOST_REGISTER": "0"}),
                 ("flat phases over RCCL (BINE_DIRECT=0)", {"BINE_DIRECT": "0"}),
