@@ -5,6 +5,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
- "r6r_dropin:400:python -u -m pytest tests/test_gpu.py -k 'pico_core or libbine or op_check' -q --timeout 300 --timeout-method thread -p no:cacheprovider" \
- "r6r_c1p1:200:python -u tools/e2e_staging.py 1 float 262144 500 c1 > gpurun_out/r6r_c1p1.json" \
- "r6r_c1p4:200:GPU_MAX_HW_QUEUES=2 python -u tools/e2e_staging.py 4 float 262144 300 c1 > gpurun_out/r6r_c1p4.json"
+ "r6s_suite:900:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
+ "r6s_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "r6s_bench:240:python -u bench.py > gpurun_out/r6s_bench.json"
