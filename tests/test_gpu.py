@@ -826,7 +826,10 @@ PICO_CORE = os.path.join(ROOT, "integration", "_build", "pico_core")
 # (the reference's literal schedule over RCCL P2P); "rccl" = BINE_DIRECT=0 (the
 # flat phases over RCCL P2P).  BINE_FAKE_HOSTS is the harness's (two ranks on
 # one GPU need distinct RCCL host ids, integration/run_pico_core.sh).
-FORMS = {"default": {}, "literal": {"BINE_LITERAL": "1"}, "rccl": {"BINE_DIRECT": "0"}}
+FORMS = {"default": {}, "literal": {"BINE_LITERAL": "1"}, "rccl": {"BINE_DIRECT": "0"},
+         # the default forms with small host buffers staged through device
+         # buffers instead of addressed in place (zero copy)
+         "staged": {"BINE_HOST_ZERO_COPY_BYTES": "0"}}
 
 
 @pytest.mark.skipif(not os.path.exists(PICO_CORE), reason="reference pico_core not built (integration/Makefile)")
@@ -872,16 +875,18 @@ def test_reference_pico_core_dropin(dev, tmp_path, np_, coll, algo, dtype, form,
 
 @pytest.mark.skipif(not os.path.exists(PICO_CORE), reason="reference pico_core not built (integration/Makefile)")
 @pytest.mark.parametrize("algo,form", [("bine_bdw_remap_over", "default"), ("bine_bdw_remap_over", "literal"),
-                                       ("bine_bdw_remap_over", "rccl"), ("bine_lat_over", "default")])
+                                       ("bine_bdw_remap_over", "rccl"), ("bine_lat_over", "default"),
+                                       ("bine_bdw_remap_over", "staged")])
 def test_reference_pico_core_c1(dev, tmp_path, algo, form):
     """BASELINE configs[0] (C1) through the GPU path exactly as the reference
     runs it: the unchanged pico_core, 4 ranks, 262,144 fp32 elements (1 MiB)
     per rank, allreduce SUM (pico_core_utils.h:262), 20 iterations, every one
     checked by pico_core against MPICH's PMPI_Allreduce (pico_core_utils.c:
     553-610, 960-992); the 4 ranks share the GPU through RCCL's socket
-    transport (distinct NCCL_HOSTIDs); host buffers, staged by libbine.so.
-    "default": no BINE_* setting -- libbine.so's own choice (VERDICT r5 item
-    4: the flat phases over the direct transport, one k_dm_fused launch)"""
+    transport (distinct NCCL_HOSTIDs); host buffers.  "default": no BINE_*
+    setting -- libbine.so's own choice (the flat phases over
+    the direct transport, one k_dm_fused launch, the host buffers addressed in
+    place); "staged": the same through device buffers"""
     env = dict(os.environ, PICO_OUT=str(tmp_path), BINE_FAKE_HOSTS="1", **FORMS[form])
     for k in ("BINE_LITERAL", "BINE_DIRECT", "BINE_FLAT_RS", "BINE_FLAT_AG"):
         if k not in FORMS[form]:
@@ -899,7 +904,7 @@ OP_CHECK = os.path.join(ROOT, "integration", "_build", "op_check")
 
 
 @pytest.mark.skipif(not os.path.exists(OP_CHECK), reason="integration/op_check not built (integration/Makefile)")
-@pytest.mark.parametrize("np_,form", [(1, "default"), (2, "literal"), (2, "default"), (2, "rccl")])
+@pytest.mark.parametrize("np_,form", [(1, "default"), (2, "literal"), (2, "default"), (2, "rccl"), (2, "staged")])
 def test_mpi_typed_entry_points_match_mpich(dev, np_, form):
     """integration/op_check: libbine.so's MPI-typed entry points (allreduce,
     reduce_scatter, reduce, bcast, allgather, gather, scatter, alltoall; host
