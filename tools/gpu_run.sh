@@ -5,6 +5,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
- "r6s_suite:900:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
- "r6s_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
- "r6s_bench:240:python -u bench.py > gpurun_out/r6s_bench.json"
+ "r6t_staged:300:python -u -m pytest tests/test_gpu.py -k 'staged' -v --timeout 200 --timeout-method thread -p no:cacheprovider"
