@@ -15,7 +15,7 @@ Configuration set "c1" (BASELINE config C1: 262,144 fp32 per rank at P = 4,
 the reference's own CPU-runnable case): the transports libbine.so offers --
 RCCL, RCCL with the flat phases, the direct transport, the direct transport
 with the flat phases (one k_dm_fused launch per call).
-usage: python tools/e2e_staging.py [NP] [DTYPE] [COUNT] [ITERS] [chunks|pipeline|c1]"""
+usage: python tools/e2e_staging.py [NP] [DTYPE] [COUNT] [ITERS] [chunks|pipeline|c1|zc]"""
 import json
 import os
 import statistics
@@ -78,6 +78,11 @@ if __name__ == "__main__":
                 ("default forms, pageable (HIP's own staging)", {"BINE_HOST_REGISTER": "0"}),
                 ("flat phases over RCCL (BINE_DIRECT=0)", {"BINE_DIRECT": "0"}),
                 ("literal schedule over RCCL (BINE_LITERAL=1, round 5's default)", {"BINE_LITERAL": "1"})]
+    if len(sys.argv) > 5 and sys.argv[5] == "zc":
+        # the zero-copy threshold (BINE_HOST_ZERO_COPY_BYTES): the default forms
+        # with the host buffers addressed in place vs staged through device buffers
+        cfgs = [("zero copy (BINE_HOST_ZERO_COPY_BYTES=1 GiB)", {"BINE_HOST_ZERO_COPY_BYTES": str(1 << 30)}),
+                ("staged (BINE_HOST_ZERO_COPY_BYTES=0)", {"BINE_HOST_ZERO_COPY_BYTES": "0"})]
     for name, env in cfgs:
         r = run(np_, dtype, count, iters, env)
         if "ms_median" in r:
