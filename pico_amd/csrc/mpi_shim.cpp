@@ -88,15 +88,18 @@ void *bounce_buf(Entry *e, int slot, size_t bytes) {
 // Small host buffers in place (zero copy): on a communicator whose
 // collectives are kernels end to end (Entry::kernels_only), a call whose
 // host buffers are at most this many bytes (BINE_HOST_ZERO_COPY_BYTES,
-// default 4 MiB; 0 = off) page-locks them for the call, mapped into the GPU's
+// default 16 MiB; 0 = off) page-locks them for the call, mapped into the GPU's
 // address space, and hands their device addresses to the collective: its
 // kernels read the input and write the result over PCIe themselves -- no
 // staging copies, no device workspace round trip (C1: one k_dm_fused launch
-// instead of copy in, launch, copy out).
+// instead of copy in, launch, copy out).  Measured through pico_core on one
+// GPU (profiles/r6_zero_copy_threshold.txt): faster than staging at 1, 4 and
+// 16 MiB per rank for P = 1, 2, 4 (by 10-28 %); from 32 MiB the staging is
+// pipelined (into the collective at P > 1) instead.
 size_t zero_copy_bytes() {
   static const size_t v = getenv("BINE_HOST_ZERO_COPY_BYTES")
                               ? (size_t)strtoull(getenv("BINE_HOST_ZERO_COPY_BYTES"), nullptr, 10)
-                              : (size_t)4 << 20;
+                              : (size_t)16 << 20;
   return v;
 }
 
