@@ -4,11 +4,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+R="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 bash tools/gpu_steps.sh \
- "r6w_sizes1:200:BINE_COPY_SMALL_U=1 python -u -m pytest tests/test_gpu_bench_sizes.py -q --timeout 150 --timeout-method thread -p no:cacheprovider" \
- "r6w_u8:100:python -u tools/e2e_staging.py 1 float 262144 500 zc > gpurun_out/r6w_u8.json" \
- "r6w_u4:100:BINE_COPY_SMALL_U=4 python -u tools/e2e_staging.py 1 float 262144 500 zc > gpurun_out/r6w_u4.json" \
- "r6w_u2:100:BINE_COPY_SMALL_U=2 python -u tools/e2e_staging.py 1 float 262144 500 zc > gpurun_out/r6w_u2.json" \
- "r6w_u1:100:BINE_COPY_SMALL_U=1 python -u tools/e2e_staging.py 1 float 262144 500 zc > gpurun_out/r6w_u1.json" \
- "r6w_u1_4m:100:BINE_COPY_SMALL_U=1 python -u tools/e2e_staging.py 1 float 1048576 200 zc > gpurun_out/r6w_u1_4m.json" \
- "r6w_u8_4m:100:python -u tools/e2e_staging.py 1 float 1048576 200 zc > gpurun_out/r6w_u8_4m.json"
+ "r6x_suite:800:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
+ "r6x_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "r6x_bench:240:python -u bench.py > gpurun_out/r6x_bench.json" \
+ "r6x_b8:300:GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 8 --master-port 29515 bench.py --gpus 8 --steps 20 --warmup 5 > gpurun_out/r6x_b8.json"
