@@ -1056,6 +1056,14 @@ static bool plan_fused_env(const FusedEnv &e, const Schedule &sc, Ptr ptr, size_
   return true;
 }
 
+// the direct transport is on and other ranks of this communicator share this
+// rank's GPU (BINE_SHARED_GPU_SINGLE_STREAM=0: keep two streams there too)
+static bool shared_gpu_direct(bine_comm *c) {
+  static const bool on = !getenv("BINE_SHARED_GPU_SINGLE_STREAM") || atoi(getenv("BINE_SHARED_GPU_SINGLE_STREAM")) != 0;
+  auto *rt = dynamic_cast<RcclTransport *>(c->tx.get());
+  return on && rt && rt->dm_on && rt->dm && rt->dm->share > 1;
+}
+
 template <typename Ptr>
 static bool plan_fused(bine_comm *c, const Schedule &sc, Ptr ptr, size_t esz, int dtype, int op, bool single,
                        std::vector<DmFusedArgs> &out) {
@@ -1731,7 +1739,7 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
     roctxRangePushA(lbl);
   }
   // one rank: local ops only, so one stream (and a one-branch graph)
-  const bool single = bytes <= c->single_stream_bytes || c->size == 1;
+  bool single = bytes <= c->single_stream_bytes || c->size == 1;
   if (stg) {
     auto sit = c->stage_cache.find(key);
     if (sit == c->stage_cache.end()) {
@@ -1744,6 +1752,12 @@ static int run_collective(bine_comm *c, PlanArgs &a, const void *sbuf, void *rbu
   const void *src = a.in_place ? rbuf : sbuf;
   const bool fused = !single && !stg && fused_for(c, key, sc, src, rbuf, a.esz, dtype, op);
   const DmTreePlan *tpl = single || stg || fused ? nullptr : tree_plan_for(c, key, sc, src, rbuf, a.esz, dtype, op);
+  // ranks sharing ONE GPU over the direct transport: a call that would hand
+  // its chunks between the comm stream and the caller's stream (no one-launch
+  // form, no trees inside the exchanges) runs on the caller's stream alone --
+  // with 8 processes on one GPU those hand-offs cost 100-1,300 ms per C3 call,
+  // one stream 3-4 ms (profiles/r6_single_stream_shared.txt)
+  if (!single && !fused && !tpl && shared_gpu_direct(c)) single = true;
   rc = order_begin(c, K);
   if (rc) {
   } else if (c->graphs && K && !c->hub && !c->profile && !roctx_on() && !trace_on() && !stg &&

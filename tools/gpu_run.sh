@@ -4,8 +4,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+R="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 bash tools/gpu_steps.sh \
- "r6y_dm2s:150:PROBE_TRANSPORT=direct+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6y_dm2s.json" \
- "r6y_dm1s:150:BINE_SINGLE_STREAM_BYTES=1073741824 PROBE_TRANSPORT=direct+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6y_dm1s.json" \
- "r6y_fdm1s:150:BINE_SINGLE_STREAM_BYTES=1073741824 PROBE_TRANSPORT=flatrs+flat+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6y_fdm1s.json" \
- "r6y_fdm2s:150:PROBE_TRANSPORT=flatrs+flat+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6y_fdm2s.json"
+ "r6z_dm:150:PROBE_TRANSPORT=direct+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6z_dm.json" \
+ "r6z_b8:300:GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 8 --master-port 29515 bench.py --gpus 8 --steps 20 --warmup 5 > gpurun_out/r6z_b8.json" \
+ "r6z_suite:800:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15"
