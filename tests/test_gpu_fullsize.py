@@ -293,6 +293,8 @@ def test_full_size_configs_eight_processes():
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = _sub.run_kw([sys.executable, "-u", os.path.join(ROOT, "tools", "fullsize_multirank.py"), "8"], env=env,
                        capture_output=True, text=True, timeout=680, ranks=8)
-    tail = "\n".join(r.stdout.splitlines()[-20:])
-    assert r.returncode == 0, tail + "\n" + r.stderr[-2000:]
+    # every MISMATCH line first (which case, on which rank), then the tail
+    bad = [x for x in r.stdout.splitlines() if "MISMATCH" in x]
+    tail = "\n".join(bad[:64] + r.stdout.splitlines()[-12:])
+    assert r.returncode == 0, tail + "\n" + r.stderr[-1500:]
     assert "RESULT P=8: ok" in r.stdout
