@@ -4,8 +4,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-R="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 bash tools/gpu_steps.sh \
- "r6z_dm:150:PROBE_TRANSPORT=direct+dm PROBE_CHUNK_MIB=16 GPU_MAX_HW_QUEUES=1 python -u tools/fused8_probe.py 8 3 2 > gpurun_out/r6z_dm.json" \
- "r6z_b8:300:GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 8 --master-port 29515 bench.py --gpus 8 --steps 20 --warmup 5 > gpurun_out/r6z_b8.json" \
- "r6z_suite:800:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15"
+ "r6ab_ss1:200:BINE_SHARED_GPU_SINGLE_STREAM=1 GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_ss1.txt" \
+ "r6ab_ss2:200:BINE_SHARED_GPU_SINGLE_STREAM=1 GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_ss2.txt" \
+ "r6ab_ss3:200:BINE_SHARED_GPU_SINGLE_STREAM=1 GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_ss3.txt" \
+ "r6ab_def:200:GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_def.txt"
