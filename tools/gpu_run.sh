@@ -5,7 +5,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
- "r6ab_ss1:200:BINE_SHARED_GPU_SINGLE_STREAM=1 GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_ss1.txt" \
- "r6ab_ss2:200:BINE_SHARED_GPU_SINGLE_STREAM=1 GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_ss2.txt" \
- "r6ab_ss3:200:BINE_SHARED_GPU_SINGLE_STREAM=1 GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_ss3.txt" \
- "r6ab_def:200:GPU_MAX_HW_QUEUES=2 python -u tools/fullsize_multirank.py 8 > gpurun_out/r6ab_def.txt"
+ "r6ac_suite:800:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
+ "r6ac_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "r6ac_bench:240:python -u bench.py > gpurun_out/r6ac_bench.json"
