@@ -910,9 +910,10 @@ __device__ __forceinline__ void dm_stamp(uint64_t *st, uint32_t serial, int kind
 // exchange flips the inbox word), leave what it waited for in the host words
 // (dm::TimeoutRecord, read by DirectState::describe): which kernel and phase,
 // the peer, the slot, the sequence number wanted and the flag value last
-// seen, the launch's serial, the workgroup and how long it waited.  The
-// record's stores come before the poison word's (release), so a host that
-// sees the word set sees the record.
+// seen, the launch's serial, the workgroup and how long it waited.  Only
+// that waiter sets the host word, after its record (release), so a host that
+// sees the word set sees the record (a later waiter setting the word could
+// let the host see it before the first one's record had landed).
 __device__ __noinline__ void dm_time_out(uint32_t *poison, uint32_t *host, uint32_t kind, uint32_t phase, int rank,
                                          int peer, uint64_t slot, uint64_t want, uint64_t seen, uint32_t serial,
                                          uint64_t waited) {
@@ -932,8 +933,8 @@ __device__ __noinline__ void dm_time_out(uint32_t *poison, uint32_t *host, uint3
 #pragma unroll
     for (int i = 0; i < dm::kRecWords; i++)
       __hip_atomic_store(h + dm::kRecFirst + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __hip_atomic_store(host, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // one workgroup's share of message mi (workgroup wi of a.wgs): wait, copy,
