@@ -4,11 +4,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
+R="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 bash tools/gpu_steps.sh \
- "r6ad_suite:800:python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider --durations=15" \
- "r6ad_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
- "bench:240:python -u bench.py > gpurun_out/bench.json" \
- "prof:200:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline" \
- "pmcf:70:BENCH_NO_SMALL_WINDOWS=1 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --no-cpu-baseline" \
- "pmcw:70:BENCH_NO_SMALL_WINDOWS=1 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --no-cpu-baseline"
+ "r6ae_bench:240:python -u bench.py > gpurun_out/r6ae_bench.json" \
+ "r6ae_b8:300:GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 8 --master-port 29515 bench.py --gpus 8 --steps 20 --warmup 5 > gpurun_out/r6ae_b8.json" \
+ "r6ae_b2:300:GPU_MAX_HW_QUEUES=1 BINE_FAKE_HOSTS=1 $R --nproc-per-node 2 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 > gpurun_out/r6ae_b2.json"
