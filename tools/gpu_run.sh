@@ -5,4 +5,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 bash tools/gpu_steps.sh \
- "r6af_suite_ss:800:BINE_SHARED_GPU_SINGLE_STREAM=1 python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider"
+ "r6ag_smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "r6ag_sub:400:python -u -m pytest tests/test_gpu.py tests/test_gpu_rccl.py -k 'pico_core or rebuilt or launch_caps or reduce_local' -q --timeout 300 --timeout-method thread -p no:cacheprovider" \
+ "r6ag_bench:240:python -u bench.py > gpurun_out/r6ag_bench.json"
